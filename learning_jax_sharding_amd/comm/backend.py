@@ -1,0 +1,278 @@
+"""Collective backends.
+
+Two personalities, one interface (every call takes ``{device_id: tensor}`` for
+the *local* participants and a list of device groups that partition the
+participating devices):
+
+* :class:`LocalComm` - every device lives in this process (host devices, or
+  virtual devices on one MI355X).  Collectives are direct tensor copies and
+  sums on the owning torch device; this is also the "loopback" backend the
+  survey asks for, since an RCCL communicator cannot contain the
+  same GPU twice.
+* :class:`DistComm` - one device per process (``torchrun``): RCCL over xGMI on
+  GPUs (``nccl`` backend), gloo on CPU.  Sub-group process groups are created
+  for a whole partition at once, in a deterministic order, so every rank makes
+  the same ``new_group`` calls (a requirement of ``torch.distributed``).
+
+Reductions accumulate bf16/f16 in f32 in the local backend; RCCL reduces in the
+tensor dtype (gradients are f32 here, so this only affects bf16 activations).
+
+Every call is also reported to the active :mod:`~..spmd.plan` recorder so the
+partitioner's collective plan can be printed and tested.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..runtime.devices import is_distributed, local_devices, process_index
+
+__all__ = ["get_comm", "reset_comm", "LocalComm", "DistComm", "Transfer"]
+
+Groups = Sequence[Tuple[int, ...]]
+
+
+class Transfer:
+    """Copy ``src_slices`` of device ``src``'s tensor into ``dst_slices`` of device ``dst``'s output."""
+
+    __slots__ = ("dst", "src", "src_slices", "dst_slices")
+
+    def __init__(self, dst: int, src: int, src_slices, dst_slices):
+        self.dst, self.src = int(dst), int(src)
+        self.src_slices = tuple(src_slices)
+        self.dst_slices = tuple(dst_slices)
+
+    def reversed(self) -> "Transfer":
+        return Transfer(self.src, self.dst, self.dst_slices, self.src_slices)
+
+    def __repr__(self):
+        return f"Transfer({self.src}->{self.dst})"
+
+
+def _acc_dtype(dt: torch.dtype) -> torch.dtype:
+    return torch.float32 if dt in (torch.bfloat16, torch.float16) else dt
+
+
+class LocalComm:
+    kind = "local"
+
+    def all_gather(self, xs: Dict[int, torch.Tensor], groups: Groups, dim: int) -> Dict[int, torch.Tensor]:
+        out = {}
+        for g in groups:
+            parts = [xs[d] for d in g]
+            for d in g:
+                dev = xs[d].device
+                out[d] = torch.cat([p.to(dev) for p in parts], dim)
+        return out
+
+    def reduce_scatter(self, xs, groups, dim):
+        out = {}
+        for g in groups:
+            if len(g) == 1:
+                out[g[0]] = xs[g[0]].clone()
+                continue
+            dev0 = xs[g[0]].device
+            dt = xs[g[0]].dtype
+            total = None
+            for d in g:
+                v = xs[d].to(dev0, _acc_dtype(dt))
+                total = v if total is None else total + v
+            chunks = total.to(dt).chunk(len(g), dim)
+            for i, d in enumerate(g):
+                out[d] = chunks[i].to(xs[d].device).contiguous()
+        return out
+
+    def all_reduce(self, xs, groups):
+        out = {}
+        for g in groups:
+            if len(g) == 1:
+                out[g[0]] = xs[g[0]].clone()
+                continue
+            dev0 = xs[g[0]].device
+            dt = xs[g[0]].dtype
+            total = None
+            for d in g:
+                v = xs[d].to(dev0, _acc_dtype(dt))
+                total = v if total is None else total + v
+            total = total.to(dt)
+            for d in g:
+                out[d] = total.to(xs[d].device, copy=True)
+        return out
+
+    def all_to_all(self, xs, groups, split_dim: int, concat_dim: int, perms=None):
+        """Member i receives chunk ``perm_j[i]`` of every member j's tensor, concatenated in member order."""
+        out = {}
+        for gi, g in enumerate(groups):
+            n = len(g)
+            perm = perms[gi] if perms is not None else list(range(n))
+            chunks = {d: xs[d].chunk(n, split_dim) for d in g}
+            for i, d in enumerate(g):
+                dev = xs[d].device
+                out[d] = torch.cat([chunks[s][perm[i]].to(dev) for s in g], concat_dim).contiguous()
+        return out
+
+    def exchange(self, xs, transfers: Sequence[Transfer], out_meta: Dict[int, Tuple[tuple, torch.dtype, torch.device]],
+                 accumulate: bool = False):
+        out = {}
+        for d, (shape, dt, dev) in out_meta.items():
+            out[d] = torch.zeros(shape, dtype=dt, device=dev) if accumulate else torch.empty(shape, dtype=dt, device=dev)
+        for t in transfers:
+            if t.dst not in out:
+                continue
+            piece = xs[t.src][t.src_slices].to(out[t.dst].device)
+            if accumulate:
+                out[t.dst][t.dst_slices] += piece
+            else:
+                out[t.dst][t.dst_slices] = piece
+        return out
+
+
+class DistComm:
+    """One local device per process; groups map to torch process groups."""
+
+    kind = "dist"
+
+    def __init__(self):
+        self.me = local_devices()[0].id
+        self._pgs: Dict[Tuple[Tuple[int, ...], ...], Dict[Tuple[int, ...], object]] = {}
+        self._lock = threading.Lock()
+
+    def _group_of(self, groups: Groups) -> Tuple[Tuple[int, ...], object]:
+        key = tuple(tuple(int(x) for x in g) for g in groups)
+        with self._lock:
+            pgs = self._pgs.get(key)
+            if pgs is None:
+                pgs = {}
+                world = dist.get_world_size()
+                for g in key:
+                    if len(g) == 1:
+                        continue
+                    if len(g) == world and sorted(g) == list(range(world)) and list(g) == sorted(g):
+                        pgs[g] = dist.group.WORLD
+                    else:
+                        # every rank creates every group of the partition, in the same order
+                        pgs[g] = dist.new_group(ranks=sorted(g))
+                self._pgs[key] = pgs
+        for g in key:
+            if self.me in g:
+                return g, pgs.get(g)
+        raise RuntimeError(f"device {self.me} is in none of the groups {key}")
+
+    def _member_order_ok(self, g) -> bool:
+        # torch process-group ranks follow sorted global ranks; our groups may list members in
+        # tile order, so data is permuted explicitly below when they differ.
+        return list(g) == sorted(g)
+
+    def all_gather(self, xs, groups, dim):
+        g, pg = self._group_of(groups)
+        x = xs[self.me].contiguous()
+        if pg is None:
+            return {self.me: x.clone()}
+        n = len(g)
+        buf = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(buf.view((n * x.shape[0],) + tuple(x.shape[1:])) if x.dim() else buf.view(n), x, group=pg)
+        if not self._member_order_ok(g):
+            order = [sorted(g).index(d) for d in g]
+            buf = buf[order]
+        out = buf.movedim(0, dim).reshape(x.shape[:dim] + (n * x.shape[dim],) + x.shape[dim + 1:])
+        return {self.me: out.contiguous()}
+
+    def reduce_scatter(self, xs, groups, dim):
+        g, pg = self._group_of(groups)
+        x = xs[self.me]
+        if pg is None:
+            return {self.me: x.clone()}
+        n = len(g)
+        s = x.shape[dim] // n
+        xt = x.reshape(x.shape[:dim] + (n, s) + x.shape[dim + 1:]).movedim(dim, 0)
+        if not self._member_order_ok(g):
+            # chunk k belongs to member g[k]; the collective hands chunk r to the r-th sorted rank
+            srt = sorted(g)
+            xt = xt[[g.index(d) for d in srt]]
+        xt = xt.contiguous()
+        out = torch.empty(xt.shape[1:], dtype=x.dtype, device=x.device)
+        dist.reduce_scatter_tensor(out.view(-1), xt.view(-1), group=pg)
+        return {self.me: out}
+
+    def all_reduce(self, xs, groups):
+        g, pg = self._group_of(groups)
+        x = xs[self.me].clone()
+        if pg is not None:
+            dist.all_reduce(x, group=pg)
+        return {self.me: x}
+
+    def all_to_all(self, xs, groups, split_dim, concat_dim, perms=None):
+        g, pg = self._group_of(groups)
+        x = xs[self.me]
+        n = len(g)
+        if pg is None:
+            return {self.me: x.clone()}
+        gi = [tuple(gg) for gg in groups].index(tuple(g))
+        perm = perms[gi] if perms is not None else list(range(n))
+        srt = sorted(g)
+        s = x.shape[split_dim] // n
+        chunks = x.reshape(x.shape[:split_dim] + (n, s) + x.shape[split_dim + 1:]).movedim(split_dim, 0)
+        # the chunk sent to group member at tile position i is chunk perm[i]; order sends by sorted rank
+        send = chunks[[perm[g.index(r)] for r in srt]].contiguous()
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv.view(n, -1), send.view(n, -1), group=pg)
+        # recv[k] came from sorted rank srt[k]; concatenate in member (tile) order
+        recv = recv[[srt.index(d) for d in g]]
+        out = recv.movedim(0, concat_dim)
+        shp = list(recv.shape[1:])
+        shp[concat_dim] *= n
+        return {self.me: out.reshape(shp).contiguous()}
+
+    def exchange(self, xs, transfers, out_meta, accumulate=False):
+        me = self.me
+        out = {}
+        if me in out_meta:
+            shape, dt, dev = out_meta[me]
+            out[me] = torch.zeros(shape, dtype=dt, device=dev) if accumulate else torch.empty(shape, dtype=dt, device=dev)
+        ops = []
+        recv_bufs = []
+        for t in transfers:
+            if t.src == me and t.dst == me:
+                piece = xs[me][t.src_slices]
+                if accumulate:
+                    out[me][t.dst_slices] += piece
+                else:
+                    out[me][t.dst_slices] = piece
+            elif t.src == me:
+                ops.append(dist.P2POp(dist.isend, xs[me][t.src_slices].contiguous(), t.dst))
+            elif t.dst == me:
+                shape = tuple(s.stop - s.start for s in t.dst_slices)
+                buf = torch.empty(shape, dtype=out[me].dtype, device=out[me].device)
+                recv_bufs.append((t, buf))
+                ops.append(dist.P2POp(dist.irecv, buf, t.src))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        for t, buf in recv_bufs:
+            if accumulate:
+                out[me][t.dst_slices] += buf
+            else:
+                out[me][t.dst_slices] = buf
+        return out
+
+
+_COMM = None
+_COMM_LOCK = threading.Lock()
+
+
+def get_comm():
+    global _COMM
+    if _COMM is None:
+        with _COMM_LOCK:
+            if _COMM is None:
+                _COMM = DistComm() if is_distributed() else LocalComm()
+    return _COMM
+
+
+def reset_comm():
+    global _COMM
+    with _COMM_LOCK:
+        _COMM = None

@@ -1,0 +1,135 @@
+"""Per-device compute: hand-written HIP kernels on MI355X, torch on host devices.
+
+Every function here takes and returns *local* torch tensors (one device's
+shard).  On a ROCm tensor the call goes to the gfx950 HIP extension
+(:mod:`.hip`); that path fails loudly if the extension is not built - there
+is no silent torch fallback for GPU tensors (``LJS_ALLOW_TORCH_FALLBACK=1``
+opts in, for debugging only).  Host-device (CPU) tensors use torch, which is
+also the numerical oracle the GPU tests compare against.
+
+Numerics follow the reference's bf16 recipe (``case6_attention.py:46,120-130``):
+bf16 operands, f32 accumulation, f32 softmax, probabilities rounded to bf16
+before P·V.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+__all__ = ["cast", "reduce_sum", "dot_general", "linear", "softmax", "attention", "use_hip"]
+
+_LOW = (torch.bfloat16, torch.float16)
+
+
+def use_hip(t: torch.Tensor) -> bool:
+    return t.is_cuda and not t.is_meta
+
+
+def _hip():
+    from . import hip
+    return hip
+
+
+# ----------------------------------------------------------------------------- casts / reductions
+def cast(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    if t.dtype == dtype:
+        return t
+    if use_hip(t) and _hip().supports_cast(t.dtype, dtype):
+        return _hip().cast(t, dtype)
+    return t.to(dtype)
+
+
+def reduce_sum(t: torch.Tensor, axes: Sequence[int], keepdim: bool, acc_dtype: torch.dtype) -> torch.Tensor:
+    if not axes:
+        return t.to(acc_dtype)
+    if use_hip(t) and len(axes) == t.dim() and not keepdim:
+        return _hip().sum_all(t, acc_dtype)
+    return t.sum(dim=tuple(axes), keepdim=keepdim, dtype=acc_dtype)
+
+
+# ----------------------------------------------------------------------------- matmuls
+def _to_bmk(a: torch.Tensor, batch, free, contract):
+    perm = list(batch) + list(free) + list(contract)
+    x = a.permute(perm)
+    B = 1
+    for i in batch:
+        B *= a.shape[i]
+    M = 1
+    for i in free:
+        M *= a.shape[i]
+    Kd = 1
+    for i in contract:
+        Kd *= a.shape[i]
+    return x.reshape(B, M, Kd)
+
+
+def dot_general(a: torch.Tensor, b: torch.Tensor, lc, rc, lb, rb, out_dtype: torch.dtype) -> torch.Tensor:
+    lf = [i for i in range(a.dim()) if i not in lc and i not in lb]
+    rf = [i for i in range(b.dim()) if i not in rc and i not in rb]
+    A = _to_bmk(a, lb, lf, lc)                       # (B, M, K)
+    Bt = _to_bmk(b, rb, rf, rc)                      # (B, N, K)
+    out_shape = [a.shape[i] for i in lb] + [a.shape[i] for i in lf] + [b.shape[i] for i in rf]
+    if use_hip(a):
+        C = _hip().bmm_nt(A, Bt, out_dtype)          # C[b] = A[b] @ Bt[b]^T
+    else:
+        if A.dtype in _LOW or Bt.dtype in _LOW:
+            C = torch.bmm(A.float(), Bt.float().transpose(1, 2)).to(out_dtype)
+        else:
+            C = torch.bmm(A.to(out_dtype if out_dtype.is_floating_point else A.dtype),
+                          Bt.to(out_dtype if out_dtype.is_floating_point else Bt.dtype).transpose(1, 2)).to(out_dtype)
+    return C.reshape(out_shape)
+
+
+def linear(x: torch.Tensor, ws: Sequence[torch.Tensor], b: Optional[torch.Tensor], compute_dtype: torch.dtype,
+           relu: bool = False, out_dtype: Optional[torch.dtype] = None) -> List[torch.Tensor]:
+    """``[x @ w (+ b)(relu) for w in ws]`` in ``compute_dtype`` (flax ``Dense`` semantics)."""
+    out_dtype = out_dtype or compute_dtype
+    if use_hip(x):
+        return _hip().linear(x, list(ws), b, compute_dtype, relu, out_dtype)
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    xc = x2.to(compute_dtype)
+    outs = []
+    for w in ws:
+        wc = w.to(compute_dtype)
+        if compute_dtype in _LOW:
+            y = xc.float() @ wc.float()
+            if b is not None:
+                y = y + b.to(compute_dtype).float()
+        else:
+            y = xc @ wc
+            if b is not None:
+                y = y + b.to(compute_dtype)
+        if relu:
+            y = torch.relu(y)
+        outs.append(y.to(out_dtype).reshape(tuple(lead) + (w.shape[-1],)))
+    return outs
+
+
+# ----------------------------------------------------------------------------- softmax / attention
+def softmax(t: torch.Tensor, axis: int) -> torch.Tensor:
+    if use_hip(t) and axis % t.dim() == t.dim() - 1 and t.dtype == torch.float32:
+        return _hip().softmax_lastdim(t)
+    return torch.softmax(t.float(), dim=axis).to(t.dtype)
+
+
+def attention_reference(q, k, v, scale: float, causal: bool = False, q_offset: int = 0) -> torch.Tensor:
+    """Plain torch oracle of ``case6_attention.py:120-133`` on (b, s, n, h) tensors."""
+    qf, kf = q.float(), k.float()
+    s = torch.einsum("btnh,bfnh->bnft", kf, qf) * scale
+    if causal:
+        sq, sk = q.shape[1], k.shape[1]
+        qi = torch.arange(sq, device=q.device)[:, None] + q_offset
+        ki = torch.arange(sk, device=q.device)[None, :]
+        s = s.masked_fill(ki > qi, float("-inf"))
+    p = torch.softmax(s, dim=-1).to(v.dtype)
+    o = torch.einsum("bnft,btnh->bfnh", p.float(), v.float())
+    return o.to(v.dtype)
+
+
+def attention(q, k, v, scale: float, causal: bool = False, q_offset: int = 0) -> torch.Tensor:
+    if use_hip(q):
+        return _hip().attention(q, k, v, scale, causal, q_offset)
+    return attention_reference(q, k, v, scale, causal, q_offset)

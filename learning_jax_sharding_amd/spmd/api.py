@@ -1,0 +1,370 @@
+"""``jit`` / ``grad`` / ``value_and_grad`` / ``eval_shape``.
+
+* ``jit(f, in_shardings, out_shardings, static_argnums, donate_argnums)``
+  (``case6_attention.py:192-194,206-207,229-230``): reshard inputs to
+  ``in_shardings``, run ``f`` through the eager SPMD partitioner
+  (:mod:`..ops.core`), reshard outputs to ``out_shardings``.  Instead of a
+  tracing compiler, the MI355X fast path is a **HIP graph**: with
+  ``capture=True`` (or ``LJS_JIT_GRAPH=1``) the second call with a given
+  signature is captured into a ``torch.cuda.CUDAGraph`` (hipGraph on ROCm) and
+  every later call is one graph replay - no Python, no partitioning, no
+  per-kernel launch cost.  Outputs of a captured function live in the graph's
+  static buffers and are overwritten by the next call (the same contract as
+  donated buffers).
+* ``grad`` (``case6_attention.py:212``): reverse mode through torch autograd
+  on the per-device shards.  Collectives are differentiable with transposed
+  collectives (:mod:`..comm.collectives`).  The per-device cotangents of a
+  parameter are partial; they are summed over each tile's replica group with
+  one bucketed all-reduce per replica-group pattern - this *is* the data
+  parallel gradient all-reduce, derived from the shardings.
+* ``eval_shape`` (``case6_attention.py:189``): run ``f`` on meta tensors.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..array import ShapeDtypeStruct, ShardedArray, device_put
+from ..comm import collectives as C
+from ..sharding.shardings import Sharding, SingleDeviceSharding
+from ..sharding.tile import TileAssignment
+from ..utils import tree as T
+from . import plan as _plan
+from . import state as _state
+from .reshard import reshard
+
+__all__ = ["jit", "grad", "value_and_grad", "eval_shape", "Jitted", "reduce_replica_grads"]
+
+
+def _is_arraylike(x) -> bool:
+    import numpy as np
+    return isinstance(x, (ShardedArray, torch.Tensor, np.ndarray))
+
+
+def _apply_shardings(tree, shardings):
+    """Reshard / place every array leaf of ``tree`` per the (prefix) tree ``shardings``."""
+    if shardings is None:
+        return tree
+
+    def place(x, s):
+        if s is None or not _is_arraylike(x):
+            return x
+        if isinstance(x, ShardedArray):
+            return reshard(x, s)
+        return device_put(x, s)
+
+    return T.tree_map(place, tree, shardings, is_leaf=lambda x: isinstance(x, (ShardedArray, ShapeDtypeStruct)))
+
+
+def _leaf_is_array(x):
+    return isinstance(x, ShardedArray)
+
+
+class Lowered:
+    def __init__(self, plan: _plan.PlanRecorder):
+        self.plan = plan
+
+    def as_text(self) -> str:
+        return self.plan.as_text()
+
+    def compile(self):
+        return self
+
+
+class _Captured:
+    """A hipGraph of one call signature: static inputs, static outputs."""
+
+    def __init__(self, graph, in_leaves, out_tree):
+        self.graph = graph
+        self.in_leaves = in_leaves  # list of ShardedArray (static buffers)
+        self.out_tree = out_tree
+
+
+class Jitted:
+    def __init__(self, fun: Callable, in_shardings=None, out_shardings=None, static_argnums=(),
+                 donate_argnums=(), capture: Optional[bool] = None, warmup_calls: int = 1):
+        self.fun = fun
+        self.in_shardings = in_shardings
+        self.out_shardings = out_shardings
+        self.static_argnums = (static_argnums,) if isinstance(static_argnums, int) else tuple(static_argnums)
+        self.donate_argnums = (donate_argnums,) if isinstance(donate_argnums, int) else tuple(donate_argnums)
+        if capture is None:
+            capture = os.environ.get("LJS_JIT_GRAPH", "0") == "1"
+        self.capture = capture
+        self.warmup_calls = warmup_calls
+        self._calls: Dict[Any, int] = {}
+        self._graphs: Dict[Any, _Captured] = {}
+        self.__wrapped__ = fun
+
+    # ------------------------------------------------------------------ helpers
+    def _split(self, args):
+        dyn, static = [], []
+        for i, a in enumerate(args):
+            (static if i in self.static_argnums else dyn).append((i, a))
+        return dyn, static
+
+    def _signature(self, dyn, static):
+        leaves, td = T.tree_flatten([a for _, a in dyn], is_leaf=_leaf_is_array)
+        sig = []
+        for l in leaves:
+            if isinstance(l, ShardedArray):
+                sig.append(("A", l.shape, l.dtype, l.tile))
+            else:
+                sig.append(("O", type(l).__name__, repr(l) if not _is_arraylike(l) else getattr(l, "shape", None)))
+        skey = []
+        for i, a in static:
+            try:
+                hash(a)
+                skey.append((i, a))
+            except TypeError:
+                skey.append((i, id(a)))
+        return (td, tuple(sig), tuple(skey))
+
+    def _run(self, args, kwargs):
+        dyn, static = self._split(args)
+        dyn_vals = [a for _, a in dyn]
+        if self.in_shardings is not None:
+            ins = self.in_shardings
+            if not isinstance(ins, (tuple, list)) or len(dyn_vals) == 1 and not isinstance(ins, tuple):
+                ins = (ins,) if len(dyn_vals) == 1 else ins
+            dyn_vals = list(_apply_shardings(tuple(dyn_vals), tuple(ins)))
+        full = list(args)
+        for (i, _), v in zip(dyn, dyn_vals):
+            full[i] = v
+        donated = set()
+        for i in self.donate_argnums:
+            for l in T.tree_leaves(full[i], is_leaf=_leaf_is_array):
+                if isinstance(l, ShardedArray):
+                    donated.update(id(t) for t in l.local.values())
+        with _state.donating(donated):
+            out = self.fun(*full, **kwargs)
+        if self.out_shardings is not None:
+            out = _apply_shardings(out, self.out_shardings)
+        return out, full
+
+    # ------------------------------------------------------------------ call
+    def __call__(self, *args, **kwargs):
+        if not self.capture or kwargs or not torch.cuda.is_available():
+            return self._run(args, kwargs)[0]
+        dyn, static = self._split(args)
+        sig = self._signature(dyn, static)
+        cap = self._graphs.get(sig)
+        if cap is not None:
+            return self._replay(cap, args)
+        n = self._calls.get(sig, 0)
+        self._calls[sig] = n + 1
+        if n < self.warmup_calls:
+            return self._run(args, kwargs)[0]
+        return self._capture(sig, args)
+
+    def _capture(self, sig, args):
+        # static input buffers: private copies of this call's inputs
+        dyn, static = self._split(args)
+        full = list(args)
+        in_leaves = []
+        for i, a in dyn:
+            def cp(x):
+                if isinstance(x, ShardedArray):
+                    y = ShardedArray(x.shape, x.dtype, x.sharding, {d: t.detach().clone() for d, t in x.local.items()})
+                    in_leaves.append(y)
+                    return y
+                return x
+            full[i] = T.tree_map(cp, a, is_leaf=_leaf_is_array)
+        torch.cuda.synchronize()
+        # warm the caching allocator on a side stream as torch requires
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out, _ = self._run(tuple(full), {})
+        cap = _Captured(g, in_leaves, out)
+        self._graphs[sig] = cap
+        return self._replay(cap, args)
+
+    def _replay(self, cap: _Captured, args):
+        dyn, _ = self._split(args)
+        leaves = [l for _, a in dyn for l in T.tree_leaves(a, is_leaf=_leaf_is_array) if isinstance(l, ShardedArray)]
+        for src, dst in zip(leaves, cap.in_leaves):
+            for d, t in dst.local.items():
+                s = src.local[d]
+                if s.data_ptr() != t.data_ptr():
+                    t.copy_(s)
+        cap.graph.replay()
+        return cap.out_tree
+
+    def lower(self, *args, **kwargs) -> Lowered:
+        with _plan.record_plan() as rec:
+            self._run(args, kwargs)
+        return Lowered(rec)
+
+
+def jit(fun: Optional[Callable] = None, *, in_shardings=None, out_shardings=None, static_argnums=(),
+        donate_argnums=(), capture: Optional[bool] = None, warmup_calls: int = 1):
+    if fun is None:
+        return lambda f: jit(f, in_shardings=in_shardings, out_shardings=out_shardings,
+                             static_argnums=static_argnums, donate_argnums=donate_argnums,
+                             capture=capture, warmup_calls=warmup_calls)
+    return Jitted(fun, in_shardings, out_shardings, static_argnums, donate_argnums, capture, warmup_calls)
+
+
+# ----------------------------------------------------------------------------- grad
+def _fresh_leaf(x: ShardedArray) -> ShardedArray:
+    loc = {}
+    for d, t in x.local.items():
+        if t.dtype.is_floating_point:
+            loc[d] = t.detach().requires_grad_(True)
+        else:
+            loc[d] = t
+    return ShardedArray(x.shape, x.dtype, x.sharding, loc)
+
+
+def reduce_replica_grads(pairs: List[Tuple[ShardedArray, Dict[int, torch.Tensor]]],
+                         bucket_bytes: int = 256 << 20) -> List[Dict[int, torch.Tensor]]:
+    """Sum partial per-device gradients over each tile's replica group (bucketed all-reduce).
+
+    ``pairs`` = [(param, {dev: partial grad})].  Params whose replica groups
+    coincide share flat buckets (one all-reduce per bucket).  On MI355X the
+    bucket size defaults to 256 MB: with 288 GB of HBM per GPU there is no
+    memory reason to split, and fewer, larger RCCL calls amortise latency on
+    point-to-point xGMI rings.
+    """
+    out: List[Optional[Dict[int, torch.Tensor]]] = [None] * len(pairs)
+    buckets: Dict[Tuple, List[int]] = {}
+    for i, (p, g) in enumerate(pairs):
+        ta = p.tile
+        if ta.num_replicas == 1:
+            out[i] = g
+            continue
+        groups = tuple(tuple(ta.holders(t)) for t in sorted(set(ta.coords.values())))
+        key = (groups, next(iter(g.values())).dtype if g else None)
+        buckets.setdefault(key, []).append(i)
+    for (groups, dt), idxs in buckets.items():
+        # split into size-capped buckets (in parameter order)
+        cur: List[int] = []
+        cur_bytes = 0
+        chunks: List[List[int]] = []
+        for i in idxs:
+            nb = max(t.numel() * t.element_size() for t in pairs[i][1].values()) if pairs[i][1] else 0
+            if cur and cur_bytes + nb > bucket_bytes:
+                chunks.append(cur)
+                cur, cur_bytes = [], 0
+            cur.append(i)
+            cur_bytes += nb
+        if cur:
+            chunks.append(cur)
+        for chunk in chunks:
+            devs = list(pairs[chunk[0]][1].keys())
+            flat = {d: torch.cat([pairs[i][1][d].reshape(-1) for i in chunk]) for d in devs}
+            red = C.all_reduce(flat, groups, note="grad.replica_sum")
+            for d in devs:
+                off = 0
+                for i in chunk:
+                    t = pairs[i][1][d]
+                    n = t.numel()
+                    if out[i] is None:
+                        out[i] = {}
+                    out[i][d] = red[d][off:off + n].view(t.shape)
+                    off += n
+    return out  # type: ignore
+
+
+def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
+    multi = isinstance(argnums, (tuple, list))
+    argnums_t = tuple(argnums) if multi else (argnums,)
+
+    def vg(*args, **kwargs):
+        args = list(args)
+        diff_leaves: List[List[ShardedArray]] = []
+        for a in argnums_t:
+            new = T.tree_map(lambda x: _fresh_leaf(x) if isinstance(x, ShardedArray) else x, args[a],
+                             is_leaf=_leaf_is_array)
+            args[a] = new
+            diff_leaves.append([l for l in T.tree_leaves(new, is_leaf=_leaf_is_array) if isinstance(l, ShardedArray)])
+        with torch.enable_grad():
+            res = fun(*args, **kwargs)
+        out, aux = (res if has_aux else (res, None))
+        if not isinstance(out, ShardedArray) or out.size != 1:
+            raise TypeError("grad requires a scalar-output function")
+        ta = out.tile
+        n_holders = ta.num_devices
+        outs, seeds = [], []
+        for d, t in out.local.items():
+            if t.requires_grad:
+                outs.append(t)
+                seeds.append(torch.full_like(t, 1.0 / n_holders))
+        grads_per_arg = []
+        all_leaves = [l for ls in diff_leaves for l in ls]
+        inputs = [t for l in all_leaves for t in l.local.values() if t.requires_grad]
+        if outs and inputs:
+            gs = torch.autograd.grad(outs, inputs, seeds, allow_unused=True)
+        else:
+            gs = [None] * len(inputs)
+        gmap = {id(t): g for t, g in zip(inputs, gs)}
+        pairs = []
+        for l in all_leaves:
+            loc = {}
+            for d, t in l.local.items():
+                g = gmap.get(id(t))
+                loc[d] = torch.zeros_like(t) if g is None else g
+            pairs.append((l, loc))
+        reduced = reduce_replica_grads(pairs)
+        gi = 0
+        for a, ls in zip(argnums_t, diff_leaves):
+            it = iter(range(gi, gi + len(ls)))
+            gi += len(ls)
+
+            def mk(x):
+                if isinstance(x, ShardedArray):
+                    i = next(it)
+                    p = all_leaves[i]
+                    return ShardedArray(p.shape, p.dtype, p.sharding,
+                                        {d: t.detach() for d, t in reduced[i].items()})
+                return x
+            grads_per_arg.append(T.tree_map(mk, args[a], is_leaf=_leaf_is_array))
+        g = tuple(grads_per_arg) if multi else grads_per_arg[0]
+        val = ShardedArray(out.shape, out.dtype, out.sharding, {d: t.detach() for d, t in out.local.items()})
+        if has_aux:
+            return (val, aux), g
+        return val, g
+
+    return vg
+
+
+def grad(fun: Callable, argnums=0, has_aux: bool = False):
+    vg = value_and_grad(fun, argnums, has_aux)
+
+    def g_clean(*args, **kwargs):
+        if has_aux:
+            (val, aux), grads = vg(*args, **kwargs)
+            return grads, aux
+        return vg(*args, **kwargs)[1]
+
+    return g_clean
+
+
+# ----------------------------------------------------------------------------- eval_shape
+def _to_abstract(x):
+    if isinstance(x, ShardedArray):
+        loc = {d: torch.empty(t.shape, dtype=t.dtype, device="meta") for d, t in x.local.items()}
+        return ShardedArray(x.shape, x.dtype, x.sharding, loc)
+    if isinstance(x, ShapeDtypeStruct):
+        from ..runtime.devices import devices
+        sh = x.sharding or SingleDeviceSharding(devices()[0])
+        ta = sh.tile_assignment(len(x.shape))
+        loc = {d: torch.empty(ta.shard_shape(x.shape), dtype=x.dtype, device="meta") for d in ta.device_ids
+               if _addressable(d)}
+        return ShardedArray(x.shape, x.dtype, sh, loc)
+    return x
+
+
+def _addressable(d):
+    from ..runtime.devices import get_device, process_index
+    return get_device(d).process_index == process_index()
+
+
+def eval_shape(fun: Callable, *args, **kwargs):
+    a2 = T.tree_map(_to_abstract, list(args), is_leaf=lambda x: isinstance(x, (ShardedArray, ShapeDtypeStruct)))
+    with _state.abstract(), torch.no_grad():
+        out = fun(*a2, **kwargs)
+    return T.tree_map(lambda x: ShapeDtypeStruct(x.shape, x.dtype) if isinstance(x, ShardedArray) else x, out,
+                      is_leaf=_leaf_is_array)
