@@ -327,7 +327,8 @@ def device_put(x, device=None, *, may_alias=None, donate=None):
             return _tree.tree_map(lambda a, s: device_put(a, s), x, device)
         return _tree.tree_map(lambda a: device_put(a, device), x)
     if device is None:
-        sharding = SingleDeviceSharding(_all_devices()[0])
+        from .sharding.shardings import default_sharding
+        sharding = default_sharding()
     elif isinstance(device, Device):
         sharding = SingleDeviceSharding(device)
     elif isinstance(device, Sharding):

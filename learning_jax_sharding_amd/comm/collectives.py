@@ -127,6 +127,8 @@ class _CollectiveFn(torch.autograd.Function):
                 g = torch.zeros(shape, dtype=dt, device=dev)
             gd[d] = g.contiguous()
         tspec = _transpose(ctx.spec, ctx.in_meta)
+        kind = "collective_permute" if tspec.kind == "exchange" else tspec.kind
+        _plan.record(kind, groups=tspec.groups, note="backward", bytes_in=_per_device_bytes(gd))
         out = _run(tspec, gd)
         return (None, None, None) + tuple(out.get(d) for d in ctx.in_devs)
 

@@ -1,0 +1,3 @@
+"""Model families: the case5/case6 attention blocks and an attention+FF transformer layer."""
+from .attention import MultiHeadAttention, attention_block_flops  # noqa: F401
+from .transformer import TransformerLayer, transformer_layer_flops  # noqa: F401

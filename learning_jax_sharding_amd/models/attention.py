@@ -1,0 +1,126 @@
+"""The case6 multi-head self-attention block (the north-star workload).
+
+Same parameters, logical axes and sharding constraints as
+``FlaxAttention`` in ``case6_attention.py:42-143``:
+
+* ``to_q``/``to_k``/``to_v``: Dense(inner_dim, no bias), kernel axes ``('embed','heads')``
+  (``case6_attention.py:56-82``);
+* ``to_out_0``: Dense(query_dim, bias), kernel axes ``('heads','embed')``
+  (``case6_attention.py:83-90``);
+* constraints ``('batch','embed',None)`` on q/k/v (``:105-107``), the head split
+  (``:109-116``), ``('batch','kv','heads')`` after merging heads (``:137``) and
+  ``('batch','embed')`` on the output (``:141``).
+
+MI355X design: the three projections run as ONE batched MFMA GEMM over the
+concatenated kernels (``fused_qkv``), and QKᵀ → scale → softmax → P·V is one
+flash-style HIP kernel (``impl="fused"``).  ``impl="einsum"`` runs the
+reference's literal einsum/softmax formulation (used by the parity tests).
+"""
+from __future__ import annotations
+
+from typing import Any, Optional
+
+import torch
+
+from .. import dtypes as _dt
+from ..array import ShardedArray
+from ..nn import initializers as init
+from ..nn.layers import Dense, Dropout
+from ..nn.module import Module
+from ..nn.partitioning import with_logical_constraint, with_logical_partitioning
+from ..ops import core
+
+__all__ = ["MultiHeadAttention", "attention_block_flops"]
+
+
+class MultiHeadAttention(Module):
+    query_dim: int
+    heads: int = 8
+    dim_head: int = 64
+    dropout: float = 0.0
+    dtype: Any = torch.bfloat16
+    impl: str = "fused"            # "fused" (HIP flash attention) | "einsum" (reference formulation)
+    fused_qkv: bool = True
+    kernel_axes_in: tuple = ("embed", "heads")
+    kernel_axes_out: tuple = ("heads", "embed")
+    verbose: bool = False
+
+    def setup(self):
+        inner_dim = self.dim_head * self.heads
+        self.scale = self.dim_head ** -0.5
+        qkv_init = with_logical_partitioning(init.lecun_normal(), self.kernel_axes_in)
+        self.query = Dense(inner_dim, kernel_init=qkv_init, use_bias=False, dtype=self.dtype, name="to_q")
+        self.key = Dense(inner_dim, kernel_init=qkv_init, use_bias=False, dtype=self.dtype, name="to_k")
+        self.value = Dense(inner_dim, kernel_init=qkv_init, use_bias=False, dtype=self.dtype, name="to_v")
+        self.proj_attn = Dense(self.query_dim,
+                               kernel_init=with_logical_partitioning(init.lecun_normal(), self.kernel_axes_out),
+                               dtype=self.dtype, name="to_out_0")
+        self.dropout_layer = Dropout(rate=self.dropout)
+
+    def _log(self, *a):
+        if self.verbose:
+            print(*a)
+
+    def __call__(self, hidden_states: ShardedArray, context: Optional[ShardedArray] = None,
+                 deterministic: bool = True) -> ShardedArray:
+        self_attn = context is None
+        context = hidden_states if context is None else context
+        self._log("context.shape: ", context.shape)
+        dt = _dt.canonicalize(self.dtype)
+        if self.fused_qkv and self_attn:
+            m = hidden_states.shape[-1]
+            wq = self.query.kernel_param(m)
+            wk = self.key.kernel_param(m)
+            wv = self.value.kernel_param(m)
+            query_proj, key_proj, value_proj = core.dense(hidden_states, [wq, wk, wv], None, compute_dtype=dt)
+        else:
+            query_proj = self.query(hidden_states)
+            key_proj = self.key(context)
+            value_proj = self.value(context)
+        self._log("query_proj.shape: ", query_proj.shape)
+
+        # (batch, seq, heads*head_dim); the head split is metadata-only because heads is replicated
+        query_proj = with_logical_constraint(query_proj, ("batch", "embed", None))
+        key_proj = with_logical_constraint(key_proj, ("batch", "embed", None))
+        value_proj = with_logical_constraint(value_proj, ("batch", "embed", None))
+
+        b = hidden_states.shape[0]
+        q = core.reshape(query_proj, (b, -1, self.heads, self.dim_head))
+        k = core.reshape(key_proj, (b, -1, self.heads, self.dim_head))
+        v = core.reshape(value_proj, (b, -1, self.heads, self.dim_head))
+        q = with_logical_constraint(q, ("batch", "embed", None, None))
+        k = with_logical_constraint(k, ("batch", "embed", None, None))
+        v = with_logical_constraint(v, ("batch", "embed", None, None))
+        self._log("query_states.shape: ", q.shape)
+
+        if self.impl == "fused":
+            hidden = core.dot_product_attention(q, k, v, self.scale)
+        else:
+            qf = core.convert(q, torch.float32)
+            kf = core.convert(k, torch.float32)
+            scores = core.einsum("b t n h, b f n h -> b n f t", kf, qf)
+            scores = core.binary("mul", scores, self.scale)
+            probs = core.softmax(scores, axis=-1)
+            probs = core.convert(probs, dt)
+            hidden = core.einsum("b n f t, b t n h -> b f n h", probs, v)
+        hidden = core.reshape(hidden, (b, -1, self.heads * self.dim_head))
+        hidden = with_logical_constraint(hidden, ("batch", "kv", "heads"))
+        hidden = self.proj_attn(hidden)
+        hidden = with_logical_constraint(hidden, ("batch", "embed"))
+        return self.dropout_layer(hidden, deterministic=deterministic)
+
+
+def attention_block_flops(batch: int, seq: int, dim: int, heads: int, dim_head: int, train: bool) -> float:
+    """Matmul FLOPs of the case6 block: fwd 6.442 GFLOP at B=8,S=256,M=640; train 15.30."""
+    t = batch * seq
+    inner = heads * dim_head
+    qkv = 3 * 2 * t * dim * inner
+    qk = 2 * batch * heads * seq * seq * dim_head
+    pv = qk
+    out = 2 * t * inner * dim
+    fwd = qkv + qk + pv + out
+    if not train:
+        return float(fwd)
+    # backward: dWo + dh (2 out-proj GEMMs), attention bwd (dV, dP, dQ, dK = 4 seq^2 GEMMs), dWqkv (no dx)
+    bwd = 2 * out + 4 * qk + qkv
+    return float(fwd + bwd)

@@ -1,0 +1,155 @@
+"""Layers: Dense, Dropout, FeedForward, activations.
+
+``Dense`` follows flax semantics (``case6_attention.py:61-90``): kernel
+``(in, out)`` in ``param_dtype`` (f32), inputs/kernel/bias promoted to
+``dtype`` (bf16) for the matmul, bias default on.  The matmul is the fused
+MFMA GEMM with a bias epilogue (:func:`..ops.core.dense`).
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Optional, Sequence, Tuple
+
+import torch
+
+from .. import dtypes as _dt
+from ..array import ShardedArray
+from ..ops import core
+from . import initializers as init
+from .module import Module, compact
+from .partitioning import with_logical_constraint, with_logical_partitioning
+
+__all__ = ["Dense", "DenseGeneral", "Dropout", "FeedForward", "relu", "gelu", "softmax", "Embed", "LayerNorm"]
+
+
+def relu(x):
+    return core.unary("relu", x)
+
+
+def gelu(x):
+    return core.binary("mul", x, core.unary("sigmoid", core.binary("mul", x, 1.702)))
+
+
+def softmax(x, axis: int = -1):
+    return core.softmax(x, axis)
+
+
+class Dense(Module):
+    features: int
+    use_bias: bool = True
+    dtype: Any = None
+    param_dtype: Any = torch.float32
+    precision: Any = None
+    kernel_init: Callable = init.lecun_normal()
+    bias_init: Callable = init.zeros
+
+    def kernel_param(self, in_features: int) -> ShardedArray:
+        return self.param("kernel", self.kernel_init, (in_features, self.features),
+                          _dt.canonicalize(self.param_dtype))
+
+    def bias_param(self) -> Optional[ShardedArray]:
+        if not self.use_bias:
+            return None
+        return self.param("bias", self.bias_init, (self.features,), _dt.canonicalize(self.param_dtype))
+
+    def __call__(self, inputs: ShardedArray) -> ShardedArray:
+        kernel = self.kernel_param(inputs.shape[-1])
+        bias = self.bias_param()
+        dtype = _dt.canonicalize(self.dtype) or _dt.result_type(inputs.dtype, kernel.dtype)
+        return core.dense(inputs, [kernel], bias, compute_dtype=dtype)[0]
+
+
+DenseGeneral = Dense
+
+
+class Dropout(Module):
+    """``nn.Dropout`` (``case6_attention.py:91,143``): identity when deterministic or rate 0."""
+
+    rate: float = 0.0
+    deterministic: Optional[bool] = None
+
+    def __call__(self, x: ShardedArray, deterministic: Optional[bool] = None, rng=None) -> ShardedArray:
+        det = self.deterministic if deterministic is None else deterministic
+        if det or self.rate == 0.0:
+            return x
+        from .. import random as _random
+        k = rng if rng is not None else self.make_rng("dropout")
+        keep = 1.0 - self.rate
+        u = _random.uniform(k, x.shape, torch.float32, sharding=x.sharding)
+        scaled = core.binary("div", x, keep)
+        return core.where(_lt(u, keep), scaled, 0.0)
+
+
+def _lt(u: ShardedArray, v: float) -> ShardedArray:
+    return ShardedArray(u.shape, torch.bool, u.sharding, {d: t < v for d, t in u.local.items()})
+
+
+class FeedForward(Module):
+    """``y = relu(x Win) Wout`` - the FF layer of the reference's comments (``case6_attention.py:36-40``).
+
+    Logical axes ``Win: ('embed','hidden')``, ``Wout: ('hidden','embed')`` so the
+    declared rule ``('hidden','model')`` (``case6_attention.py:186``) shards the
+    hidden dim Megatron-style.  ``fp8=True`` runs both GEMMs on the CDNA4 fp8
+    (e4m3) MFMA path with per-tensor scaling.
+    """
+
+    hidden_dim: int
+    dtype: Any = torch.bfloat16
+    fp8: bool = False
+
+    @compact
+    def __call__(self, x: ShardedArray) -> ShardedArray:
+        d = x.shape[-1]
+        w_in = self.param("w_in", with_logical_partitioning(init.lecun_normal(), ("embed", "hidden")),
+                          (d, self.hidden_dim), torch.float32)
+        w_out = self.param("w_out", with_logical_partitioning(init.lecun_normal(), ("hidden", "embed")),
+                           (self.hidden_dim, d), torch.float32)
+        dt = _dt.canonicalize(self.dtype)
+        if self.fp8:
+            from ..ops.fp8 import fp8_dense
+            h = fp8_dense(x, w_in, relu=True, out_dtype=dt)
+            h = with_logical_constraint(h, ("batch", "length", "hidden"))
+            return fp8_dense(h, w_out, relu=False, out_dtype=dt)
+        h = core.dense(x, [w_in], None, compute_dtype=dt, relu=True)[0]
+        h = with_logical_constraint(h, ("batch", "length", "hidden"))
+        return core.dense(h, [w_out], None, compute_dtype=dt)[0]
+
+
+class Embed(Module):
+    num_embeddings: int
+    features: int
+    param_dtype: Any = torch.float32
+
+    def __call__(self, ids: ShardedArray) -> ShardedArray:
+        table = self.param("embedding", init.normal(1.0), (self.num_embeddings, self.features),
+                           _dt.canonicalize(self.param_dtype))
+        # rows gathered locally: the table is replicated onto the ids' devices first
+        from ..sharding.tile import TileAssignment
+        from ..spmd.reshard import reshard_tile
+        tab = reshard_tile(table, TileAssignment.replicated(ids.tile.device_ids, 2))
+        loc = {d: tab.local[d][ids.local[d].long()] for d in ids.local}
+        tile = ids.tile.insert_dims(list(range(ids.ndim)), ids.ndim + 1)
+        from ..sharding.shardings import sharding_from_tile
+        return ShardedArray(tuple(ids.shape) + (self.features,), table.dtype,
+                            sharding_from_tile(tile, like=[ids.sharding]), loc)
+
+
+class LayerNorm(Module):
+    epsilon: float = 1e-6
+    dtype: Any = None
+    use_bias: bool = True
+    use_scale: bool = True
+
+    def __call__(self, x: ShardedArray) -> ShardedArray:
+        d = x.shape[-1]
+        scale = self.param("scale", init.ones, (d,), torch.float32) if self.use_scale else None
+        bias = self.param("bias", init.zeros, (d,), torch.float32) if self.use_bias else None
+        xf = core.convert(x, torch.float32)
+        mean = core.reduce_mean(xf, -1, keepdims=True)
+        xc = core.binary("sub", xf, mean)
+        var = core.reduce_mean(core.binary("mul", xc, xc), -1, keepdims=True)
+        y = core.binary("mul", xc, core.unary("rsqrt", core.binary("add", var, self.epsilon)))
+        if scale is not None:
+            y = core.binary("mul", y, scale)
+        if bias is not None:
+            y = core.binary("add", y, bias)
+        return core.convert(y, _dt.canonicalize(self.dtype) or x.dtype)

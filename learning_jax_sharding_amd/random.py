@@ -146,7 +146,8 @@ def _generate(k: Key, shape, dtype, sharding: Optional[Sharding], dist: str, lo=
     shape = tuple(int(s) for s in shape)
     dtype = _dt.canonicalize(dtype) if dtype is not None else torch.float32
     if sharding is None:
-        sharding = SingleDeviceSharding(_devices()[0])
+        from .sharding.shardings import default_sharding
+        sharding = default_sharding()
     ta = sharding.tile_assignment(len(shape))
     ta.check_shape(shape)
     pi = process_index()

@@ -6,6 +6,8 @@ from .shardings import (  # noqa: F401
     P,
     PartitionSpec,
     PositionalSharding,
+    ReplicatedSharding,
+    default_sharding,
     Sharding,
     SingleDeviceSharding,
     sharding_from_tile,

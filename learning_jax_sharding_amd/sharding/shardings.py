@@ -37,6 +37,8 @@ class PartitionSpec(tuple):
     Shorter than the array rank means trailing dims are replicated.
     """
 
+    __pytree_leaf__ = True  # a spec is a leaf of sharding trees, not a container
+
     def __new__(cls, *parts):
         norm = []
         for p in parts:
@@ -308,6 +310,43 @@ class SingleDeviceSharding(Sharding):
 
     def __hash__(self):
         return hash(("single", self.device.id))
+
+
+class ReplicatedSharding(Sharding):
+    """Every device holds the whole array (rank independent)."""
+
+    def __init__(self, devices: Sequence[Device]):
+        self._devices = tuple(devices)
+
+    def tile_assignment(self, ndim: int) -> TileAssignment:
+        return TileAssignment.replicated([d.id for d in self._devices], ndim)
+
+    @property
+    def _device_assignment(self):
+        return self._devices
+
+    def __repr__(self):
+        return f"ReplicatedSharding({[d.id for d in self._devices]})"
+
+    def __eq__(self, other):
+        return isinstance(other, ReplicatedSharding) and other._devices == self._devices
+
+    def __hash__(self):
+        return hash(("repl", tuple(d.id for d in self._devices)))
+
+
+def default_sharding() -> Sharding:
+    """Where unplaced arrays live: device 0 (JAX's default device) in one process; replicated
+    on every device when one process drives each GPU (each rank computes its own copy)."""
+    from ..runtime.devices import devices, is_distributed
+    from ..spmd.state import default_placement
+    placed = default_placement()
+    if placed is not None:
+        return placed
+    devs = devices()
+    if is_distributed():
+        return ReplicatedSharding(devs)
+    return SingleDeviceSharding(devs[0])
 
 
 def sharding_from_tile(tile: TileAssignment, like: Sequence[Sharding] = ()) -> Sharding:

@@ -138,18 +138,42 @@ class Jitted:
             for l in T.tree_leaves(full[i], is_leaf=_leaf_is_array):
                 if isinstance(l, ShardedArray):
                     donated.update(id(t) for t in l.local.values())
-        with _state.donating(donated):
+        placed = self._placement(full)
+        with _state.donating(donated), _state.placement(placed):
             out = self.fun(*full, **kwargs)
         if self.out_shardings is not None:
             out = _apply_shardings(out, self.out_shardings)
         return out, full
 
+    def _placement(self, full):
+        """The jit's device set: where arrays created inside the function are placed."""
+        from ..sharding.shardings import NamedSharding, ReplicatedSharding
+        cands = []
+        for tree in (self.in_shardings, self.out_shardings):
+            if tree is not None:
+                cands += [s for s in T.tree_leaves(tree, is_leaf=lambda x: isinstance(x, Sharding))
+                          if isinstance(s, NamedSharding)]
+        for a in full:
+            cands += [l.sharding for l in T.tree_leaves(a, is_leaf=_leaf_is_array)
+                      if isinstance(l, ShardedArray) and isinstance(l.sharding, NamedSharding)]
+        if not cands:
+            return None
+        return ReplicatedSharding(tuple(cands[0].mesh.devices.flat))
+
     # ------------------------------------------------------------------ call
     def __call__(self, *args, **kwargs):
-        if not self.capture or kwargs or not torch.cuda.is_available():
-            return self._run(args, kwargs)[0]
         dyn, static = self._split(args)
         sig = self._signature(dyn, static)
+        if not self.capture or kwargs or not torch.cuda.is_available():
+            # Python side effects (print) run once per signature, as at JAX trace time
+            n = self._calls.get(sig, 0)
+            self._calls[sig] = n + 1
+            if n == 0 or os.environ.get("LJS_TRACE_PRINTS") == "always":
+                return self._run(args, kwargs)[0]
+            import contextlib
+            import io
+            with contextlib.redirect_stdout(io.StringIO()):
+                return self._run(args, kwargs)[0]
         cap = self._graphs.get(sig)
         if cap is not None:
             return self._replay(cap, args)

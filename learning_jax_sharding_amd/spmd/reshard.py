@@ -202,11 +202,12 @@ def reshard_tile(x: ShardedArray, dst: TileAssignment, sharding: Optional[Shardi
     out_meta = {}
     ss = dst.shard_shape(shape)
     any_local = next(iter(x.local.values())) if x.local else None
+    meta = any(t.is_meta for t in x.local.values())
     for d in dst.device_ids:
         dev = get_device(d)
         if dev.process_index != pi:
             continue
-        out_meta[d] = (ss, x.dtype, dev.torch_device)
+        out_meta[d] = (ss, x.dtype, torch.device("meta") if meta else dev.torch_device)
     loc = C.exchange(x.local, p.info["transfers"], out_meta, kind=k, note=note)
     return ShardedArray(shape, x.dtype, sharding, loc)
 

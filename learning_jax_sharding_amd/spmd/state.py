@@ -20,6 +20,24 @@ def abstract():
         _TLS.abstract -= 1
 
 
+def default_placement():
+    s = getattr(_TLS, "placement", None)
+    return s[-1] if s else None
+
+
+@contextmanager
+def placement(sharding):
+    """Inside ``jit``: unplaced arrays are created replicated on the jit's devices, not device 0."""
+    s = getattr(_TLS, "placement", None)
+    if s is None:
+        s = _TLS.placement = []
+    s.append(sharding)
+    try:
+        yield
+    finally:
+        s.pop()
+
+
 def donated_ids() -> set:
     s = getattr(_TLS, "donated", None)
     if s is None:

@@ -32,6 +32,8 @@ def _is_namedtuple(x) -> bool:
 
 
 def is_container(x) -> bool:
+    if getattr(type(x), "__pytree_leaf__", False):
+        return False
     return (x is None or isinstance(x, (dict, list, tuple)) or type(x) in _REGISTRY)
 
 
@@ -73,6 +75,9 @@ def _flatten(x, leaves: List[Any], is_leaf) -> TreeDef:
     if x is None:
         return TreeDef("none", None, [])
     t = type(x)
+    if getattr(t, "__pytree_leaf__", False):
+        leaves.append(x)
+        return TreeDef("leaf", None, [])
     if t in _REGISTRY:
         children, aux = _REGISTRY[t][0](x)
         return TreeDef(t, aux, [_flatten(c, leaves, is_leaf) for c in children])

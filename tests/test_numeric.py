@@ -1,0 +1,182 @@
+"""Sharded == unsharded numerics (SURVEY §4 'numeric' tier), on host devices."""
+import itertools
+import random as pyrandom
+
+import numpy as np
+import pytest
+import torch
+
+import learning_jax_sharding_amd as ljs
+from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
+from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
+from learning_jax_sharding_amd.spmd.plan import record_plan
+
+AXES = [None, "x", "y", ("x", "y"), ("y", "x")]
+
+
+def _valid(spec):
+    used = [a for p in spec if p is not None for a in ((p,) if isinstance(p, str) else p)]
+    return len(used) == len(set(used))
+
+
+def test_dot_all_layouts(host_devices):
+    host_devices(8)
+    mesh = Mesh(create_device_mesh((2, 4)), ("x", "y"))
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((8, 16)).astype(np.float32)
+    B = rng.standard_normal((16, 8)).astype(np.float32)
+    ref = A @ B
+    combos = [c for c in itertools.product(AXES, repeat=4) if _valid(c[:2]) and _valid(c[2:])]
+    pyrandom.Random(0).shuffle(combos)
+    for a0, a1, b0, b1 in combos[:60]:
+        a = ljs.device_put(A, NamedSharding(mesh, P(a0, a1)))
+        b = ljs.device_put(B, NamedSharding(mesh, P(b0, b1)))
+        c = ljs.lax.dot(a, b)
+        np.testing.assert_allclose(np.asarray(c), ref, rtol=1e-5, atol=1e-4, err_msg=str((a0, a1, b0, b1)))
+        # every device holds exactly its tile of the result
+        for sh in c.addressable_shards:
+            np.testing.assert_allclose(np.asarray(sh.data), ref[sh.index], rtol=1e-5, atol=1e-4)
+
+
+def test_reshard_roundtrips(host_devices):
+    host_devices(8)
+    mesh = Mesh(create_device_mesh((2, 4)), ("x", "y"))
+    X = np.arange(8 * 8 * 4, dtype=np.float32).reshape(8, 8, 4)
+    specs = [P(), P("x"), P("y"), P(None, "y"), P("x", "y"), P("y", "x"), P(("x", "y")), P(None, ("x", "y")),
+             P("x", None, "y")]
+    for s1, s2 in itertools.product(specs, repeat=2):
+        try:
+            a = ljs.device_put(X, NamedSharding(mesh, s1))
+            b = ljs.device_put(a, NamedSharding(mesh, s2))
+        except ValueError:
+            continue
+        for sh in b.addressable_shards:
+            np.testing.assert_array_equal(np.asarray(sh.data), X[sh.index])
+
+
+def test_reshard_grad_transpose(host_devices):
+    """The gradient of a reshard is the transposed collective (AG<->RS, A2A<->A2A, permute)."""
+    host_devices(4)
+    mesh = Mesh(create_device_mesh((2, 2)), ("x", "y"))
+    X = np.random.default_rng(1).standard_normal((4, 8)).astype(np.float32)
+    W = np.random.default_rng(2).standard_normal((4, 8)).astype(np.float32)
+    for s1, s2 in [(P("x", "y"), P("x")), (P("x"), P(None, "x")), (P(None, "y"), P("y")), (P("y"), P("x"))]:
+        a = ljs.device_put(X, NamedSharding(mesh, s1))
+        w = ljs.device_put(W, NamedSharding(mesh, s2))
+
+        def f(a):
+            b = ljs.with_sharding_constraint(a, NamedSharding(mesh, s2))
+            return (b * w).sum()
+
+        g = ljs.grad(f)(a)
+        np.testing.assert_allclose(np.asarray(g), W, rtol=1e-6, atol=1e-6, err_msg=str((s1, s2)))
+
+
+def test_einsum_batched(host_devices):
+    host_devices(8)
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((8, 4, 16)).astype(np.float32)
+    B = rng.standard_normal((8, 16, 4)).astype(np.float32)
+    mesh = Mesh(create_device_mesh((2, 4)), ("x", "y"))
+    a = ljs.device_put(A, NamedSharding(mesh, P("x", None, "y")))
+    b = ljs.device_put(B, NamedSharding(mesh, P("x", "y")))
+    c = ljs.numpy.einsum("ABC,ACD->ABD", a, b)
+    np.testing.assert_allclose(np.asarray(c), np.einsum("abc,acd->abd", A, B), rtol=1e-5, atol=1e-4)
+
+
+def _block_loss_and_grads(mesh_shape, impl="fused", fused_qkv=True, B=4, S=32, M=64, heads=4, dh=16):
+    from learning_jax_sharding_amd import nn
+    from learning_jax_sharding_amd.models import MultiHeadAttention
+    n = int(np.prod(mesh_shape))
+    mesh = Mesh(create_device_mesh(mesh_shape), ("data", "model"))
+    rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
+    model = MultiHeadAttention(M, heads=heads, dim_head=dh, impl=impl, fused_qkv=fused_qkv)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (B, S, M))
+    params = model.init(ljs.random.PRNGKey(1), x)["params"]
+    specs = nn.get_partition_spec(params)
+    shard = nn.logical_to_mesh_sharding(specs, mesh, rules)
+    params = ljs.device_put(params, shard)
+    x = ljs.device_put(x, NamedSharding(mesh, P("data", "model")))
+
+    def loss(p):
+        return model.apply({"params": p}, x).sum()
+
+    with mesh, nn.axis_rules(rules):
+        val, g = ljs.value_and_grad(loss)(params)
+    g = nn.unbox(g)
+    return float(np.asarray(val)), ljs.tree_map(lambda a: np.asarray(a), g)
+
+
+@pytest.mark.parametrize("mesh_shape", [(1, 2), (2, 1), (2, 2), (2, 4), (4, 2)])
+def test_attention_block_sharded_matches_unsharded(host_devices, mesh_shape):
+    host_devices(8)
+    v1, g1 = _block_loss_and_grads((1, 1))
+    vn, gn = _block_loss_and_grads(mesh_shape)
+    assert abs(v1 - vn) <= 2e-2 * max(1.0, abs(v1))
+    for k in g1:
+        for name in g1[k]:
+            a, b = g1[k][name], gn[k][name]
+            np.testing.assert_allclose(b, a, rtol=3e-2, atol=3e-2 * np.abs(a).max(), err_msg=f"{k}/{name}")
+
+
+def test_attention_fused_matches_einsum(host_devices):
+    host_devices(4)
+    v1, g1 = _block_loss_and_grads((2, 2), impl="einsum", fused_qkv=False)
+    v2, g2 = _block_loss_and_grads((2, 2), impl="fused", fused_qkv=True)
+    assert abs(v1 - v2) <= 2e-2 * max(1.0, abs(v1))
+    for k in g1:
+        for name in g1[k]:
+            np.testing.assert_allclose(g2[k][name], g1[k][name], rtol=3e-2, atol=3e-2 * np.abs(g1[k][name]).max())
+
+
+def test_attention_reference_oracle(host_devices):
+    """Our fused attention op == a plain torch f32 transcription of case6_attention.py:120-133."""
+    host_devices(1)
+    from learning_jax_sharding_amd.ops import kernels as K
+    g = torch.Generator().manual_seed(0)
+    q = torch.randn(2, 16, 4, 8, generator=g).bfloat16()
+    k = torch.randn(2, 16, 4, 8, generator=g).bfloat16()
+    v = torch.randn(2, 16, 4, 8, generator=g).bfloat16()
+    s = torch.einsum("btnh,bfnh->bnft", k.float(), q.float()) * 8 ** -0.5
+    p = torch.softmax(s, -1).bfloat16().float()
+    ref = torch.einsum("bnft,btnh->bfnh", p, v.float())
+    out = K.attention(q, k, v, 8 ** -0.5)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_adam_matches_torch(host_devices):
+    host_devices(2)
+    from learning_jax_sharding_amd import optim
+    from learning_jax_sharding_amd.training import TrainState
+    mesh = Mesh(create_device_mesh((2,)), ("data",))
+    rng = np.random.default_rng(0)
+    P0 = rng.standard_normal((6, 4)).astype(np.float32)
+    G = [rng.standard_normal((6, 4)).astype(np.float32) for _ in range(3)]
+    p = {"w": ljs.device_put(P0, NamedSharding(mesh, P("data")))}
+    st = TrainState.create(apply_fn=None, params=p, tx=optim.adam(1e-2))
+    tp = torch.tensor(P0, requires_grad=True)
+    topt = torch.optim.Adam([tp], lr=1e-2, betas=(0.9, 0.999), eps=1e-8)
+    for g in G:
+        st = st.apply_gradients(grads={"w": ljs.device_put(g, NamedSharding(mesh, P("data")))})
+        tp.grad = torch.tensor(g)
+        topt.step()
+    np.testing.assert_allclose(np.asarray(st.params["w"]), tp.detach().numpy(), rtol=1e-5, atol=1e-6)
+    assert int(np.asarray(st.step)) == 3
+
+
+def test_plan_case6_forward(host_devices):
+    """case6 forward lowers to the SURVEY §2.7 plan: AG W, AG K, AG V, AG heads, A2A."""
+    host_devices(4)
+    from learning_jax_sharding_amd import nn
+    from learning_jax_sharding_amd.models import MultiHeadAttention
+    mesh = Mesh(create_device_mesh((2, 2)), ("data", "model"))
+    rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
+    model = MultiHeadAttention(64, heads=4, dim_head=16)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (4, 32, 64))
+    params = model.init(ljs.random.PRNGKey(1), x)["params"]
+    params = ljs.device_put(params, nn.logical_to_mesh_sharding(nn.get_partition_spec(params), mesh, rules))
+    x = ljs.device_put(x, NamedSharding(mesh, P("data", "model")))
+    with mesh, nn.axis_rules(rules), record_plan() as plan:
+        model.apply({"params": params}, x)
+    kinds = plan.collective_kinds()
+    assert kinds == ["all_gather"] * 6 + ["all_to_all"], kinds
