@@ -1,0 +1,172 @@
+"""Headline benchmark: case6 sharded attention block train step (fwd + bwd + Adam).
+
+Metric (BASELINE.json): "step-time ms + TFLOPS/GPU, case6 sharded attention block at 1/2/4/8
+MI355X".  The model is the reference's FlaxAttention (``case6_attention.py:42-143``:
+M=640, 8 heads x 64, bf16 compute, f32 params, Adam lr 1e-3) with the reference's
+logical-axis rules; S=256 as in the reference.  Data is synthetic (random normal inputs,
+random-init weights).  Work per GPU is fixed as N grows (weak scaling): the global batch is
+``--batch-per-gpu x N`` sequences.
+
+Single GPU: ``python bench.py``.  N GPUs: ``torchrun --nproc-per-node N bench.py --gpus N``
+(one process per GPU, RCCL over xGMI).  The step is a jitted, donated, HIP-graph-captured
+function; the timed region is K full steps bracketed by barrier + device synchronize, and
+the reported time is the max over ranks.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "step-time ms + TFLOPS/GPU, case6 sharded attention block at 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("LJS_BENCH_BPG", "64")))
+    p.add_argument("--seq", type=int, default=256)
+    p.add_argument("--dim", type=int, default=640)
+    p.add_argument("--heads", type=int, default=8)
+    p.add_argument("--dim-head", type=int, default=64)
+    p.add_argument("--mesh", default=os.environ.get("LJS_BENCH_MESH", "dp"),
+                   help="dp: (N,1) data x model; 2d: (N/2, 2); or explicit 'DxM'")
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--mode", default="train", choices=["train", "fwd"])
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        os.environ.setdefault("LJS_PLATFORM", "gpu")
+    else:
+        os.environ.setdefault("LJS_NUM_DEVICES", "1")
+    import torch
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd import nn, optim
+    from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
+    from learning_jax_sharding_amd.models import MultiHeadAttention, attention_block_flops
+    from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
+    from learning_jax_sharding_amd.training import TrainState
+
+    n = ljs.device_count()
+    if args.mesh == "dp":
+        mshape = (n, 1)
+    elif args.mesh == "2d":
+        mshape = (max(1, n // 2), 2 if n >= 2 else 1)
+    else:
+        mshape = tuple(int(v) for v in args.mesh.split("x"))
+    assert mshape[0] * mshape[1] == n, (mshape, n)
+    mesh = Mesh(create_device_mesh(mshape), ("data", "model"))
+    rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
+    B = args.batch_per_gpu * n
+    S, M = args.seq, args.dim
+    model = MultiHeadAttention(M, heads=args.heads, dim_head=args.dim_head)
+    x_sharding = NamedSharding(mesh, P("data", "model"))
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (B, S, M), sharding=x_sharding)
+
+    def init_fn(k, x):
+        params = model.init(k, x)["params"]
+        return TrainState.create(apply_fn=model.apply, params=params, tx=optim.adam(1e-3))
+
+    abstract = ljs.eval_shape(init_fn, ljs.random.PRNGKey(1), x)
+    state_sharding = nn.logical_to_mesh_sharding(nn.get_partition_spec(abstract), mesh, rules)
+    state = ljs.jit(init_fn, out_shardings=state_sharding)(ljs.random.PRNGKey(1), x)
+
+    def train_step(state, x):
+        def loss_fn(params):
+            return model.apply({"params": params}, x).sum()
+        grads = ljs.grad(loss_fn)(state.params)
+        return state.apply_gradients(grads=grads)
+
+    def fwd_step(state, x):
+        return model.apply({"params": state.params}, x)
+
+    capture = not args.no_graph and torch.cuda.is_available()
+    if args.mode == "train":
+        step = ljs.jit(train_step, in_shardings=(state_sharding, x_sharding), out_shardings=state_sharding,
+                       donate_argnums=0, capture=capture)
+    else:
+        step = ljs.jit(fwd_step, in_shardings=(state_sharding, x_sharding), out_shardings=x_sharding,
+                       capture=capture)
+
+    def run(k):
+        nonlocal state
+        out = None
+        for _ in range(k):
+            if args.mode == "train":
+                state = step(state, x)
+            else:
+                out = step(state, x)
+        return out
+
+    import torch.distributed as dist
+    dist_on = dist.is_available() and dist.is_initialized()
+
+    cuda = torch.cuda.is_available()
+
+    def barrier_sync():
+        if cuda:
+            torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        if cuda:
+            torch.cuda.synchronize()
+
+    with mesh, nn.axis_rules(rules):
+        run(max(1, args.warmup))
+        barrier_sync()
+        t0 = time.perf_counter()
+        run(args.steps)
+        barrier_sync()
+        t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist_on:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if cuda else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    flops = attention_block_flops(B, S, M, args.heads, args.dim_head, train=args.mode == "train")
+    tflops_total = flops / (ms * 1e-3) / 1e12
+    tokens_per_s = B * S / (ms * 1e-3)
+    rank = int(os.environ.get("RANK", "0"))
+    if rank == 0:
+        par = f"dp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
+        rec = {
+            "metric": METRIC,
+            "value": round(tflops_total, 3),
+            "unit": "TFLOPS (whole job, matmul FLOPs of fwd+bwd)",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "tflops_per_gpu": round(tflops_total / n, 3),
+            "tokens_per_s": round(tokens_per_s, 1),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random normal x, random-init weights)",
+            "config": {"model": f"case6 attention block (M={M}, heads={args.heads}x{args.dim_head}, "
+                                f"bf16 compute, f32 params, Adam)",
+                       "global_batch": B, "seq_len": S, "parallelism": par, "mode": args.mode,
+                       "hip_graph": capture},
+        }
+        print(json.dumps(rec), flush=True)
+    if dist_on:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

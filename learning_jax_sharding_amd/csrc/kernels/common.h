@@ -1,0 +1,71 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define LJS_API extern "C" __attribute__((visibility("default")))
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef unsigned short bf16_t;  // raw bf16 bits in memory
+
+#define LDS_PTR(T) __attribute__((address_space(3))) T*
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 (NaN-preserving via the hardware cvt when available)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16: per 16-lane group a 4(row) x 16(col) block of 16-bit elements is read
+// transposed; lane i of the group gets column i, rows 0..3.  Lane 4q+p supplies the address of
+// row q, columns 4p..4p+3.
+__device__ __forceinline__ s16x4 lds_read_tr16(const bf16_t* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(lds_addr));
+}
+
+__device__ __forceinline__ bf16x8 join_bf16x8(s16x4 lo, s16x4 hi) {
+  s16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// XCD-aware bijective remap of a linear block id (MI355X: 8 XCDs, blocks dealt round-robin).
+// Blocks that share an XCD get a contiguous range of tile ids, so neighbouring tiles (which
+// share operand panels) hit the same L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int nx = 8;
+  if (nwg < nx) return bid;
+  int q = nwg / nx, r = nwg % nx;
+  int xcd = bid % nx, idx = bid / nx;
+  int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + idx;
+}
+
+__device__ __forceinline__ float warp_max64(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float warp_sum64(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

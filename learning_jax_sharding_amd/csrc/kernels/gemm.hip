@@ -1,0 +1,320 @@
+// Batched bf16 GEMM on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), f32 accumulation.
+//
+//   C[b] = alpha * op(A[b]) @ op(B[b]) (+ bias) (relu)        (bf16 or f32 out, optional split-K)
+//
+// Operand layouts (template flags), covering every GEMM of the attention block's
+// forward and backward without transposing anything in memory:
+//   A_KC : A[m][k] at A + m*lda + k   (k contiguous)      | !A_KC : A[m][k] at A + k*lda + m
+//   B_KC : B[k][n] at B + n*ldb + k   (k contiguous)      | !B_KC : B[k][n] at B + k*ldb + n
+// k-contiguous operands are staged as [rows][64] LDS tiles read with ds_read_b128;
+// m/n-contiguous operands as [64][rows] tiles read with the gfx950 transposing LDS read
+// (ds_read_b64_tr_b16), so e.g. dW = X^T @ dY reads X and dY in their natural layouts.
+//
+// Structure: 256 threads = 4 waves (2x2), block tile BM x BN, BK = 64, LDS double buffer
+// with register staging (issue next tile's global loads before the MFMAs, write them to
+// the other LDS buffer after; one barrier per K-tile), XOR-swizzled LDS images so both
+// the row reads and the transposed reads are bank-conflict free, XCD-aware tile order.
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64;
+
+struct GemmArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* C;
+  const void* bias;
+  long lda, ldb, ldc;
+  long sA, sB, sC, sBias;
+  int M, N, K;
+  int batch, splitk, kt_per_split;
+  float alpha;
+  int flags;  // 1 relu, 2 bias, 4 bias f32, 8 accumulate into C (f32 out)
+};
+
+// swizzled 8-byte-chunk index for the m/n-contiguous image (rows of R bf16)
+template <int R>
+__device__ __forceinline__ int swz_mn(int krow, int c8) {
+  int f;
+  if constexpr (R == 128) f = ((krow & 3) | (((krow >> 3) & 1) << 2)) << 2;
+  else f = ((((krow >> 1) & 1)) | (((krow >> 3) & 1) << 1)) << 2;
+  return c8 ^ f;
+}
+
+// swizzled 16-byte-chunk index for the k-contiguous image (rows of 64 bf16 = 8 chunks)
+__device__ __forceinline__ int swz_k(int row, int c16) { return c16 ^ ((row >> 1) & 7); }
+
+template <int R, bool KC>
+struct Stage {
+  static constexpr int CHUNKS = R * BK * 2 / 16 / 256;  // 16-byte chunks per thread
+  u32x4 v[CHUNKS];
+
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ base, long ld, int r0, int k0, int R_lim,
+                                       int K, int tid) {
+#pragma unroll
+    for (int i = 0; i < CHUNKS; ++i) {
+      int c = tid + 256 * i;
+      if constexpr (KC) {
+        int row = c >> 3, kc = c & 7;
+        int gr = r0 + row, gk = k0 + kc * 8;
+        if (gr < R_lim && gk < K)
+          v[i] = *reinterpret_cast<const u32x4*>(base + (long)gr * ld + gk);
+        else
+          v[i] = u32x4{0, 0, 0, 0};
+      } else {
+        constexpr int CPR = R / 8;  // 16B chunks per k-row
+        int krow = c / CPR, mc = c % CPR;
+        int gk = k0 + krow, gr = r0 + mc * 8;
+        if (gk < K && gr < R_lim)
+          v[i] = *reinterpret_cast<const u32x4*>(base + (long)gk * ld + gr);
+        else
+          v[i] = u32x4{0, 0, 0, 0};
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(bf16_t* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < CHUNKS; ++i) {
+      int c = tid + 256 * i;
+      if constexpr (KC) {
+        int row = c >> 3, kc = c & 7;
+        *reinterpret_cast<u32x4*>(lds + row * BK + swz_k(row, kc) * 8) = v[i];
+      } else {
+        constexpr int CPR = R / 8;
+        int krow = c / CPR, mc = c % CPR;
+        *reinterpret_cast<u32x4*>(lds + krow * R + swz_mn<R>(krow, mc * 2) * 4) = v[i];
+      }
+    }
+  }
+};
+
+// MFMA operand fragment: 16 rows (m or n) starting at rb, k-step ks (32 deep)
+template <int R, bool KC>
+__device__ __forceinline__ bf16x8 frag(const bf16_t* lds, int rb, int ks, int lane) {
+  if constexpr (KC) {
+    int row = rb + (lane & 15);
+    int kc = ks * 4 + (lane >> 4);
+    u32x4 raw = *reinterpret_cast<const u32x4*>(lds + row * BK + swz_k(row, kc) * 8);
+    return __builtin_bit_cast(bf16x8, raw);
+  } else {
+    int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    int kr0 = ks * 32 + 8 * g + q;
+    int c8 = (rb >> 2) + p;
+    s16x4 lo = lds_read_tr16(lds + kr0 * R + swz_mn<R>(kr0, c8) * 4);
+    int kr1 = kr0 + 4;
+    s16x4 hi = lds_read_tr16(lds + kr1 * R + swz_mn<R>(kr1, c8) * 4);
+    return join_bf16x8(lo, hi);
+  }
+}
+
+template <int BM, int BN, bool A_KC, bool B_KC, bool OUT_F32>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
+  constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 MFMA tiles per wave (2x2 waves)
+  constexpr int A_TILE = BM * BK, B_TILE = BN * BK;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (A_TILE + B_TILE)];
+  // (pointer arrays into LDS would become static initializers: index arithmetically)
+#define As(i) (smem + (i) * A_TILE)
+#define Bs(i) (smem + 2 * A_TILE + (i) * B_TILE)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm_i = tile / ntn, tn_i = tile % ntn;
+  if (tm_i >= ntm) return;
+  const int bz = blockIdx.y;
+  const int b = bz / p.splitk, split = bz % p.splitk;
+  const int m0 = tm_i * BM, n0 = tn_i * BN;
+
+  const bf16_t* Ab = p.A + (long)b * p.sA;
+  const bf16_t* Bb = p.B + (long)b * p.sB;
+
+  const int nkt_total = (p.K + BK - 1) / BK;
+  const int kt_begin = split * p.kt_per_split;
+  const int kt_end = min(nkt_total, kt_begin + p.kt_per_split);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage<BM, A_KC> sa;
+  Stage<BN, B_KC> sb;
+  if (kt_begin < kt_end) {
+    sa.load(Ab, p.lda, m0, kt_begin * BK, p.M, p.K, tid);
+    sb.load(Bb, p.ldb, n0, kt_begin * BK, p.N, p.K, tid);
+    sa.store(As(0), tid);
+    sb.store(Bs(0), tid);
+  }
+  __syncthreads();
+
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int cur = (kt - kt_begin) & 1;
+    const bool more = kt + 1 < kt_end;
+    if (more) {
+      sa.load(Ab, p.lda, m0, (kt + 1) * BK, p.M, p.K, tid);
+      sb.load(Bb, p.ldb, n0, (kt + 1) * BK, p.N, p.K, tid);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag<BM, A_KC>(As(cur), wr * (BM / 2) + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, B_KC>(Bs(cur), wc * (BN / 2) + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+    }
+    if (more) {
+      sa.store(As(cur ^ 1), tid);
+      sb.store(Bs(cur ^ 1), tid);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const bool relu = p.flags & 1;
+  const bool has_bias = (p.flags & 2) && p.splitk == 1;
+  const bool bias_f32 = p.flags & 4;
+  const bool accumulate = p.flags & 8;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
+      if (col >= p.N) continue;
+      float bv = 0.f;
+      if (has_bias) {
+        const long bo = (long)b * p.sBias + col;
+        bv = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo]
+                      : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        if (row >= p.M) continue;
+        float v = acc[i][j][r] * p.alpha + bv;
+        if (relu) v = fmaxf(v, 0.f);
+        const long off = (long)b * p.sC + (long)row * p.ldc + col;
+        if constexpr (OUT_F32) {
+          float* C = reinterpret_cast<float*>(p.C);
+          if (p.splitk > 1) atomicAdd(C + off, v);
+          else if (accumulate) C[off] += v;
+          else C[off] = v;
+        } else {
+          reinterpret_cast<bf16_t*>(p.C)[off] = f2bf(v);
+        }
+      }
+    }
+  }
+}
+
+#undef As
+#undef Bs
+
+template <int BM, int BN, bool AK, bool BKc, bool OF>
+hipError_t launch_t(const GemmArgs& a, hipStream_t s) {
+  int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  dim3 grid(ntm * ntn, a.batch * a.splitk);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AK, BKc, OF>), grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int BM, int BN>
+hipError_t dispatch_layout(const GemmArgs& a, int a_kc, int b_kc, int out_f32, hipStream_t s) {
+#define LJS_CASE(AK, BK_, OF) \
+  if (a_kc == AK && b_kc == BK_ && out_f32 == OF) return launch_t<BM, BN, AK, BK_, OF>(a, s);
+  LJS_CASE(1, 1, 0) LJS_CASE(1, 1, 1) LJS_CASE(0, 0, 0) LJS_CASE(0, 0, 1)
+  LJS_CASE(1, 0, 0) LJS_CASE(1, 0, 1) LJS_CASE(0, 1, 0) LJS_CASE(0, 1, 1)
+#undef LJS_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// Returns 0 on success.  Preconditions checked here (the Python wrapper checks them too):
+// K % 8 == 0; for an m/n-contiguous operand its M (or N) % 8 == 0; 16-byte aligned bases
+// and leading dimensions that are multiples of 8 elements.
+LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
+                          long lda, long ldb, long ldc, long sA, long sB, long sC, long sBias, int batch,
+                          int a_kc, int b_kc, int out_f32, int flags, float alpha, int splitk, int tile,
+                          hipStream_t stream) {
+  if (K % 8 || (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
+  if (splitk > 1 && !out_f32) return (int)hipErrorInvalidValue;
+  GemmArgs a;
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = C;
+  a.bias = bias;
+  a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.sA = sA; a.sB = sB; a.sC = sC; a.sBias = sBias;
+  a.M = M; a.N = N; a.K = K;
+  a.batch = batch;
+  a.alpha = alpha;
+  a.flags = flags;
+  int nkt = (K + BK - 1) / BK;
+  if (splitk < 1) splitk = 1;
+  if (splitk > nkt) splitk = nkt;
+  a.kt_per_split = (nkt + splitk - 1) / splitk;
+  a.splitk = (nkt + a.kt_per_split - 1) / a.kt_per_split;
+  hipError_t e;
+  if (tile == 64)
+    e = dispatch_layout<64, 64>(a, a_kc, b_kc, out_f32, stream);
+  else
+    e = dispatch_layout<128, 128>(a, a_kc, b_kc, out_f32, stream);
+  return (int)e;
+}
+
+// ============================================================================ f32 GEMM
+// Exact-f32 GEMM on the f32-input MFMA (v_mfma_f32_16x16x4_f32: a k-ordered fmaf chain, no
+// reduced-precision path).  Arbitrary element strides, so any transpose is free; operands are
+// read straight from global (this serves the small f32 matmuls of cases 1-4 and generic
+// f32 dot_general; large GEMMs run in bf16 above).  One wave per 16x16 output tile, 2x2 waves.
+namespace {
+struct GemmF32Args {
+  const float* A; const float* B; float* C;
+  long a_rs, a_cs, b_rs, b_cs, c_rs;
+  long sA, sB, sC;
+  int M, N, K;
+};
+
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m0 = blockIdx.x * 32 + (wave >> 1) * 16, n0 = blockIdx.y * 32 + (wave & 1) * 16;
+  const int b = blockIdx.z;
+  const float* A = p.A + b * p.sA;
+  const float* B = p.B + b * p.sB;
+  const int am = m0 + (lane & 15), bn = n0 + (lane & 15), kk = lane >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < p.K; k0 += 4) {
+    const int k = k0 + kk;
+    float a = (am < p.M && k < p.K) ? A[am * p.a_rs + k * p.a_cs] : 0.f;
+    float bb = (bn < p.N && k < p.K) ? B[k * p.b_rs + bn * p.b_cs] : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc, 0, 0, 0);
+  }
+  const int col = n0 + (lane & 15);
+  if (col >= p.N) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = m0 + (lane >> 4) * 4 + r;
+    if (row < p.M) p.C[b * p.sC + row * p.c_rs + col] = acc[r];
+  }
+}
+}  // namespace
+
+LJS_API int ljs_gemm_f32(const void* A, const void* B, void* C, int M, int N, int K, long a_rs, long a_cs, long b_rs,
+                         long b_cs, long c_rs, long sA, long sB, long sC, int batch, hipStream_t stream) {
+  GemmF32Args p;
+  p.A = (const float*)A; p.B = (const float*)B; p.C = (float*)C;
+  p.a_rs = a_rs; p.a_cs = a_cs; p.b_rs = b_rs; p.b_cs = b_cs; p.c_rs = c_rs;
+  p.sA = sA; p.sB = sB; p.sC = sC;
+  p.M = M; p.N = N; p.K = K;
+  dim3 grid((M + 31) / 32, (N + 31) / 32, batch);
+  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, stream, p);
+  return (int)hipGetLastError();
+}

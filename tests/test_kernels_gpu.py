@@ -1,0 +1,214 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (run on a real MI355X: -m gpu)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def hip():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from learning_jax_sharding_amd.ops import hip as H
+    H.lib()
+    return H
+
+
+def _rand(*shape, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randn(*shape, generator=g).to(dtype).to(dev)
+
+
+def _stored(mat, kc_rowmajor: bool):
+    """Return (storage tensor, ld) for a logical [R][K] matrix in KC or MN-contiguous layout."""
+    if kc_rowmajor:
+        return mat.contiguous(), mat.shape[1]
+    return mat.t().contiguous(), mat.shape[0]
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (0, 0), (1, 0), (0, 1)])
+@pytest.mark.parametrize("out_f32", [0, 1])
+@pytest.mark.parametrize("tile", [64, 128])
+@pytest.mark.parametrize("M,N,K", [(256, 192, 320), (136, 72, 40), (512, 1536, 640)])
+def test_gemm_layouts(hip, a_kc, b_kc, out_f32, tile, M, N, K):
+    A = _rand(M, K, seed=1)
+    B = _rand(K, N, seed=2)
+    ref = A.float() @ B.float()
+    As, lda = _stored(A, a_kc)               # KC: [M][K]; MN: [K][M]
+    Bs, ldb = _stored(B.t(), b_kc)           # KC: [N][K]; MN: [K][N]
+    C = torch.full((M, N), float("nan"), dtype=torch.float32 if out_f32 else torch.bfloat16, device=dev)
+    hip.gemm(As, Bs, C, M, N, K, lda, ldb, N, bool(a_kc), bool(b_kc), tile=tile)
+    torch.cuda.synchronize()
+    tol = 2e-2 if not out_f32 else 1e-3
+    torch.testing.assert_close(C.float(), ref, rtol=tol, atol=tol * math.sqrt(K))
+
+
+def test_gemm_identity_asymmetric(hip):
+    """A = I with an asymmetric B catches a transposed C write."""
+    n = 64
+    A = torch.eye(n, dtype=torch.bfloat16, device=dev)
+    B = (torch.arange(n * n, device=dev).reshape(n, n) % 97).to(torch.bfloat16)
+    C = torch.empty((n, n), dtype=torch.float32, device=dev)
+    hip.gemm(A, B.t().contiguous(), C, n, n, n, n, n, n, True, True)
+    torch.testing.assert_close(C, B.float())
+
+
+def test_gemm_bias_relu_batched_splitk(hip):
+    M, N, K, nb = 128, 256, 512, 3
+    A = _rand(M, K, seed=3)
+    Bt = _rand(nb, N, K, seed=4)
+    bias = _rand(N, dtype=torch.float32, seed=5)
+    out = torch.empty((M, nb * N), dtype=torch.bfloat16, device=dev)
+    hip.gemm(A, Bt, out, M, N, K, K, K, nb * N, True, True, batch=nb, sA=0, sB=N * K, sC=N, bias=bias, relu=True)
+    ref = torch.relu(torch.einsum("mk,bnk->bmn", A.float(), Bt.float()) + bias)
+    for i in range(nb):
+        torch.testing.assert_close(out[:, i * N:(i + 1) * N].float(), ref[i], rtol=2e-2, atol=5e-2)
+    # split-K accumulation into f32
+    C = torch.zeros((M, N), dtype=torch.float32, device=dev)
+    hip.gemm(A, Bt[0], C, M, N, K, K, K, N, True, True, splitk=4)
+    torch.testing.assert_close(C, A.float() @ Bt[0].float().t(), rtol=1e-3, atol=1e-2)
+
+
+def test_gemm_f32_strided(hip):
+    A = torch.randn(3, 20, 36, device=dev)
+    B = torch.randn(3, 36, 12, device=dev)
+    C = torch.empty(3, 20, 12, device=dev)
+    hip._gemm_f32(A, B, C, 20, 12, 36, 36, 1, 12, 1, 12, 20 * 36, 36 * 12, 20 * 12, 3)
+    torch.testing.assert_close(C, A @ B, rtol=1e-5, atol=1e-4)
+    # transposed operand through strides
+    At = A.transpose(1, 2).contiguous()
+    hip._gemm_f32(At, B, C, 20, 12, 36, 1, 20, 12, 1, 12, 20 * 36, 36 * 12, 20 * 12, 3)
+    torch.testing.assert_close(C, A @ B, rtol=1e-5, atol=1e-4)
+
+
+def test_bmm_nt_autograd(hip):
+    for dt in (torch.float32, torch.bfloat16):
+        A = torch.randn(2, 24, 40, device=dev, dtype=dt, requires_grad=True)
+        Bt = torch.randn(2, 16, 40, device=dev, dtype=dt, requires_grad=True)
+        C = hip.bmm_nt(A, Bt, torch.float32)
+        g = torch.randn_like(C)
+        (C * g).sum().backward()
+        A2 = A.detach().float().requires_grad_()
+        B2 = Bt.detach().float().requires_grad_()
+        C2 = A2 @ B2.transpose(1, 2)
+        (C2 * g).sum().backward()
+        tol = 1e-4 if dt == torch.float32 else 3e-2
+        torch.testing.assert_close(C, C2, rtol=tol, atol=tol * 10)
+        torch.testing.assert_close(A.grad.float(), A2.grad, rtol=tol, atol=tol * 10)
+        torch.testing.assert_close(Bt.grad.float(), B2.grad, rtol=tol, atol=tol * 10)
+
+
+def _attn_ref(q, k, v, scale, causal=False, q_offset=0):
+    from learning_jax_sharding_amd.ops.kernels import attention_reference
+    return attention_reference(q, k, v, scale, causal, q_offset)
+
+
+@pytest.mark.parametrize("B,S,H", [(2, 256, 8), (1, 200, 4), (3, 64, 2)])
+@pytest.mark.parametrize("causal", [False, True])
+def test_attention_fwd_bwd(hip, B, S, H, causal):
+    D = 64
+    # q/k/v as column slices of one fused QKV buffer, exactly as the model produces them
+    qkv = _rand(B, S, 3 * H * D, seed=7).reshape(B, S, 3, H, D)
+    q, k, v = (qkv[:, :, i] for i in range(3))
+    scale = D ** -0.5
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, scale, causal).float()
+    out = hip.attention(q, k, v, scale, causal)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    # backward vs autograd of the f32 reference
+    q1, k1, v1 = (t.detach().clone().requires_grad_() for t in (q, k, v))
+    out1 = hip.attention(q1, k1, v1, scale, causal)
+    g = _rand(*out1.shape, seed=9)
+    (out1.float() * g.float()).sum().backward()
+    s = torch.einsum("btnh,bfnh->bnft", kr, qr) * scale
+    if causal:
+        s = s.masked_fill(torch.arange(S, device=dev)[None, :] > torch.arange(S, device=dev)[:, None], -float("inf"))
+    o = torch.einsum("bnft,btnh->bfnh", torch.softmax(s, -1), vr)
+    (o * g.float()).sum().backward()
+    for a, b_, name in ((q1.grad, qr.grad, "dq"), (k1.grad, kr.grad, "dk"), (v1.grad, vr.grad, "dv")):
+        err = (a.float() - b_).abs().max().item()
+        assert err <= 3e-2 * max(1.0, b_.abs().max().item()), (name, err)
+
+
+def test_attention_online_softmax_rescale(hip):
+    """Force a running-max jump at a late key tile (exercises the rescale branch)."""
+    B, S, H, D = 1, 256, 1, 64
+    q = torch.zeros(B, S, H, D, device=dev, dtype=torch.bfloat16)
+    k = torch.zeros_like(q)
+    v = _rand(B, S, H, D, seed=3)
+    q[:, :, :, 0] = 1.0
+    k[:, 200, :, 0] = 40.0  # one very large score in the 4th key tile
+    out = hip.attention(q, k, v, D ** -0.5)
+    ref = _attn_ref(q, k, v, D ** -0.5)
+    torch.testing.assert_close(out.float(), ref.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_elementwise(hip):
+    x = torch.randn(1000003, device=dev)
+    torch.testing.assert_close(hip.cast(x, torch.bfloat16), x.bfloat16())
+    xb = x.bfloat16()
+    torch.testing.assert_close(hip.cast(xb, torch.float32), xb.float())
+    torch.testing.assert_close(hip.sum_all(x, torch.float32), x.sum(), rtol=1e-4, atol=1e-2)
+    m = torch.randn(333, 77, device=dev)
+    torch.testing.assert_close(hip.colsum(m), m.sum(0), rtol=1e-5, atol=1e-4)
+    s = torch.randn(17, 300, device=dev)
+    torch.testing.assert_close(hip.softmax_lastdim(s), torch.softmax(s, -1), rtol=1e-5, atol=1e-6)
+    w = torch.randn(640, 512, device=dev)
+    torch.testing.assert_close(hip.cast_transpose_bf16(w), w.t().bfloat16())
+
+
+def test_adam_kernel(hip):
+    p = torch.randn(4099, device=dev)
+    g = torch.randn(4099, device=dev)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    tp = p.clone().requires_grad_()
+    opt = torch.optim.Adam([tp], lr=1e-3)
+    step = torch.zeros((), dtype=torch.int32, device=dev)
+    for i in range(3):
+        step += 1
+        p, m, v = hip.adam(p, g, m, v, step, 1e-3, 0.9, 0.999, 1e-8, 0.0, inplace=True)
+        tp.grad = g.clone()
+        opt.step()
+    torch.testing.assert_close(p, tp.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_rng_matches_host(hip):
+    import learning_jax_sharding_amd.random as R
+    k = R.PRNGKey(3)
+    for dist, lo, hi in (("normal", 0, 1), ("uniform", -2, 3), ("truncated_normal", -2, 2)):
+        shape = (6, 10)
+        region = ((2, 5), (4, 10))
+        gpu = hip.rng_fill(shape, region, k.k0, k.k1, dist, lo, hi, torch.float32, dev).cpu().numpy()
+        idx = (np.arange(2, 5)[:, None] * 10 + np.arange(4, 10)[None, :]).astype(np.uint64)
+        host = R._dist_np(idx.reshape(-1), k, dist, lo, hi).reshape(idx.shape)
+        np.testing.assert_allclose(gpu, host, rtol=1e-5, atol=1e-5)
+
+
+def test_linear_autograd(hip):
+    x = _rand(256, 640, dtype=torch.float32, seed=11).requires_grad_()
+    ws = [(_rand(640, 512, dtype=torch.float32, seed=20 + i) * 0.05).requires_grad_() for i in range(3)]
+    ys = hip.linear(x, ws, None, torch.bfloat16, False, torch.bfloat16)
+    gs = [_rand(256, 512, seed=30 + i) for i in range(3)]
+    sum((y.float() * g.float()).sum() for y, g in zip(ys, gs)).backward()
+    xr = x.detach().clone().requires_grad_()
+    wr = [w.detach().clone().requires_grad_() for w in ws]
+    yr = [xr.bfloat16().float() @ w.bfloat16().float() for w in wr]
+    sum((y * g.float()).sum() for y, g in zip(yr, gs)).backward()
+    for y, r in zip(ys, yr):
+        torch.testing.assert_close(y.float(), r, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=3e-2, atol=3e-2)
+    for w, r in zip(ws, wr):
+        torch.testing.assert_close(w.grad, r.grad, rtol=3e-2, atol=3e-1)
+    # bias + relu path
+    b = _rand(512, dtype=torch.float32, seed=40).requires_grad_()
+    (y,) = hip.linear(x, [ws[0]], b, torch.bfloat16, True, torch.bfloat16)
+    y.float().sum().backward()
+    yr = torch.relu(xr.bfloat16().float() @ wr[0].bfloat16().float() + b.detach().bfloat16().float())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(b.grad, (yr > 0).float().sum(0), rtol=1e-2, atol=2.0)
