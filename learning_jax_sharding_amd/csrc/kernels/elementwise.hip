@@ -92,6 +92,68 @@ __global__ void sum_all_kernel(const T* __restrict__ in, long n, float* __restri
   }
 }
 
+// 16-byte vectorised sum of a bf16 / f32 array
+template <typename T>
+__global__ void sum_all_vec_kernel(const T* __restrict__ in, long n, float* __restrict__ out) {
+  constexpr int V = 16 / sizeof(T);
+  float s = 0.f;
+  long nv = n / V;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long stride = (long)gridDim.x * blockDim.x;
+  for (; i < nv; i += stride) {
+    u32x4 v = *reinterpret_cast<const u32x4*>(in + i * V);
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += __uint_as_float(v[k] << 16) + __uint_as_float(v[k] & 0xffff0000u);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += __uint_as_float(v[k]);
+    }
+  }
+  if (blockIdx.x == 0)
+    for (long j = nv * V + threadIdx.x; j < n; j += blockDim.x) s += ldv<T>(in, j);
+  s = warp_sum64(s);
+  __shared__ float part[16];
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) part[w] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += part[k];
+    atomicAdd(out, t);
+  }
+}
+
+// column sums of a bf16 [R][C] matrix (C % 8 == 0, row stride ld; ld may be 0 = broadcast row):
+// block = 8 column-lanes (16 B each, 64 columns) x 32 row-lanes; LDS reduction, one atomic per column.
+__global__ void colsum_vec_kernel(const bf16_t* __restrict__ in, int R, int C, long ld, int rows_per_block,
+                                  float* __restrict__ out) {
+  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * 64 + cl * 8;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(R, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 < C) {
+    for (int r = r0 + rl; r < r1; r += 32) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(in + (long)r * ld + c0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[2 * k] += __uint_as_float(v[k] << 16);
+        acc[2 * k + 1] += __uint_as_float(v[k] & 0xffff0000u);
+      }
+    }
+  }
+  __shared__ float red[32][65];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rl][cl * 8 + k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+    for (int r = 0; r < 32; ++r) s += red[r][threadIdx.x];
+    int c = blockIdx.x * 64 + threadIdx.x;
+    if (c < C) atomicAdd(out + c, s);
+  }
+}
+
 // out[c] (+)= sum_r in[r][c]; grid.x over column blocks of 256, grid.y over row slabs.
 template <typename T>
 __global__ void colsum_kernel(const T* __restrict__ in, int R, int C, long ld, float* __restrict__ out) {
@@ -162,6 +224,66 @@ __global__ void adam_kernel(const float* __restrict__ p, const G* __restrict__ g
         mo[j] = mm;
         vo[j] = vv;
       }
+    }
+  }
+}
+
+// Multi-tensor Adam over 64x64 tiles of up to 32 parameters per launch (pointers passed by value
+// in the kernel arguments, so the launch is HIP-graph capturable).  Besides p/m/v (in place) it
+// refreshes the parameter's bf16 "shadows" used by the next step's MFMA GEMMs: the plain [R][C]
+// copy and the transposed [C][R] copy (staged through LDS so both writes are coalesced).  This
+// removes every per-step f32->bf16 weight cast kernel from the training step.
+struct AdamTensor {
+  long p, g, m, v, st, sn, R, C, g_bf16, tiles_c;
+};
+constexpr int kAdamMax = 32;
+struct AdamBatch {
+  AdamTensor t[kAdamMax];
+  int tile_start[kAdamMax + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, const int* __restrict__ step, float lr,
+                                                         float b1, float b2, float eps, float wd) {
+  __shared__ float tr[64][65];
+  const int id = blockIdx.x;
+  int ti = 0;
+  while (ti + 1 < batch.n && id >= batch.tile_start[ti + 1]) ++ti;
+  const AdamTensor T = batch.t[ti];
+  const int local = id - batch.tile_start[ti];
+  const int tr_i = local / (int)T.tiles_c, tc_i = local % (int)T.tiles_c;
+  const float t = (float)(*step);
+  const float inv_bc1 = 1.f / (1.f - powf(b1, t)), inv_sqrt_bc2 = rsqrtf(1.f - powf(b2, t));
+  float* P = reinterpret_cast<float*>(T.p);
+  float* Mm = reinterpret_cast<float*>(T.m);
+  float* Vv = reinterpret_cast<float*>(T.v);
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int col = tc_i * 64 + tx;
+#pragma unroll 4
+  for (int rr = 0; rr < 16; ++rr) {
+    const int rl = ty + 4 * rr, row = tr_i * 64 + rl;
+    float newp = 0.f;
+    if (row < T.R && col < T.C) {
+      const long i = (long)row * T.C + col;
+      float g = T.g_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(T.g)[i]) : reinterpret_cast<const float*>(T.g)[i];
+      float m = b1 * Mm[i] + (1.f - b1) * g;
+      float v = b2 * Vv[i] + (1.f - b2) * g * g;
+      float p = P[i];
+      newp = p - lr * ((m * inv_bc1) / (sqrtf(v) * inv_sqrt_bc2 + eps) + wd * p);
+      P[i] = newp;
+      Mm[i] = m;
+      Vv[i] = v;
+      if (T.sn) reinterpret_cast<bf16_t*>(T.sn)[i] = f2bf(newp);
+    }
+    tr[rl][tx] = newp;
+  }
+  if (T.st) {
+    __syncthreads();
+    const int orow0 = tc_i * 64, ocol = tr_i * 64 + tx;  // shadow_t[c][r]
+#pragma unroll 4
+    for (int rr = 0; rr < 16; ++rr) {
+      const int cl = ty + 4 * rr, c = orow0 + cl;
+      if (c < T.C && ocol < T.R) reinterpret_cast<bf16_t*>(T.st)[(long)c * T.R + ocol] = f2bf(tr[tx][cl]);
     }
   }
 }
@@ -244,6 +366,17 @@ LJS_API int ljs_cast_transpose_f32_bf16(const void* in, void* out, int R, int C,
 // out (f32 scalar) = sum(in); in is f32 (is_bf16=0) or bf16
 LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, hipStream_t s) {
   (void)hipMemsetAsync(out, 0, sizeof(float), s);
+  const bool aligned = (((uintptr_t)in) & 15) == 0;
+  if (aligned) {
+    long per = 256L * (is_bf16 ? 8 : 4) * 4;  // ~4 vector loads per thread
+    int g = grid_for(n, (int)per);
+    if (g > 1024) g = 1024;
+    if (is_bf16)
+      hipLaunchKernelGGL(sum_all_vec_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, (float*)out);
+    else
+      hipLaunchKernelGGL(sum_all_vec_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)in, n, (float*)out);
+    return (int)hipGetLastError();
+  }
   int g = grid_for(n, 256 * 16);
   if (is_bf16)
     hipLaunchKernelGGL(sum_all_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, (float*)out);
@@ -255,6 +388,17 @@ LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, hipStrea
 // out[C] f32 = column sums of in[R][C]; accumulate=1 adds into out
 LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void* out, int accumulate, hipStream_t s) {
   if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * C, s);
+  if (is_bf16 && C % 8 == 0 && ld % 8 == 0 && (((uintptr_t)in) & 15) == 0) {
+    int cb = (C + 63) / 64;
+    int want = 512 / cb;
+    int gy = want < 1 ? 1 : want;
+    int rpb = (R + gy - 1) / gy;
+    if (rpb < 32) rpb = 32;
+    gy = (R + rpb - 1) / rpb;
+    hipLaunchKernelGGL(colsum_vec_kernel, dim3(cb, gy), dim3(256), 0, s, (const bf16_t*)in, R, C, ld, rpb,
+                       (float*)out);
+    return (int)hipGetLastError();
+  }
   int gy = R / 256;
   if (gy < 1) gy = 1;
   if (gy > 64) gy = 64;
@@ -310,5 +454,26 @@ LJS_API int ljs_rng_fill(void* out, int is_bf16, int ndim, const long* start, co
   else
     hipLaunchKernelGGL(rng_kernel<float>, dim3(g), dim3(256), 0, s, (float*)out, reg, n, k0, k1, dist, lo, hi, erf_a,
                        erf_b);
+  return (int)hipGetLastError();
+}
+
+// table: n x 10 int64 {p, g, m, v, shadow_t, shadow_n, R, C, g_bf16, unused}; up to 32 per call
+LJS_API int ljs_adam_multi(const long* table, int n, const void* step, float lr, float b1, float b2, float eps,
+                           float wd, hipStream_t s) {
+  if (n < 1 || n > kAdamMax) return (int)hipErrorInvalidValue;
+  AdamBatch b;
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const long* r = table + 10 * i;
+    AdamTensor& t = b.t[i];
+    t.p = r[0]; t.g = r[1]; t.m = r[2]; t.v = r[3]; t.st = r[4]; t.sn = r[5]; t.R = r[6]; t.C = r[7];
+    t.g_bf16 = r[8];
+    t.tiles_c = (t.C + 63) / 64;
+    b.tile_start[i] = tiles;
+    tiles += (int)(((t.R + 63) / 64) * t.tiles_c);
+  }
+  b.tile_start[n] = tiles;
+  b.n = n;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3(tiles), dim3(256), 0, s, b, (const int*)step, lr, b1, b2, eps, wd);
   return (int)hipGetLastError();
 }

@@ -262,6 +262,13 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if (splitk > nkt) splitk = nkt;
   a.kt_per_split = (nkt + splitk - 1) / splitk;
   a.splitk = (nkt + a.kt_per_split - 1) / a.kt_per_split;
+  if (flags & 16) {  // zero C first (split-K accumulates with atomics); C must be one dense block
+    if (batch > 1 && sC != (long)M * ldc) return (int)hipErrorInvalidValue;
+    size_t es = out_f32 ? 4 : 2;
+    size_t bytes = ((size_t)(batch - 1) * sC + (size_t)(M - 1) * ldc + N) * es;
+    hipError_t me = hipMemsetAsync(C, 0, bytes, stream);
+    if (me != hipSuccess) return (int)me;
+  }
   hipError_t e;
   if (tile == 64)
     e = dispatch_layout<64, 64>(a, a_kc, b_kc, out_f32, stream);

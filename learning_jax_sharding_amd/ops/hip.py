@@ -45,6 +45,7 @@ _SIGS = {
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ljs_adam_f32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
+    "ljs_adam_multi": [_LP, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float, c_void_p],
     "ljs_rng_fill": [c_void_p, c_int, c_int, _LP, _LP, _LP, c_uint, c_uint, c_int, c_float, c_float, c_float,
                      c_float, c_void_p],
 }
@@ -99,12 +100,17 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
          a_kc: bool, b_kc: bool, batch: int = 1, sA: int = 0, sB: int = 0, sC: int = 0,
          bias: Optional[torch.Tensor] = None, sBias: int = 0, relu: bool = False, alpha: float = 1.0,
          accumulate: bool = False, splitk: int = 1, tile: Optional[int] = None, a_off: int = 0, b_off: int = 0,
-         c_off: int = 0) -> None:
-    """Raw launcher.  A/B bf16; C bf16 or f32 (split-K/accumulate need f32 C)."""
+         c_off: int = 0, zero_c: bool = False) -> None:
+    """Raw launcher.  A/B bf16; C bf16 or f32 (split-K/accumulate need f32 C).
+
+    ``lda``/``ldb`` may be 0 for an operand that repeats one row (a broadcast gradient).
+    ``zero_c`` zeroes C inside the launch sequence (needed before split-K accumulation).
+    """
     assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
     out_f32 = C.dtype == torch.float32
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
-        (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0)
+        (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
+        (16 if zero_c else 0)
     if tile is None:
         tiles128 = -(-M // 128) * -(-N // 128) * batch * max(1, splitk)
         tile = 128 if tiles128 >= 160 else 64
@@ -329,117 +335,16 @@ def softmax_lastdim(x: torch.Tensor) -> torch.Tensor:
 
 
 # ============================================================================ dense / linear
-class _Linear(torch.autograd.Function):
-    """ys[i] = x @ W_i (+ b) (relu): one batched MFMA GEMM over the stacked bf16 kernels.
-
-    Forward casts each f32 kernel to a transposed bf16 copy (k-contiguous) so the GEMM is
-    (KC, KC); backward: dX = sum_i dY_i W_i^T (KC, KC against a bf16 W), dW_i = X^T dY_i
-    (MN-contiguous operands read in place through the transposing LDS read, split-K f32),
-    db = column sums.
-    """
-
-    @staticmethod
-    def forward(ctx, x, b, compute_dtype, relu, out_dtype, *ws):
-        lead = x.shape[:-1]
-        K = x.shape[-1]
-        x2 = x.reshape(-1, K)
-        M = x2.shape[0]
-        xb = _cast_raw(x2.contiguous(), torch.bfloat16)
-        nw = len(ws)
-        N = ws[0].shape[1]
-        same = all(w.shape == ws[0].shape for w in ws)
-        wt = torch.empty((nw, N, K), dtype=torch.bfloat16, device=x.device)
-        for i, w in enumerate(ws):
-            if w.dtype == torch.float32 and w.stride(1) == 1:
-                cast_transpose_bf16(w, wt[i])
-            else:
-                wt[i].copy_(w.t().to(torch.bfloat16))
-        od = out_dtype if out_dtype in (torch.bfloat16, torch.float32) else torch.float32
-        out = torch.empty((M, nw * N), dtype=od, device=x.device)
-        bias = None
-        if b is not None:
-            bias = b if b.dtype in (torch.float32, torch.bfloat16) else b.float()
-            bias = bias.contiguous()
-        assert same
-        gemm(xb, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=N * K, sC=N,
-             bias=bias, sBias=0, relu=relu)
-        ys = [out[:, i * N:(i + 1) * N].reshape(tuple(lead) + (N,)) for i in range(nw)]
-        if od != out_dtype:
-            ys = [y.to(out_dtype) for y in ys]
-        ctx.save_for_backward(xb, b, *ws, *(ys if relu else []))
-        ctx.meta = (lead, K, M, N, nw, relu, x.dtype, b is not None)
-        return tuple(ys)
-
-    @staticmethod
-    def backward(ctx, *dys):
-        lead, K, M, N, nw, relu, xdtype, has_b = ctx.meta
-        saved = ctx.saved_tensors
-        xb, b = saved[0], saved[1]
-        ws = saved[2:2 + nw]
-        ys = saved[2 + nw:] if relu else None
-        dev = xb.device
-        d2 = []
-        for i, dy in enumerate(dys):
-            if dy is None:
-                d2.append(None)
-                continue
-            dy = dy.reshape(M, N)
-            if relu:
-                dy = dy * (ys[i].reshape(M, N) > 0)
-            d2.append(_cast_raw(dy.contiguous(), torch.bfloat16))
-        dx = db = None
-        dws = [None] * nw
-        if ctx.needs_input_grad[0]:
-            acc = torch.zeros((M, K), dtype=torch.float32, device=dev) if nw > 1 else None
-            for i, dy in enumerate(d2):
-                if dy is None:
-                    continue
-                wb = _cast_raw(ws[i].contiguous(), torch.bfloat16)        # [K][N]: B[k=n][n=k] k-contig
-                if acc is None:
-                    out = torch.empty((M, K), dtype=torch.bfloat16 if xdtype == torch.bfloat16 else torch.float32,
-                                      device=dev)
-                    gemm(dy, wb, out, M, K, N, N, N, K, True, True)
-                    dx = out
-                else:
-                    gemm(dy, wb, acc, M, K, N, N, N, K, True, True, accumulate=True)
-            if acc is not None:
-                dx = acc
-            if dx is not None:
-                dx = dx.to(xdtype).reshape(tuple(lead) + (K,))
-        for i, dy in enumerate(d2):
-            if dy is None or not ctx.needs_input_grad[5 + i]:
-                continue
-            w = ws[i]
-            dw = torch.zeros((K, N), dtype=torch.float32, device=dev)
-            sk = _choose_splitk(K, N, M, 1)
-            if M % 8 == 0 and K % 8 == 0 and N % 8 == 0:
-                # dW[k][n] = sum_t X[t][k] dY[t][n]: A = X^T (m-contig), B = dY (n-contig)
-                gemm(xb, dy, dw, K, N, M, K, N, N, False, False, splitk=sk)
-            else:
-                dw = (xb.float().t() @ dy.float())
-            dws[i] = dw.to(w.dtype)
-        if has_b and ctx.needs_input_grad[1]:
-            tot = None
-            for dy in d2:
-                if dy is not None:
-                    tot = colsum(dy, tot, accumulate=tot is not None)
-            db = tot.to(b.dtype) if tot is not None else None
-        return (dx, db, None, None, None, *dws)
-
-
 def linear(x: torch.Tensor, ws: List[torch.Tensor], b: Optional[torch.Tensor], compute_dtype: torch.dtype,
            relu: bool, out_dtype: torch.dtype) -> List[torch.Tensor]:
-    K = x.shape[-1]
-    N = ws[0].shape[1]
-    ok = (compute_dtype == torch.bfloat16 and K % 8 == 0 and N % 8 == 0
-          and all(w.shape == ws[0].shape for w in ws) and (b is None or len(ws) == 1))
-    if not ok:
-        from .kernels import linear as _ref_linear  # pragma: no cover - shape fallback still runs on GPU via torch
-        outs = []
-        for w in ws:
-            outs.append(_torch_linear(x, w, b if len(ws) == 1 else None, compute_dtype, relu, out_dtype))
-        return outs
-    return list(_Linear.apply(x, b, compute_dtype, relu, out_dtype, *ws))
+    """Fused dense layer (see :mod:`.linear`); shapes the MFMA path cannot take use torch."""
+    from . import linear as _lin
+    if compute_dtype == torch.bfloat16 and _lin.supported(x, ws, b):
+        return _lin.linear(x, list(ws), b, relu, out_dtype)
+    outs = []
+    for w in ws:
+        outs.append(_torch_linear(x, w, b if len(ws) == 1 else None, compute_dtype, relu, out_dtype))
+    return outs
 
 
 def _torch_linear(x, w, b, compute_dtype, relu, out_dtype):
@@ -449,6 +354,16 @@ def _torch_linear(x, w, b, compute_dtype, relu, out_dtype):
     if relu:
         y = torch.relu(y)
     return y.to(out_dtype)
+
+
+def colsum_ld(t: torch.Tensor, R: int, C: int, ld: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Column sums of an [R][C] matrix with row stride ``ld`` (0 = one repeated row)."""
+    acc = out is not None
+    if out is None:
+        out = torch.empty((C,), dtype=torch.float32, device=t.device)
+    rc = lib().ljs_colsum(_p(t), int(t.dtype == torch.bfloat16), R, C, ld, _p(out), int(acc), _stream(t))
+    _ck(rc, "colsum")
+    return out
 
 
 # ============================================================================ attention
@@ -481,9 +396,19 @@ class _Attention(torch.autograd.Function):
         do = do.to(torch.bfloat16)
         if do.stride(3) != 1:
             do = do.contiguous()
-        dq = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
-        dk = torch.empty((B, Sk, H, D), dtype=torch.bfloat16, device=q.device)
-        dv = torch.empty((B, Sk, H, D), dtype=torch.bfloat16, device=q.device)
+        st = q.stride()
+        fused = (Sq == Sk and k.stride() == st and v.stride() == st and st[3] == 1 and st[2] == D
+                 and k.data_ptr() - q.data_ptr() == H * D * 2 and v.data_ptr() - q.data_ptr() == 2 * H * D * 2
+                 and st[1] == 3 * H * D and st[0] == Sq * st[1])
+        if fused:
+            # q/k/v are column blocks of one fused-QKV buffer: write dq/dk/dv the same way so the
+            # dense backward sees one [M, 3*H*D] gradient and runs ONE batched weight-grad GEMM
+            dqkv = torch.empty((B, Sq, 3, H, D), dtype=torch.bfloat16, device=q.device)
+            dq, dk, dv = dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2]
+        else:
+            dq = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
+            dk = torch.empty((B, Sk, H, D), dtype=torch.bfloat16, device=q.device)
+            dv = torch.empty((B, Sk, H, D), dtype=torch.bfloat16, device=q.device)
         delta = torch.empty((B, H, Sq), dtype=torch.float32, device=q.device)
         rc = lib().ljs_attn_bwd(_p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(delta), _p(dq), _p(dk), _p(dv), B, Sq,
                                 Sk, H, _longs(_strides3(q)), _longs(_strides3(k)), _longs(_strides3(v)),
@@ -520,6 +445,34 @@ def adam(p, g, m, v, step, lr, b1, b2, eps, wd, inplace):
                             _p(step_i), p.numel(), lr, b1, b2, eps, wd, _stream(p))
     _ck(rc, "ljs_adam_f32")
     return po.view(p.shape), mo.view(m.shape), vo.view(v.shape)
+
+
+def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd) -> None:
+    """In-place fused Adam over many params (one launch per 32): entries = [(p, g, m, v)].
+
+    Also rewrites each param's registered bf16 shadows (see :mod:`.shadow`)."""
+    from . import shadow
+    import numpy as np
+    rows = []
+    for p, g, m, v in entries:
+        assert p.is_contiguous() and m.is_contiguous() and v.is_contiguous() and p.dtype == torch.float32
+        if g.dtype not in (torch.float32, torch.bfloat16) or not g.is_contiguous():
+            g = g.float().contiguous() if g.dtype not in (torch.float32, torch.bfloat16) else g.contiguous()
+        bufs = shadow.kinds_of(p) if p.dim() == 2 else {}
+        st, sn = bufs.get("T"), bufs.get("N")
+        R, C = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
+        rows.append(([p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
+                      st.data_ptr() if st is not None else 0, sn.data_ptr() if sn is not None else 0,
+                      R, C, int(g.dtype == torch.bfloat16), 0], g))
+    step_i = step if step.dtype == torch.int32 else step.to(torch.int32)
+    for i in range(0, len(rows), 32):
+        chunk = rows[i:i + 32]
+        tab = np.asarray([r[0] for r in chunk], dtype=np.int64).reshape(-1)
+        arr = (ctypes.c_long * tab.size)(*tab.tolist())
+        rc = lib().ljs_adam_multi(arr, len(chunk), _p(step_i), lr, b1, b2, eps, wd, _stream(step_i))
+        _ck(rc, "ljs_adam_multi")
+    for p, _, _, _ in entries:
+        shadow.mark_fresh(p)
 
 
 # ============================================================================ RNG

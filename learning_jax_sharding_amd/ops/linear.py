@@ -1,0 +1,168 @@
+"""Fused dense layer on the MFMA GEMM: ``ys[i] = x @ W_i (+ b) (relu)``.
+
+Forward: one batched GEMM launch over the stacked kernels (Q/K/V share x), reading each
+f32 weight through its persistent bf16 transposed shadow (:mod:`.shadow`; refreshed by the
+fused Adam kernel, so no per-step cast).  Output columns of the kernels are interleaved in
+one ``[M, n*N]`` buffer, so downstream slices (the attention's q/k/v) are views.
+
+Backward:
+* ``dX = sum_i dY_i W_i^T``    - (KC, KC) GEMM against the plain bf16 shadow of W_i
+  (f32 accumulation across kernels);
+* ``dW_i = X^T dY_i``          - both operands read in their natural row-major layout
+  through the transposing LDS read (MN-contiguous operands), split-K with f32 atomics; when
+  the dY_i are column blocks of one buffer (the attention backward writes dq/dk/dv into one
+  ``[M, 3N]`` buffer) all of them go in ONE batched launch;
+* ``db = colsum(dY)``.
+Gradients that are a broadcast row (the cotangent of ``y.sum()``) are consumed with a zero
+leading dimension instead of being materialised.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import hip
+from . import shadow
+
+__all__ = ["linear"]
+
+
+def _splitk(M: int, N: int, K: int, batch: int, tile: int) -> int:
+    tiles = -(-M // tile) * -(-N // tile) * batch
+    if tiles >= 200:
+        return 1
+    s = max(1, min(16, round(400 / tiles), K // 1024))
+    return s
+
+
+def _row_view(dy: torch.Tensor, M: int, N: int) -> Tuple[torch.Tensor, int]:
+    """(bf16 tensor, ld) describing dy as an [M][N] matrix with unit column stride.
+
+    A gradient that repeats one row (stride 0 over rows, e.g. the cotangent of ``y.sum()``)
+    is returned as that single bf16 row with ld = 0: the GEMMs and the column sum read it
+    M times, exactly as they would read a materialised matrix, without writing one.
+    """
+    d2 = dy.reshape(M, N)
+    if d2.stride(0) == 0:
+        row = d2[0].contiguous()
+        row = _bf16(row)
+        return row.unsqueeze(0).expand(M, N), 0
+    if d2.stride(1) != 1 or d2.stride(0) < N:
+        d2 = d2.contiguous()
+    if d2.dtype != torch.bfloat16:
+        d2 = _bf16(d2.contiguous())
+    return d2, d2.stride(0)
+
+
+def _bf16(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype == torch.bfloat16:
+        return t
+    if t.is_contiguous():
+        return hip._cast_raw(t, torch.bfloat16)
+    return t.to(torch.bfloat16)
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b, relu, out_dtype, *ws):
+        lead = x.shape[:-1]
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        M = x2.shape[0]
+        xb = _bf16(x2 if x2.is_contiguous() else x2.contiguous())
+        nw = len(ws)
+        N = ws[0].shape[1]
+        if nw == 1:
+            wt = shadow.get(ws[0], "T")
+            sB = 0
+        else:
+            # one [nw][N][K] operand: stack the transposed shadows (tiny copies), or cast directly
+            wt = torch.empty((nw, N, K), dtype=torch.bfloat16, device=x.device)
+            for i, w in enumerate(ws):
+                wt[i].copy_(shadow.get(w, "T"))
+            sB = N * K
+        od = out_dtype if out_dtype in (torch.bfloat16, torch.float32) else torch.float32
+        out = torch.empty((M, nw * N), dtype=od, device=x.device)
+        bias = None
+        if b is not None:
+            bias = (b if b.dtype in (torch.float32, torch.bfloat16) else b.float()).contiguous()
+        hip.gemm(xb, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=sB, sC=N,
+                 bias=bias, sBias=0, relu=relu)
+        ys = [out[:, i * N:(i + 1) * N].view(tuple(lead) + (N,)) for i in range(nw)]
+        if od != out_dtype:
+            ys = [y.to(out_dtype) for y in ys]
+        ctx.save_for_backward(xb, b, *ws, *(ys if relu else []))
+        ctx.meta = (lead, K, M, N, nw, relu, x.dtype, b is not None)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        lead, K, M, N, nw, relu, xdtype, has_b = ctx.meta
+        saved = ctx.saved_tensors
+        xb, b = saved[0], saved[1]
+        ws = saved[2:2 + nw]
+        ys = saved[2 + nw:] if relu else None
+        dev = xb.device
+        mats: List[Optional[Tuple[torch.Tensor, int]]] = []
+        for i, dy in enumerate(dys):
+            if dy is None:
+                mats.append(None)
+                continue
+            if relu:
+                dy = (dy * (ys[i] > 0)).reshape(M, N)
+            mats.append(_row_view(dy, M, N))
+        dx = db = None
+        dws = [None] * nw
+        live = [i for i in range(nw) if mats[i] is not None]
+        # ---- dX
+        if ctx.needs_input_grad[0] and live:
+            out_dt = torch.bfloat16 if (xdtype == torch.bfloat16 and len(live) == 1) else torch.float32
+            dx = torch.empty((M, K), dtype=out_dt, device=dev)
+            for j, i in enumerate(live):
+                t, ld = mats[i]
+                wn = shadow.get(ws[i], "N")                  # [K][N]: B[k=n][n'=k], k-contiguous
+                hip.gemm(t, wn, dx, M, K, N, ld, N, K, True, True, accumulate=j > 0)
+            dx = dx.to(xdtype).view(tuple(lead) + (K,))
+        # ---- dW (MN-contiguous operands: X^T and dY read in place)
+        want = [i for i in live if ctx.needs_input_grad[4 + i]]
+        if want:
+            t0, ld0 = mats[want[0]]
+            batched = (len(want) == nw and nw > 1 and ld0 > 0 and all(
+                mats[i][1] == ld0 and mats[i][0].data_ptr() == t0.data_ptr() + i * N * 2 for i in want))
+            tile = 128 if (K >= 256 and N >= 256) else 64
+            if batched:
+                dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
+                sk = _splitk(K, N, M, nw, tile)
+                hip.gemm(xb, t0, dW, K, N, M, K, ld0, N, False, False, batch=nw, sA=0, sB=N, sC=K * N,
+                         splitk=sk, tile=tile, zero_c=True)
+                for i in want:
+                    dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
+            else:
+                for i in want:
+                    t, ld = mats[i]
+                    dW = torch.empty((K, N), dtype=torch.float32, device=dev)
+                    sk = _splitk(K, N, M, 1, tile)
+                    hip.gemm(xb, t, dW, K, N, M, K, ld, N, False, False, splitk=sk, tile=tile, zero_c=True)
+                    dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
+        # ---- db
+        if has_b and ctx.needs_input_grad[1] and live:
+            tot = None
+            for i in live:
+                t, ld = mats[i]
+                tot = hip.colsum_ld(t, M, N, ld, tot)
+            db = tot.to(b.dtype)
+        return (dx, db, None, None, *dws)
+
+
+def supported(x: torch.Tensor, ws: Sequence[torch.Tensor], b) -> bool:
+    K = x.shape[-1]
+    N = ws[0].shape[1]
+    return (K % 8 == 0 and N % 8 == 0 and all(w.shape == ws[0].shape and w.dim() == 2 for w in ws)
+            and all(w.dtype == torch.float32 and w.stride(1) == 1 for w in ws)
+            and (b is None or len(ws) == 1))
+
+
+def linear(x: torch.Tensor, ws: List[torch.Tensor], b: Optional[torch.Tensor], relu: bool,
+           out_dtype: torch.dtype) -> List[torch.Tensor]:
+    return list(_Linear.apply(x, b, relu, out_dtype, *ws))

@@ -146,6 +146,13 @@ class _Adam:
         gl = T.tree_leaves(grads, is_leaf=_is_arr)
         ml = T.tree_leaves(st.mu, is_leaf=_is_arr)
         vl = T.tree_leaves(st.nu, is_leaf=_is_arr)
+        fused = self._apply_multi(pl, gl, ml, vl, new_count, inplace)
+        if fused is not None:
+            new_p, new_m, new_v = fused
+            params2 = T.tree_unflatten(ptd, new_p)
+            mu = T.tree_unflatten(T.tree_structure(st.mu, is_leaf=_is_arr), new_m)
+            nu = T.tree_unflatten(T.tree_structure(st.nu, is_leaf=_is_arr), new_v)
+            return params2, (ScaleByAdamState(new_count, mu, nu), empty)
         new_p, new_m, new_v = [], [], []
         for p, g, m, v in zip(pl, gl, ml, vl):
             if not _is_arr(p):
@@ -164,6 +171,40 @@ class _Adam:
         mu = T.tree_unflatten(T.tree_structure(st.mu, is_leaf=_is_arr), new_m)
         nu = T.tree_unflatten(T.tree_structure(st.nu, is_leaf=_is_arr), new_v)
         return params2, (ScaleByAdamState(new_count, mu, nu), empty)
+
+
+def _adam_multi_apply(self, pl, gl, ml, vl, count, inplace):
+    """MI355X path: every local shard of every param in ONE multi-tensor kernel per device
+    (it also refreshes the params' bf16 GEMM shadows).  Returns None to use the per-leaf path."""
+    arrs = [(p, g, m, v) for p, g, m, v in zip(pl, gl, ml, vl) if _is_arr(p)]
+    if not arrs or len(arrs) != len(pl):
+        return None
+    for p, g, m, v in arrs:
+        for d, t in p.local.items():
+            if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+                return None
+            if not (m.local[d].is_contiguous() and v.local[d].is_contiguous()):
+                return None
+    from ..ops import hip
+    new_loc = [({}, {}, {}) for _ in arrs]
+    by_dev = {}
+    for i, (p, g, m, v) in enumerate(arrs):
+        for d, pt in p.local.items():
+            mt, vt = m.local[d], v.local[d]
+            if inplace and _state.is_donated(pt):
+                tp, tm, tv = pt, mt, vt
+            else:
+                tp, tm, tv = pt.clone(), mt.clone(), vt.clone()
+            new_loc[i][0][d], new_loc[i][1][d], new_loc[i][2][d] = tp, tm, tv
+            by_dev.setdefault(d, []).append((tp, g.local[d], tm, tv))
+    for d, entries in by_dev.items():
+        hip.adam_multi(entries, count.local[d], self._lr(), self.b1, self.b2, self.eps, self.weight_decay)
+    mk = lambda a, loc: ShardedArray(a.shape, a.dtype, a.sharding, loc)  # noqa: E731
+    return ([mk(a[0], l[0]) for a, l in zip(arrs, new_loc)], [mk(a[2], l[1]) for a, l in zip(arrs, new_loc)],
+            [mk(a[3], l[2]) for a, l in zip(arrs, new_loc)])
+
+
+_Adam._apply_multi = _adam_multi_apply
 
 
 def adam(learning_rate: float, b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8, eps_root: float = 0.0):

@@ -189,9 +189,14 @@ class Jitted:
         full = list(args)
         in_leaves = []
         for i, a in dyn:
-            def cp(x):
+            donated = i in self.donate_argnums
+
+            def cp(x, donated=donated):
                 if isinstance(x, ShardedArray):
-                    y = ShardedArray(x.shape, x.dtype, x.sharding, {d: t.detach().clone() for d, t in x.local.items()})
+                    # donated buffers become the graph's static inputs as they are (their bf16
+                    # weight shadows stay valid); others are copied into private buffers
+                    y = x if donated else ShardedArray(x.shape, x.dtype, x.sharding,
+                                                       {d: t.detach().clone() for d, t in x.local.items()})
                     in_leaves.append(y)
                     return y
                 return x

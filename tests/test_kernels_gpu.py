@@ -212,3 +212,44 @@ def test_linear_autograd(hip):
     yr = torch.relu(xr.bfloat16().float() @ wr[0].bfloat16().float() + b.detach().bfloat16().float())
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
     torch.testing.assert_close(b.grad, (yr > 0).float().sum(0), rtol=1e-2, atol=2.0)
+
+
+def test_adam_multi_and_shadows(hip):
+    from learning_jax_sharding_amd.ops import shadow
+    ws = [torch.randn(640, 512, device=dev), torch.randn(512, 640, device=dev), torch.randn(640, device=dev)]
+    gs = [torch.randn_like(w) for w in ws]
+    ms = [torch.zeros_like(w) for w in ws]
+    vs = [torch.zeros_like(w) for w in ws]
+    refs = [w.clone().requires_grad_() for w in ws]
+    opt = torch.optim.Adam(refs, lr=1e-3)
+    shadow.get(ws[0], "T")
+    shadow.get(ws[1], "N")
+    step = torch.zeros((), dtype=torch.int32, device=dev)
+    for _ in range(2):
+        step += 1
+        hip.adam_multi(list(zip(ws, gs, ms, vs)), step, 1e-3, 0.9, 0.999, 1e-8, 0.0)
+        for r, g in zip(refs, gs):
+            r.grad = g.clone()
+        opt.step()
+    for w, r in zip(ws, refs):
+        torch.testing.assert_close(w, r.detach(), rtol=1e-5, atol=1e-6)
+    # shadows were refreshed by the kernel (no re-cast needed) and equal the new weights
+    e0 = shadow.entry(ws[0], create=False)
+    assert e0.versions["T"] == ws[0]._version
+    torch.testing.assert_close(e0.bufs["T"], ws[0].t().bfloat16())
+    torch.testing.assert_close(shadow.entry(ws[1], create=False).bufs["N"], ws[1].bfloat16())
+
+
+def test_linear_broadcast_grad_and_strided(hip):
+    """dY that repeats one row (cotangent of y.sum()) is read with ld=0, not materialised."""
+    x = _rand(128, 256, dtype=torch.float32, seed=1)
+    w = (_rand(256, 320, dtype=torch.float32, seed=2) * 0.05).requires_grad_()
+    b = torch.zeros(320, device=dev, requires_grad=True)
+    xr = x.clone().requires_grad_()
+    (y,) = hip.linear(xr, [w], b, torch.bfloat16, False, torch.bfloat16)
+    y.float().sum().backward()
+    xf = x.bfloat16().float()
+    torch.testing.assert_close(w.grad, xf.sum(0)[:, None].expand(256, 320), rtol=1e-2, atol=1e-1)
+    torch.testing.assert_close(b.grad, torch.full((320,), 128.0, device=dev))
+    torch.testing.assert_close(xr.grad, w.detach().bfloat16().float().sum(1)[None, :].expand(128, 256),
+                               rtol=2e-2, atol=5e-2)
