@@ -370,7 +370,7 @@ LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, hipStrea
   if (aligned) {
     long per = 256L * (is_bf16 ? 8 : 4) * 4;  // ~4 vector loads per thread
     int g = grid_for(n, (int)per);
-    if (g > 1024) g = 1024;
+    if (g > 256) g = 256;  // one block per CU: bounds the same-address atomics to 256
     if (is_bf16)
       hipLaunchKernelGGL(sum_all_vec_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, (float*)out);
     else

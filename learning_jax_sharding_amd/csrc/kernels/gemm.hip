@@ -182,6 +182,48 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
   const bool has_bias = (p.flags & 2) && p.splitk == 1;
   const bool bias_f32 = p.flags & 4;
   const bool accumulate = p.flags & 8;
+  if constexpr (!OUT_F32) {
+    // bf16 output: stage the tile in LDS (the K loop's last barrier freed it), then write whole
+    // rows with 16-byte stores instead of 2-byte scattered accumulator-layout stores.
+    constexpr int LDC = BN + 8;
+    bf16_t* ct = smem;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cl = wc * (BN / 2) + j * 16 + (lane & 15);
+      const int col = n0 + cl;
+      float bv = 0.f;
+      if (has_bias && col < p.N) {
+        const long bo = (long)b * p.sBias + col;
+        bv = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo]
+                      : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] * p.alpha + bv;
+          if (relu) v = fmaxf(v, 0.f);
+          ct[(wr * (BM / 2) + i * 16 + (lane >> 4) * 4 + r) * LDC + cl] = f2bf(v);
+        }
+    }
+    __syncthreads();
+    bf16_t* Cb = reinterpret_cast<bf16_t*>(p.C) + (long)b * p.sC;
+    constexpr int CPR = BN / 8;
+    const bool vec_ok = (p.ldc % 8 == 0) && ((((uintptr_t)Cb) & 15) == 0);
+    for (int c = tid; c < BM * CPR; c += 256) {
+      const int rl = c / CPR, cc = c % CPR;
+      const int row = m0 + rl, col = n0 + cc * 8;
+      if (row >= p.M || col >= p.N) continue;
+      const bf16_t* src = ct + rl * LDC + cc * 8;
+      bf16_t* dst = Cb + (long)row * p.ldc + col;
+      if (vec_ok && col + 8 <= p.N) {
+        *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
+      } else {
+        for (int e = 0; e < 8 && col + e < p.N; ++e) dst[e] = src[e];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll

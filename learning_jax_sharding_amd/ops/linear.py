@@ -77,10 +77,8 @@ class _Linear(torch.autograd.Function):
             wt = shadow.get(ws[0], "T")
             sB = 0
         else:
-            # one [nw][N][K] operand: stack the transposed shadows (tiny copies), or cast directly
-            wt = torch.empty((nw, N, K), dtype=torch.bfloat16, device=x.device)
-            for i, w in enumerate(ws):
-                wt[i].copy_(shadow.get(w, "T"))
+            # one [nw][N][K] operand: the weights' transposed shadows live in one allocation
+            wt = shadow.get_stacked(ws)
             sB = N * K
         od = out_dtype if out_dtype in (torch.bfloat16, torch.float32) else torch.float32
         out = torch.empty((M, nw * N), dtype=od, device=x.device)

@@ -5,22 +5,26 @@ The reference keeps f32 parameters and casts them to bf16 inside every Dense cal
 memory-bound kernel per weight per step.  Instead each f32 weight gets persistent bf16
 shadows - ``"T"`` (transposed, ``[out][in]``, the k-contiguous B operand of the forward
 GEMM) and ``"N"`` (plain ``[in][out]``, used by the backward input-gradient GEMM) - which
-the fused multi-tensor Adam kernel rewrites in the same pass that updates the weight.  A
-shadow is trusted only while the weight tensor object is alive and its autograd version
-counter matches, so any other in-place write to the weight forces a re-cast.
+the fused multi-tensor Adam kernel rewrites in the same pass that updates the weight.
+
+Keying: by storage address + layout, validated by (a) a weak reference to the tensor that
+owns the storage (the optimizer's parameter; while it lives the address cannot be reused)
+and (b) torch's version counter, which ``detach()`` views share with their base - so the
+autograd leaves ``grad`` creates for a step hit the same shadow, and any in-place write
+that is not the fused optimizer forces a re-cast.
 """
 from __future__ import annotations
 
 import weakref
-from typing import Dict, Optional
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-__all__ = ["get", "entry", "mark_fresh", "kinds_of"]
+__all__ = ["get", "get_stacked", "entry", "adopt", "mark_fresh", "kinds_of"]
 
 
 class _Entry:
-    __slots__ = ("ref", "bufs", "versions", "__weakref__")
+    __slots__ = ("ref", "bufs", "versions")
 
     def __init__(self, w: torch.Tensor):
         self.ref = weakref.ref(w)
@@ -28,23 +32,37 @@ class _Entry:
         self.versions: Dict[str, int] = {}
 
 
-_REG: Dict[int, _Entry] = {}
+_REG: Dict[Tuple, _Entry] = {}
+
+
+def _key(w: torch.Tensor):
+    return (w.data_ptr(), w.dtype, tuple(w.shape), tuple(w.stride()), w.device)
 
 
 def entry(w: torch.Tensor, create: bool = True) -> Optional[_Entry]:
-    e = _REG.get(id(w))
-    if e is not None and e.ref() is not w:
-        e = None
-        _REG.pop(id(w), None)
+    k = _key(w)
+    e = _REG.get(k)
+    if e is not None:
+        owner = e.ref()
+        if owner is None or owner.data_ptr() != w.data_ptr():
+            e = None
+            _REG.pop(k, None)
     if e is None and create:
         e = _Entry(w)
-        _REG[id(w)] = e
-        weakref.finalize(w, _REG.pop, id(w), None)
+        _REG[k] = e
+    return e
+
+
+def adopt(w: torch.Tensor) -> Optional[_Entry]:
+    """The optimizer's parameter tensor becomes the owner of its storage's shadows."""
+    e = entry(w, create=False)
+    if e is not None and e.ref() is not w:
+        e.ref = weakref.ref(w)
     return e
 
 
 def kinds_of(w: torch.Tensor):
-    e = entry(w, create=False)
+    e = adopt(w)
     return {} if e is None else e.bufs
 
 
@@ -54,14 +72,9 @@ def _alloc(w: torch.Tensor, kind: str) -> torch.Tensor:
     return torch.empty(shape, dtype=torch.bfloat16, device=w.device)
 
 
-def get(w: torch.Tensor, kind: str) -> torch.Tensor:
-    """bf16 copy of the 2-D f32 weight ``w`` (``kind`` "T": transposed, "N": plain)."""
+def _refresh(w: torch.Tensor, e: _Entry, kind: str) -> torch.Tensor:
     from . import hip
-    e = entry(w)
-    buf = e.bufs.get(kind)
-    if buf is None:
-        buf = e.bufs[kind] = _alloc(w, kind)
-        e.versions[kind] = -1
+    buf = e.bufs[kind]
     if e.versions.get(kind) != w._version:
         if kind == "T":
             hip.cast_transpose_bf16(w, buf)
@@ -69,6 +82,42 @@ def get(w: torch.Tensor, kind: str) -> torch.Tensor:
             buf.copy_(hip._cast_raw(w.contiguous(), torch.bfloat16))
         e.versions[kind] = w._version
     return buf
+
+
+def get(w: torch.Tensor, kind: str) -> torch.Tensor:
+    """bf16 copy of the 2-D f32 weight ``w`` (``kind`` "T": transposed, "N": plain)."""
+    e = entry(w)
+    if kind not in e.bufs:
+        e.bufs[kind] = _alloc(w, kind)
+        e.versions[kind] = -1
+    return _refresh(w, e, kind)
+
+
+def get_stacked(ws: Sequence[torch.Tensor]) -> torch.Tensor:
+    """``[n][N][K]`` transposed shadows of same-shape weights as ONE buffer (batched GEMM operand).
+
+    The first call moves the weights' "T" shadows into consecutive slices of one allocation;
+    the fused Adam then writes them there directly, so no per-step stacking copy remains.
+    """
+    es = [entry(w) for w in ws]
+    K, N = ws[0].shape
+    bufs = [e.bufs.get("T") for e in es]
+    base = bufs[0]
+    ok = all(b is not None for b in bufs) and base is not None and all(
+        b.data_ptr() == base.data_ptr() + i * N * K * 2 for i, b in enumerate(bufs))
+    if not ok:
+        group = torch.empty((len(ws), N, K), dtype=torch.bfloat16, device=ws[0].device)
+        for i, (w, e) in enumerate(zip(ws, es)):
+            old = e.bufs.get("T")
+            e.bufs["T"] = group[i]
+            if old is not None and e.versions.get("T") == w._version:
+                group[i].copy_(old)
+            else:
+                e.versions["T"] = -1
+    for w, e in zip(ws, es):
+        _refresh(w, e, "T")
+    b0 = es[0].bufs["T"]
+    return b0.as_strided((len(ws), N, K), (N * K, K, 1))
 
 
 def mark_fresh(w: torch.Tensor) -> None:
