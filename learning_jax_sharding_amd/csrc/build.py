@@ -37,8 +37,16 @@ def _digest(files):
     return h.hexdigest()[:16]
 
 
+def _file_flags(src):
+    """Per-file extra flags from a first-line ``// LJS_HIPCC_FLAGS: ...`` comment."""
+    with open(src) as f:
+        first = f.readline()
+    tag = "LJS_HIPCC_FLAGS:"
+    return first.split(tag, 1)[1].split() if tag in first else []
+
+
 def _compile(src, obj, extra):
-    cmd = [HIPCC] + FLAGS + extra + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + extra + _file_flags(src) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

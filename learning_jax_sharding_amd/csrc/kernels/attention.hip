@@ -1,3 +1,4 @@
+// LJS_HIPCC_FLAGS: -mllvm -amdgpu-mfma-vgpr-form
 // Fused multi-head attention for gfx950 (head_dim 64), forward and backward.
 //
 // Semantics (case6_attention.py:120-133): scores = f32(q) . f32(k) * scale, f32 softmax over
@@ -13,6 +14,12 @@
 // with V^T delivered by the transposing LDS read (ds_read_b64_tr_b16).  The backward uses
 // the same trick for every product: dV^T = dO^T P, dK^T = Q^T dS (one kernel per key block)
 // and dQ^T = K^T dS^T (one kernel per query block), so no atomics and no S x S buffers.
+//
+// VALU budget (D = 64 gives only 256 MFMA FLOPs per softmax element, so these kernels are
+// VALU-bound unless the per-element work is minimal): masking is compiled only into the
+// boundary tiles (MASK template), the softmax scale is folded into one FMA before the raw
+// v_exp_f32 (no libm range reduction), and the MFMA accumulators stay in VGPRs
+// (-amdgpu-mfma-vgpr-form) so no AGPR<->VGPR copies surround the softmax.
 //
 // Tensors are (batch, seq, heads, 64) with arbitrary batch/seq/head strides (d contiguous),
 // so Q/K/V can be column slices of the fused QKV GEMM output.
@@ -37,23 +44,13 @@ struct AttnArgs {
   int causal, q_offset;
 };
 
-// ---- LDS images: [64 rows][64 d] bf16, 128-byte rows
-// k-contiguous row reads (ds_read_b128) + transposed reads: 16-byte chunk XOR (row>>1)&7
-__device__ __forceinline__ int img_k(int row, int c16) { return row * D + ((c16 ^ ((row >> 1) & 7)) << 3); }
-// transposed reads only: 8-byte chunk XOR 4*((row>>1)&3) (conflict-free tr_b16 reads)
-__device__ __forceinline__ int img_t(int row, int c8) { return row * D + ((c8 ^ (((row >> 1) & 3) << 2)) << 2); }
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-template <bool TR_ONLY>
-__device__ __forceinline__ int img_chunk16(int row, int c16) {
-  if constexpr (TR_ONLY) return img_t(row, c16 * 2);
-  else return img_k(row, c16);
-}
-
-template <bool TR_ONLY>
-__device__ __forceinline__ int img_chunk8(int row, int c8) {
-  if constexpr (TR_ONLY) return img_t(row, c8);
-  else return row * D + (((c8 >> 1) ^ ((row >> 1) & 7)) << 3) + ((c8 & 1) << 2);
-}
+// ---- LDS image: [64 rows][64 d] bf16, 128-byte rows.  16-byte chunk XOR 2*((row>>1)&3):
+// bank-conflict free for BOTH the ds_read_b128 row reads (MFMA operand rows) and the
+// ds_read_b64_tr_b16 transposed reads (found by exhaustive bank simulation of both patterns).
+__device__ __forceinline__ int img16(int row, int c16) { return row * D + ((c16 ^ (((row >> 1) & 3) << 1)) << 3); }
+__device__ __forceinline__ int img8(int row, int c8) { return img16(row, c8 >> 1) + ((c8 & 1) << 2); }
 
 // register-staged tile: rows [r0, r0+64) of a (seq, d) slab with row stride ld
 struct TileRegs {
@@ -66,31 +63,29 @@ struct TileRegs {
       v[i] = r < rlim ? *reinterpret_cast<const u32x4*>(base + (long)r * ld + c16 * 8) : u32x4{0, 0, 0, 0};
     }
   }
-  template <bool TR_ONLY>
   __device__ __forceinline__ void store(bf16_t* lds, int tid) const {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       int c = tid + 256 * i, row = c >> 3, c16 = c & 7;
-      *reinterpret_cast<u32x4*>(lds + img_chunk16<TR_ONLY>(row, c16)) = v[i];
+      *reinterpret_cast<u32x4*>(lds + img16(row, c16)) = v[i];
     }
   }
 };
 
-// MFMA operand from rows [rb, rb+16) of a k-contiguous image, k-step ks (d 32ks..32ks+31)
+// MFMA operand from rows [rb, rb+16) of an image, k-step ks (d 32ks..32ks+31)
 __device__ __forceinline__ bf16x8 frag_rows(const bf16_t* lds, int rb, int ks, int lane) {
   int row = rb + (lane & 15);
   int c16 = ks * 4 + (lane >> 4);
-  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + img_k(row, c16)));
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + img16(row, c16)));
 }
 
 // MFMA A operand A[m = d][k = row]: d = db + (lane&15); elements 0..3 = rows base0+0..3,
 // elements 4..7 = rows base1+0..3 (base0/base1 already include the lane group's offset)
-template <bool TR_ONLY>
 __device__ __forceinline__ bf16x8 frag_tr(const bf16_t* lds, int base0, int base1, int db, int lane) {
   int i = lane & 15, q = i >> 2, p = i & 3;
   int c8 = (db >> 2) + p;
-  s16x4 lo = lds_read_tr16(lds + img_chunk8<TR_ONLY>(base0 + q, c8));
-  s16x4 hi = lds_read_tr16(lds + img_chunk8<TR_ONLY>(base1 + q, c8));
+  s16x4 lo = lds_read_tr16(lds + img8(base0 + q, c8));
+  s16x4 hi = lds_read_tr16(lds + img8(base1 + q, c8));
   return join_bf16x8(lo, hi);
 }
 
@@ -122,13 +117,73 @@ __device__ __forceinline__ void store_row_T(bf16_t* rowp, const f32x4 (&acc)[4],
 }
 
 // ============================================================================ forward
+struct FwdState {
+  f32x4 o[4];
+  float m, l;
+};
+
+template <bool MASK>
+__device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const bf16_t* Kt, const bf16_t* Vt,
+                                         const bf16x8 (&qf)[2], int kbase, int qrow, int lane) {
+  const int g = lane >> 4;
+  f32x4 s[4];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    s[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) s[jt] = mfma16x16x32(frag_rows(Kt, 16 * jt, ks, lane), qf[ks], s[jt]);
+  }
+  if constexpr (MASK) {
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int key = kbase + 16 * jt + 4 * g + r;
+        bool masked = key >= a.Sk || (a.causal && key > qrow + a.q_offset);
+        s[jt][r] = masked ? -INFINITY : s[jt][r];
+      }
+  }
+  float tmax = fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3]));
+#pragma unroll
+  for (int jt = 1; jt < 4; ++jt)
+    tmax = fmaxf(tmax, fmaxf(fmaxf(s[jt][0], s[jt][1]), fmaxf(s[jt][2], s[jt][3])));
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+  // scores are compared raw (scale > 0 preserves order); the scale is applied in one FMA below
+  const float m_new = fmaxf(st.m, tmax * a.scale_log2);
+  float m_use = m_new;
+  if constexpr (MASK) m_use = m_new == -INFINITY ? 0.f : m_new;  // row fully masked so far: p = 0
+  const float alpha = fast_exp2(st.m - m_use);
+  float psum = 0.f;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pv = fast_exp2(fmaf(s[jt][r], a.scale_log2, -m_use));
+      s[jt][r] = pv;
+      psum += pv;
+    }
+  st.l = st.l * alpha + psum;
+  st.m = m_new;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) st.o[dt] *= alpha;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    bf16x8 pb = frag_acc(s[2 * s2], s[2 * s2 + 1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x8 va = frag_tr(Vt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+      st.o[dt] = mfma16x16x32(va, pb, st.o[dt]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
-#define Ks(i) (smem + (i) * BLK * D)
-#define Vs(i) (smem + (2 + (i)) * BLK * D)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int qrow = qb * BLK + wave * 16 + (lane & 15);
+  const int qrow0 = qb * BLK + wave * 16;
+  const int qrow = qrow0 + (lane & 15);
   const bool qok = qrow < a.Sq;
 
   const bf16_t* qp = a.q + b * a.q_sb + (long)qrow * a.q_ss + h * a.q_sh;
@@ -140,17 +195,18 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   if (a.causal) kend = min(a.Sk, a.q_offset + (qb + 1) * BLK);
   const int nkt = (kend + BLK - 1) / BLK;
 
-  f32x4 o[4];
+  FwdState st;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int i = 0; i < 4; ++i) st.o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  st.m = -INFINITY;
+  st.l = 0.f;
 
   TileRegs tk, tv;
   if (nkt > 0) {
     tk.load(kb, a.k_ss, 0, a.Sk, tid);
     tv.load(vb, a.v_ss, 0, a.Sk, tid);
-    tk.store<false>(Ks(0), tid);
-    tv.store<true>(Vs(0), tid);
+    tk.store(smem, tid);
+    tv.store(smem + 2 * BLK * D, tid);
   }
   __syncthreads();
 
@@ -161,73 +217,32 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       tk.load(kb, a.k_ss, (kt + 1) * BLK, a.Sk, tid);
       tv.load(vb, a.v_ss, (kt + 1) * BLK, a.Sk, tid);
     }
-    // S^T = K Q^T : rows = keys (16jt + 4g + r), col = this lane's query
-    f32x4 s[4];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      s[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) s[jt] = mfma16x16x32(frag_rows(Ks(cur), 16 * jt, ks, lane), qf[ks], s[jt]);
-    }
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int key = kt * BLK + 16 * jt + 4 * g + r;
-        float x = s[jt][r] * a.scale_log2;
-        bool masked = key >= a.Sk || (a.causal && key > qrow + a.q_offset);
-        x = masked ? -INFINITY : x;
-        s[jt][r] = x;
-        tmax = fmaxf(tmax, x);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m, tmax);
-    const bool dead = m_new == -INFINITY;
-    const float alpha = dead ? 1.f : exp2f(m - m_new);
-    float psum = 0.f;
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float pv = dead ? 0.f : exp2f(s[jt][r] - m_new);
-        s[jt][r] = pv;
-        psum += pv;
-      }
-    l = l * alpha + psum;
-    m = m_new;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-    // O^T += V^T P^T
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 pb = frag_acc(s[2 * s2], s[2 * s2 + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        bf16x8 va = frag_tr<true>(Vs(cur), 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
-        o[dt] = mfma16x16x32(va, pb, o[dt]);
-      }
-    }
+    const bf16_t* Kt = smem + cur * BLK * D;
+    const bf16_t* Vt = smem + (2 + cur) * BLK * D;
+    const int kbase = kt * BLK;
+    // wave-uniform: does any key of this tile need masking for any of this wave's queries?
+    const bool need_mask = kbase + BLK > a.Sk || (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
+    if (need_mask) fwd_tile<true>(a, st, Kt, Vt, qf, kbase, qrow, lane);
+    else fwd_tile<false>(a, st, Kt, Vt, qf, kbase, qrow, lane);
     if (more) {
-      tk.store<false>(Ks(cur ^ 1), tid);
-      tv.store<true>(Vs(cur ^ 1), tid);
+      tk.store(smem + (cur ^ 1) * BLK * D, tid);
+      tv.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
     }
     __syncthreads();
   }
-  float lt = l;
+  float lt = st.l;
   lt += __shfl_xor(lt, 16, 64);
   lt += __shfl_xor(lt, 32, 64);
   if (qok) {
     const float inv = lt > 0.f ? 1.f / lt : 0.f;
     bf16_t* op = a.out + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
-    store_row_T(op, o, inv, lane);
-    if (g == 0 && a.lse) a.lse[((long)b * a.H + h) * a.Sq + qrow] = lt > 0.f ? m + log2f(lt) : INFINITY;
+    store_row_T(op, st.o, inv, lane);
+    if ((lane >> 4) == 0 && a.lse) a.lse[((long)b * a.H + h) * a.Sq + qrow] = lt > 0.f ? st.m + __log2f(lt) : INFINITY;
   }
 }
 
 // ============================================================================ backward
-// delta[q] = sum_d dO[q][d] * O[q][d]   (one wave handles 64 rows, one lane per row)
+// delta[q] = sum_d dO[q][d] * O[q][d]   (one lane per row)
 __global__ void attn_bwd_delta_kernel(AttnArgs a) {
   const int b = blockIdx.z, h = blockIdx.y;
   const int q = blockIdx.x * 256 + threadIdx.x;
@@ -248,14 +263,77 @@ __global__ void attn_bwd_delta_kernel(AttnArgs a) {
   const_cast<float*>(a.delta)[((long)b * a.H + h) * a.Sq + q] = s;
 }
 
+// per-lane row constants of one 64-query block: lse/delta for queries q0 + 16t + 4g + r
+struct RowConst {
+  f32x4 lse[4], dl[4];
+  __device__ __forceinline__ void load(const float* __restrict__ lse_row, const float* __restrict__ dl_row, int q0,
+                                       int Sq, int g, bool vec) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      int q = q0 + 16 * t + 4 * g;
+      if (vec && q + 4 <= Sq) {
+        lse[t] = *reinterpret_cast<const f32x4*>(lse_row + q);
+        dl[t] = *reinterpret_cast<const f32x4*>(dl_row + q);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          lse[t][r] = q + r < Sq ? lse_row[q + r] : INFINITY;
+          dl[t][r] = q + r < Sq ? dl_row[q + r] : 0.f;
+        }
+      }
+    }
+  }
+};
+
+template <bool MASK>
+__device__ __forceinline__ void dkv_tile(const AttnArgs& a, const bf16_t* Qt, const bf16_t* Ot, const RowConst& rc,
+                                         const bf16x8 (&kf)[2], const bf16x8 (&vf)[2], f32x4 (&dk)[4],
+                                         f32x4 (&dv)[4], int q0, int key, int lane) {
+  const int g = lane >> 4;
+  // S = Q K^T (rows = queries 16t + 4g + r, col = this lane's key); P; dP = dO V^T; dS
+  f32x4 p[4], ds[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      s = mfma16x16x32(frag_rows(Qt, 16 * t, ks, lane), kf[ks], s);
+      dp = mfma16x16x32(frag_rows(Ot, 16 * t, ks, lane), vf[ks], dp);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pv = fast_exp2(fmaf(s[r], a.scale_log2, -rc.lse[t][r]));
+      if constexpr (MASK) {
+        int q = q0 + 16 * t + 4 * g + r;
+        bool ok = q < a.Sq && key < a.Sk && !(a.causal && key > q + a.q_offset);
+        pv = ok ? pv : 0.f;
+      }
+      p[t][r] = pv;
+      ds[t][r] = pv * (dp[r] - rc.dl[t][r]);
+    }
+  }
+  // dV^T += dO^T P ; dK^T += Q^T dS   (k = queries)
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    bf16x8 pb = frag_acc(p[2 * s2], p[2 * s2 + 1]);
+    bf16x8 sb = frag_acc(ds[2 * s2], ds[2 * s2 + 1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x8 oa = frag_tr(Ot, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+      dv[dt] = mfma16x16x32(oa, pb, dv[dt]);
+      bf16x8 qa = frag_tr(Qt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+      dk[dt] = mfma16x16x32(qa, sb, dk[dt]);
+    }
+  }
+}
+
 // dK, dV for one 64-key block (each wave: 16 keys), sweeping all query blocks
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
-#define Qs(i) (smem + (i) * BLK * D)
-#define Os(i) (smem + (2 + (i)) * BLK * D)  // dO tiles
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int kblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int key = kblk * BLK + wave * 16 + (lane & 15);
+  const int key0 = kblk * BLK + wave * 16;
+  const int key = key0 + (lane & 15);
   const bool kok = key < a.Sk;
   const bf16_t* kp = a.k + b * a.k_sb + (long)key * a.k_ss + h * a.k_sh;
   const bf16_t* vp = a.v + b * a.v_sb + (long)key * a.v_ss + h * a.v_sh;
@@ -265,6 +343,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   const bf16_t* ob = a.dout + b * a.do_sb + h * a.do_sh;
   const float* lse = a.lse + ((long)b * a.H + h) * a.Sq;
   const float* delta = a.delta + ((long)b * a.H + h) * a.Sq;
+  const bool vec = (a.Sq % 4) == 0;
 
   int qstart = 0;
   if (a.causal) qstart = max(0, (kblk * BLK - a.q_offset) / BLK * BLK);
@@ -277,11 +356,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   TileRegs tq, tdo;
+  RowConst rc;
   if (nqt > 0) {
     tq.load(qb, a.q_ss, qstart, a.Sq, tid);
     tdo.load(ob, a.do_ss, qstart, a.Sq, tid);
-    tq.store<false>(Qs(0), tid);
-    tdo.store<false>(Os(0), tid);
+    rc.load(lse, delta, qstart, a.Sq, g, vec);
+    tq.store(smem, tid);
+    tdo.store(smem + 2 * BLK * D, tid);
   }
   __syncthreads();
   for (int it = 0; it < nqt; ++it) {
@@ -292,42 +373,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
       tq.load(qb, a.q_ss, q0 + BLK, a.Sq, tid);
       tdo.load(ob, a.do_ss, q0 + BLK, a.Sq, tid);
     }
-    // S = Q K^T (rows = queries 16t + 4g + r, col = this lane's key); P; dP = dO V^T; dS
-    f32x4 p[4], ds[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        s = mfma16x16x32(frag_rows(Qs(cur), 16 * t, ks, lane), kf[ks], s);
-        dp = mfma16x16x32(frag_rows(Os(cur), 16 * t, ks, lane), vf[ks], dp);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int q = q0 + 16 * t + 4 * g + r;
-        bool ok = q < a.Sq && kok && !(a.causal && key > q + a.q_offset);
-        float pv = ok ? exp2f(s[r] * a.scale_log2 - lse[q]) : 0.f;
-        float dl = ok ? delta[q] : 0.f;
-        p[t][r] = pv;
-        ds[t][r] = pv * (dp[r] - dl);
-      }
-    }
-    // dV^T += dO^T P ; dK^T += Q^T dS   (k = queries)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 pb = frag_acc(p[2 * s2], p[2 * s2 + 1]);
-      bf16x8 sb = frag_acc(ds[2 * s2], ds[2 * s2 + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        bf16x8 oa = frag_tr<false>(Os(cur), 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
-        dv[dt] = mfma16x16x32(oa, pb, dv[dt]);
-        bf16x8 qa = frag_tr<false>(Qs(cur), 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
-        dk[dt] = mfma16x16x32(qa, sb, dk[dt]);
-      }
-    }
+    const bf16_t* Qt = smem + cur * BLK * D;
+    const bf16_t* Ot = smem + (2 + cur) * BLK * D;
+    const bool need_mask = q0 + BLK > a.Sq || key0 + 16 > a.Sk ||
+                           (a.causal && key0 + 15 > q0 + a.q_offset);
+    if (need_mask) dkv_tile<true>(a, Qt, Ot, rc, kf, vf, dk, dv, q0, key, lane);
+    else dkv_tile<false>(a, Qt, Ot, rc, kf, vf, dk, dv, q0, key, lane);
     if (more) {
-      tq.store<false>(Qs(cur ^ 1), tid);
-      tdo.store<false>(Os(cur ^ 1), tid);
+      rc.load(lse, delta, q0 + BLK, a.Sq, g, vec);
+      tq.store(smem + (cur ^ 1) * BLK * D, tid);
+      tdo.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
     }
     __syncthreads();
   }
@@ -337,20 +392,56 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
+template <bool MASK>
+__device__ __forceinline__ void dq_tile(const AttnArgs& a, const bf16_t* Kt, const bf16_t* Vt, const bf16x8 (&qf)[2],
+                                        const bf16x8 (&df)[2], float lse_q, float dl_q, f32x4 (&dq)[4], int kbase,
+                                        int qrow, int lane) {
+  const int g = lane >> 4;
+  f32x4 ds[4];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      s = mfma16x16x32(frag_rows(Kt, 16 * jt, ks, lane), qf[ks], s);
+      dp = mfma16x16x32(frag_rows(Vt, 16 * jt, ks, lane), df[ks], dp);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pv = fast_exp2(fmaf(s[r], a.scale_log2, -lse_q));
+      if constexpr (MASK) {
+        int key = kbase + 16 * jt + 4 * g + r;
+        bool ok = qrow < a.Sq && key < a.Sk && !(a.causal && key > qrow + a.q_offset);
+        pv = ok ? pv : 0.f;
+      }
+      ds[jt][r] = pv * (dp[r] - dl_q);
+    }
+  }
+  // dQ^T += K^T dS^T   (k = keys)
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    bf16x8 sb = frag_acc(ds[2 * s2], ds[2 * s2 + 1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x8 ka = frag_tr(Kt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+      dq[dt] = mfma16x16x32(ka, sb, dq[dt]);
+    }
+  }
+}
+
 // dQ for one 64-query block (each wave: 16 queries), sweeping key blocks
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
-#define Ks(i) (smem + (i) * BLK * D)
-#define Vs(i) (smem + (2 + (i)) * BLK * D)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int qrow = qb * BLK + wave * 16 + (lane & 15);
+  const int qrow0 = qb * BLK + wave * 16;
+  const int qrow = qrow0 + (lane & 15);
   const bool qok = qrow < a.Sq;
   const bf16_t* qp = a.q + b * a.q_sb + (long)qrow * a.q_ss + h * a.q_sh;
   const bf16_t* dop = a.dout + b * a.do_sb + (long)qrow * a.do_ss + h * a.do_sh;
   bf16x8 qf[2] = {load_row_frag(qp, qok, 0, lane), load_row_frag(qp, qok, 1, lane)};
   bf16x8 df[2] = {load_row_frag(dop, qok, 0, lane), load_row_frag(dop, qok, 1, lane)};
-  const float lse_q = qok ? a.lse[((long)b * a.H + h) * a.Sq + qrow] : 0.f;
+  const float lse_q = qok ? a.lse[((long)b * a.H + h) * a.Sq + qrow] : INFINITY;
   const float dl_q = qok ? a.delta[((long)b * a.H + h) * a.Sq + qrow] : 0.f;
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
@@ -365,8 +456,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   if (nkt > 0) {
     tk.load(kb, a.k_ss, 0, a.Sk, tid);
     tv.load(vb, a.v_ss, 0, a.Sk, tid);
-    tk.store<false>(Ks(0), tid);
-    tv.store<false>(Vs(0), tid);
+    tk.store(smem, tid);
+    tv.store(smem + 2 * BLK * D, tid);
   }
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
@@ -376,46 +467,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
       tk.load(kb, a.k_ss, (kt + 1) * BLK, a.Sk, tid);
       tv.load(vb, a.v_ss, (kt + 1) * BLK, a.Sk, tid);
     }
-    f32x4 ds[4];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        s = mfma16x16x32(frag_rows(Ks(cur), 16 * jt, ks, lane), qf[ks], s);
-        dp = mfma16x16x32(frag_rows(Vs(cur), 16 * jt, ks, lane), df[ks], dp);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int key = kt * BLK + 16 * jt + 4 * g + r;
-        bool ok = qok && key < a.Sk && !(a.causal && key > qrow + a.q_offset);
-        float pv = ok ? exp2f(s[r] * a.scale_log2 - lse_q) : 0.f;
-        ds[jt][r] = pv * (dp[r] - dl_q);
-      }
-    }
-    // dQ^T += K^T dS^T   (k = keys)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 sb = frag_acc(ds[2 * s2], ds[2 * s2 + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        bf16x8 ka = frag_tr<false>(Ks(cur), 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
-        dq[dt] = mfma16x16x32(ka, sb, dq[dt]);
-      }
-    }
+    const bf16_t* Kt = smem + cur * BLK * D;
+    const bf16_t* Vt = smem + (2 + cur) * BLK * D;
+    const int kbase = kt * BLK;
+    const bool need_mask = kbase + BLK > a.Sk || qrow0 + 16 > a.Sq ||
+                           (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
+    if (need_mask) dq_tile<true>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow, lane);
+    else dq_tile<false>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow, lane);
     if (more) {
-      tk.store<false>(Ks(cur ^ 1), tid);
-      tv.store<false>(Vs(cur ^ 1), tid);
+      tk.store(smem + (cur ^ 1) * BLK * D, tid);
+      tv.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
     }
     __syncthreads();
   }
   if (qok) store_row_T(a.out + b * a.out_sb + (long)qrow * a.out_ss + h * a.out_sh, dq, a.scale, lane);
 }
 
-#undef Ks
-#undef Vs
-#undef Qs
-#undef Os
 }  // namespace
 
 // strides are in elements, ordered (batch, seq, head); head_dim must be 64 and contiguous.
@@ -456,12 +523,10 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
   a.scale = scale; a.scale_log2 = scale * LOG2E;
   a.causal = causal; a.q_offset = q_offset;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((Sq + 255) / 256, H, B), dim3(256), 0, stream, a);
-  // dK, dV
   AttnArgs b = a;
   b.out = (bf16_t*)dk; b.out_sb = dks[0]; b.out_ss = dks[1]; b.out_sh = dks[2];
   b.out2 = (bf16_t*)dv; b.out2_sb = dvs[0]; b.out2_ss = dvs[1]; b.out2_sh = dvs[2];
   hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((Sk + BLK - 1) / BLK, H, B), dim3(256), 0, stream, b);
-  // dQ
   AttnArgs c = a;
   c.out = (bf16_t*)dq; c.out_sb = dqs[0]; c.out_ss = dqs[1]; c.out_sh = dqs[2];
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Sq + BLK - 1) / BLK, H, B), dim3(256), 0, stream, c);
