@@ -70,6 +70,11 @@ def build_lib(name: str, sub: str, extra_link=(), force: bool = False, verbose: 
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed for {out}:\n{r.stderr}")
+    # a kernel whose host launch stub was not emitted links fine but fails at dlopen: catch it here
+    nm = subprocess.run(["nm", "-D", "--undefined-only", out], capture_output=True, text=True)
+    missing = [l for l in nm.stdout.splitlines() if "__device_stub__" in l]
+    if missing:
+        raise RuntimeError(f"{out}: undefined kernel stubs (add explicit instantiations):\n" + "\n".join(missing))
     with open(stamp, "w") as f:
         f.write(dig)
     if verbose:

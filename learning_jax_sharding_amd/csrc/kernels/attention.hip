@@ -242,27 +242,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 }
 
 // ============================================================================ backward
-// delta[q] = sum_d dO[q][d] * O[q][d]   (one lane per row)
-__global__ void attn_bwd_delta_kernel(AttnArgs a) {
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= a.Sq) return;
-  const bf16_t* op = a.o + b * a.o_sb + (long)q * a.o_ss + h * a.o_sh;
-  const bf16_t* dp = a.dout + b * a.do_sb + (long)q * a.do_ss + h * a.do_sh;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    u32x4 x = *reinterpret_cast<const u32x4*>(op + 8 * c);
-    u32x4 y = *reinterpret_cast<const u32x4*>(dp + 8 * c);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      s += __uint_as_float(x[k] << 16) * __uint_as_float(y[k] << 16);
-      s += __uint_as_float(x[k] & 0xffff0000u) * __uint_as_float(y[k] & 0xffff0000u);
-    }
-  }
-  const_cast<float*>(a.delta)[((long)b * a.H + h) * a.Sq + q] = s;
-}
-
 // per-lane row constants of one 64-query block: lse/delta for queries q0 + 16t + 4g + r
 struct RowConst {
   f32x4 lse[4], dl[4];
@@ -442,7 +421,27 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   bf16x8 qf[2] = {load_row_frag(qp, qok, 0, lane), load_row_frag(qp, qok, 1, lane)};
   bf16x8 df[2] = {load_row_frag(dop, qok, 0, lane), load_row_frag(dop, qok, 1, lane)};
   const float lse_q = qok ? a.lse[((long)b * a.H + h) * a.Sq + qrow] : INFINITY;
-  const float dl_q = qok ? a.delta[((long)b * a.H + h) * a.Sq + qrow] : 0.f;
+  // delta[q] = sum_d dO[q][d] O[q][d] from the dO fragments already in registers (the 4 lane
+  // groups hold d-chunks 8g..8g+7 and 32+8g..): no separate kernel; published for dK/dV.
+  float dl_q;
+  {
+    const bf16_t* op = a.o + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const u32x4 x = __builtin_bit_cast(u32x4, load_row_frag(op, qok, ks, lane));
+      const u32x4 y = __builtin_bit_cast(u32x4, df[ks]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s = fmaf(__uint_as_float(x[k] << 16), __uint_as_float(y[k] << 16), s);
+        s = fmaf(__uint_as_float(x[k] & 0xffff0000u), __uint_as_float(y[k] & 0xffff0000u), s);
+      }
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    dl_q = s;
+    if (qok && (lane >> 4) == 0) const_cast<float*>(a.delta)[((long)b * a.H + h) * a.Sq + qrow] = s;
+  }
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
   int kend = a.Sk;
@@ -522,13 +521,13 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
   a.Sq = Sq; a.Sk = Sk; a.H = H;
   a.scale = scale; a.scale_log2 = scale * LOG2E;
   a.causal = causal; a.q_offset = q_offset;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((Sq + 255) / 256, H, B), dim3(256), 0, stream, a);
+  // dQ first: it also computes delta, which the dK/dV kernel consumes (stream order)
+  AttnArgs c = a;
+  c.out = (bf16_t*)dq; c.out_sb = dqs[0]; c.out_ss = dqs[1]; c.out_sh = dqs[2];
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Sq + BLK - 1) / BLK, H, B), dim3(256), 0, stream, c);
   AttnArgs b = a;
   b.out = (bf16_t*)dk; b.out_sb = dks[0]; b.out_ss = dks[1]; b.out_sh = dks[2];
   b.out2 = (bf16_t*)dv; b.out2_sb = dvs[0]; b.out2_ss = dvs[1]; b.out2_sh = dvs[2];
   hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((Sk + BLK - 1) / BLK, H, B), dim3(256), 0, stream, b);
-  AttnArgs c = a;
-  c.out = (bf16_t*)dq; c.out_sb = dqs[0]; c.out_ss = dqs[1]; c.out_sh = dqs[2];
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Sq + BLK - 1) / BLK, H, B), dim3(256), 0, stream, c);
   return (int)hipGetLastError();
 }

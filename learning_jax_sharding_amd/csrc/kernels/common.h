@@ -61,6 +61,27 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + idx;
 }
 
+// ---- in-launch "last arriver" hand-off (cdna_hip_programming.md §6 Guideline 16, valid form:
+// write-through (sc1) payload stores by ONE wave, that wave's vmcnt(0), one lane's agent-scope
+// atomic ticket add; the block whose add returns n-1 reads every payload with sc1 loads and
+// re-arms the ticket).  Tickets live in a persistent workspace zeroed once at allocation.
+__device__ __forceinline__ void sc1_store(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float sc1_load(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// returns true in exactly one block (the last of `n` arrivals); call from ONE lane after the
+// storing wave's `s_waitcnt vmcnt(0)`
+__device__ __forceinline__ bool ticket_last(unsigned* ticket, unsigned n) {
+  unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == n - 1) {
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  return false;
+}
+
 __device__ __forceinline__ float warp_max64(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;

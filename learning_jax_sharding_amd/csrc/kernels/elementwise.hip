@@ -124,6 +124,127 @@ __global__ void sum_all_vec_kernel(const T* __restrict__ in, long n, float* __re
   }
 }
 
+// Whole-array sum with the in-launch last-arriver reduction: no memset, no second kernel, and
+// the result is written directly in the output dtype (f32 or bf16).
+template <typename T>
+__global__ void sum_all_ticket_kernel(const T* __restrict__ in, long n, float* __restrict__ partials,
+                                      unsigned* __restrict__ ticket, void* __restrict__ out, int out_bf16) {
+  constexpr int V = 16 / sizeof(T);
+  constexpr int U = 4;  // independent 16-byte loads in flight per thread
+  float s = 0.f;
+  const long nv = n / V;
+  const long stride = (long)gridDim.x * blockDim.x;
+  auto acc = [&](const u32x4& v) {
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += __uint_as_float(v[k] << 16) + __uint_as_float(v[k] & 0xffff0000u);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += __uint_as_float(v[k]);
+    }
+  };
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < nv; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(in + (i + u * stride) * V);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc(v[u]);
+  }
+  for (; i < nv; i += stride) acc(*reinterpret_cast<const u32x4*>(in + i * V));
+  if (blockIdx.x == 0)
+    for (long j = nv * V + threadIdx.x; j < n; j += blockDim.x) s += ldv<T>(in, j);
+  s = warp_sum64(s);
+  __shared__ float part[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) part[w] = s;
+  __syncthreads();
+  if (w == 0) {
+    if (lane == 0) {
+      float t = 0.f;
+      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += part[k];
+      sc1_store(partials + blockIdx.x, t);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) last = ticket_last(ticket, gridDim.x);
+    last = __shfl(last, 0, 64);
+    if (last) {
+      float v = 0.f;
+      for (int i = lane; i < (int)gridDim.x; i += 64) v += sc1_load(partials + i);
+      v = warp_sum64(v);
+      if (lane == 0) {
+        if (out_bf16) *reinterpret_cast<bf16_t*>(out) = f2bf(v);
+        else *reinterpret_cast<float*>(out) = v;
+      }
+    }
+  }
+}
+
+// column sums of a bf16 [R][C] matrix, partial slabs + last-arriver per column block (no memset)
+__global__ void colsum_ticket_kernel(const bf16_t* __restrict__ in, int R, int C, long ld, int rows_per_block,
+                                     float* __restrict__ partials, unsigned* __restrict__ tickets,
+                                     float* __restrict__ out, int accumulate) {
+  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * 64 + cl * 8;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(R, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto add = [&](const u32x4& v) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[2 * k] += __uint_as_float(v[k] << 16);
+      acc[2 * k + 1] += __uint_as_float(v[k] & 0xffff0000u);
+    }
+  };
+  if (c0 < C) {
+    int r = r0 + rl;
+    for (; r + 96 < r1; r += 128) {  // 4 independent row loads in flight
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(in + (long)(r + 32 * u) * ld + c0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(v[u]);
+    }
+    for (; r < r1; r += 32) add(*reinterpret_cast<const u32x4*>(in + (long)r * ld + c0));
+  }
+  __shared__ float red[32][65];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rl][cl * 8 + k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    float s = 0.f;
+    for (int r = 0; r < 32; ++r) s += red[r][lane];
+    const int c = blockIdx.x * 64 + lane;
+    if (c < C) sc1_store(partials + (long)blockIdx.y * C + c, s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) last = ticket_last(tickets + blockIdx.x, gridDim.y);
+    last = __shfl(last, 0, 64);
+    if (last && c < C) {
+      float v = 0.f;
+      for (int y = 0; y < (int)gridDim.y; ++y) v += sc1_load(partials + (long)y * C + c);
+      out[c] = accumulate ? out[c] + v : v;
+    }
+  }
+}
+
+// column sums of a matrix whose R rows are all the same row (row stride 0)
+__global__ void colsum_bcast_kernel(const void* __restrict__ in, int is_bf16, int R, int C, float* __restrict__ out,
+                                    int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float v = is_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(in)[c]) : reinterpret_cast<const float*>(in)[c];
+  out[c] = (accumulate ? out[c] : 0.f) + v * (float)R;
+}
+
+// out[0..n) = (bf16) *g: materialises the broadcast row of a scalar cotangent (e.g. of y.sum())
+__global__ void fill_row_kernel(const void* __restrict__ g, int g_bf16, bf16_t* __restrict__ out, long n) {
+  const float v = g_bf16 ? bf2f(*reinterpret_cast<const bf16_t*>(g)) : *reinterpret_cast<const float*>(g);
+  const bf16_t b = f2bf(v);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) out[i] = b;
+}
+
 // column sums of a bf16 [R][C] matrix (C % 8 == 0, row stride ld; ld may be 0 = broadcast row):
 // block = 8 column-lanes (16 B each, 64 columns) x 32 row-lanes; LDS reduction, one atomic per column.
 __global__ void colsum_vec_kernel(const bf16_t* __restrict__ in, int R, int C, long ld, int rows_per_block,
@@ -243,8 +364,11 @@ struct AdamBatch {
   int n;
 };
 
-__global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, const int* __restrict__ step, float lr,
-                                                         float b1, float b2, float eps, float wd) {
+// `step_offset`/`ticket`: with a ticket the kernel uses t = *step + step_offset and its last
+// arriving block stores *step + 1 (the optimizer's count increment, folded in: no extra launch).
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* __restrict__ step, int step_offset,
+                                                         unsigned* __restrict__ ticket, float lr, float b1, float b2,
+                                                         float eps, float wd) {
   __shared__ float tr[64][65];
   const int id = blockIdx.x;
   int ti = 0;
@@ -252,7 +376,8 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, const 
   const AdamTensor T = batch.t[ti];
   const int local = id - batch.tile_start[ti];
   const int tr_i = local / (int)T.tiles_c, tc_i = local % (int)T.tiles_c;
-  const float t = (float)(*step);
+  const int s0 = *step;
+  const float t = (float)(s0 + step_offset);
   const float inv_bc1 = 1.f / (1.f - powf(b1, t)), inv_sqrt_bc2 = rsqrtf(1.f - powf(b2, t));
   float* P = reinterpret_cast<float*>(T.p);
   float* Mm = reinterpret_cast<float*>(T.m);
@@ -285,6 +410,12 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, const 
       const int cl = ty + 4 * rr, c = orow0 + cl;
       if (c < T.C && ocol < T.R) reinterpret_cast<bf16_t*>(T.st)[(long)c * T.R + ocol] = f2bf(tr[tx][cl]);
     }
+  }
+  if (ticket) {
+    // every thread of this block has consumed its read of *step before the ticket is drawn
+    __syncthreads();
+    if (threadIdx.x == 0 && ticket_last(ticket, gridDim.x))
+      __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -363,20 +494,26 @@ LJS_API int ljs_cast_transpose_f32_bf16(const void* in, void* out, int R, int C,
   return (int)hipGetLastError();
 }
 
-// out (f32 scalar) = sum(in); in is f32 (is_bf16=0) or bf16
-LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, hipStream_t s) {
-  (void)hipMemsetAsync(out, 0, sizeof(float), s);
+// out (scalar, f32 or bf16 per out_bf16) = sum(in); in is f32 (is_bf16=0) or bf16.
+// ws: persistent workspace of >= 257 floats whose last word (the ticket) is zero at rest.
+LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, int out_bf16, void* ws, hipStream_t s) {
+  float* partials = (float*)ws;
+  unsigned* ticket = (unsigned*)ws + 256;
   const bool aligned = (((uintptr_t)in) & 15) == 0;
   if (aligned) {
     long per = 256L * (is_bf16 ? 8 : 4) * 4;  // ~4 vector loads per thread
     int g = grid_for(n, (int)per);
-    if (g > 256) g = 256;  // one block per CU: bounds the same-address atomics to 256
+    if (g > 256) g = 256;
     if (is_bf16)
-      hipLaunchKernelGGL(sum_all_vec_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, (float*)out);
+      hipLaunchKernelGGL(sum_all_ticket_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, partials,
+                         ticket, out, out_bf16);
     else
-      hipLaunchKernelGGL(sum_all_vec_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)in, n, (float*)out);
+      hipLaunchKernelGGL(sum_all_ticket_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)in, n, partials,
+                         ticket, out, out_bf16);
     return (int)hipGetLastError();
   }
+  if (out_bf16) return (int)hipErrorInvalidValue;
+  (void)hipMemsetAsync(out, 0, sizeof(float), s);
   int g = grid_for(n, 256 * 16);
   if (is_bf16)
     hipLaunchKernelGGL(sum_all_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, (float*)out);
@@ -386,8 +523,17 @@ LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, hipStrea
 }
 
 // out[C] f32 = column sums of in[R][C]; accumulate=1 adds into out
-LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void* out, int accumulate, hipStream_t s) {
-  if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * C, s);
+// ws (may be null): persistent workspace, >= kColsumWsFloats floats, tickets zero at rest; with it
+// the bf16 vector path needs no memset (per-column-block last-arriver combine).
+constexpr long kColsumWsFloats = 1L << 20;
+LJS_API long ljs_colsum_ws_floats() { return kColsumWsFloats; }
+LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void* out, int accumulate, void* ws,
+                       hipStream_t s) {
+  if (ld == 0) {  // one repeated row: out = R * row
+    hipLaunchKernelGGL(colsum_bcast_kernel, dim3((C + 255) / 256), dim3(256), 0, s, in, is_bf16, R, C, (float*)out,
+                       accumulate);
+    return (int)hipGetLastError();
+  }
   if (is_bf16 && C % 8 == 0 && ld % 8 == 0 && (((uintptr_t)in) & 15) == 0) {
     int cb = (C + 63) / 64;
     int want = 512 / cb;
@@ -395,10 +541,18 @@ LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void*
     int rpb = (R + gy - 1) / gy;
     if (rpb < 32) rpb = 32;
     gy = (R + rpb - 1) / rpb;
+    // workspace layout: [tickets: 4096 words][partials: gy * C floats]
+    if (ws && cb <= 4096 && (long)gy * C + 4096 <= kColsumWsFloats) {
+      hipLaunchKernelGGL(colsum_ticket_kernel, dim3(cb, gy), dim3(256), 0, s, (const bf16_t*)in, R, C, ld, rpb,
+                         (float*)ws + 4096, (unsigned*)ws, (float*)out, accumulate);
+      return (int)hipGetLastError();
+    }
+    if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * C, s);
     hipLaunchKernelGGL(colsum_vec_kernel, dim3(cb, gy), dim3(256), 0, s, (const bf16_t*)in, R, C, ld, rpb,
                        (float*)out);
     return (int)hipGetLastError();
   }
+  if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * C, s);
   int gy = R / 256;
   if (gy < 1) gy = 1;
   if (gy > 64) gy = 64;
@@ -407,6 +561,13 @@ LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void*
     hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)in, R, C, ld, (float*)out);
   else
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)in, R, C, ld, (float*)out);
+  return (int)hipGetLastError();
+}
+
+LJS_API int ljs_fill_row_bf16(const void* g, int g_bf16, void* out, long n, hipStream_t s) {
+  int grid = grid_for(n, 256);
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(fill_row_kernel, dim3(grid), dim3(256), 0, s, g, g_bf16, (bf16_t*)out, n);
   return (int)hipGetLastError();
 }
 
@@ -458,8 +619,8 @@ LJS_API int ljs_rng_fill(void* out, int is_bf16, int ndim, const long* start, co
 }
 
 // table: n x 10 int64 {p, g, m, v, shadow_t, shadow_n, R, C, g_bf16, unused}; up to 32 per call
-LJS_API int ljs_adam_multi(const long* table, int n, const void* step, float lr, float b1, float b2, float eps,
-                           float wd, hipStream_t s) {
+LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset, void* ticket, float lr, float b1,
+                           float b2, float eps, float wd, hipStream_t s) {
   if (n < 1 || n > kAdamMax) return (int)hipErrorInvalidValue;
   AdamBatch b;
   int tiles = 0;
@@ -474,6 +635,7 @@ LJS_API int ljs_adam_multi(const long* table, int n, const void* step, float lr,
   }
   b.tile_start[n] = tiles;
   b.n = n;
-  hipLaunchKernelGGL(adam_multi_kernel, dim3(tiles), dim3(256), 0, s, b, (const int*)step, lr, b1, b2, eps, wd);
+  hipLaunchKernelGGL(adam_multi_kernel, dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset, (unsigned*)ticket,
+                     lr, b1, b2, eps, wd);
   return (int)hipGetLastError();
 }

@@ -15,6 +15,7 @@
 // the other LDS buffer after; one barrier per K-tile), XOR-swizzled LDS images so both
 // the row reads and the transposed reads are bank-conflict free, XCD-aware tile order.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -259,6 +260,333 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
 #undef As
 #undef Bs
 
+// ============================================================================ LDS-DMA GEMM
+// Persistent, pipelined MFMA GEMM for the large bench shapes.
+//  * Staging by the buffer LDS-DMA (buffer_load_dwordx4 ... lds): global -> LDS with no VGPRs
+//    and no ds_write (the VGPR->LDS transfer, ~79 B/clk/CU, bounds a register-staged loop).
+//    Swizzles are applied on the SOURCE address (the DMA writes a wave's 64 x 16 B
+//    contiguously), so the LDS images are those of the kernel above (conflict-free reads).
+//  * Persistent blocks walk a FLATTENED (work item, K-tile) sequence through an NST-deep LDS
+//    ring with one raw s_barrier per K-tile and a counted vmcnt, so the next item's first
+//    tiles are already in flight while the current item's epilogue runs: no per-tile
+//    prologue bubble (K = 512/640 projections have only 8-10 K-tiles per item).
+//  * The MFMA operands are swapped (C^T = B^T A^T per 16x16 block), so each lane ends with 4
+//    CONSECUTIVE columns of one output row: bf16 results leave as packed 8-byte stores and
+//    f32 as 16-byte stores straight from the accumulators (no LDS round trip).
+//  * Work items are ordered (batch, split, tile-row, tile-col) and dealt XCD-aware, so blocks
+//    sharing an XCD's L2 work on neighbouring tiles (shared operand panels).
+// Edges: rows/cols past M/N read garbage that only reaches discarded outputs; the buffer
+// descriptor's range check turns every out-of-range read into 0 without faulting; K must be a
+// multiple of 64 and the split must divide the K-tiles (checked by the launcher).
+
+// XOR applied to the 16-byte chunk index of k-row `krow` of an m/n-contiguous image (R rows)
+template <int R>
+__device__ __forceinline__ int swz_mn16(int krow) {
+  if constexpr (R == 128) return ((krow & 3) | (((krow >> 3) & 1) << 2)) << 1;
+  else return ((((krow >> 1) & 1)) | (((krow >> 3) & 1) << 1)) << 1;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long bytes) {
+  // readfirstlane the inputs so the compiler can prove the descriptor wave-uniform (no waterfall)
+  const unsigned long long b = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes));
+  void* p = (void*)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, nb, 0x00020000);
+}
+
+// One operand tile (R rows x BK) of one K-tile: its 1 KiB DMA pieces, split over NW waves.
+// Per-lane offsets are relative to (row 0, k 0); the tile origin goes in the scalar offset.
+template <int R, bool KC, int NW>
+struct DmaTile {
+  static constexpr int PIECES = R * BK * 2 / 1024;
+  static constexpr int PER_WAVE = PIECES / NW;
+  static_assert(PIECES % NW == 0, "pieces must split evenly over the waves");
+  int voff[PER_WAVE];
+
+  __device__ __forceinline__ void init(long ld, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int q = wave + NW * i;
+      long e;
+      if constexpr (KC) {
+        const int row = 8 * q + (lane >> 3), slot = lane & 7;
+        e = (long)row * ld + 8 * (slot ^ ((row >> 1) & 7));
+      } else {
+        constexpr int CPR = R / 8;     // 16 B chunks per k-row
+        constexpr int KPP = 64 / CPR;  // k-rows per piece
+        const int krow = KPP * q + lane / CPR, slot = lane % CPR;
+        e = (long)krow * ld + 8 * (slot ^ swz_mn16<R>(krow));
+      }
+      voff[i] = (int)(e * 2);
+    }
+  }
+
+  // soff: byte offset of the tile origin (row r0, k-tile kt), wave-uniform
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, bf16_t* lds, int soff, int wave) const {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_PTR(void))(lds + (wave + NW * i) * 512), 16, voff[i], soff,
+                                               0, 0);
+  }
+};
+
+struct WorkItem {
+  int b, m0, n0, kt0;
+};
+
+__device__ __forceinline__ WorkItem decode_item(const GemmArgs& p, int item, int ntm, int ntn) {
+  WorkItem w;
+  const int tn_i = item % ntn;
+  int r = item / ntn;
+  const int tm_i = r % ntm;
+  r /= ntm;
+  const int split = r % p.splitk;
+  w.b = r / p.splitk;
+  w.m0 = tm_i;
+  w.n0 = tn_i;
+  w.kt0 = split * p.kt_per_split;
+  return w;
+}
+
+template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int A_TILE = BM * BK, B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
+  using TA = DmaTile<BM, A_KC, NW>;
+  using TB = DmaTile<BN, B_KC, NW>;
+  constexpr int L = TA::PER_WAVE + TB::PER_WAVE;  // DMA instructions per wave per K-tile
+  // bf16 output: C^T blocks (operands swapped), lanes pair up into 16-byte row chunks and
+  // leave through exactly S_EPI buffer stores per lane (masked lanes get an out-of-range
+  // offset, so the count is exact and the next K-step's counted vmcnt stays valid).
+  // f32 output (split-K atomics / weight grads): plain orientation, full drain after it.
+  constexpr bool SWAP = !OUT_F32;
+  static_assert(!SWAP || TN % 2 == 0, "column blocks pair up for 16-byte stores");
+  constexpr int S_EPI = TM * TN / 2;
+  static_assert(L * (NST - 1) + S_EPI <= 63, "vmcnt immediate range");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int items = p.batch * p.splitk * ntm * ntn;
+  const int G = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, G);   // same-XCD blocks take neighbouring items
+  const int my_items = slot < items ? (items - slot + G - 1) / G : 0;
+  const int nk = p.kt_per_split;               // K-tiles per item (the split divides them)
+  const int total = my_items * nk;
+
+  const long a_bytes = 2 * (A_KC ? (long)(p.M - 1) * p.lda + p.K : (long)(p.K - 1) * p.lda + p.M);
+  const long b_bytes = 2 * (B_KC ? (long)(p.N - 1) * p.ldb + p.K : (long)(p.K - 1) * p.ldb + p.N);
+  const long a_kt = A_KC ? (long)BK * 2 : (long)BK * p.lda * 2;  // bytes per K-tile step
+  const long b_kt = B_KC ? (long)BK * 2 : (long)BK * p.ldb * 2;
+
+  TA ta;
+  TB tb;
+  ta.init(p.lda, wave, lane);
+  tb.init(p.ldb, wave, lane);
+
+  // issue-side cursor: the item whose K-tiles are being fetched (advanced incrementally)
+  int is_item = 0, is_kt = 0;
+  __amdgpu_buffer_rsrc_t ra, rb;
+  long a_org = 0, b_org = 0;
+  auto load_item = [&](int k) {
+    const WorkItem w = decode_item(p, slot + G * k, ntm, ntn);
+    ra = make_rsrc(p.A + (long)w.b * p.sA, a_bytes);
+    rb = make_rsrc(p.B + (long)w.b * p.sB, b_bytes);
+    a_org = (A_KC ? (long)w.m0 * BM * p.lda : (long)w.m0 * BM) * 2 + w.kt0 * a_kt;
+    b_org = (B_KC ? (long)w.n0 * BN * p.ldb : (long)w.n0 * BN) * 2 + w.kt0 * b_kt;
+  };
+  auto issue_next = [&](int st) {
+    if (is_kt == 0) load_item(is_item);
+    ta.issue(ra, smem + st * STAGE, __builtin_amdgcn_readfirstlane((int)(a_org + is_kt * a_kt)), wave);
+    tb.issue(rb, smem + st * STAGE + A_TILE, __builtin_amdgcn_readfirstlane((int)(b_org + is_kt * b_kt)), wave);
+    if (++is_kt == nk) { is_kt = 0; ++is_item; }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < total) issue_next(s);
+
+  const bool relu = p.flags & 1;
+  const bool has_bias = (p.flags & 2) && p.splitk == 1;
+  const bool bias_f32 = p.flags & 4;
+  const bool accumulate = p.flags & 8;
+  const __amdgpu_buffer_rsrc_t rc =
+      make_rsrc(p.C, (OUT_F32 ? 4 : 2) * ((long)(p.batch - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
+  bool after_epi = false;
+
+  for (int it = 0, f = 0; it < my_items; ++it) {
+  for (int kk = 0; kk < nk; ++kk, ++f) {
+    // step f landed (this wave's pieces); the younger steps (and, right after an epilogue,
+    // its S_EPI stores) may stay in flight
+    const bool tail = f + NST - 2 >= total;
+    if constexpr (NST >= 3) {
+      if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (SWAP && after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2) + S_EPI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");
+    } else {
+      if (SWAP && after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    after_epi = false;
+    // every wave's reads of the stage about to be refilled completed (lgkmcnt) before it
+    // arrives; every wave's pieces of step f are in LDS once all have arrived
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (f + NST - 1 < total) issue_next((f + NST - 1) % NST);
+    const bf16_t* As_ = smem + (f % NST) * STAGE;
+    const bf16_t* Bs_ = As_ + A_TILE;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) af[ii] = frag<BM, A_KC>(As_, wr * (BM / WM) + ii * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, B_KC>(Bs_, wc * (BN / WN) + j * 16, ks, lane);
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (SWAP) acc[ii][j] = mfma16x16x32(bfr[j], af[ii], acc[ii][j]);  // C^T block
+          else acc[ii][j] = mfma16x16x32(af[ii], bfr[j], acc[ii][j]);
+        }
+    }
+  }
+
+    // ------------------------------------------------------------ epilogue of this item
+    const WorkItem w = decode_item(p, slot + G * it, ntm, ntn);
+    const int m0 = w.m0 * BM + wr * (BM / WM), n0 = w.n0 * BN + wc * (BN / WN);
+    const int g = lane >> 4;
+    if constexpr (SWAP) {
+      // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]; lanes g, g^1 trade halves so
+      // even g owns cols 16 j0 + 4 g .. +7 and odd g owns 16 j1 + 4 (g - 1) .. +7
+      const bool even = (g & 1) == 0;
+      float bvs[TN / 2][8];
+#pragma unroll
+      for (int q = 0; q < TN / 2; ++q) {
+        const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          bvs[q][e] = 0.f;
+          if (has_bias && col + e < p.N) {
+            const long bo = (long)w.b * p.sBias + col + e;
+            bvs[q][e] = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo]
+                                 : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo]);
+          }
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) {
+#pragma unroll
+        for (int q = 0; q < TN / 2; ++q) {  // both halves of a row's 128 B back to back
+          const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
+          const float* bv = bvs[q];
+          const f32x4 a0 = acc[ii][2 * q] * p.alpha, a1 = acc[ii][2 * q + 1] * p.alpha;
+          acc[ii][2 * q] = f32x4{0.f, 0.f, 0.f, 0.f};
+          acc[ii][2 * q + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+          const f32x4 keep = even ? a0 : a1, send = even ? a1 : a0;
+          f32x4 recv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) recv[e] = __shfl_xor(send[e], 16, 64);
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = even ? keep[e] : recv[e];
+            v[4 + e] = even ? recv[e] : keep[e];
+          }
+          u32x4 pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x0 = v[2 * e] + bv[2 * e], x1 = v[2 * e + 1] + bv[2 * e + 1];
+            if (relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+            pk[e] = pack_bf16x2(x0, x1);
+          }
+          const int row = m0 + ii * 16 + (lane & 15);
+          const bool ok = row < p.M && col < p.N;  // N % 8 == 0 (launcher): chunks are whole
+          const int off = ok ? (int)(((long)w.b * p.sC + (long)row * p.ldc + col) * 2) : 0x7ffffff0;
+          __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, 0);
+        }
+      }
+      after_epi = true;
+    } else {
+      // lane holds C[16 ii + 4 g + r][16 j + (lane & 15)]
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + j * 16 + (lane & 15);
+        float bv = 0.f;
+        if (has_bias && col < p.N) {
+          const long bo = (long)w.b * p.sBias + col;
+          bv = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo]
+                        : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo]);
+        }
+#pragma unroll
+        for (int ii = 0; ii < TM; ++ii) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + ii * 16 + 4 * g + r;
+            float v = acc[ii][j][r] * p.alpha + bv;
+            if (relu) v = fmaxf(v, 0.f);
+            if (row >= p.M || col >= p.N) continue;
+            float* C = reinterpret_cast<float*>(p.C) + (long)w.b * p.sC + (long)row * p.ldc + col;
+            if (p.splitk > 1) atomicAdd(C, v);
+            else *C = accumulate ? *C + v : v;
+          }
+          acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+}
+
+// explicit instantiations: hipcc (ROCm 7.2) otherwise leaves some of these kernels' host stubs
+// undefined when they are only named inside launch_dma's instantiations
+#define LJS_DMA_INST(BM, BN, WM, WN, NST, AK, BKc, OF) \
+  template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, AK, BKc, OF>(GemmArgs);
+#define LJS_DMA_INST_LAYOUTS(NST)                                                                           \
+  LJS_DMA_INST(128, 128, 2, 2, NST, true, true, false) LJS_DMA_INST(128, 128, 2, 2, NST, true, true, true)     \
+  LJS_DMA_INST(128, 128, 2, 2, NST, false, false, false) LJS_DMA_INST(128, 128, 2, 2, NST, false, false, true) \
+  LJS_DMA_INST(128, 128, 2, 2, NST, true, false, false) LJS_DMA_INST(128, 128, 2, 2, NST, true, false, true)   \
+  LJS_DMA_INST(128, 128, 2, 2, NST, false, true, false) LJS_DMA_INST(128, 128, 2, 2, NST, false, true, true)
+LJS_DMA_INST_LAYOUTS(2)
+LJS_DMA_INST_LAYOUTS(4)
+LJS_DMA_INST(256, 128, 4, 2, 3, true, true, false)
+LJS_DMA_INST(256, 128, 4, 2, 3, true, true, true)
+#undef LJS_DMA_INST_LAYOUTS
+#undef LJS_DMA_INST
+
+int g_cus = 0;
+
+template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF>
+hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
+  if (!g_cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_cus <= 0) g_cus = 256;
+  }
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  const int items = ntm * ntn * a.batch * a.splitk;
+  static const int bpc_env = getenv("LJS_DMA_BPC") ? atoi(getenv("LJS_DMA_BPC")) : 0;  // tuning override
+  // blocks_per_cu 0 = one block per work item (measured best at the bench shapes: the
+  // dispatcher balances), else a persistent grid of blocks_per_cu x CUs
+  const int bpc = bpc_env > 0 ? bpc_env : blocks_per_cu;
+  int grid = bpc > 0 ? g_cus * bpc : items;
+  if (grid > items) grid = items;
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, NST, AK, BKc, OF>), dim3(grid), dim3(WM * WN * 64), 0, s, a);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, bool AK, bool BKc, bool OF>
 hipError_t launch_t(const GemmArgs& a, hipStream_t s) {
   int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
@@ -312,10 +640,37 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     if (me != hipSuccess) return (int)me;
   }
   hipError_t e;
-  if (tile == 64)
+  // Persistent LDS-DMA kernels (tile codes): 2561 = 256x128, 8 waves, 3 stages, 1 block/CU
+  // (k-contiguous operands only); 1284 = 128x128, 4 waves, 4 stages, 1 block/CU; 1282 =
+  // 128x128, 4 waves, 2 stages, 2 blocks/CU.  They need K % 64 == 0, a split that divides the
+  // K-tiles and operands addressable with 32-bit byte offsets.
+  const int nkt64 = K / BK;
+  const bool dma_ok = K % BK == 0 && nkt64 % a.splitk == 0 &&
+                      (a_kc ? (long)M * lda : (long)K * lda) < (1L << 30) &&
+                      (b_kc ? (long)N * ldb : (long)K * ldb) < (1L << 30);
+  const bool dma_store_ok = out_f32 || (N % 8 == 0 && ldc % 8 == 0 && (sC % 8 == 0 || batch == 1) &&
+                                        (((uintptr_t)C) & 15) == 0);
+  if (tile > 1000 && !(dma_ok && dma_store_ok)) tile = 128;
+  if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
+  if (tile == 2561) {
+    if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);
+    else e = launch_dma<256, 128, 4, 2, 3, true, true, false>(a, stream, 0);
+  } else if (tile == 1284 || tile == 1282) {
+    // (plain if/else, not ?: -- see the explicit-instantiation note above)
+#define LJS_DMA(AK, BK_, OF)                                                              \
+  if (a_kc == AK && b_kc == BK_ && out_f32 == OF) {                                       \
+    if (tile == 1284) return (int)launch_dma<128, 128, 2, 2, 4, AK, BK_, OF>(a, stream, 0); \
+    return (int)launch_dma<128, 128, 2, 2, 2, AK, BK_, OF>(a, stream, 0);                  \
+  }
+    LJS_DMA(1, 1, 0) LJS_DMA(1, 1, 1) LJS_DMA(0, 0, 0) LJS_DMA(0, 0, 1)
+    LJS_DMA(1, 0, 0) LJS_DMA(1, 0, 1) LJS_DMA(0, 1, 0) LJS_DMA(0, 1, 1)
+#undef LJS_DMA
+    e = hipErrorInvalidValue;
+  } else if (tile == 64) {
     e = dispatch_layout<64, 64>(a, a_kc, b_kc, out_f32, stream);
-  else
+  } else {
     e = dispatch_layout<128, 128>(a, a_kc, b_kc, out_f32, stream);
+  }
   return (int)e;
 }
 

@@ -40,12 +40,14 @@ _SIGS = {
     "ljs_cast_f32_bf16": [c_void_p, c_void_p, c_long, c_void_p],
     "ljs_cast_bf16_f32": [c_void_p, c_void_p, c_long, c_void_p],
     "ljs_cast_transpose_f32_bf16": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p],
-    "ljs_sum_all": [c_void_p, c_int, c_long, c_void_p, c_void_p],
-    "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p],
+    "ljs_sum_all": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
+    "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
+    "ljs_fill_row_bf16": [c_void_p, c_int, c_void_p, c_long, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ljs_adam_f32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
-    "ljs_adam_multi": [_LP, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float, c_void_p],
+    "ljs_adam_multi": [_LP, c_int, c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float,
+                       c_void_p],
     "ljs_rng_fill": [c_void_p, c_int, c_int, _LP, _LP, _LP, c_uint, c_uint, c_int, c_float, c_float, c_float,
                      c_float, c_void_p],
 }
@@ -86,6 +88,23 @@ def _ck(rc: int, name: str):
         raise RuntimeError(f"{name} failed with hipError {rc}")
 
 
+_WS = {}
+
+
+def _workspace(dev: torch.device, name: str, nbytes: int) -> torch.Tensor:
+    """Persistent zero-initialised per-(device, stream) scratch for in-launch last-arriver
+    reductions: its ticket words are re-armed by the kernels themselves, so no per-call memset."""
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, name)
+    t = _WS.get(key)
+    if t is None or t.numel() * 4 < nbytes:
+        t = torch.zeros((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+        _WS[key] = t
+    return t
+
+
+_COLSUM_WS_BYTES = 4 << 20  # = ljs_colsum_ws_floats() * 4
+
+
 def _p(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -112,14 +131,45 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
         (16 if zero_c else 0)
     if tile is None:
-        tiles128 = -(-M // 128) * -(-N // 128) * batch * max(1, splitk)
-        tile = 128 if tiles128 >= 160 else 64
+        tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc)
     eA = A.element_size()
     rc = lib().ljs_gemm_bf16(ctypes.c_void_p(A.data_ptr() + a_off * eA), ctypes.c_void_p(B.data_ptr() + b_off * eA),
                              ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb,
                              ldc, sA, sB, sC, sBias, batch, int(a_kc), int(b_kc), int(out_f32), flags, alpha,
                              splitk, tile, _stream(C))
     _ck(rc, "ljs_gemm_bf16")
+
+
+def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f32: bool, splitk: int = 1,
+              ldc: int = 0) -> int:
+    """Kernel/tile choice (measured on MI355X at the bench shapes, ``scripts/gemm_one.py``):
+    the LDS-DMA kernels (codes 2561 = 256x128 8 waves, 1282 = 128x128 4 waves x 2 blocks/CU)
+    whenever K is a multiple of 64, else the register-staged 128/64 tiles."""
+    tiles128 = -(-M // 128) * -(-N // 128) * batch * max(1, splitk)
+    if K % 64 == 0 and tiles128 >= 96 and (out_f32 or (N % 8 == 0 and ldc % 8 == 0)):
+        if a_kc and b_kc and not out_f32 and M >= 4096 and N >= 1024 and N % 128 == 0:
+            return 2561
+        return 1282
+    return 128 if tiles128 >= 160 else 64
+
+
+def pick_splitk_dma(M: int, N: int, K: int, batch: int) -> int:
+    """Split of the reduction for the 128x128 LDS-DMA kernel (weight-grad GEMMs): a divisor of
+    the K-tiles giving ~512 work items (2 resident blocks per CU on 256 CUs), >= 4 K-tiles each."""
+    if K % 64:
+        return 1
+    nkt = K // 64
+    tiles = -(-M // 128) * -(-N // 128) * batch
+    if tiles >= 384:
+        return 1
+    best, score = 1, None
+    for s in range(1, min(32, nkt // 4) + 1):
+        if nkt % s:
+            continue
+        sc = abs(tiles * s - 512)
+        if score is None or sc < score:
+            best, score = s, sc
+    return best
 
 
 def _choose_splitk(M: int, N: int, K: int, batch: int) -> int:
@@ -276,10 +326,13 @@ def cast_transpose_bf16(w: torch.Tensor, out: Optional[torch.Tensor] = None) -> 
 
 
 # ============================================================================ reductions
-def _sum_all_raw(t: torch.Tensor) -> torch.Tensor:
+def _sum_all_raw(t: torch.Tensor, out_dtype: torch.dtype = torch.float32) -> torch.Tensor:
     t = t.contiguous()
-    out = torch.empty((), dtype=torch.float32, device=t.device)
-    rc = lib().ljs_sum_all(_p(t), int(t.dtype == torch.bfloat16), t.numel(), _p(out), _stream(t))
+    out_bf16 = out_dtype == torch.bfloat16 and t.data_ptr() % 16 == 0
+    out = torch.empty((), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=t.device)
+    ws = _workspace(t.device, "sum_all", 257 * 4)
+    rc = lib().ljs_sum_all(_p(t), int(t.dtype == torch.bfloat16), t.numel(), _p(out), int(out_bf16), _p(ws),
+                           _stream(t))
     _ck(rc, "sum_all")
     return out
 
@@ -288,10 +341,20 @@ class _SumAll(torch.autograd.Function):
     @staticmethod
     def forward(ctx, t, acc_dtype):
         ctx.shape, ctx.dtype = t.shape, t.dtype
-        return _sum_all_raw(t).to(acc_dtype)
+        r = _sum_all_raw(t, acc_dtype)
+        return r if r.dtype == acc_dtype else r.to(acc_dtype)
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.dtype == torch.bfloat16 and g.dtype in (torch.float32, torch.bfloat16) and g.is_cuda \
+                and len(ctx.shape) >= 1:
+            # one bf16 row holding g, broadcast (stride 0) over every leading dim: the consumers
+            # (GEMMs, column sums) read it with ld = 0 and nothing of the full shape is written
+            n = ctx.shape[-1]
+            row = torch.empty((n,), dtype=torch.bfloat16, device=g.device)
+            rc = lib().ljs_fill_row_bf16(_p(g), int(g.dtype == torch.bfloat16), _p(row), n, _stream(g))
+            _ck(rc, "fill_row")
+            return row.expand(ctx.shape), None
         return g.to(ctx.dtype).expand(ctx.shape), None
 
 
@@ -307,8 +370,9 @@ def colsum(t2d: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bo
         t2d = t2d.contiguous()
     if out is None:
         out = torch.empty((C,), dtype=torch.float32, device=t2d.device)
+    ws = _workspace(t2d.device, "colsum", _COLSUM_WS_BYTES)
     rc = lib().ljs_colsum(_p(t2d), int(t2d.dtype == torch.bfloat16), R, C, t2d.stride(0), _p(out), int(accumulate),
-                          _stream(t2d))
+                          _p(ws), _stream(t2d))
     _ck(rc, "colsum")
     return out
 
@@ -361,7 +425,8 @@ def colsum_ld(t: torch.Tensor, R: int, C: int, ld: int, out: Optional[torch.Tens
     acc = out is not None
     if out is None:
         out = torch.empty((C,), dtype=torch.float32, device=t.device)
-    rc = lib().ljs_colsum(_p(t), int(t.dtype == torch.bfloat16), R, C, ld, _p(out), int(acc), _stream(t))
+    ws = _workspace(t.device, "colsum", _COLSUM_WS_BYTES)
+    rc = lib().ljs_colsum(_p(t), int(t.dtype == torch.bfloat16), R, C, ld, _p(out), int(acc), _p(ws), _stream(t))
     _ck(rc, "colsum")
     return out
 
@@ -447,10 +512,12 @@ def adam(p, g, m, v, step, lr, b1, b2, eps, wd, inplace):
     return po.view(p.shape), mo.view(m.shape), vo.view(v.shape)
 
 
-def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd) -> None:
+def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step: bool = False) -> None:
     """In-place fused Adam over many params (one launch per 32): entries = [(p, g, m, v)].
 
-    Also rewrites each param's registered bf16 shadows (see :mod:`.shadow`)."""
+    Also rewrites each param's registered bf16 shadows (see :mod:`.shadow`).  With
+    ``increment_step`` the bias corrections use ``step + 1`` and the last launch's last
+    arriving block stores ``step + 1`` (int32 ``step`` updated in place, no extra kernel)."""
     from . import shadow
     import numpy as np
     rows = []
@@ -464,12 +531,18 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd) -> None:
         rows.append(([p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
                       st.data_ptr() if st is not None else 0, sn.data_ptr() if sn is not None else 0,
                       R, C, int(g.dtype == torch.bfloat16), 0], g))
+    if increment_step:
+        assert step.dtype == torch.int32 and step.is_contiguous()
     step_i = step if step.dtype == torch.int32 else step.to(torch.int32)
+    ticket = _workspace(step_i.device, "adam_ticket", 16) if increment_step else None
     for i in range(0, len(rows), 32):
         chunk = rows[i:i + 32]
         tab = np.asarray([r[0] for r in chunk], dtype=np.int64).reshape(-1)
         arr = (ctypes.c_long * tab.size)(*tab.tolist())
-        rc = lib().ljs_adam_multi(arr, len(chunk), _p(step_i), lr, b1, b2, eps, wd, _stream(step_i))
+        last = i + 32 >= len(rows)
+        rc = lib().ljs_adam_multi(arr, len(chunk), _p(step_i), int(increment_step),
+                                  _p(ticket) if (increment_step and last) else None, lr, b1, b2, eps, wd,
+                                  _stream(step_i))
         _ck(rc, "ljs_adam_multi")
     for p, _, _, _ in entries:
         shadow.mark_fresh(p)

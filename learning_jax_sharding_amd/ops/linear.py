@@ -128,10 +128,11 @@ class _Linear(torch.autograd.Function):
             t0, ld0 = mats[want[0]]
             batched = (len(want) == nw and nw > 1 and ld0 > 0 and all(
                 mats[i][1] == ld0 and mats[i][0].data_ptr() == t0.data_ptr() + i * N * 2 for i in want))
-            tile = 128 if (K >= 256 and N >= 256) else 64
+            dma = M % 64 == 0
+            tile = 1282 if dma else (128 if (K >= 256 and N >= 256) else 64)
             if batched:
                 dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
-                sk = _splitk(K, N, M, nw, tile)
+                sk = hip.pick_splitk_dma(K, N, M, nw) if dma else _splitk(K, N, M, nw, tile)
                 hip.gemm(xb, t0, dW, K, N, M, K, ld0, N, False, False, batch=nw, sA=0, sB=N, sC=K * N,
                          splitk=sk, tile=tile, zero_c=True)
                 for i in want:
@@ -140,7 +141,7 @@ class _Linear(torch.autograd.Function):
                 for i in want:
                     t, ld = mats[i]
                     dW = torch.empty((K, N), dtype=torch.float32, device=dev)
-                    sk = _splitk(K, N, M, 1, tile)
+                    sk = hip.pick_splitk_dma(K, N, M, 1) if dma else _splitk(K, N, M, 1, tile)
                     hip.gemm(xb, t, dW, K, N, M, K, ld, N, False, False, splitk=sk, tile=tile, zero_c=True)
                     dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
         # ---- db

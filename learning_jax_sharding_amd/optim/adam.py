@@ -136,23 +136,24 @@ class _Adam:
         st, empty = state
         count = st.count
         inplace = all(_state.is_donated(t) for t in count.local.values())
+        pl, ptd = T.tree_flatten(params, is_leaf=_is_arr)
+        gl = T.tree_leaves(grads, is_leaf=_is_arr)
+        ml = T.tree_leaves(st.mu, is_leaf=_is_arr)
+        vl = T.tree_leaves(st.nu, is_leaf=_is_arr)
+        # multi-tensor kernel; with a donated counter it also performs the count increment
+        fused = self._apply_multi(pl, gl, ml, vl, count, inplace)
+        if fused is not None:
+            new_p, new_m, new_v, new_count = fused
+            params2 = T.tree_unflatten(ptd, new_p)
+            mu = T.tree_unflatten(T.tree_structure(st.mu, is_leaf=_is_arr), new_m)
+            nu = T.tree_unflatten(T.tree_structure(st.nu, is_leaf=_is_arr), new_v)
+            return params2, (ScaleByAdamState(new_count, mu, nu), empty)
         if inplace:
             for t in count.local.values():
                 t.add_(1)
             new_count = count
         else:
             new_count = ShardedArray((), torch.int32, count.sharding, {d: t + 1 for d, t in count.local.items()})
-        pl, ptd = T.tree_flatten(params, is_leaf=_is_arr)
-        gl = T.tree_leaves(grads, is_leaf=_is_arr)
-        ml = T.tree_leaves(st.mu, is_leaf=_is_arr)
-        vl = T.tree_leaves(st.nu, is_leaf=_is_arr)
-        fused = self._apply_multi(pl, gl, ml, vl, new_count, inplace)
-        if fused is not None:
-            new_p, new_m, new_v = fused
-            params2 = T.tree_unflatten(ptd, new_p)
-            mu = T.tree_unflatten(T.tree_structure(st.mu, is_leaf=_is_arr), new_m)
-            nu = T.tree_unflatten(T.tree_structure(st.nu, is_leaf=_is_arr), new_v)
-            return params2, (ScaleByAdamState(new_count, mu, nu), empty)
         new_p, new_m, new_v = [], [], []
         for p, g, m, v in zip(pl, gl, ml, vl):
             if not _is_arr(p):
@@ -197,11 +198,18 @@ def _adam_multi_apply(self, pl, gl, ml, vl, count, inplace):
                 tp, tm, tv = pt.clone(), mt.clone(), vt.clone()
             new_loc[i][0][d], new_loc[i][1][d], new_loc[i][2][d] = tp, tm, tv
             by_dev.setdefault(d, []).append((tp, g.local[d], tm, tv))
+    fold = inplace and all(t.dtype == torch.int32 and t.is_cuda for t in count.local.values()) \
+        and set(count.local) == set(by_dev)
+    if fold:
+        new_count = count   # incremented in place by the kernel's last arriving block
+    else:
+        new_count = ShardedArray((), torch.int32, count.sharding, {d: t + 1 for d, t in count.local.items()})
     for d, entries in by_dev.items():
-        hip.adam_multi(entries, count.local[d], self._lr(), self.b1, self.b2, self.eps, self.weight_decay)
+        hip.adam_multi(entries, new_count.local[d], self._lr(), self.b1, self.b2, self.eps, self.weight_decay,
+                       increment_step=fold)
     mk = lambda a, loc: ShardedArray(a.shape, a.dtype, a.sharding, loc)  # noqa: E731
     return ([mk(a[0], l[0]) for a, l in zip(arrs, new_loc)], [mk(a[2], l[1]) for a, l in zip(arrs, new_loc)],
-            [mk(a[3], l[2]) for a, l in zip(arrs, new_loc)])
+            [mk(a[3], l[2]) for a, l in zip(arrs, new_loc)], new_count)
 
 
 _Adam._apply_multi = _adam_multi_apply

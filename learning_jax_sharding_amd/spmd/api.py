@@ -76,10 +76,11 @@ class Lowered:
 class _Captured:
     """A hipGraph of one call signature: static inputs, static outputs."""
 
-    def __init__(self, graph, in_leaves, out_tree):
+    def __init__(self, graph, in_leaves, out_tree, aliased):
         self.graph = graph
         self.in_leaves = in_leaves  # list of ShardedArray (static buffers)
         self.out_tree = out_tree
+        self.aliased = aliased      # per leaf: the caller's own buffers (read-only in the graph)
 
 
 class Jitted:
@@ -176,48 +177,58 @@ class Jitted:
                 return self._run(args, kwargs)[0]
         cap = self._graphs.get(sig)
         if cap is not None:
-            return self._replay(cap, args)
+            return self._replay(cap, args, sig)
         n = self._calls.get(sig, 0)
         self._calls[sig] = n + 1
         if n < self.warmup_calls:
             return self._run(args, kwargs)[0]
         return self._capture(sig, args)
 
-    def _capture(self, sig, args):
-        # static input buffers: private copies of this call's inputs
+    def _capture(self, sig, args, alias: bool = True):
+        """Capture one call into a hipGraph.  Static inputs: donated buffers as they are (the
+        graph updates them in place; their bf16 weight shadows stay valid); other inputs are
+        aliased too (the graph only reads them), so a caller that passes the same arrays again
+        costs no copy.  A later call with different buffers re-captures once with private
+        static copies, into which every further call's inputs are copied."""
         dyn, static = self._split(args)
         full = list(args)
-        in_leaves = []
+        in_leaves, aliased = [], []
         for i, a in dyn:
             donated = i in self.donate_argnums
 
             def cp(x, donated=donated):
                 if isinstance(x, ShardedArray):
-                    # donated buffers become the graph's static inputs as they are (their bf16
-                    # weight shadows stay valid); others are copied into private buffers
-                    y = x if donated else ShardedArray(x.shape, x.dtype, x.sharding,
-                                                       {d: t.detach().clone() for d, t in x.local.items()})
+                    keep = donated or alias
+                    y = x if keep else ShardedArray(x.shape, x.dtype, x.sharding,
+                                                    {d: t.detach().clone() for d, t in x.local.items()})
                     in_leaves.append(y)
+                    aliased.append(keep and not donated)
                     return y
                 return x
             full[i] = T.tree_map(cp, a, is_leaf=_leaf_is_array)
         torch.cuda.synchronize()
-        # warm the caching allocator on a side stream as torch requires
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             out, _ = self._run(tuple(full), {})
-        cap = _Captured(g, in_leaves, out)
+        cap = _Captured(g, in_leaves, out, aliased)
         self._graphs[sig] = cap
-        return self._replay(cap, args)
+        return self._replay(cap, args, sig)
 
-    def _replay(self, cap: _Captured, args):
+    def _replay(self, cap: _Captured, args, sig=None):
         dyn, _ = self._split(args)
         leaves = [l for _, a in dyn for l in T.tree_leaves(a, is_leaf=_leaf_is_array) if isinstance(l, ShardedArray)]
-        for src, dst in zip(leaves, cap.in_leaves):
+        copies = []
+        for src, dst, al in zip(leaves, cap.in_leaves, cap.aliased):
             for d, t in dst.local.items():
                 s = src.local[d]
-                if s.data_ptr() != t.data_ptr():
-                    t.copy_(s)
+                if s.data_ptr() != t.data_ptr() or s.stride() != t.stride():
+                    if al:  # never write into a caller's buffer: re-capture with private inputs
+                        if sig is None:
+                            sig = self._signature(*self._split(args))
+                        return self._capture(sig, args, alias=False)
+                    copies.append((t, s))
+        for t, s in copies:
+            t.copy_(s)
         cap.graph.replay()
         return cap.out_tree
 
@@ -297,6 +308,22 @@ def reduce_replica_grads(pairs: List[Tuple[ShardedArray, Dict[int, torch.Tensor]
     return out  # type: ignore
 
 
+_SEEDS: Dict[Tuple, torch.Tensor] = {}
+
+
+def _seed(t: torch.Tensor, value: float) -> torch.Tensor:
+    """Constant cotangent seed, cached per (device, dtype, shape, value): autograd only reads
+    it, so a captured train step replays without a fill kernel."""
+    key = (t.device, t.dtype, tuple(t.shape), value)
+    s = _SEEDS.get(key)
+    if s is None:
+        s = torch.full(t.shape, value, dtype=t.dtype, device=t.device)
+        if t.device.type == "meta" or (t.is_cuda and torch.cuda.is_current_stream_capturing()):
+            return s
+        _SEEDS[key] = s
+    return s
+
+
 def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
     multi = isinstance(argnums, (tuple, list))
     argnums_t = tuple(argnums) if multi else (argnums,)
@@ -320,7 +347,7 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
         for d, t in out.local.items():
             if t.requires_grad:
                 outs.append(t)
-                seeds.append(torch.full_like(t, 1.0 / n_holders))
+                seeds.append(_seed(t, 1.0 / n_holders))
         grads_per_arg = []
         all_leaves = [l for ls in diff_leaves for l in ls]
         inputs = [t for l in all_leaves for t in l.local.values() if t.requires_grad]

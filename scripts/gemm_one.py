@@ -1,0 +1,60 @@
+"""Run ONE bench-shape GEMM configuration repeatedly (for rocprofv3 counter runs / A-B timing).
+
+usage: python scripts/gemm_one.py {qkv,out,dattn,dwqkv,dwo,dwo_slabs} TILE [SPLITK] [ITERS]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from learning_jax_sharding_amd.ops import hip  # noqa: E402
+from scripts.gemm_tune import timeit  # noqa: E402
+
+dev = torch.device("cuda")
+T = 16384
+
+
+def build(case, tile, sk):
+    if case == "qkv":
+        X, W = torch.randn(T, 640, device=dev).bfloat16(), torch.randn(1536, 640, device=dev).bfloat16()
+        C = torch.empty(T, 1536, device=dev).bfloat16()
+        return lambda: hip.gemm(X, W, C, T, 1536, 640, 640, 640, 1536, True, True, tile=tile), 2 * T * 1536 * 640
+    if case == "out":
+        X, W = torch.randn(T, 512, device=dev).bfloat16(), torch.randn(640, 512, device=dev).bfloat16()
+        C = torch.empty(T, 640, device=dev).bfloat16()
+        return lambda: hip.gemm(X, W, C, T, 640, 512, 512, 512, 640, True, True, tile=tile), 2 * T * 640 * 512
+    if case == "dattn":
+        X, W = torch.randn(T, 640, device=dev).bfloat16(), torch.randn(512, 640, device=dev).bfloat16()
+        C = torch.empty(T, 512, device=dev).bfloat16()
+        return lambda: hip.gemm(X, W, C, T, 512, 640, 640, 640, 512, True, True, tile=tile), 2 * T * 640 * 512
+    if case == "dwqkv":
+        X, dY = torch.randn(T, 640, device=dev).bfloat16(), torch.randn(T, 1536, device=dev).bfloat16()
+        dW = torch.empty(3, 640, 512, device=dev)
+        return (lambda: hip.gemm(X, dY, dW, 640, 512, T, 640, 1536, 512, False, False, batch=3, sA=0, sB=512,
+                                 sC=640 * 512, splitk=sk, tile=tile, zero_c=True), 2 * T * 640 * 1536)
+    if case == "dwo":
+        X, dY = torch.randn(T, 512, device=dev).bfloat16(), torch.randn(T, 640, device=dev).bfloat16()
+        dW = torch.empty(512, 640, device=dev)
+        return (lambda: hip.gemm(X, dY, dW, 512, 640, T, 512, 640, 640, False, False, splitk=sk, tile=tile,
+                                 zero_c=True), 2 * T * 512 * 640)
+    if case == "dwo_slabs":  # split-K as a batch over K-chunks writing separate f32 slabs (no atomics)
+        X, dY = torch.randn(T, 512, device=dev).bfloat16(), torch.randn(T, 640, device=dev).bfloat16()
+        dW = torch.empty(sk, 512, 640, device=dev)
+        kc = T // sk
+        return (lambda: hip.gemm(X, dY, dW, 512, 640, kc, 512, 640, 640, False, False, batch=sk, sA=kc * 512,
+                                 sB=kc * 640, sC=512 * 640, tile=tile), 2 * T * 512 * 640)
+    raise SystemExit(f"unknown case {case}")
+
+
+def main():
+    case, tile = sys.argv[1], int(sys.argv[2])
+    sk = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    iters = int(sys.argv[4]) if len(sys.argv) > 4 else 50
+    f, flops = build(case, tile, sk)
+    us = timeit(f, iters=iters, rounds=3)
+    print(f"{case} tile={tile} sk={sk}: {us:.2f} us  {flops / us / 1e6:.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -33,8 +33,8 @@ def _stored(mat, kc_rowmajor: bool):
 
 @pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (0, 0), (1, 0), (0, 1)])
 @pytest.mark.parametrize("out_f32", [0, 1])
-@pytest.mark.parametrize("tile", [64, 128])
-@pytest.mark.parametrize("M,N,K", [(256, 192, 320), (136, 72, 40), (512, 1536, 640)])
+@pytest.mark.parametrize("tile", [64, 128, 2561, 1284, 1282])
+@pytest.mark.parametrize("M,N,K", [(256, 192, 320), (136, 72, 40), (512, 1536, 640), (304, 136, 128)])
 def test_gemm_layouts(hip, a_kc, b_kc, out_f32, tile, M, N, K):
     A = _rand(M, K, seed=1)
     B = _rand(K, N, seed=2)
@@ -46,6 +46,25 @@ def test_gemm_layouts(hip, a_kc, b_kc, out_f32, tile, M, N, K):
     torch.cuda.synchronize()
     tol = 2e-2 if not out_f32 else 1e-3
     torch.testing.assert_close(C.float(), ref, rtol=tol, atol=tol * math.sqrt(K))
+
+
+@pytest.mark.parametrize("tile", [1284, 1282, 2561])
+def test_gemm_dma_splitk_batched_broadcast(hip, tile):
+    """LDS-DMA kernels: weight-grad layout (both operands m/n-contiguous) with split-K atomics
+    into a zeroed f32 C, batched column blocks, and a broadcast (ld = 0) k-contiguous row."""
+    T, M, N, nb = 2048, 320, 128, 3
+    X = _rand(T, M, seed=7)
+    dY = _rand(T, nb * N, seed=8)
+    dW = torch.full((nb, M, N), float("nan"), dtype=torch.float32, device=dev)
+    hip.gemm(X, dY, dW, M, N, T, M, nb * N, N, False, False, batch=nb, sA=0, sB=N, sC=M * N, splitk=4,
+             tile=tile, zero_c=True)
+    for i in range(nb):
+        torch.testing.assert_close(dW[i], X.float().t() @ dY[:, i * N:(i + 1) * N].float(), rtol=1e-3, atol=5e-2)
+    row = _rand(1, 256, seed=9)
+    W = _rand(320, 256, seed=10)
+    out = torch.empty((500, 320), dtype=torch.bfloat16, device=dev)
+    hip.gemm(row, W, out, 500, 320, 256, 0, 256, 320, True, True, tile=tile)
+    torch.testing.assert_close(out.float(), (row.float() @ W.float().t()).expand(500, 320), rtol=2e-2, atol=5e-2)
 
 
 def test_gemm_identity_asymmetric(hip):
@@ -253,3 +272,50 @@ def test_linear_broadcast_grad_and_strided(hip):
     torch.testing.assert_close(b.grad, torch.full((320,), 128.0, device=dev))
     torch.testing.assert_close(xr.grad, w.detach().bfloat16().float().sum(1)[None, :].expand(128, 256),
                                rtol=2e-2, atol=5e-2)
+
+
+def test_ticket_reductions_rearm(hip):
+    """Last-arriver reductions (sum_all, colsum) re-arm their tickets: repeated calls with
+    different data and grid sizes stay exact, and sum_all writes bf16 directly."""
+    for i, n in enumerate((1 << 22, 3 * (1 << 20) + 8, 4096, 1 << 22)):
+        x = _rand(n, seed=100 + i)
+        ref = x.float().sum()
+        torch.testing.assert_close(hip.sum_all(x, torch.float32), ref, rtol=1e-3, atol=1e-1)
+        got = hip.sum_all(x, torch.bfloat16)
+        assert got.dtype == torch.bfloat16
+        torch.testing.assert_close(got.float(), ref, rtol=1e-2, atol=1.0)
+    for i, (R, C) in enumerate(((16384, 1536), (1000, 64), (16384, 640), (77, 8))):
+        m = _rand(R, C, seed=200 + i)
+        out = hip.colsum(m)
+        torch.testing.assert_close(out, m.float().sum(0), rtol=1e-4, atol=5e-2)
+        hip.colsum(m, out=out, accumulate=True)
+        torch.testing.assert_close(out, 2 * m.float().sum(0), rtol=1e-4, atol=1e-1)
+    row = _rand(320, seed=300)
+    got = hip.colsum_ld(row, 1000, 320, 0)
+    torch.testing.assert_close(got, row.float() * 1000, rtol=1e-5, atol=1e-3)
+
+
+def test_sum_backward_broadcast_row(hip):
+    x = _rand(8, 16, 96, seed=5).requires_grad_()
+    s = hip.sum_all(x, torch.bfloat16)
+    (g,) = torch.autograd.grad(s, [x], torch.tensor(0.25, dtype=torch.bfloat16, device=dev))
+    assert g.shape == x.shape and g.stride()[:2] == (0, 0)
+    torch.testing.assert_close(g.float(), torch.full(x.shape, 0.25, device=dev))
+
+
+def test_adam_multi_folded_step_increment(hip):
+    ws = [torch.randn(64 * 7, 130, device=dev) for _ in range(40)]  # > 32 tensors: two launches
+    gs = [torch.randn_like(w) for w in ws]
+    ms = [torch.zeros_like(w) for w in ws]
+    vs = [torch.zeros_like(w) for w in ws]
+    refs = [w.clone().requires_grad_() for w in ws]
+    opt = torch.optim.Adam(refs, lr=1e-3)
+    step = torch.zeros((), dtype=torch.int32, device=dev)
+    for k in range(3):
+        hip.adam_multi(list(zip(ws, gs, ms, vs)), step, 1e-3, 0.9, 0.999, 1e-8, 0.0, increment_step=True)
+        assert int(step) == k + 1
+        for r, g in zip(refs, gs):
+            r.grad = g.clone()
+        opt.step()
+    for w, r in zip(ws, refs):
+        torch.testing.assert_close(w, r.detach(), rtol=1e-5, atol=1e-6)
