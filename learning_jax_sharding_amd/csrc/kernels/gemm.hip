@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
 //  * The MFMA operands are swapped (C^T = B^T A^T per 16x16 block), so each lane ends with 4
 //    CONSECUTIVE columns of one output row: bf16 results leave as packed 8-byte stores and
 //    f32 as 16-byte stores straight from the accumulators (no LDS round trip).
-//  * Work items are ordered (batch, split, tile-row, tile-col) and dealt XCD-aware, so blocks
+//  * Work items are ordered (split, batch, tile-row, tile-col) and dealt XCD-aware, so blocks
 //    sharing an XCD's L2 work on neighbouring tiles (shared operand panels).
 // Edges: rows/cols past M/N read garbage that only reaches discarded outputs; the buffer
 // descriptor's range check turns every out-of-range read into 0 without faulting; K must be a
@@ -336,14 +336,16 @@ struct WorkItem {
   int b, m0, n0, kt0;
 };
 
+// item order (split, batch, tile-row, tile-col), tile-col fastest: with the XCD-aware deal,
+// an XCD's blocks share one K-range (split), so its L2 holds that range's operand panels
 __device__ __forceinline__ WorkItem decode_item(const GemmArgs& p, int item, int ntm, int ntn) {
   WorkItem w;
   const int tn_i = item % ntn;
   int r = item / ntn;
   const int tm_i = r % ntm;
   r /= ntm;
-  const int split = r % p.splitk;
-  w.b = r / p.splitk;
+  w.b = r % p.batch;
+  const int split = r / p.batch;
   w.m0 = tm_i;
   w.n0 = tn_i;
   w.kt0 = split * p.kt_per_split;

@@ -312,7 +312,10 @@ def _reduce(x: ShardedArray, axis, keepdims: bool, local_fn, combine: str, dtype
     axes = _norm_axes(axis, x.ndim)
     sharded = [a for a in axes if x.tile.tile_shape[a] > 1]
     out_dtype = _dt.canonicalize(dtype) or x.dtype
-    acc = torch.float32 if out_dtype in (torch.bfloat16, torch.float16) and combine == "sum" else out_dtype
+    # low-precision sums accumulate in f32 inside the kernels; an f32 intermediate is only
+    # materialised when partial sums still have to be all-reduced across shards
+    acc = torch.float32 if out_dtype in (torch.bfloat16, torch.float16) and combine == "sum" and sharded \
+        else out_dtype
     loc = _map(x, lambda t: local_fn(t, axes, keepdims, acc))
     if sharded:
         groups = x.tile.groups_along(sharded)
@@ -321,7 +324,7 @@ def _reduce(x: ShardedArray, axis, keepdims: bool, local_fn, combine: str, dtype
         else:
             gathered = C.all_gather({d: t.unsqueeze(0) for d, t in loc.items()}, groups, 0, note="reduce")
             loc = {d: (t.amax(0) if combine == "max" else t.amin(0)) for d, t in gathered.items()}
-    loc = {d: t.to(out_dtype) for d, t in loc.items()}
+    loc = {d: (t if t.dtype == out_dtype else t.to(out_dtype)) for d, t in loc.items()}
     if keepdims:
         tile = x.tile.unshard(axes)
         shape = tuple(1 if i in axes else s for i, s in enumerate(x.shape))

@@ -92,9 +92,12 @@ _WS = {}
 
 
 def _workspace(dev: torch.device, name: str, nbytes: int) -> torch.Tensor:
-    """Persistent zero-initialised per-(device, stream) scratch for in-launch last-arriver
-    reductions: its ticket words are re-armed by the kernels themselves, so no per-call memset."""
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, name)
+    """Persistent zero-initialised per-device scratch for in-launch last-arriver reductions:
+    its ticket words are re-armed by the kernels themselves, so no per-call memset.  (Keyed
+    by device only: a HIP graph captures on a side stream, and a workspace first created
+    inside a capture would replay its zero-fill every step.  The kernels using one
+    workspace are never run concurrently on two streams.)"""
+    key = (dev.index, name)
     t = _WS.get(key)
     if t is None or t.numel() * 4 < nbytes:
         t = torch.zeros((nbytes + 3) // 4, dtype=torch.float32, device=dev)
@@ -163,7 +166,7 @@ def pick_splitk_dma(M: int, N: int, K: int, batch: int) -> int:
     if tiles >= 384:
         return 1
     best, score = 1, None
-    for s in range(1, min(32, nkt // 4) + 1):
+    for s in range(1, min(16, nkt // 4) + 1):
         if nkt % s:
             continue
         sc = abs(tiles * s - 512)

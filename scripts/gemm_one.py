@@ -44,6 +44,22 @@ def build(case, tile, sk):
         kc = T // sk
         return (lambda: hip.gemm(X, dY, dW, 512, 640, kc, 512, 640, 640, False, False, batch=sk, sA=kc * 512,
                                  sB=kc * 640, sC=512 * 640, tile=tile), 2 * T * 512 * 640)
+    if case == "dwall":  # the fused dWqkv as one [640][1536] GEMM (MN x MN), split-K atomics
+        X, dY = torch.randn(T, 640, device=dev).bfloat16(), torch.randn(T, 1536, device=dev).bfloat16()
+        dW = torch.empty(640, 1536, device=dev)
+        return (lambda: hip.gemm(X, dY, dW, 640, 1536, T, 640, 1536, 1536, False, False, splitk=sk, tile=tile,
+                                 zero_c=True), 2 * T * 640 * 1536)
+    if case == "dwall_slabs":  # same, K-chunks as a batch writing separate f32 slabs (no atomics)
+        X, dY = torch.randn(T, 640, device=dev).bfloat16(), torch.randn(T, 1536, device=dev).bfloat16()
+        dW = torch.empty(sk, 640, 1536, device=dev)
+        kc = T // sk
+        return (lambda: hip.gemm(X, dY, dW, 640, 1536, kc, 640, 1536, 1536, False, False, batch=sk,
+                                 sA=kc * 640, sB=kc * 1536, sC=640 * 1536, tile=tile), 2 * T * 640 * 1536)
+    if case == "dwall_kc":  # diagnostic: operands pre-transposed to k-contiguous (ds_read_b128 path)
+        Xt, dYt = torch.randn(640, T, device=dev).bfloat16(), torch.randn(1536, T, device=dev).bfloat16()
+        dW = torch.empty(640, 1536, device=dev)
+        return (lambda: hip.gemm(Xt, dYt, dW, 640, 1536, T, T, T, 1536, True, True, splitk=sk, tile=tile,
+                                 zero_c=True), 2 * T * 640 * 1536)
     raise SystemExit(f"unknown case {case}")
 
 
