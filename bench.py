@@ -41,6 +41,10 @@ def parse():
                    help="dp: (N,1) data x model; 2d: (N/2, 2); or explicit 'DxM'")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--mode", default="train", choices=["train", "fwd"])
+    p.add_argument("--model", default="attention", choices=["attention", "layer"],
+                   help="attention: the case6 block (headline); layer: attention + FF transformer layer")
+    p.add_argument("--ff-dim", type=int, default=2560)
+    p.add_argument("--fp8", action="store_true", help="layer: MX-fp8 FF GEMMs (CDNA4 block-scaled MFMA)")
     return p.parse_args()
 
 
@@ -55,7 +59,8 @@ def main():
     import learning_jax_sharding_amd as ljs
     from learning_jax_sharding_amd import nn, optim
     from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
-    from learning_jax_sharding_amd.models import MultiHeadAttention, attention_block_flops
+    from learning_jax_sharding_amd.models import (MultiHeadAttention, TransformerLayer, attention_block_flops,
+                                                  transformer_layer_flops)
     from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
     from learning_jax_sharding_amd.training import TrainState
 
@@ -71,7 +76,10 @@ def main():
     rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
     B = args.batch_per_gpu * n
     S, M = args.seq, args.dim
-    model = MultiHeadAttention(M, heads=args.heads, dim_head=args.dim_head)
+    if args.model == "layer":
+        model = TransformerLayer(M, heads=args.heads, dim_head=args.dim_head, ff_dim=args.ff_dim, fp8=args.fp8)
+    else:
+        model = MultiHeadAttention(M, heads=args.heads, dim_head=args.dim_head)
     x_sharding = NamedSharding(mesh, P("data", "model"))
     x = ljs.random.normal(ljs.random.PRNGKey(0), (B, S, M), sharding=x_sharding)
 
@@ -136,7 +144,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
-    flops = attention_block_flops(B, S, M, args.heads, args.dim_head, train=args.mode == "train")
+    if args.model == "layer":
+        flops = transformer_layer_flops(B, S, M, args.heads, args.dim_head, args.ff_dim, train=args.mode == "train")
+    else:
+        flops = attention_block_flops(B, S, M, args.heads, args.dim_head, train=args.mode == "train")
     tflops_total = flops / (ms * 1e-3) / 1e12
     tokens_per_s = B * S / (ms * 1e-3)
     rank = int(os.environ.get("RANK", "0"))
@@ -157,8 +168,10 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (random normal x, random-init weights)",
-            "config": {"model": f"case6 attention block (M={M}, heads={args.heads}x{args.dim_head}, "
-                                f"bf16 compute, f32 params, Adam)",
+            "config": {"model": (f"case6 attention block (M={M}, heads={args.heads}x{args.dim_head}, "
+                                 f"bf16 compute, f32 params, Adam)") if args.model == "attention" else
+                                (f"attention+FF transformer layer (M={M}, heads={args.heads}x{args.dim_head}, "
+                                 f"ff={args.ff_dim}, FF GEMMs {'MX-fp8' if args.fp8 else 'bf16'}, f32 params, Adam)"),
                        "global_batch": B, "seq_len": S, "parallelism": par, "mode": args.mode,
                        "hip_graph": capture},
         }

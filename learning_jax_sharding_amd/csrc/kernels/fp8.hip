@@ -1,0 +1,332 @@
+// MX-fp8 (OCP e4m3 elements + e8m0 block scales, 32 elements per block along K) quantization
+// and the block-scaled MFMA GEMM for gfx950 (v_mfma_scale_f32_16x16x128_f8f6f4: twice the
+// bf16 MFMA rate per clock).
+//
+//   quant   : x[R][K] (f32 or bf16)          -> q[R][K] e4m3, s[R][K/32] e8m0   (blocks along rows)
+//   quant_t : w[K][N] (f32 or bf16, row-major) -> q[N][K] e4m3, s[N][K/32] e8m0 (transposed)
+//   gemm    : C[M][N] = sum_k (qa[m][k] 2^sa[m][k/32]) (qb[n][k] 2^sb[n][k/32])  (+bias)(relu)
+//
+// Scale rule: OCP MX v1.0's shared exponent floor(log2(amax)) - 8 (8 = emax of e4m3), raised by
+// one when the block max would exceed 448; elements RNE-rounded to e4m3 after division by 2^exp.
+//
+// MFMA operand layout (measured with scripts/mfma_f8_layout.py): lane l (g = l >> 4) holds row
+// l & 15, bytes 0-15 = k 16g..16g+15 and bytes 16-31 = k 64+16g..64+16g+15; the scale of
+// 32-element k-block kb of row r is byte 0 of lane r + 16 kb's scale operand.
+//
+// GEMM structure: 128x128 output tile, 4 waves (2x2, 64x64 each), BK = 128 (one MFMA K step),
+// buffer LDS-DMA staging of the fp8 tiles (128-byte rows, the same XOR-swizzled image as the
+// bf16 kernels) AND of the per-row scale words, two-stage ring, counted vmcnt, one raw
+// barrier per K-tile.  The MFMA operands are swapped (C^T blocks) so each lane ends with 4
+// consecutive output columns: packed 16-byte row stores after a lane-pair exchange.
+#include "common.h"
+
+namespace {
+
+constexpr int F8_BK = 128;  // K elements (bytes) per K-tile and per MFMA
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+__device__ __forceinline__ float ldf(const void* p, long i, int is_bf16) {
+  return is_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(p)[i]) : reinterpret_cast<const float*>(p)[i];
+}
+
+// shared e8m0 exponent of a block from its amax; returns the unbiased exponent X (2^X scale).
+// OCP's floor(log2 amax) - 8, plus one when amax / 2^X would exceed 448 (mantissa > 1.75), so
+// no element of the block saturates.
+__device__ __forceinline__ int mx_exponent(float amax) {
+  if (!(amax > 0.f)) return -127;
+  int e;
+  const float m = frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1): floor(log2 amax) = e - 1
+  int x = e - 1 - 8 + (m > 0.875f ? 1 : 0);
+  return x < -127 ? -127 : (x > 127 ? 127 : x);
+}
+
+__device__ __forceinline__ unsigned pack4_e4m3(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f);
+  d = fminf(fmaxf(d, -448.f), 448.f);
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);   // bytes 0,1
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, lo, true);   // bytes 2,3
+  return (unsigned)hi;
+}
+
+// one thread per 32-element block of a row
+__global__ void quant_mx_rows_kernel(const void* __restrict__ in, int is_bf16, long ld, int R, int K,
+                                     unsigned char* __restrict__ q, unsigned char* __restrict__ s) {
+  const long nb = (long)R * (K / 32);
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nb) return;
+  const int r = (int)(t / (K / 32)), kb = (int)(t % (K / 32));
+  const long base = (long)r * ld + (long)kb * 32;
+  float v[32];
+  if (is_bf16) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(in) + base);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      u32x4 w = p[c];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[8 * c + 2 * k] = __uint_as_float(w[k] << 16);
+        v[8 * c + 2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+      }
+    }
+  } else {
+    const f32x4* p = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(in) + base);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      f32x4 w = p[c];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[4 * c + k] = w[k];
+    }
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
+  const int x = mx_exponent(amax);
+  const float inv = ldexpf(1.f, -x);
+  u32x4 o[2];
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    o[c >> 2][c & 3] = pack4_e4m3(v[4 * c] * inv, v[4 * c + 1] * inv, v[4 * c + 2] * inv, v[4 * c + 3] * inv);
+  u32x4* qo = reinterpret_cast<u32x4*>(q + (long)r * K + (long)kb * 32);
+  qo[0] = o[0];
+  qo[1] = o[1];
+  s[t] = (unsigned char)(x + 127);
+}
+
+// w[K][N] row-major -> q[N][K], s[N][K/32]: thread (n, kb); consecutive threads take
+// consecutive n so every k-row read is coalesced
+__global__ void quant_mx_cols_kernel(const void* __restrict__ in, int is_bf16, long ld, int K, int N,
+                                     unsigned char* __restrict__ q, unsigned char* __restrict__ s) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int kb = blockIdx.y;
+  if (n >= N) return;
+  float v[32];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    v[i] = ldf(in, (long)(kb * 32 + i) * ld + n, is_bf16);
+    amax = fmaxf(amax, fabsf(v[i]));
+  }
+  const int x = mx_exponent(amax);
+  const float inv = ldexpf(1.f, -x);
+  u32x4 o[2];
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    o[c >> 2][c & 3] = pack4_e4m3(v[4 * c] * inv, v[4 * c + 1] * inv, v[4 * c + 2] * inv, v[4 * c + 3] * inv);
+  u32x4* qo = reinterpret_cast<u32x4*>(q + (long)n * K + (long)kb * 32);
+  qo[0] = o[0];
+  qo[1] = o[1];
+  s[(long)n * (K / 32) + kb] = (unsigned char)(x + 127);
+}
+
+// ---------------------------------------------------------------------------- GEMM
+struct F8Args {
+  const unsigned char *A, *B, *SA, *SB;  // A[M][K], B[N][K] e4m3; SA[M][K/32], SB[N][K/32] e8m0
+  void* C;
+  const void* bias;
+  long ldc;
+  int M, N, K;
+  int flags;  // 1 relu, 2 bias, 4 bias f32, 32 f32 output
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t f8_rsrc(const void* base, long bytes) {
+  const unsigned long long b = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, nb, 0x00020000);
+}
+
+// 16-byte chunk c of a 128-byte LDS row, XOR-swizzled (conflict-free row reads)
+__device__ __forceinline__ int f8_swz(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+constexpr int F8_TILE = 128 * F8_BK;           // bytes of one operand tile
+constexpr int F8_STAGE = 2 * F8_TILE + 2 * 512;  // A, B tiles + A, B scale words (128 rows x 4 B)
+
+__global__ __launch_bounds__(256) void gemm_mx_fp8_kernel(F8Args p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * F8_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntn = (p.N + 127) / 128;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / ntn) * 128, n0 = (tile % ntn) * 128;
+  if (m0 >= p.M) return;
+  const int KB = p.K / 32;  // scale bytes per row
+  const int nk = p.K / F8_BK;
+
+  const __amdgpu_buffer_rsrc_t ra = f8_rsrc(p.A, (long)p.M * p.K);
+  const __amdgpu_buffer_rsrc_t rb = f8_rsrc(p.B, (long)p.N * p.K);
+  const __amdgpu_buffer_rsrc_t rsa = f8_rsrc(p.SA, (long)p.M * KB);
+  const __amdgpu_buffer_rsrc_t rsb = f8_rsrc(p.SB, (long)p.N * KB);
+
+  // data pieces: 16 per operand tile (8 rows x 128 B each), 4 per wave per operand
+  int voa[4], vob[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = wave + 4 * i;
+    const int row = 8 * q + (lane >> 3), slot = lane & 7;
+    const int c = f8_swz(row, slot);
+    voa[i] = (m0 + row) * p.K + 16 * c;
+    vob[i] = (n0 + row) * p.K + 16 * c;
+  }
+  // scale pieces (4 B per lane, 64 rows per instruction): wave 0,1 -> A rows 0-63,64-127;
+  // wave 2,3 -> B rows
+  const int srow = 64 * (wave & 1) + lane;
+  const int vos = ((wave < 2 ? m0 : n0) + srow) * KB;
+  const __amdgpu_buffer_rsrc_t rs = wave < 2 ? rsa : rsb;
+
+  auto issue = [&](int kt, int st) {
+    unsigned char* base = smem + st * F8_STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = wave + 4 * i;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_PTR(void))(base + q * 1024), 16, voa[i], kt * F8_BK, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_PTR(void))(base + F8_TILE + q * 1024), 16, vob[i],
+                                               kt * F8_BK, 0, 0);
+    }
+    unsigned char* sbase = base + 2 * F8_TILE + (wave < 2 ? 0 : 512) + 256 * (wave & 1);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_PTR(void))sbase, 4, vos, kt * 4, 0, 0);
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  const int g = lane >> 4, r16 = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    const unsigned char* As_ = smem + (kt & 1) * F8_STAGE;
+    const unsigned char* Bs_ = As_ + F8_TILE;
+    const unsigned* Sa = reinterpret_cast<const unsigned*>(As_ + 2 * F8_TILE);
+    const unsigned* Sb = reinterpret_cast<const unsigned*>(As_ + 2 * F8_TILE + 512);
+    i32x8 af[4], bfr[4];
+    int sa[4], sb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr * 64 + 16 * i + r16;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(As_ + row * 128 + 16 * f8_swz(row, g));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(As_ + row * 128 + 16 * f8_swz(row, g + 4));
+      af[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      sa[i] = (int)((Sa[row] >> (8 * g)) & 0xff);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wc * 64 + 16 * j + r16;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs_ + row * 128 + 16 * f8_swz(row, g));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs_ + row * 128 + 16 * f8_swz(row, g + 4));
+      bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      sb[j] = (int)((Sb[row] >> (8 * g)) & 0xff);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // C^T block: B rows as the MFMA A operand
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0, 0, 0, sb[j], 0,
+                                                                     sa[i]);
+  }
+
+  // epilogue: lane holds C[row 16 i + r16][cols 16 j + 4 g .. +3]; lane pairs (g, g^1) trade
+  // halves -> 8 consecutive columns per lane -> one 16-byte (bf16) / 2 x 16-byte (f32) store
+  const bool relu = p.flags & 1, has_bias = p.flags & 2, bias_f32 = p.flags & 4, out_f32 = p.flags & 32;
+  const bool even = (g & 1) == 0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int col = n0 + wc * 64 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
+    float bv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bv[e] = 0.f;
+      if (has_bias && col + e < p.N) bv[e] = bias_f32 ? reinterpret_cast<const float*>(p.bias)[col + e]
+                                                      : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[col + e]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 a0 = acc[i][2 * q], a1 = acc[i][2 * q + 1];
+      const f32x4 keep = even ? a0 : a1, send = even ? a1 : a0;
+      f32x4 recv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) recv[e] = __shfl_xor(send[e], 16, 64);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = (even ? keep[e] : recv[e]) + bv[e];
+        v[4 + e] = (even ? recv[e] : keep[e]) + bv[4 + e];
+        if (relu) {
+          v[e] = fmaxf(v[e], 0.f);
+          v[4 + e] = fmaxf(v[4 + e], 0.f);
+        }
+      }
+      const int row = m0 + wr * 64 + 16 * i + r16;
+      if (row >= p.M || col >= p.N) continue;  // N % 8 == 0 (launcher)
+      if (out_f32) {
+        float* C = reinterpret_cast<float*>(p.C) + (long)row * p.ldc + col;
+        *reinterpret_cast<f32x4*>(C) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        u32x4 pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+        *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(p.C) + (long)row * p.ldc + col) = pk;
+      }
+    }
+  }
+}
+
+// one wave, one block-scaled MFMA on raw per-lane operands (layout validation in the tests)
+__global__ void debug_mfma_f8_kernel(const i32x8* a, const i32x8* b, const int* sa, const int* sb, f32x4* c) {
+  const int l = threadIdx.x;
+  c[l] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[l], b[l], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0, sa[l], 0,
+                                                          sb[l]);
+}
+
+}  // namespace
+
+// a, b: 64 lanes x 32 bytes; sa, sb: 64 ints (scale byte in bits 0-7); c: 64 lanes x 4 floats
+LJS_API int ljs_debug_mfma_f8(const void* a, const void* b, const void* sa, const void* sb, void* c,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(debug_mfma_f8_kernel, dim3(1), dim3(64), 0, stream, (const i32x8*)a, (const i32x8*)b,
+                     (const int*)sa, (const int*)sb, (f32x4*)c);
+  return (int)hipGetLastError();
+}
+
+// x[R][K] (row stride ld elements) -> q[R][K], s[R][K/32]; K % 32 == 0, 16-byte aligned rows
+LJS_API int ljs_quant_mx_rows(const void* in, int is_bf16, long ld, int R, int K, void* q, void* s,
+                              hipStream_t stream) {
+  if (K % 32 || ld % 8) return (int)hipErrorInvalidValue;
+  const long nb = (long)R * (K / 32);
+  hipLaunchKernelGGL(quant_mx_rows_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, stream, in, is_bf16, ld,
+                     R, K, (unsigned char*)q, (unsigned char*)s);
+  return (int)hipGetLastError();
+}
+
+// w[K][N] (row stride ld) -> q[N][K], s[N][K/32]
+LJS_API int ljs_quant_mx_cols(const void* in, int is_bf16, long ld, int K, int N, void* q, void* s,
+                              hipStream_t stream) {
+  if (K % 32) return (int)hipErrorInvalidValue;
+  dim3 grid((N + 63) / 64, K / 32);
+  hipLaunchKernelGGL(quant_mx_cols_kernel, grid, dim3(64), 0, stream, in, is_bf16, ld, K, N, (unsigned char*)q,
+                     (unsigned char*)s);
+  return (int)hipGetLastError();
+}
+
+// C[M][N] (bf16, or f32 with flags & 32) = A . B^T of MX-fp8 operands; K % 128 == 0, N % 8 == 0
+LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const void* SB, void* C, const void* bias,
+                            int M, int N, int K, long ldc, int flags, hipStream_t stream) {
+  if (K % F8_BK || N % 8 || ldc % 8 || (long)M * K >= (1L << 31) || (long)N * K >= (1L << 31))
+    return (int)hipErrorInvalidValue;
+  F8Args a;
+  a.A = (const unsigned char*)A; a.B = (const unsigned char*)B;
+  a.SA = (const unsigned char*)SA; a.SB = (const unsigned char*)SB;
+  a.C = C; a.bias = bias; a.ldc = ldc; a.M = M; a.N = N; a.K = K; a.flags = flags;
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  hipLaunchKernelGGL(gemm_mx_fp8_kernel, dim3(tiles), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}

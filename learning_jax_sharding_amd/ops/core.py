@@ -612,23 +612,25 @@ def dot_product_attention(q: ShardedArray, k: ShardedArray, v: ShardedArray, sca
 
 # ----------------------------------------------------------------------------- fused dense
 def dense(x: ShardedArray, kernels: Sequence[ShardedArray], bias: Optional[ShardedArray] = None,
-          compute_dtype=None, relu: bool = False) -> List[ShardedArray]:
+          compute_dtype=None, relu: bool = False, fp8: bool = False) -> List[ShardedArray]:
     """``y_i = x @ W_i (+ b)`` in ``compute_dtype`` for several kernels sharing one sharding.
 
     The kernels are concatenated along the output features on the fly (one
     batched MFMA GEMM launch for Q/K/V).  Returns one array per kernel.  Bias
     and ReLU are fused into the GEMM epilogue when the contraction is local.
+    ``fp8`` runs the local GEMMs in MX-fp8 (:mod:`.fp8`).
     """
     kernels = list(kernels)
     w0 = kernels[0]
     compute_dtype = _dt.canonicalize(compute_dtype) or _dt.result_type(x.dtype, w0.dtype)
     same = all(k.tile == w0.tile and k.shape == w0.shape for k in kernels)
     if not same or (w0.ndim == 2 and w0.tile.tile_shape[1] > 1 and len(kernels) > 1):
-        outs = [dense(x, [k], bias if len(kernels) == 1 else None, compute_dtype, relu)[0] for k in kernels]
+        outs = [dense(x, [k], bias if len(kernels) == 1 else None, compute_dtype, relu, fp8)[0] for k in kernels]
         return outs
     lc, rc = (x.ndim - 1,), (0,)
     p = _plan_dot(x, w0, lc, rc, (), ())
-    _plan.record("dense", k_source=p.k_source, out_tiles=p.out_tile.tile_shape, n_kernels=len(kernels))
+    _plan.record("dense", k_source=p.k_source, out_tiles=p.out_tile.tile_shape, n_kernels=len(kernels),
+                 **({"fp8": True} if fp8 else {}))
     x2 = reshard_tile(x, p.lhs_tile, note="dense.x")
     ws = [reshard_tile(k, p.rhs_tile, note="dense.w") for k in kernels]
     partial = p.k_groups is not None
@@ -644,7 +646,7 @@ def dense(x: ShardedArray, kernels: Sequence[ShardedArray], bias: Optional[Shard
         loc_lists[d] = K.linear(x2.local[d], [w.local[d] for w in ws],
                                 b_loc[d] if fuse_bias else None, compute_dtype,
                                 relu=relu and not partial,
-                                out_dtype=torch.float32 if partial else compute_dtype)
+                                out_dtype=torch.float32 if partial else compute_dtype, fp8=fp8)
     outs = []
     sh = sharding_from_tile(p.out_tile, like=[x.sharding, w0.sharding])
     for i in range(len(kernels)):

@@ -1,0 +1,225 @@
+"""MX-fp8 (OCP e4m3 + e8m0 block scales) dense layers on CDNA4 block-scaled MFMA.
+
+North-star config "attention+FF transformer layer, 2D mesh, fp8 MFMA (CDNA4)" (BASELINE.json;
+the FF formula of ``case6_attention.py:36-40``).  Recipe:
+
+* forward GEMM in MX-fp8: activations quantized per row in 32-element blocks along K
+  (shared exponent = OCP's floor(log2 amax) - 8, plus one when the block max would
+  saturate, i.e. its mantissa exceeds 1.75),
+  weights quantized per output column (also along K) and cached per weight version;
+  ``v_mfma_scale_f32_16x16x128_f8f6f4`` applies the block scales inside the MFMA and
+  accumulates in f32 (twice the bf16 MFMA rate per clock); bias/ReLU fused in the epilogue;
+* backward in bf16 with the same kernels as :mod:`.linear` (gradients keep bf16 range,
+  the common fp8-training split).
+
+On host devices (CPU) the same math runs as an exact emulation (quantize -> dequantize ->
+f32 matmul), so sharded CPU runs and the GPU kernels agree up to f32 summation order.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import hip
+from .linear import _Linear, _bf16
+
+__all__ = ["quantize_mx_ref", "dequantize_mx_ref", "mx_linear_ref", "quant_rows", "quant_cols", "gemm_mx",
+           "linear_fp8", "fp8_dense", "E4M3_MAX", "BLOCK"]
+
+E4M3_MAX = 448.0
+BLOCK = 32
+
+_SIGS = {
+    "ljs_quant_mx_rows": [ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                          ctypes.c_void_p, ctypes.c_void_p],
+    "ljs_quant_mx_cols": [ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                          ctypes.c_void_p, ctypes.c_void_p],
+    "ljs_gemm_mx_fp8": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                        ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int,
+                        ctypes.c_void_p],
+}
+_bound = False
+
+
+def _lib():
+    global _bound
+    L = hip.lib()
+    if not _bound:
+        for name, argt in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = ctypes.c_int
+        _bound = True
+    return L
+
+
+# ----------------------------------------------------------------------------- host reference
+def _block_exponent(amax: torch.Tensor) -> torch.Tensor:
+    """Shared exponent: OCP MX's floor(log2(amax)) - emax(e4m3 = 8), raised by one when the
+    block max would still exceed 448 (mantissa > 1.75), so no element saturates; clamped to
+    e8m0's range."""
+    m, e = torch.frexp(amax)
+    x = e - 1 - 8 + (m > 0.875).to(e.dtype)
+    x = torch.where(amax > 0, x, torch.full_like(x, -127))
+    return x.clamp(-127, 127)
+
+
+def quantize_mx_ref(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """x[..., K] -> (e4m3 values as float8_e4m3fn [..., K], int exponents [..., K/32])."""
+    K = x.shape[-1]
+    assert K % BLOCK == 0, K
+    xb = x.float().reshape(*x.shape[:-1], K // BLOCK, BLOCK)
+    ex = _block_exponent(xb.abs().amax(-1))
+    scaled = xb * torch.ldexp(torch.ones_like(ex, dtype=torch.float32), -ex)[..., None]
+    q = scaled.clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn)
+    return q.reshape(x.shape), ex
+
+
+def dequantize_mx_ref(q: torch.Tensor, ex: torch.Tensor) -> torch.Tensor:
+    K = q.shape[-1]
+    qb = q.float().reshape(*q.shape[:-1], K // BLOCK, BLOCK)
+    return (qb * torch.ldexp(torch.ones_like(ex, dtype=torch.float32), ex)[..., None]).reshape(q.shape)
+
+
+def mx_linear_ref(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], relu: bool,
+                  out_dtype: torch.dtype) -> torch.Tensor:
+    """Emulation of the GPU path: y = deq(q(x)) @ deq(q(w^T))^T (+b)(relu), f32 accumulate."""
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    xd = dequantize_mx_ref(*quantize_mx_ref(x2))
+    wd = dequantize_mx_ref(*quantize_mx_ref(w.t().contiguous()))  # [N][K], blocks along K
+    y = xd @ wd.t()
+    if b is not None:
+        y = y + b.to(out_dtype).float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(out_dtype).reshape(tuple(lead) + (w.shape[1],))
+
+
+# ----------------------------------------------------------------------------- HIP path
+def quant_rows(x2: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """x[R][K] (f32/bf16, unit column stride) -> (q uint8 [R][K], s uint8 [R][K/32])."""
+    R, K = x2.shape
+    if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    q = torch.empty((R, K), dtype=torch.uint8, device=x2.device)
+    s = torch.empty((R, K // BLOCK), dtype=torch.uint8, device=x2.device)
+    rc = _lib().ljs_quant_mx_rows(hip._p(x2), int(x2.dtype == torch.bfloat16), x2.stride(0), R, K, hip._p(q),
+                                  hip._p(s), hip._stream(x2))
+    hip._ck(rc, "quant_mx_rows")
+    return q, s
+
+
+def quant_cols(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """w[K][N] -> (q uint8 [N][K], s uint8 [N][K/32]) (blocks along K, i.e. quantized W^T)."""
+    K, N = w.shape
+    if w.stride(1) != 1:
+        w = w.contiguous()
+    q = torch.empty((N, K), dtype=torch.uint8, device=w.device)
+    s = torch.empty((N, K // BLOCK), dtype=torch.uint8, device=w.device)
+    rc = _lib().ljs_quant_mx_cols(hip._p(w), int(w.dtype == torch.bfloat16), w.stride(0), K, N, hip._p(q), hip._p(s),
+                                  hip._stream(w))
+    hip._ck(rc, "quant_mx_cols")
+    return q, s
+
+
+_WCACHE = {}
+
+
+def _weight_q(w: torch.Tensor):
+    """Cached MX quantization of a weight, refreshed whenever the weight's version moves."""
+    key = (w.data_ptr(), tuple(w.shape), w.dtype, w.device)
+    ent = _WCACHE.get(key)
+    if ent is not None and ent[0] == w._version:
+        return ent[1], ent[2]
+    q, s = quant_cols(w.detach())
+    _WCACHE[key] = (w._version, q, s)
+    return q, s
+
+
+def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: torch.Tensor, bias: Optional[torch.Tensor] = None,
+            relu: bool = False) -> torch.Tensor:
+    flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
+        (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (32 if out.dtype == torch.float32 else 0)
+    rc = _lib().ljs_gemm_mx_fp8(hip._p(qa), hip._p(sa), hip._p(qb), hip._p(sb), hip._p(out), hip._p(bias), M, N, K,
+                                out.stride(0), flags, hip._stream(out))
+    hip._ck(rc, "gemm_mx_fp8")
+    return out
+
+
+class _Fp8Linear(torch.autograd.Function):
+    """Forward on MX-fp8 MFMA; backward = :class:`.linear._Linear`'s bf16 backward (same ctx)."""
+
+    @staticmethod
+    def forward(ctx, x, b, relu, out_dtype, w):
+        lead = x.shape[:-1]
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        M, N = x2.shape[0], w.shape[1]
+        qa, sa = quant_rows(x2)
+        qb, sb = _weight_q(w)
+        od = out_dtype if out_dtype in (torch.bfloat16, torch.float32) else torch.float32
+        out = torch.empty((M, N), dtype=od, device=x.device)
+        bias = None if b is None else (b if b.dtype in (torch.float32, torch.bfloat16) else b.float()).contiguous()
+        gemm_mx(qa, sa, qb, sb, M, N, K, out, bias, relu)
+        y = out.view(tuple(lead) + (N,))
+        if od != out_dtype:
+            y = y.to(out_dtype)
+        xb = _bf16(x2 if x2.is_contiguous() else x2.contiguous())
+        ctx.save_for_backward(xb, b, w, *([y] if relu else []))
+        ctx.meta = (lead, K, M, N, 1, relu, x.dtype, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _Linear.backward(ctx, dy)
+
+
+class _Fp8LinearRef(torch.autograd.Function):
+    """Host emulation with the GPU path's autograd: MX-fp8 forward, bf16 straight-through
+    backward (dX = dY W^T, dW = X^T dY on bf16-rounded operands, f32 accumulation)."""
+
+    @staticmethod
+    def forward(ctx, x, b, relu, out_dtype, w):
+        y = mx_linear_ref(x, w, b, relu, out_dtype)
+        ctx.save_for_backward(x, b, w, y if relu else None)
+        ctx.relu = relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, b, w, y = ctx.saved_tensors
+        K, N = w.shape
+        g = dy.reshape(-1, N).float()
+        if ctx.relu:
+            g = g * (y.reshape(-1, N) > 0).float()
+        g = g.to(torch.bfloat16).float()
+        xb = x.reshape(-1, K).to(torch.bfloat16).float()
+        dx = (g @ w.to(torch.bfloat16).float().t()).to(x.dtype).reshape(x.shape) if ctx.needs_input_grad[0] else None
+        dw = (xb.t() @ g).to(w.dtype) if ctx.needs_input_grad[4] else None
+        db = g.sum(0).to(b.dtype) if (b is not None and ctx.needs_input_grad[1]) else None
+        return dx, db, None, None, dw
+
+
+def supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    K, N = w.shape
+    return x.is_cuda and K % 128 == 0 and N % 8 == 0 and x.shape[-1] == K
+
+
+def linear_fp8(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], relu: bool,
+               out_dtype: torch.dtype) -> torch.Tensor:
+    """Local (per-shard) fp8 dense: HIP block-scaled MFMA on GPU, exact emulation on CPU."""
+    if x.is_cuda:
+        if not supported(x, w):
+            raise ValueError(f"fp8 dense needs K % 128 == 0 and N % 8 == 0, got x {tuple(x.shape)} w {tuple(w.shape)}")
+        return _Fp8Linear.apply(x, b, relu, out_dtype, w)
+    return _Fp8LinearRef.apply(x, b, relu, out_dtype, w)
+
+
+def fp8_dense(x, w, bias=None, relu: bool = False, out_dtype=torch.bfloat16):
+    """Global-view ``relu?(x @ w + b)`` on sharded arrays with MX-fp8 forward GEMMs; the
+    partitioning (weight gathers, partial sums over a sharded contraction) is :func:`core.dense`'s."""
+    from . import core
+    return core.dense(x, [w], bias, compute_dtype=out_dtype, relu=relu, fp8=True)[0]

@@ -83,9 +83,13 @@ def dot_general(a: torch.Tensor, b: torch.Tensor, lc, rc, lb, rb, out_dtype: tor
 
 
 def linear(x: torch.Tensor, ws: Sequence[torch.Tensor], b: Optional[torch.Tensor], compute_dtype: torch.dtype,
-           relu: bool = False, out_dtype: Optional[torch.dtype] = None) -> List[torch.Tensor]:
-    """``[x @ w (+ b)(relu) for w in ws]`` in ``compute_dtype`` (flax ``Dense`` semantics)."""
+           relu: bool = False, out_dtype: Optional[torch.dtype] = None, fp8: bool = False) -> List[torch.Tensor]:
+    """``[x @ w (+ b)(relu) for w in ws]`` in ``compute_dtype`` (flax ``Dense`` semantics);
+    ``fp8`` = MX-fp8 forward GEMMs (HIP block-scaled MFMA, exact emulation on CPU)."""
     out_dtype = out_dtype or compute_dtype
+    if fp8:
+        from . import fp8 as F8
+        return [F8.linear_fp8(x, w, b, relu, out_dtype) for w in ws]
     if use_hip(x):
         return _hip().linear(x, list(ws), b, compute_dtype, relu, out_dtype)
     lead = x.shape[:-1]

@@ -105,3 +105,43 @@ def test_jit_graph_train_step_matches_eager(gpu_devices):
     pe, pg = ljs.tree_util.tree_leaves(se.params), ljs.tree_util.tree_leaves(sg.params)
     for a, b in zip(pe, pg):
         np.testing.assert_allclose(np.asarray(b), np.asarray(a), rtol=1e-4, atol=1e-5)
+
+
+def _run_layer(mesh_shape, fp8, B=2, S=128, M=640, ff=2560):
+    import learning_jax_sharding_amd as ljs
+    import learning_jax_sharding_amd.numpy as jnp
+    from learning_jax_sharding_amd import nn
+    from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
+    from learning_jax_sharding_amd.models import TransformerLayer
+    from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
+    mesh = Mesh(create_device_mesh(mesh_shape), ("data", "model"))
+    rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
+    model = TransformerLayer(M, ff_dim=ff, fp8=fp8)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (B, S, M))
+    params = model.init(ljs.random.PRNGKey(1), x)["params"]
+    params = ljs.device_put(params, nn.logical_to_mesh_sharding(nn.get_partition_spec(params), mesh, rules))
+    x = ljs.device_put(x, NamedSharding(mesh, P("data", "model")))
+
+    def loss(p):
+        return model.apply({"params": p}, x).astype(jnp.float32).sum()
+
+    with mesh, nn.axis_rules(rules):
+        val, g = ljs.value_and_grad(loss)(params)
+    return float(np.asarray(val)), ljs.tree_map(lambda a: np.asarray(a), nn.unbox(g))
+
+
+@pytest.mark.parametrize("mesh_shape", [(1, 1), (2, 2)])
+def test_fp8_layer_gpu_matches_host_emulation(host_devices, gpu_devices, mesh_shape):
+    """attention + MX-fp8 FF layer: HIP block-scaled MFMA path == host emulation."""
+    n = int(np.prod(mesh_shape))
+    host_devices(n)
+    vh, gh = _run_layer(mesh_shape, True)
+    gpu_devices(n)
+    vg, gg = _run_layer(mesh_shape, True)
+    assert abs(vh - vg) <= 3e-2 * max(1.0, abs(vh)), (vh, vg)
+    for path in gh:
+        for k in gh[path]:
+            a, b = gh[path][k], gg[path][k]
+            pairs = [(a[n_], b[n_], n_) for n_ in a] if isinstance(a, dict) else [(a, b, "")]
+            for x_, y_, n_ in pairs:
+                np.testing.assert_allclose(y_, x_, rtol=5e-2, atol=5e-2 * np.abs(x_).max(), err_msg=f"{path}/{k}/{n_}")

@@ -319,3 +319,55 @@ def test_adam_multi_folded_step_increment(hip):
         opt.step()
     for w, r in zip(ws, refs):
         torch.testing.assert_close(w, r.detach(), rtol=1e-5, atol=1e-6)
+
+
+# ----------------------------------------------------------------------------- MX-fp8
+def test_fp8_quantization_matches_reference(hip):
+    from learning_jax_sharding_amd.ops import fp8 as F
+    x = _rand(300, 256, dtype=torch.float32, seed=40) * 3
+    x[5, :32] = 0.0                       # all-zero block
+    x[7, 40] = 1e4                        # outlier block
+    q, s = F.quant_rows(x)
+    qr, er = F.quantize_mx_ref(x.cpu())
+    assert torch.equal(s.cpu().long(), (er + 127).long())
+    assert torch.equal(q.cpu(), qr.view(torch.uint8))
+    qb, sb = F.quant_rows(x.bfloat16())
+    qr2, er2 = F.quantize_mx_ref(x.bfloat16().cpu())
+    assert torch.equal(qb.cpu(), qr2.view(torch.uint8)) and torch.equal(sb.cpu().long(), (er2 + 127).long())
+    w = _rand(256, 136, dtype=torch.float32, seed=41) * 0.05
+    qc, sc = F.quant_cols(w)
+    qr3, er3 = F.quantize_mx_ref(w.t().contiguous().cpu())
+    assert torch.equal(qc.cpu(), qr3.view(torch.uint8)) and torch.equal(sc.cpu().long(), (er3 + 127).long())
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (300, 136, 256), (1024, 2560, 640)])
+@pytest.mark.parametrize("bias,relu,out_f32", [(False, False, True), (True, True, False)])
+def test_fp8_gemm_matches_emulation(hip, M, N, K, bias, relu, out_f32):
+    from learning_jax_sharding_amd.ops import fp8 as F
+    x = _rand(M, K, dtype=torch.float32, seed=42)
+    w = _rand(K, N, dtype=torch.float32, seed=43) * 0.05
+    b = _rand(N, dtype=torch.float32, seed=44) if bias else None
+    qa, sa = F.quant_rows(x)
+    qb, sb = F.quant_cols(w)
+    out = torch.empty((M, N), dtype=torch.float32 if out_f32 else torch.bfloat16, device=dev)
+    F.gemm_mx(qa, sa, qb, sb, M, N, K, out, b, relu)
+    ref = F.mx_linear_ref(x.cpu(), w.cpu(), None if b is None else b.cpu(), relu, out.dtype)
+    tol = 1e-3 if out_f32 else 2e-2
+    torch.testing.assert_close(out.float().cpu(), ref.float(), rtol=tol, atol=tol * 4)
+
+
+def test_fp8_linear_autograd(hip):
+    from learning_jax_sharding_amd.ops import fp8 as F
+    x = _rand(256, 512, dtype=torch.bfloat16, seed=45).requires_grad_()
+    w = (_rand(512, 384, dtype=torch.float32, seed=46) * 0.05).requires_grad_()
+    b = torch.zeros(384, device=dev, requires_grad=True)
+    y = F.linear_fp8(x, w, b, True, torch.bfloat16)
+    g = _rand(256, 384, seed=47)
+    (y.float() * g.float()).sum().backward()
+    ref = F.mx_linear_ref(x.detach().cpu(), w.detach().cpu(), b.detach().cpu(), True, torch.bfloat16)
+    torch.testing.assert_close(y.float().cpu(), ref.float(), rtol=2e-2, atol=3e-2)
+    mask = (y > 0).float()
+    gm = g.float() * mask
+    torch.testing.assert_close(w.grad, x.detach().float().t() @ gm, rtol=3e-2, atol=3e-1)
+    torch.testing.assert_close(x.grad.float(), gm @ w.detach().bfloat16().float().t(), rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(b.grad, gm.sum(0), rtol=1e-2, atol=1e-1)

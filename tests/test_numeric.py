@@ -7,6 +7,7 @@ import pytest
 import torch
 
 import learning_jax_sharding_amd as ljs
+import learning_jax_sharding_amd.numpy as jnp
 from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
 from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
 from learning_jax_sharding_amd.spmd.plan import record_plan
@@ -180,3 +181,48 @@ def test_plan_case6_forward(host_devices):
         model.apply({"params": params}, x)
     kinds = plan.collective_kinds()
     assert kinds == ["all_gather"] * 6 + ["all_to_all"], kinds
+
+
+def _layer_loss_and_grads(mesh_shape, fp8, B=4, S=32, M=128, heads=4, dh=32, ff=256):
+    from learning_jax_sharding_amd import nn
+    from learning_jax_sharding_amd.models import TransformerLayer
+    mesh = Mesh(create_device_mesh(mesh_shape), ("data", "model"))
+    rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
+    model = TransformerLayer(M, heads=heads, dim_head=dh, ff_dim=ff, fp8=fp8)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (B, S, M))
+    params = model.init(ljs.random.PRNGKey(1), x)["params"]
+    params = ljs.device_put(params, nn.logical_to_mesh_sharding(nn.get_partition_spec(params), mesh, rules))
+    x = ljs.device_put(x, NamedSharding(mesh, P("data", "model")))
+
+    def loss(p):
+        return model.apply({"params": p}, x).astype(jnp.float32).sum()
+
+    with mesh, nn.axis_rules(rules):
+        val, g = ljs.value_and_grad(loss)(params)
+    return float(np.asarray(val)), ljs.tree_map(lambda a: np.asarray(a), nn.unbox(g))
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_transformer_layer_sharded_matches_unsharded(host_devices, fp8):
+    """attention + FF layer (MX-fp8 FF GEMMs when fp8): 2x2 mesh == 1 device.  MX blocks never
+    straddle shards (32 | local K), so the fp8 quantization itself is mesh-invariant."""
+    host_devices(4)
+    v1, g1 = _layer_loss_and_grads((1, 1), fp8)
+    v4, g4 = _layer_loss_and_grads((2, 2), fp8)
+    assert abs(v1 - v4) <= 2e-2 * max(1.0, abs(v1)), (v1, v4)
+    for path in g1:
+        for k in g1[path]:
+            a, b = g1[path][k], g4[path][k]
+            if isinstance(a, dict):
+                for n in a:
+                    np.testing.assert_allclose(b[n], a[n], rtol=5e-2, atol=5e-2 * np.abs(a[n]).max(),
+                                               err_msg=f"{path}/{k}/{n}")
+            else:
+                np.testing.assert_allclose(b, a, rtol=5e-2, atol=5e-2 * np.abs(a).max(), err_msg=f"{path}/{k}")
+
+
+def test_fp8_emulation_close_to_bf16(host_devices):
+    host_devices(1)
+    vb, _ = _layer_loss_and_grads((1, 1), False)
+    vf, _ = _layer_loss_and_grads((1, 1), True)
+    assert abs(vb - vf) <= 5e-2 * max(1.0, abs(vb)), (vb, vf)
