@@ -198,8 +198,12 @@ class DistComm:
         return {self.me: out}
 
     def all_reduce(self, xs, groups):
+        return self.all_reduce_({self.me: xs[self.me].clone()}, groups)
+
+    def all_reduce_(self, xs, groups):
+        """In-place all-reduce of this rank's (fresh, contiguous) buffer."""
         g, pg = self._group_of(groups)
-        x = xs[self.me].clone()
+        x = xs[self.me]
         if pg is not None:
             dist.all_reduce(x, group=pg)
         return {self.me: x}

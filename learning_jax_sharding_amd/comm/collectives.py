@@ -55,6 +55,15 @@ class _Spec:
 
 def _run(spec: _Spec, xs: Dict[int, torch.Tensor]) -> Dict[int, torch.Tensor]:
     comm = get_comm()
+    if comm.kind == "dist" and any(t.is_cuda for t in xs.values()):
+        # cross-process (RCCL) collectives are cut points of a segmented HIP-graph capture
+        from ..spmd import graphs
+        if graphs.current() is not None:
+            return graphs.run_collective(lambda: _run_local(comm, spec, xs))[0]
+    return _run_local(comm, spec, xs)
+
+
+def _run_local(comm, spec: _Spec, xs: Dict[int, torch.Tensor]) -> Dict[int, torch.Tensor]:
     k = spec.kind
     if k == "all_gather":
         return comm.all_gather(xs, spec.groups, spec.dim)

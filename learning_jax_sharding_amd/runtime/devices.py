@@ -112,7 +112,7 @@ class _Backend:
             devs = []
             for r in range(world):
                 if platform == "gpu":
-                    local_rank = int(os.environ.get("LOCAL_RANK", r % max(1, torch.cuda.device_count())))
+                    local_rank = _local_gpu(r)
                     td = torch.device("cuda", local_rank if r == rank else 0)
                     phys = local_rank if r == rank else -1
                 else:
@@ -144,6 +144,14 @@ _LOCK = threading.Lock()
 _BACKEND: Optional[_Backend] = None
 
 
+def _local_gpu(rank: Optional[int] = None) -> int:
+    """This process's GPU: LOCAL_RANK, wrapped onto the visible devices (several ranks may
+    share one GPU in tests; ``torch.cuda.device_count`` does not initialise the GPU)."""
+    n = max(1, torch.cuda.device_count())
+    r = int(os.environ.get("LOCAL_RANK", rank if rank is not None else 0))
+    return r % n
+
+
 def initialize_distributed(backend: Optional[str] = None) -> None:
     """Initialise ``torch.distributed`` from the torchrun environment.
 
@@ -160,13 +168,15 @@ def initialize_distributed(backend: Optional[str] = None) -> None:
         return
     platform = os.environ.get("LJS_PLATFORM", "").lower() or ("gpu" if torch.cuda.is_available() else "cpu")
     if backend is None:
-        backend = "nccl" if platform == "gpu" else "gloo"
+        # LJS_DIST_BACKEND=gloo runs GPU ranks over gloo (e.g. several ranks sharing one GPU in
+        # tests, which RCCL does not allow)
+        backend = os.environ.get("LJS_DIST_BACKEND") or ("nccl" if platform == "gpu" else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if platform == "gpu":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     kwargs = {}
     if platform == "gpu":
-        kwargs["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(_local_gpu())
+        if backend == "nccl":
+            kwargs["device_id"] = torch.device("cuda", _local_gpu())
     dist.init_process_group(backend=backend, **kwargs)
     with _LOCK:
         _BACKEND = None

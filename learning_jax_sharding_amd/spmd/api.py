@@ -206,10 +206,10 @@ class Jitted:
                     return y
                 return x
             full[i] = T.tree_map(cp, a, is_leaf=_leaf_is_array)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            out, _ = self._run(tuple(full), {})
+        # one HIP graph per stretch between cross-process collectives (spmd/graphs.py)
+        from .graphs import SegmentedGraph
+        g = SegmentedGraph()
+        out, _ = g.capture(lambda: self._run(tuple(full), {}))
         cap = _Captured(g, in_leaves, out, aliased)
         self._graphs[sig] = cap
         return self._replay(cap, args, sig)
@@ -351,10 +351,27 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
         grads_per_arg = []
         all_leaves = [l for ls in diff_leaves for l in ls]
         inputs = [t for l in all_leaves for t in l.local.values() if t.requires_grad]
-        if outs and inputs:
-            gs = torch.autograd.grad(outs, inputs, seeds, allow_unused=True)
-        else:
-            gs = [None] * len(inputs)
+        # one process per GPU: replica-group gradient sums are bucketed and overlapped with
+        # the rest of the backward pass (parallel/data.py)
+        from ..parallel.data import GradReducer
+        reducer = None
+        hooks = []
+        if inputs and GradReducer.wanted(all_leaves) and all(
+                len(l.local) == 1 and next(iter(l.local.values())).requires_grad for l in all_leaves):
+            reducer = GradReducer(all_leaves)
+            hooks = reducer.attach([next(iter(l.local.values())) for l in all_leaves])
+        from . import graphs as _graphs
+        try:
+            if outs and inputs:
+                # under a segmented capture the backward must run on this thread: HIP ends a
+                # graph capture only on the thread that began it, and collectives cut captures
+                with torch.autograd.set_multithreading_enabled(_graphs.current() is None):
+                    gs = torch.autograd.grad(outs, inputs, seeds, allow_unused=True)
+            else:
+                gs = [None] * len(inputs)
+        finally:
+            for h in hooks:
+                h.remove()
         gmap = {id(t): g for t, g in zip(inputs, gs)}
         pairs = []
         for l in all_leaves:
@@ -363,7 +380,11 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
                 g = gmap.get(id(t))
                 loc[d] = torch.zeros_like(t) if g is None else g
             pairs.append((l, loc))
-        reduced = reduce_replica_grads(pairs)
+        if reducer is not None:
+            red = reducer.finish({i: loc for i, (_, loc) in enumerate(pairs)})
+            reduced = [red[i] for i in range(len(pairs))]
+        else:
+            reduced = reduce_replica_grads(pairs)
         gi = 0
         for a, ls in zip(argnums_t, diff_leaves):
             it = iter(range(gi, gi + len(ls)))

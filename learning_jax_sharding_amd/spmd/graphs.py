@@ -1,0 +1,174 @@
+"""HIP-graph capture cut at collectives ("segmented graphs").
+
+``jit(..., capture=True)`` replays a whole step as HIP graphs instead of re-running Python.
+In one-process-per-GPU runs the step contains RCCL collectives; rather than relying on
+collective capture inside graphs, the capture is CUT at every cross-process collective:
+
+    graph 0 | collective 0 (eager) | graph 1 | collective 1 (eager) | ... | graph n
+
+All segments share one graph memory pool, so tensors produced by one segment keep their
+addresses for the next; a collective's inputs are such static tensors and its outputs are
+allocated once at capture time.  On replay each graph is replayed and each collective
+re-issued on the same stream order, its fresh result copied into the static output.
+
+A collective may also be issued ASYNCHRONOUSLY (data-parallel gradient buckets): it then
+runs on a side comm stream, concurrent with the following graph segments, and the
+consumer joins it with :func:`join` (an event wait, also replayed in order).
+"""
+from __future__ import annotations
+
+import warnings
+from typing import Any, Callable, Dict, List, Optional
+
+import torch
+
+__all__ = ["SegmentedGraph", "current", "run_collective", "join"]
+
+# process-wide (one capture at a time)
+_ACTIVE: List[Optional["SegmentedGraph"]] = [None]
+
+
+def current() -> Optional["SegmentedGraph"]:
+    return _ACTIVE[0]
+
+
+def _copy_into(dst, src):
+    if isinstance(dst, dict):
+        for k, v in dst.items():
+            v.copy_(src[k])
+    elif isinstance(dst, (list, tuple)):
+        for a, b in zip(dst, src):
+            _copy_into(a, b)
+    elif isinstance(dst, torch.Tensor):
+        dst.copy_(src)
+
+
+class SegmentedGraph:
+    def __init__(self):
+        self.pool = torch.cuda.graph_pool_handle()
+        self.items: List[tuple] = []
+        self._g: Optional[torch.cuda.CUDAGraph] = None
+        self.comm_stream: Optional[torch.cuda.Stream] = None
+        self.n_collectives = 0
+
+    # ------------------------------------------------------------------ capture
+    def _begin(self):
+        self._g = torch.cuda.CUDAGraph()
+        # HIP ends a capture only on the thread that began it, so value_and_grad runs the
+        # backward single-threaded while a segmented capture is active (cuts happen inside it)
+        self._g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
+
+    def _cut(self):
+        with warnings.catch_warnings():
+            # two adjacent cut points leave an empty segment: harmless, replays as a no-op
+            warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
+            self._g.capture_end()
+        self.items.append(("graph", self._g))
+        self._g = None
+
+    def capture(self, fn: Callable[[], Any]):
+        """Run ``fn`` once under segmented capture (on a side stream, as HIP graph capture
+        requires); returns its outputs (static tensors)."""
+        torch.cuda.synchronize()
+        stream = torch.cuda.Stream()
+        stream.wait_stream(torch.cuda.current_stream())
+        prev = current()
+        _ACTIVE[0] = self
+        try:
+            with torch.cuda.stream(stream):
+                self._begin()
+                try:
+                    out = fn()
+                finally:
+                    if self._g is not None:
+                        self._cut()
+        finally:
+            _ACTIVE[0] = prev
+        torch.cuda.current_stream().wait_stream(stream)
+        torch.cuda.synchronize()
+        return out
+
+    def collective(self, fn: Callable[[], Any], async_: bool = False):
+        """Inside capture: cut the graph, run ``fn`` eagerly, record it for replay."""
+        self._cut()
+        self.n_collectives += 1
+        if async_:
+            if self.comm_stream is None:
+                self.comm_stream = torch.cuda.Stream()
+            cur = torch.cuda.current_stream()
+            self.comm_stream.wait_stream(cur)
+            with torch.cuda.stream(self.comm_stream):
+                out = fn()
+            ev = torch.cuda.Event()
+            ev.record(self.comm_stream)
+            self.items.append(("async", fn, out, ev))
+            handle = ev
+        else:
+            out = fn()
+            self.items.append(("sync", fn, out))
+            handle = None
+        self._begin()
+        return out, handle
+
+    def join(self, ev: torch.cuda.Event):
+        self._cut()
+        torch.cuda.current_stream().wait_event(ev)
+        self.items.append(("join", ev))
+        self._begin()
+
+    # ------------------------------------------------------------------ replay
+    def replay(self):
+        cur = torch.cuda.current_stream()
+        for it in self.items:
+            kind = it[0]
+            if kind == "graph":
+                it[1].replay()
+            elif kind == "sync":
+                _copy_into(it[2], it[1]())
+            elif kind == "async":
+                _, fn, out, ev = it
+                self.comm_stream.wait_stream(cur)
+                with torch.cuda.stream(self.comm_stream):
+                    _copy_into(out, fn())
+                ev.record(self.comm_stream)
+            elif kind == "join":
+                cur.wait_event(it[1])
+
+
+def run_collective(fn: Callable[[], Any], async_: bool = False):
+    """Issue a cross-process collective: directly (eager), or as a cut point of the active
+    segmented capture.  Returns (outputs, join handle or None)."""
+    seg = current()
+    if seg is None:
+        if async_ and torch.cuda.is_available():
+            cs = _side_stream()
+            cs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cs):
+                out = fn()
+            ev = torch.cuda.Event()
+            ev.record(cs)
+            return out, ev
+        return fn(), None
+    return seg.collective(fn, async_)
+
+
+def join(handle) -> None:
+    """Make the current stream wait for an asynchronous collective."""
+    if handle is None:
+        return
+    seg = current()
+    if seg is not None:
+        seg.join(handle)
+    else:
+        torch.cuda.current_stream().wait_event(handle)
+
+
+_SIDE: Dict[int, torch.cuda.Stream] = {}
+
+
+def _side_stream() -> torch.cuda.Stream:
+    d = torch.cuda.current_device()
+    s = _SIDE.get(d)
+    if s is None:
+        s = _SIDE[d] = torch.cuda.Stream()
+    return s
