@@ -487,6 +487,40 @@ class _Attention(torch.autograd.Function):
         return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), None, None, None
 
 
+def attn_fwd_lse(q, k, v, scale: float, causal: bool = False, q_offset: int = 0):
+    """Raw flash forward of one (q block, kv block) pair: (o bf16 [B,Sq,H,D], lse f32 [B,H,Sq]).
+    lse is log2 of the scaled-score partition function; +inf marks rows with no unmasked key."""
+    B, Sq, H, D = q.shape
+    Sk = k.shape[1]
+    o = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
+    lse = torch.empty((B, H, Sq), dtype=torch.float32, device=q.device)
+    rc = lib().ljs_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), B, Sq, Sk, H, _longs(_strides3(q)),
+                            _longs(_strides3(k)), _longs(_strides3(v)), _longs(_strides3(o)), scale, int(causal),
+                            q_offset, _stream(q))
+    _ck(rc, "ljs_attn_fwd")
+    return o, lse
+
+
+def attn_bwd_block(q, k, v, o, do, lse, scale: float, causal: bool = False, q_offset: int = 0):
+    """Raw flash backward of one kv block given the FINAL output ``o`` and GLOBAL ``lse``
+    (blockwise-separable): returns this block's (dq, dk, dv) contributions in bf16."""
+    B, Sq, H, D = q.shape
+    Sk = k.shape[1]
+    do = do.to(torch.bfloat16)
+    if do.stride(3) != 1:
+        do = do.contiguous()
+    dq = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
+    dk = torch.empty((B, Sk, H, D), dtype=torch.bfloat16, device=q.device)
+    dv = torch.empty((B, Sk, H, D), dtype=torch.bfloat16, device=q.device)
+    delta = torch.empty((B, H, Sq), dtype=torch.float32, device=q.device)
+    rc = lib().ljs_attn_bwd(_p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(delta), _p(dq), _p(dk), _p(dv), B, Sq, Sk,
+                            H, _longs(_strides3(q)), _longs(_strides3(k)), _longs(_strides3(v)), _longs(_strides3(o)),
+                            _longs(_strides3(do)), _longs(_strides3(dq)), _longs(_strides3(dk)), _longs(_strides3(dv)),
+                            scale, int(causal), q_offset, _stream(q))
+    _ck(rc, "ljs_attn_bwd")
+    return dq, dk, dv
+
+
 def attention(q, k, v, scale: float, causal: bool = False, q_offset: int = 0) -> torch.Tensor:
     ok = (q.shape[-1] == 64 and k.shape[-1] == 64 and v.shape[-1] == 64 and q.stride(-1) == 1
           and k.stride(-1) == 1 and v.stride(-1) == 1)

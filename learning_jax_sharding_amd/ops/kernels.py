@@ -137,3 +137,51 @@ def attention(q, k, v, scale: float, causal: bool = False, q_offset: int = 0) ->
     if use_hip(q):
         return _hip().attention(q, k, v, scale, causal, q_offset)
     return attention_reference(q, k, v, scale, causal, q_offset)
+
+
+_LOG2E = 1.4426950408889634
+
+
+def _block_scores(q, k, scale, causal, q_offset):
+    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * scale
+    if causal:
+        Sq, Sk = q.shape[1], k.shape[1]
+        qi = torch.arange(Sq, device=q.device)[:, None] + q_offset
+        ki = torch.arange(Sk, device=q.device)[None, :]
+        s = s.masked_fill(ki > qi, float("-inf"))
+    return s
+
+
+def attention_fwd_lse(q, k, v, scale: float, causal: bool = False, q_offset: int = 0):
+    """One (q block, kv block) flash forward: (o normalised within the block, lse) with lse in
+    the HIP kernels' convention - log2 of the scaled-score partition function, +inf for rows
+    without any unmasked key."""
+    if use_hip(q):
+        return _hip().attn_fwd_lse(q, k, v, scale, causal, q_offset)
+    s = _block_scores(q, k, scale, causal, q_offset)
+    m = s.amax(-1, keepdim=True)
+    empty = torch.isinf(m) & (m < 0)
+    m = torch.where(empty, torch.zeros_like(m), m)
+    p = torch.exp(s - m)
+    l = p.sum(-1, keepdim=True)
+    probs = (p / l.clamp(min=1e-30)).to(v.dtype).float()
+    o = torch.einsum("bhqk,bkhd->bqhd", probs, v.float()).to(v.dtype)
+    lse = ((m + torch.log(l)) * _LOG2E).squeeze(-1)
+    lse = torch.where(empty.squeeze(-1), torch.full_like(lse, float("inf")), lse)
+    return o, lse
+
+
+def attention_bwd_block(q, k, v, o, do, lse, scale: float, causal: bool = False, q_offset: int = 0):
+    """One kv block's (dq, dk, dv) given the final output ``o`` and global (log2) ``lse``."""
+    if use_hip(q):
+        return _hip().attn_bwd_block(q, k, v, o, do, lse, scale, causal, q_offset)
+    s = _block_scores(q, k, scale, causal, q_offset)
+    p = torch.exp(s - (lse / _LOG2E)[..., None])
+    dof = do.float()
+    dp = torch.einsum("bqhd,bkhd->bhqk", dof, v.float())
+    delta = (dof * o.float()).sum(-1).permute(0, 2, 1)[..., None]       # [b,h,q,1]
+    ds = p * (dp - delta)
+    dq = torch.einsum("bhqk,bkhd->bqhd", ds, k.float()) * scale
+    dk = torch.einsum("bhqk,bqhd->bkhd", ds, q.float()) * scale
+    dv = torch.einsum("bhqk,bqhd->bkhd", p.to(v.dtype).float(), dof)
+    return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)

@@ -1,0 +1,179 @@
+"""Sequence / context parallelism for attention.
+
+The reference shards the sequence over ``model`` through the (misnamed) ``embed`` logical
+axis on activations (``case6_attention.py:105-107,114-116,161``) and GSPMD gathers the full
+K/V before the score einsum (``case6_attention.py:125-133``; SURVEY §2.7 "AG K", "AG V").
+Two schedules are provided on (batch, seq, heads, head_dim) arrays whose seq dim is sharded:
+
+* ``mode="allgather"`` - the reference's plan: all-gather K and V over the sequence group,
+  then one flash-attention kernel per shard with its query offset (this is what
+  :func:`ops.core.dot_product_attention` lowers to);
+* ``mode="ring"`` - ring attention: the K/V blocks travel around the sequence group; each
+  step runs the flash kernel of the local queries against the block in hand and merges
+  the partial softmax through the log-sum-exp (the kernels' log2 domain), so no device
+  ever holds more than two K/V blocks.  The backward replays the ring with the GLOBAL
+  log-sum-exp and final output (flash backward is blockwise separable): dQ accumulates
+  locally, dK/dV accumulators travel with their blocks and arrive home after the last
+  hop.  Causal blocks entirely above the diagonal are skipped.
+
+Memory per device is O(S/n) for K/V instead of O(S), the stepping stone to long-context
+training on 288 GB parts; on xGMI the hop is a point-to-point neighbour transfer, one link.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..array import ShardedArray
+from ..comm import collectives as C
+from ..comm.backend import Transfer
+from ..ops import core
+from ..ops import kernels as K
+from ..spmd import plan as _plan
+from ..spmd.reshard import reshard_tile
+
+__all__ = ["context_parallel_attention", "ring_attention"]
+
+
+def context_parallel_attention(q: ShardedArray, k: ShardedArray, v: ShardedArray, scale: Optional[float] = None,
+                               causal: bool = False, mode: str = "allgather") -> ShardedArray:
+    if mode == "allgather":
+        return core.dot_product_attention(q, k, v, scale=scale, causal=causal)
+    if mode == "ring":
+        return ring_attention(q, k, v, scale=scale, causal=causal)
+    raise ValueError(f"unknown context-parallel mode {mode!r}")
+
+
+# ----------------------------------------------------------------------------- ring
+def _full(t: torch.Tensor):
+    return tuple(slice(0, s) for s in t.shape)
+
+
+def _rotate(xs: Dict[int, torch.Tensor], nxt: Dict[int, int]) -> Dict[int, torch.Tensor]:
+    """Send every device's tensor to its ring successor (one point-to-point hop).  The
+    transfer list is global (every ring member's hop, identical on all processes); each
+    process only holds - and receives into - its own devices' blocks."""
+    t0 = next(iter(xs.values()))
+    full = _full(t0)
+    transfers = [Transfer(nxt[d], d, full, full) for d in sorted(nxt)]
+    meta = {d: (tuple(t.shape), t.dtype, t.device) for d, t in xs.items()}
+    return C._run(C._Spec("exchange", transfers=transfers, out_meta=meta), xs)
+
+
+def _merge(o, lse, o_s, lse_s):
+    """Merge two partial attention results (o normalised per part, lse in log2)."""
+    neg = torch.full_like(lse, float("-inf"))
+    a = torch.where(torch.isinf(lse) & (lse > 0), neg, lse)        # +inf marks "no keys"
+    b = torch.where(torch.isinf(lse_s) & (lse_s > 0), neg, lse_s)
+    m = torch.maximum(a, b)
+    m0 = torch.where(torch.isinf(m), torch.zeros_like(m), m)
+    wa, wb = torch.exp2(a - m0), torch.exp2(b - m0)
+    tot = wa + wb
+    lse_new = torch.where(tot > 0, m0 + torch.log2(tot), torch.full_like(m, float("inf")))
+    inv = torch.where(tot > 0, 1.0 / tot, torch.zeros_like(tot))
+    ca = (wa * inv).permute(0, 2, 1)[..., None]                      # [b, q, h, 1]
+    cb = (wb * inv).permute(0, 2, 1)[..., None]
+    o_new = o.float() * ca + o_s.float() * cb
+    return o_new, lse_new
+
+
+class _RingAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, meta, devs, *flat):
+        scale, causal, pos, n, nxt, prv, s_loc = meta
+        nd = len(devs)
+        q = dict(zip(devs, flat[:nd]))
+        kk = dict(zip(devs, flat[nd:2 * nd]))
+        vv = dict(zip(devs, flat[2 * nd:]))
+        o = {d: None for d in devs}
+        lse = {d: None for d in devs}
+        kb, vb = dict(kk), dict(vv)
+        for s in range(n):
+            for d in devs:
+                j = (pos[d] - s) % n                       # global block index of the kv in hand
+                if causal and j > pos[d]:
+                    continue                               # block entirely above the diagonal
+                o_s, l_s = K.attention_fwd_lse(q[d], kb[d], vb[d], scale, causal, (pos[d] - j) * s_loc)
+                if o[d] is None:
+                    o[d], lse[d] = o_s.float(), l_s
+                else:
+                    o[d], lse[d] = _merge(o[d], lse[d], o_s, l_s)
+            if s + 1 < n:
+                kb, vb = _rotate(kb, nxt), _rotate(vb, nxt)
+        outs = []
+        for d in devs:
+            if o[d] is None:                                # only possible for n == 0
+                o[d] = torch.zeros_like(q[d], dtype=torch.float32)
+                lse[d] = torch.full(q[d].shape[:1] + q[d].shape[2:3] + q[d].shape[1:2], float("inf"),
+                                    device=q[d].device)
+            outs.append(o[d].to(vv[d].dtype))
+        ctx.meta = meta
+        ctx.devs = devs
+        ctx.save_for_backward(*flat, *outs, *[lse[d] for d in devs])
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gos):
+        scale, causal, pos, n, nxt, prv, s_loc = ctx.meta
+        devs = ctx.devs
+        nd = len(devs)
+        saved = ctx.saved_tensors
+        q = dict(zip(devs, saved[:nd]))
+        kb = dict(zip(devs, saved[nd:2 * nd]))
+        vb = dict(zip(devs, saved[2 * nd:3 * nd]))
+        o = dict(zip(devs, saved[3 * nd:4 * nd]))
+        lse = dict(zip(devs, saved[4 * nd:5 * nd]))
+        do = {d: (g if g is not None else torch.zeros_like(o[d])) for d, g in zip(devs, gos)}
+        dq = {d: torch.zeros(q[d].shape, dtype=torch.float32, device=q[d].device) for d in devs}
+        dk = {d: torch.zeros(kb[d].shape, dtype=torch.float32, device=kb[d].device) for d in devs}
+        dv = {d: torch.zeros(vb[d].shape, dtype=torch.float32, device=vb[d].device) for d in devs}
+        for s in range(n):
+            for d in devs:
+                j = (pos[d] - s) % n
+                if causal and j > pos[d]:
+                    continue
+                gq, gk, gv = K.attention_bwd_block(q[d], kb[d], vb[d], o[d], do[d], lse[d], scale, causal,
+                                                   (pos[d] - j) * s_loc)
+                dq[d] += gq.float()
+                dk[d] += gk.float()
+                dv[d] += gv.float()
+            # the kv blocks and their gradient accumulators travel together; n hops bring
+            # every accumulator back to the block's owner
+            dk, dv = _rotate(dk, nxt), _rotate(dv, nxt)
+            if s + 1 < n:
+                kb, vb = _rotate(kb, nxt), _rotate(vb, nxt)
+        grads = [dq[d].to(q[d].dtype) for d in devs] + [dk[d].to(kb[d].dtype) for d in devs] + \
+            [dv[d].to(vb[d].dtype) for d in devs]
+        return (None, None) + tuple(grads)
+
+
+def ring_attention(q: ShardedArray, k: ShardedArray, v: ShardedArray, scale: Optional[float] = None,
+                   causal: bool = False) -> ShardedArray:
+    """Ring (blockwise, log-sum-exp merged) attention over q's sequence sharding."""
+    if scale is None:
+        scale = q.shape[-1] ** -0.5
+    qt = q.tile
+    if qt.tile_shape[3] > 1:
+        q = reshard_tile(q, qt.unshard([3]), note="ring.q")
+        qt = q.tile
+    k = reshard_tile(k, qt, note="ring.k") if k.tile != qt else k
+    v = reshard_tile(v, qt, note="ring.v") if v.tile != qt else v
+    n = qt.tile_shape[1]
+    if n == 1:
+        return core.dot_product_attention(q, k, v, scale=scale, causal=causal)
+    groups = qt.groups_along([1])
+    pos, nxt, prv = {}, {}, {}
+    for g in groups:
+        for i, d in enumerate(g):
+            pos[d] = i
+            nxt[d] = g[(i + 1) % len(g)]
+            prv[d] = g[(i - 1) % len(g)]
+    s_loc = qt.shard_shape(q.shape)[1]
+    devs = tuple(sorted(q.local))
+    _plan.record("ring_attention", ring=n, q_tiles=qt.tile_shape, hops=n - 1)
+    meta = (float(scale), bool(causal), pos, n, nxt, prv, s_loc)
+    flat = [q.local[d] for d in devs] + [k.local[d] for d in devs] + [v.local[d] for d in devs]
+    outs = _RingAttention.apply(meta, devs, *flat)
+    return ShardedArray(q.shape, v.dtype, q.sharding, dict(zip(devs, outs)))

@@ -145,3 +145,39 @@ def test_fp8_layer_gpu_matches_host_emulation(host_devices, gpu_devices, mesh_sh
             pairs = [(a[n_], b[n_], n_) for n_ in a] if isinstance(a, dict) else [(a, b, "")]
             for x_, y_, n_ in pairs:
                 np.testing.assert_allclose(y_, x_, rtol=5e-2, atol=5e-2 * np.abs(x_).max(), err_msg=f"{path}/{k}/{n_}")
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_ring_attention_gpu_matches_allgather(gpu_devices, causal):
+    """Ring attention on the HIP flash kernels (per-block lse, global-lse backward) == the
+    all-gather-KV plan, on a 1x4 virtual mesh over one MI355X."""
+    gpu_devices(4)
+    import learning_jax_sharding_amd as ljs
+    import learning_jax_sharding_amd.numpy as jnp
+    from learning_jax_sharding_amd.array import ShardedArray
+    from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
+    from learning_jax_sharding_amd.parallel import sequence as SQ
+    from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
+    from learning_jax_sharding_amd.spmd.api import _fresh_leaf
+    mesh = Mesh(create_device_mesh((1, 4)), ("data", "model"))
+    g = torch.Generator().manual_seed(0)
+    arrs = [torch.randn(2, 256, 4, 64, generator=g).bfloat16() for _ in range(3)]
+    cot = torch.randn(2, 256, 4, 64, generator=g)
+    sh = NamedSharding(mesh, P("data", "model"))
+    res = {}
+    for mode in ("allgather", "ring"):
+        leaves = [_fresh_leaf(ljs.device_put(a, sh)) for a in arrs]
+        out = SQ.context_parallel_attention(*leaves, causal=causal, mode=mode)
+        loss = (out.astype(jnp.float32) * ljs.device_put(cot, sh)).sum()
+        ins = [t for l in leaves for t in l.local.values()]
+        outs = list(loss.local.values())
+        gs = torch.autograd.grad(outs, ins, [torch.full_like(t, 1.0 / len(outs)) for t in outs])
+        n_loc = len(leaves[0].local)
+        glob = []
+        for ai, leaf in enumerate(leaves):
+            loc = {d: gs[ai * n_loc + i].float() for i, d in enumerate(leaf.local)}
+            glob.append(np.asarray(ShardedArray(leaf.shape, torch.float32, leaf.sharding, loc)))
+        res[mode] = (np.asarray(out.astype(jnp.float32)), glob)
+    np.testing.assert_allclose(res["ring"][0], res["allgather"][0], rtol=2e-2, atol=2e-2)
+    for a, b in zip(res["ring"][1], res["allgather"][1]):
+        np.testing.assert_allclose(a, b, rtol=3e-2, atol=3e-2 * max(1.0, np.abs(b).max()))

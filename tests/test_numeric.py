@@ -226,3 +226,93 @@ def test_fp8_emulation_close_to_bf16(host_devices):
     vb, _ = _layer_loss_and_grads((1, 1), False)
     vf, _ = _layer_loss_and_grads((1, 1), True)
     assert abs(vb - vf) <= 5e-2 * max(1.0, abs(vb)), (vb, vf)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("mesh_shape", [(1, 4), (2, 2)])
+def test_ring_attention_matches_allgather(host_devices, causal, mesh_shape):
+    """Ring attention (K/V blocks travel, LSE-merged) == the all-gather-KV plan, values and
+    gradients, on the seq-sharded layout of case6."""
+    host_devices(4)
+    from learning_jax_sharding_amd.parallel import sequence as SQ
+    mesh = Mesh(create_device_mesh(mesh_shape), ("data", "model"))
+    g = torch.Generator().manual_seed(0)
+    B, S, H, D = 2, 32, 2, 16
+    arrs = [torch.randn(B, S, H, D, generator=g).bfloat16() for _ in range(3)]
+    cot = torch.randn(B, S, H, D, generator=g)
+    sh = NamedSharding(mesh, P("data", "model"))
+    res = {}
+    for mode in ("allgather", "ring"):
+        q, k, v = (ljs.device_put(a, sh) for a in arrs)
+        leaves = [ljs.spmd.api._fresh_leaf(a) for a in (q, k, v)]
+        out = SQ.context_parallel_attention(*leaves, causal=causal, mode=mode)
+        loss = (out.astype(jnp.float32) * ljs.device_put(cot, sh)).sum()
+        ins = [t for l in leaves for t in l.local.values()]
+        outs = [t for t in loss.local.values()]
+        gs = torch.autograd.grad(outs, ins, [torch.full_like(t, 1.0 / len(outs)) for t in outs])
+        # assemble per-argument global gradients
+        n_loc = len(leaves[0].local)
+        glob = []
+        for ai, leaf in enumerate(leaves):
+            loc = {d: gs[ai * n_loc + i] for i, d in enumerate(leaf.local)}
+            from learning_jax_sharding_amd.array import ShardedArray
+            ga = ShardedArray(leaf.shape, torch.float32, leaf.sharding, {d: t.float() for d, t in loc.items()})
+            glob.append(np.asarray(ga))
+        res[mode] = (np.asarray(out.astype(jnp.float32)), glob)
+    np.testing.assert_allclose(res["ring"][0], res["allgather"][0], rtol=2e-2, atol=2e-2)
+    for a, b in zip(res["ring"][1], res["allgather"][1]):
+        np.testing.assert_allclose(a, b, rtol=3e-2, atol=3e-2 * max(1.0, np.abs(b).max()))
+
+
+@pytest.mark.parametrize("preset", ["gspmd2d", "fsdp"])
+def test_rule_presets_match_unsharded(host_devices, preset):
+    """The attention block under the Megatron ("gspmd2d") and FSDP rule presets == 1 device."""
+    host_devices(4)
+    from learning_jax_sharding_amd import nn, parallel
+    from learning_jax_sharding_amd.models import MultiHeadAttention
+
+    def run(mesh_shape, rules):
+        mesh = Mesh(create_device_mesh(mesh_shape), ("data", "model"))
+        model = MultiHeadAttention(64, heads=4, dim_head=16)
+        x = ljs.random.normal(ljs.random.PRNGKey(0), (4, 32, 64))
+        params = model.init(ljs.random.PRNGKey(1), x)["params"]
+        params = ljs.device_put(params, nn.logical_to_mesh_sharding(nn.get_partition_spec(params), mesh, rules))
+        x = ljs.device_put(x, NamedSharding(mesh, P("data")))
+
+        def loss(p):
+            return model.apply({"params": p}, x).astype(jnp.float32).sum()
+        with mesh, nn.axis_rules(rules):
+            val, g = ljs.value_and_grad(loss)(params)
+        return float(np.asarray(val)), ljs.tree_map(lambda a: np.asarray(a), nn.unbox(g))
+
+    v1, g1 = run((1, 1), parallel.rules(preset))
+    v4, g4 = run((2, 2), parallel.rules(preset))
+    assert abs(v1 - v4) <= 2e-2 * max(1.0, abs(v1))
+    for k in g1:
+        for n in g1[k]:
+            np.testing.assert_allclose(g4[k][n], g1[k][n], rtol=3e-2, atol=3e-2 * np.abs(g1[k][n]).max())
+
+
+def test_column_row_parallel_and_fsdp_prefetch(host_devices):
+    host_devices(4)
+    from learning_jax_sharding_amd.parallel import fsdp, tensor
+    mesh = Mesh(create_device_mesh((2, 2)), ("data", "model"))
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((8, 16, 32)).astype(np.float32)
+    W1 = rng.standard_normal((32, 64)).astype(np.float32) * 0.1
+    W2 = rng.standard_normal((64, 32)).astype(np.float32) * 0.1
+    ref = np.maximum(X @ W1, 0) @ W2
+    with mesh:
+        x = ljs.device_put(X, NamedSharding(mesh, P("data")))
+        w1 = ljs.device_put(W1, NamedSharding(mesh, P(None, "model")))
+        w2 = ljs.device_put(W2, NamedSharding(mesh, P("model", None)))
+        h = tensor.column_parallel(x, w1, relu=True, compute_dtype=jnp.float32)
+        y = tensor.row_parallel(h, w2, compute_dtype=jnp.float32)
+        np.testing.assert_allclose(np.asarray(y), ref, rtol=1e-4, atol=1e-4)
+        # FSDP: params sharded over data, gathered on the side (prefetch) before use
+        params = fsdp.shard_params({"w1": W1, "w2": W2}, mesh, "data")
+        assert params["w1"].tile.tile_shape[1] == 2 or params["w1"].tile.tile_shape[0] == 2
+        full = fsdp.Prefetcher(mesh, "data").prefetch(params).wait()
+        assert full["w1"].tile.tile_shape == (1, 1)
+        y2 = ljs.numpy.matmul(x, full["w1"])
+        np.testing.assert_allclose(np.asarray(y2), X @ W1, rtol=1e-4, atol=1e-4)
