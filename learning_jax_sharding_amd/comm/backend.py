@@ -57,11 +57,36 @@ def _acc_dtype(dt: torch.dtype) -> torch.dtype:
 
 
 class LocalComm:
+    """Single-process backend.  Groups whose members are distinct physical GPUs go through
+    the native single-controller RCCL communicator (``comm/native.py``); everything else
+    (host devices, virtual devices sharing a GPU) through direct copies."""
+
     kind = "local"
+
+    def __init__(self):
+        self._native = None
+
+    def _rccl(self, g, xs):
+        from . import native
+        devs = [xs[d].device for d in g]
+        if not native.eligible(devs):
+            return None
+        if self._native is None:
+            self._native = native.NativeRccl()
+        return self._native
 
     def all_gather(self, xs: Dict[int, torch.Tensor], groups: Groups, dim: int) -> Dict[int, torch.Tensor]:
         out = {}
         for g in groups:
+            nat = self._rccl(g, xs)
+            if nat is not None:
+                n = len(g)
+                gathered = nat.all_gather([xs[d].contiguous() for d in g])
+                for d, buf in zip(g, gathered):
+                    x = xs[d]
+                    out[d] = buf.movedim(0, dim).reshape(x.shape[:dim] + (n * x.shape[dim],) +
+                                                         x.shape[dim + 1:]).contiguous()
+                continue
             parts = [xs[d] for d in g]
             for d in g:
                 dev = xs[d].device
@@ -73,6 +98,17 @@ class LocalComm:
         for g in groups:
             if len(g) == 1:
                 out[g[0]] = xs[g[0]].clone()
+                continue
+            nat = self._rccl(g, xs)
+            if nat is not None:
+                n = len(g)
+                ins = []
+                for d in g:
+                    x = xs[d]
+                    s = x.shape[dim] // n
+                    ins.append(x.reshape(x.shape[:dim] + (n, s) + x.shape[dim + 1:]).movedim(dim, 0).contiguous())
+                for d, r in zip(g, nat.reduce_scatter(ins)):
+                    out[d] = r
                 continue
             dev0 = xs[g[0]].device
             dt = xs[g[0]].dtype
@@ -86,10 +122,21 @@ class LocalComm:
         return out
 
     def all_reduce(self, xs, groups):
+        return self.all_reduce_({d: t.clone() for d, t in xs.items()}, groups)
+
+    def all_reduce_(self, xs, groups):
+        """All-reduce into the given (fresh, contiguous) tensors where the backend allows."""
         out = {}
         for g in groups:
             if len(g) == 1:
-                out[g[0]] = xs[g[0]].clone()
+                out[g[0]] = xs[g[0]]
+                continue
+            nat = self._rccl(g, xs)
+            if nat is not None:
+                ts = [xs[d].contiguous() for d in g]
+                nat.all_reduce(ts)
+                for d, t in zip(g, ts):
+                    out[d] = t
                 continue
             dev0 = xs[g[0]].device
             dt = xs[g[0]].dtype
@@ -109,6 +156,13 @@ class LocalComm:
             n = len(g)
             perm = perms[gi] if perms is not None else list(range(n))
             chunks = {d: xs[d].chunk(n, split_dim) for d in g}
+            nat = self._rccl(g, xs) if n > 1 else None
+            if nat is not None:
+                # member i sends chunk perm[r] to member r; receives member-major
+                sends = [torch.stack([chunks[d][perm[r]] for r in range(n)]).contiguous() for d in g]
+                for d, recv in zip(g, nat.all_to_all(sends)):
+                    out[d] = torch.cat(list(recv.unbind(0)), concat_dim).contiguous()
+                continue
             for i, d in enumerate(g):
                 dev = xs[d].device
                 out[d] = torch.cat([chunks[s][perm[i]].to(dev) for s in g], concat_dim).contiguous()

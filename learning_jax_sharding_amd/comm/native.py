@@ -1,0 +1,156 @@
+"""Single-controller RCCL over xGMI through the native runtime (``_lib/libljs_runtime.so``,
+``csrc/runtime/comm.cpp``).
+
+One Python process driving several physical MI355X (the JAX-like single-controller mode of
+SURVEY §2.5/§7) issues every collective of a device group for all members inside one
+``ncclGroupStart/End``, each member on its own current HIP stream.  Communicators come from
+``ncclCommInitAll`` and are cached per ordered tuple of physical GPUs.  Groups containing
+the same GPU twice (virtual devices) are not eligible: the copy-based loopback path of
+:class:`~.backend.LocalComm` serves them.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Dict, Optional, Sequence, Tuple
+
+import torch
+
+__all__ = ["available", "runtime", "device_info", "eligible", "NativeRccl"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIBPATH = os.path.join(os.path.dirname(_HERE), "_lib", "libljs_runtime.so")
+_LIB = None
+_LOCK = threading.Lock()
+_VP = ctypes.c_void_p
+
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5}
+
+
+def runtime():
+    global _LIB
+    if _LIB is None:
+        with _LOCK:
+            if _LIB is None:
+                if not os.path.exists(_LIBPATH):
+                    raise RuntimeError(f"native runtime not built: {_LIBPATH} (run csrc/build.py)")
+                L = ctypes.CDLL(_LIBPATH)
+                sig = {
+                    "ljs_rt_version": [],
+                    "ljs_rt_device_info": [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_long)],
+                    "ljs_comm_init": [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(_VP)],
+                    "ljs_comm_destroy": [_VP],
+                    "ljs_comm_all_reduce": [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.c_int, ctypes.POINTER(_VP)],
+                    "ljs_comm_all_gather": [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.POINTER(_VP)],
+                    "ljs_comm_reduce_scatter": [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.c_size_t,
+                                                ctypes.c_int, ctypes.c_int, ctypes.POINTER(_VP)],
+                    "ljs_comm_all_to_all": [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.POINTER(_VP)],
+                }
+                for name, argt in sig.items():
+                    fn = getattr(L, name)
+                    fn.argtypes = argt
+                    fn.restype = ctypes.c_int
+                L.ljs_comm_error_string.argtypes = [ctypes.c_int]
+                L.ljs_comm_error_string.restype = ctypes.c_char_p
+                _LIB = L
+    return _LIB
+
+
+def available() -> bool:
+    try:
+        runtime()
+        return True
+    except (RuntimeError, OSError):
+        return False
+
+
+def device_info(dev: int = 0) -> Dict[str, int]:
+    """CU count, LDS per CU, L2 bytes, wavefront size, XCD hint and HBM bytes of a GPU."""
+    out = (ctypes.c_int * 5)()
+    hbm = ctypes.c_long()
+    rc = runtime().ljs_rt_device_info(dev, out, ctypes.byref(hbm))
+    if rc:
+        raise RuntimeError(f"hipGetDeviceProperties failed: {rc}")
+    return {"cus": out[0], "lds_bytes": out[1], "l2_bytes": out[2], "wavefront": out[3], "xcds": out[4],
+            "hbm_bytes": hbm.value}
+
+
+def eligible(devices: Sequence[torch.device]) -> bool:
+    if os.environ.get("LJS_NATIVE_RCCL", "1") == "0" or len(devices) < 2:
+        return False
+    if not all(d.type == "cuda" for d in devices):
+        return False
+    idx = [d.index for d in devices]
+    return len(set(idx)) == len(idx) and available()
+
+
+def _ptrs(ts):
+    return (_VP * len(ts))(*[t.data_ptr() for t in ts])
+
+
+def _streams(ts):
+    return (_VP * len(ts))(*[torch.cuda.current_stream(t.device).cuda_stream for t in ts])
+
+
+class NativeRccl:
+    """Communicator cache + collectives over groups of distinct physical GPUs."""
+
+    def __init__(self):
+        self._comms: Dict[Tuple[int, ...], int] = {}
+
+    def comm(self, gpus: Tuple[int, ...]) -> int:
+        h = self._comms.get(gpus)
+        if h is None:
+            arr = (ctypes.c_int * len(gpus))(*gpus)
+            out = _VP()
+            rc = runtime().ljs_comm_init(len(gpus), arr, ctypes.byref(out))
+            self._check(rc, "ncclCommInitAll")
+            h = self._comms[gpus] = out.value
+        return h
+
+    @staticmethod
+    def _check(rc, what):
+        if rc:
+            raise RuntimeError(f"{what} failed: {runtime().ljs_comm_error_string(rc).decode()}")
+
+    def all_reduce(self, ts: Sequence[torch.Tensor]) -> None:
+        """In-place sum over the members' contiguous tensors (member order = list order)."""
+        h = self.comm(tuple(t.device.index for t in ts))
+        rc = runtime().ljs_comm_all_reduce(h, _ptrs(ts), _ptrs(ts), ts[0].numel(), _DT[ts[0].dtype], 0, _streams(ts))
+        self._check(rc, "all_reduce")
+
+    def all_gather(self, ts: Sequence[torch.Tensor]):
+        """Returns per member a [n, *shape] tensor of every member's block, member-major."""
+        n = len(ts)
+        outs = [torch.empty((n,) + tuple(t.shape), dtype=t.dtype, device=t.device) for t in ts]
+        h = self.comm(tuple(t.device.index for t in ts))
+        rc = runtime().ljs_comm_all_gather(h, _ptrs(ts), _ptrs(outs), ts[0].numel(), _DT[ts[0].dtype], _streams(ts))
+        self._check(rc, "all_gather")
+        return outs
+
+    def reduce_scatter(self, ts: Sequence[torch.Tensor]):
+        """ts[i] is [n, *chunk] (chunk r destined to member r); returns each member's summed chunk."""
+        outs = [torch.empty(tuple(t.shape[1:]), dtype=t.dtype, device=t.device) for t in ts]
+        h = self.comm(tuple(t.device.index for t in ts))
+        rc = runtime().ljs_comm_reduce_scatter(h, _ptrs(ts), _ptrs(outs), outs[0].numel(), _DT[ts[0].dtype], 0,
+                                               _streams(ts))
+        self._check(rc, "reduce_scatter")
+        return outs
+
+    def all_to_all(self, ts: Sequence[torch.Tensor]):
+        """ts[i] is [n, *chunk]; chunk r of member i lands as chunk i of member r."""
+        outs = [torch.empty_like(t) for t in ts]
+        h = self.comm(tuple(t.device.index for t in ts))
+        rc = runtime().ljs_comm_all_to_all(h, _ptrs(ts), _ptrs(outs), ts[0][0].numel(), _DT[ts[0].dtype],
+                                           _streams(ts))
+        self._check(rc, "all_to_all")
+        return outs
+
+    def close(self):
+        for h in self._comms.values():
+            runtime().ljs_comm_destroy(h)
+        self._comms.clear()

@@ -1,0 +1,157 @@
+// Single-controller RCCL communicators over xGMI (one process drives several
+// MI355X; every collective of a device group is issued for all members inside one
+// ncclGroupStart/End, each member on its own HIP stream, so one thread cannot deadlock).
+//
+// A communicator covers an ordered list of DISTINCT physical GPUs (RCCL admits a GPU once
+// per communicator; virtual devices sharing a GPU use the framework's copy-based loopback
+// backend instead).  Communicators are created with ncclCommInitAll and cached by the Python
+// side per device group.  Buffers and streams are passed per member, in member order.
+//
+// C ABI (ctypes), every call returns 0 or an ncclResult_t / hipError_t code.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#define LJS_RT_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+struct Comm {
+  std::vector<ncclComm_t> comms;  // one per member, rank = member index
+  std::vector<int> devs;
+};
+
+ncclDataType_t to_nccl(int dt) {
+  switch (dt) {
+    case 0: return ncclFloat32;
+    case 1: return ncclBfloat16;
+    case 2: return ncclFloat16;
+    case 3: return ncclInt32;
+    case 4: return ncclInt64;
+    case 5: return ncclUint8;
+    default: return ncclFloat32;
+  }
+}
+
+ncclRedOp_t to_op(int op) {
+  switch (op) {
+    case 1: return ncclMax;
+    case 2: return ncclMin;
+    case 3: return ncclProd;
+    default: return ncclSum;
+  }
+}
+
+size_t dt_size(int dt) {
+  switch (dt) {
+    case 1: case 2: return 2;
+    case 4: return 8;
+    case 5: return 1;
+    default: return 4;
+  }
+}
+
+}  // namespace
+
+LJS_RT_API int ljs_rt_version() { return 1; }
+
+LJS_RT_API int ljs_rt_device_info(int dev, int* out /* cus, lds_bytes, l2_bytes, warp, xcds_hint */,
+                                  long* hbm_bytes) {
+  hipDeviceProp_t p;
+  hipError_t e = hipGetDeviceProperties(&p, dev);
+  if (e != hipSuccess) return (int)e;
+  out[0] = p.multiProcessorCount;
+  out[1] = (int)p.maxSharedMemoryPerMultiProcessor;
+  out[2] = p.l2CacheSize;
+  out[3] = p.warpSize;
+  out[4] = p.multiProcessorCount >= 256 ? 8 : 1;
+  *hbm_bytes = (long)p.totalGlobalMem;
+  return 0;
+}
+
+// handle out; devs = n distinct physical GPU ordinals in member order
+LJS_RT_API int ljs_comm_init(int n, const int* devs, void** handle) {
+  Comm* c = new Comm();
+  c->devs.assign(devs, devs + n);
+  c->comms.resize(n);
+  ncclResult_t r = ncclCommInitAll(c->comms.data(), n, devs);
+  if (r != ncclSuccess) {
+    delete c;
+    return (int)r;
+  }
+  *handle = c;
+  return 0;
+}
+
+LJS_RT_API int ljs_comm_destroy(void* handle) {
+  Comm* c = static_cast<Comm*>(handle);
+  for (auto& cm : c->comms) ncclCommDestroy(cm);
+  delete c;
+  return 0;
+}
+
+// in-place capable: sendbufs[i] may equal recvbufs[i]
+LJS_RT_API int ljs_comm_all_reduce(void* handle, void* const* sendbufs, void* const* recvbufs, size_t count, int dt,
+                                   int op, void* const* streams) {
+  Comm* c = static_cast<Comm*>(handle);
+  ncclGroupStart();
+  for (size_t i = 0; i < c->comms.size(); ++i)
+    ncclAllReduce(sendbufs[i], recvbufs[i], count, to_nccl(dt), to_op(op), c->comms[i], (hipStream_t)streams[i]);
+  return (int)ncclGroupEnd();
+}
+
+// recvbufs[i] holds n * count elements, member-rank-major
+LJS_RT_API int ljs_comm_all_gather(void* handle, void* const* sendbufs, void* const* recvbufs, size_t count, int dt,
+                                   void* const* streams) {
+  Comm* c = static_cast<Comm*>(handle);
+  ncclGroupStart();
+  for (size_t i = 0; i < c->comms.size(); ++i)
+    ncclAllGather(sendbufs[i], recvbufs[i], count, to_nccl(dt), c->comms[i], (hipStream_t)streams[i]);
+  return (int)ncclGroupEnd();
+}
+
+// sendbufs[i] holds n * count elements (chunk r goes to member r); recv count elements
+LJS_RT_API int ljs_comm_reduce_scatter(void* handle, void* const* sendbufs, void* const* recvbufs, size_t count,
+                                       int dt, int op, void* const* streams) {
+  Comm* c = static_cast<Comm*>(handle);
+  ncclGroupStart();
+  for (size_t i = 0; i < c->comms.size(); ++i)
+    ncclReduceScatter(sendbufs[i], recvbufs[i], count, to_nccl(dt), to_op(op), c->comms[i],
+                      (hipStream_t)streams[i]);
+  return (int)ncclGroupEnd();
+}
+
+// all-to-all of n equal chunks of `count` elements: chunk r of member i lands as chunk i of member r
+LJS_RT_API int ljs_comm_all_to_all(void* handle, void* const* sendbufs, void* const* recvbufs, size_t count, int dt,
+                                   void* const* streams) {
+  Comm* c = static_cast<Comm*>(handle);
+  const size_t n = c->comms.size();
+  const size_t bytes = count * dt_size(dt);
+  ncclGroupStart();
+  for (size_t i = 0; i < n; ++i) {
+    for (size_t r = 0; r < n; ++r) {
+      ncclSend(static_cast<const char*>(sendbufs[i]) + r * bytes, count, to_nccl(dt), (int)r, c->comms[i],
+               (hipStream_t)streams[i]);
+      ncclRecv(static_cast<char*>(recvbufs[i]) + r * bytes, count, to_nccl(dt), (int)r, c->comms[i],
+               (hipStream_t)streams[i]);
+    }
+  }
+  return (int)ncclGroupEnd();
+}
+
+// point-to-point permutation: pairs (src member, dst member), buffers per pair
+LJS_RT_API int ljs_comm_permute(void* handle, int npairs, const int* src, const int* dst, void* const* sendbufs,
+                                void* const* recvbufs, size_t count, int dt, void* const* streams) {
+  Comm* c = static_cast<Comm*>(handle);
+  ncclGroupStart();
+  for (int p = 0; p < npairs; ++p) {
+    ncclSend(sendbufs[p], count, to_nccl(dt), dst[p], c->comms[src[p]], (hipStream_t)streams[src[p]]);
+    ncclRecv(recvbufs[p], count, to_nccl(dt), src[p], c->comms[dst[p]], (hipStream_t)streams[dst[p]]);
+  }
+  return (int)ncclGroupEnd();
+}
+
+LJS_RT_API const char* ljs_comm_error_string(int code) { return ncclGetErrorString((ncclResult_t)code); }

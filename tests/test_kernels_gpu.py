@@ -371,3 +371,22 @@ def test_fp8_linear_autograd(hip):
     torch.testing.assert_close(w.grad, x.detach().float().t() @ gm, rtol=3e-2, atol=3e-1)
     torch.testing.assert_close(x.grad.float(), gm @ w.detach().bfloat16().float().t(), rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(b.grad, gm.sum(0), rtol=1e-2, atol=1e-1)
+
+
+def test_native_runtime_device_info_and_single_member_comm(hip):
+    """Native runtime library: device properties and an ncclCommInitAll communicator (a
+    1-member communicator on a one-GPU box; multi-GPU groups use the same calls)."""
+    from learning_jax_sharding_amd.comm import native
+    info = native.device_info(0)
+    assert info["cus"] >= 1 and info["wavefront"] == 64 and info["hbm_bytes"] > 0
+    nat = native.NativeRccl()
+    t = torch.arange(1024, dtype=torch.float32, device=dev)
+    nat.all_reduce([t])
+    torch.cuda.synchronize()
+    torch.testing.assert_close(t, torch.arange(1024, dtype=torch.float32, device=dev))
+    g = nat.all_gather([t[:16].contiguous()])
+    torch.cuda.synchronize()
+    assert g[0].shape == (1, 16)
+    nat.close()
+    maps = open(f"/proc/{__import__('os').getpid()}/maps").read()
+    assert "libljs_runtime.so" in maps
