@@ -31,6 +31,8 @@ from .ops.core import with_sharding_constraint  # noqa: F401
 from . import debug, experimental, lax, ops, random, tree_util  # noqa: F401
 from . import nn, optim, training, models  # noqa: F401
 from . import numpy  # noqa: F401
+from . import parallel, profiler  # noqa: F401
+from .utils import checkpoint  # noqa: F401
 from .utils.tree import tree_map, tree_leaves, tree_flatten, tree_unflatten  # noqa: F401
 
 

@@ -21,6 +21,7 @@ SURVEY §3.3, realised on torch autograd instead of a separate AD system.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -55,12 +56,21 @@ class _Spec:
 
 def _run(spec: _Spec, xs: Dict[int, torch.Tensor]) -> Dict[int, torch.Tensor]:
     comm = get_comm()
+    out = None
     if comm.kind == "dist" and any(t.is_cuda for t in xs.values()):
         # cross-process (RCCL) collectives are cut points of a segmented HIP-graph capture
         from ..spmd import graphs
         if graphs.current() is not None:
-            return graphs.run_collective(lambda: _run_local(comm, spec, xs))[0]
-    return _run_local(comm, spec, xs)
+            out = graphs.run_collective(lambda: _run_local(comm, spec, xs))[0]
+    if out is None:
+        out = _run_local(comm, spec, xs)
+    if _DEBUG:
+        from ..profiler import after_collective
+        after_collective(spec.kind, out)
+    return out
+
+
+_DEBUG = os.environ.get("LJS_DEBUG_SYNC", "0") == "1" or os.environ.get("LJS_DEBUG_NANS", "0") == "1"
 
 
 def _run_local(comm, spec: _Spec, xs: Dict[int, torch.Tensor]) -> Dict[int, torch.Tensor]:

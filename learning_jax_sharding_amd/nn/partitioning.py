@@ -57,6 +57,7 @@ class Partitioned:
 
 
 LogicallyPartitioned = Partitioned
+Partitioned.__pytree_child_names__ = ("value",)
 
 T.register_pytree_node(Partitioned, lambda p: ((p.value,), (p.names, p.mesh)),
                        lambda aux, ch: Partitioned(ch[0], aux[0], aux[1]))

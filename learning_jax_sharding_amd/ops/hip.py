@@ -83,9 +83,15 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+_DEBUG_SYNC = os.environ.get("LJS_DEBUG_SYNC", "0") == "1"
+
+
 def _ck(rc: int, name: str):
     if rc != 0:
         raise RuntimeError(f"{name} failed with hipError {rc}")
+    if _DEBUG_SYNC or os.environ.get("LJS_DEBUG_SYNC") == "1":
+        from ..profiler import after_kernel
+        after_kernel(name)
 
 
 _WS = {}

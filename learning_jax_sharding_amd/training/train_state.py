@@ -48,3 +48,4 @@ def _unflatten(aux, ch):
 
 
 T.register_pytree_node(TrainState, _flatten, _unflatten)
+TrainState.__pytree_child_names__ = ("step", "params", "opt_state")

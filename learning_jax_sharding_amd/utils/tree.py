@@ -101,6 +101,41 @@ def tree_flatten(tree, is_leaf=None):
     return leaves, td
 
 
+def tree_leaves_with_path(tree, is_leaf=None) -> List[Tuple[Tuple[Any, ...], Any]]:
+    """``[(path, leaf)]`` in :func:`tree_flatten` order; path entries are dict keys, sequence
+    indices, namedtuple field names or child indices of registered nodes."""
+    out: List[Tuple[Tuple[Any, ...], Any]] = []
+
+    def walk(x, path):
+        if is_leaf is not None and is_leaf(x):
+            out.append((path, x))
+            return
+        if x is None:
+            return
+        t = type(x)
+        if getattr(t, "__pytree_leaf__", False):
+            out.append((path, x))
+        elif t in _REGISTRY:
+            children, _ = _REGISTRY[t][0](x)
+            names = getattr(x, "__pytree_child_names__", None)
+            for i, c in enumerate(children):
+                walk(c, path + ((names[i] if names else i),))
+        elif isinstance(x, dict):
+            for k in sorted(x.keys(), key=lambda k: (str(type(k)), k)):
+                walk(x[k], path + (k,))
+        elif _is_namedtuple(x):
+            for f, c in zip(x._fields, x):
+                walk(c, path + (f,))
+        elif isinstance(x, (tuple, list)):
+            for i, c in enumerate(x):
+                walk(c, path + (i,))
+        else:
+            out.append((path, x))
+
+    walk(tree, ())
+    return out
+
+
 def _unflatten(td: TreeDef, it):
     k = td.kind
     if k == "leaf":
