@@ -35,10 +35,11 @@ struct AttnArgs {
   const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* o; const bf16_t* dout;
   bf16_t* out;                     // fwd: O ; bwd dkv: dK ; bwd dq: dQ
   bf16_t* out2;                    // bwd dkv: dV
+  bf16_t* out3;                    // bwd fused: dQ (out = dK, out2 = dV)
   float* lse;                      // [B][H][Sq], log2 domain of scaled scores
   const float* delta;              // [B][H][Sq]
   long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh;
-  long do_sb, do_ss, do_sh, out_sb, out_ss, out_sh, out2_sb, out2_ss, out2_sh;
+  long do_sb, do_ss, do_sh, out_sb, out_ss, out_sh, out2_sb, out2_ss, out2_sh, out3_sb, out3_ss, out3_sh;
   int Sq, Sk, H;
   float scale, scale_log2;
   int causal, q_offset;
@@ -482,6 +483,209 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   if (qok) store_row_T(a.out + b * a.out_sb + (long)qrow * a.out_ss + h * a.out_sh, dq, a.scale, lane);
 }
 
+// ---------------------------------------------------------------- fused short-key backward
+// Sk <= 256: ONE workgroup (8 waves) per (batch, head) keeps K and V in LDS (each wave
+// owns 32 keys for dK / dV), then sweeps the query blocks once.  S and dP are computed
+// once per (query, key) -- the split dQ / dK-dV kernels compute them twice -- and dS^T goes
+// through LDS ([keys][queries] image, ds_write_b64) so dQ^T = K^T dS^T reads it with the
+// transposing LDS read.  delta = rowsum(dO o O) is formed while staging each query block.
+constexpr int FK = 256;        // max keys
+constexpr int FWAVES = 8;      // 32 keys per wave
+constexpr int FT = FWAVES * 64;
+
+// one 16-byte chunk per thread of a 64-row (seq, d) tile
+struct TileRegs1 {
+  u32x4 v;
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ base, long ld, int r0, int rlim, int tid) {
+    int row = tid >> 3, c16 = tid & 7, r = r0 + row;
+    v = r < rlim ? *reinterpret_cast<const u32x4*>(base + (long)r * ld + c16 * 8) : u32x4{0, 0, 0, 0};
+  }
+  __device__ __forceinline__ void store(bf16_t* lds, int tid) const {
+    *reinterpret_cast<u32x4*>(lds + img16(tid >> 3, tid & 7)) = v;
+  }
+};
+
+__device__ __forceinline__ float dot_bf16x8(const u32x4& x, const u32x4& y) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    s = fmaf(__uint_as_float(x[k] << 16), __uint_as_float(y[k] << 16), s);
+    s = fmaf(__uint_as_float(x[k] & 0xffff0000u), __uint_as_float(y[k] & 0xffff0000u), s);
+  }
+  return s;
+}
+
+// S/P/dP/dS for this wave's 32 keys x 64 queries; dK^T, dV^T accumulate; dS^T -> LDS
+template <bool MASK>
+__device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, const bf16_t* Ot,
+                                           const float* lse_s, const float* dl_s, bf16_t* dSt,
+                                           const bf16_t* Ks, const bf16_t* Vs, f32x4 (&dk)[2][4],
+                                           f32x4 (&dv)[2][4], int q0, int key0, int lane) {
+  const int g = lane >> 4;
+  // two 32-query halves: P / dS of a half feed the dK/dV MFMAs right away (register pressure)
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    f32x4 p[2][2], ds[2][2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 2 * s2 + tt;
+      const f32x4 lse = *reinterpret_cast<const f32x4*>(lse_s + 16 * t + 4 * g);
+      const f32x4 dl = *reinterpret_cast<const f32x4*>(dl_s + 16 * t + 4 * g);
+      const bf16x8 q0f = frag_rows(Qt, 16 * t, 0, lane), q1f = frag_rows(Qt, 16 * t, 1, lane);
+      const bf16x8 o0f = frag_rows(Ot, 16 * t, 0, lane), o1f = frag_rows(Ot, 16 * t, 1, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+        s = mfma16x16x32(q0f, frag_rows(Ks, key0 + 16 * j, 0, lane), s);
+        s = mfma16x16x32(q1f, frag_rows(Ks, key0 + 16 * j, 1, lane), s);
+        dp = mfma16x16x32(o0f, frag_rows(Vs, key0 + 16 * j, 0, lane), dp);
+        dp = mfma16x16x32(o1f, frag_rows(Vs, key0 + 16 * j, 1, lane), dp);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pv = fast_exp2(fmaf(s[r], a.scale_log2, -lse[r]));
+          if constexpr (MASK) {
+            int q = q0 + 16 * t + 4 * g + r, key = key0 + 16 * j + (lane & 15);
+            bool ok = q < a.Sq && key < a.Sk && !(a.causal && key > q + a.q_offset);
+            pv = ok ? pv : 0.f;
+          }
+          p[j][tt][r] = pv;
+          ds[j][tt][r] = pv * (dp[r] - dl[r]);
+        }
+        // dS^T row (this lane's key), queries 16t + 4g .. +3
+        u32x2 w;
+        w[0] = pack_bf16x2(ds[j][tt][0], ds[j][tt][1]);
+        w[1] = pack_bf16x2(ds[j][tt][2], ds[j][tt][3]);
+        *reinterpret_cast<u32x2*>(dSt + img8(key0 + 16 * j + (lane & 15), 4 * t + g)) = w;
+      }
+    }
+    bf16x8 pb[2], sb[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      pb[j] = frag_acc(p[j][0], p[j][1]);
+      sb[j] = frag_acc(ds[j][0], ds[j][1]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x8 oa = frag_tr(Ot, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+      bf16x8 qa = frag_tr(Qt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        dv[j][dt] = mfma16x16x32(oa, pb[j], dv[j][dt]);
+        dk[j][dt] = mfma16x16x32(qa, sb[j], dk[j][dt]);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[FK * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[FK * D];
+  __shared__ __attribute__((aligned(16))) bf16_t dSt[FK * BLK];
+  __shared__ __attribute__((aligned(16))) bf16_t QO[4 * BLK * D];  // Q[2], dO[2]
+  __shared__ __attribute__((aligned(16))) float rowc[2][2][BLK];    // [buf][lse, delta][query]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int key0 = wave * 32;
+  const bool active = key0 < a.Sk;
+  const int nk32 = (a.Sk + 31) / 32;
+
+  const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
+  const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
+#pragma unroll
+  for (int i = 0; i < FK * 8 / FT; ++i) {
+    int c = tid + FT * i, row = c >> 3, c16 = c & 7;
+    u32x4 x = row < a.Sk ? *reinterpret_cast<const u32x4*>(kb + (long)row * a.k_ss + c16 * 8) : u32x4{0, 0, 0, 0};
+    u32x4 y = row < a.Sk ? *reinterpret_cast<const u32x4*>(vb + (long)row * a.v_ss + c16 * 8) : u32x4{0, 0, 0, 0};
+    *reinterpret_cast<u32x4*>(Ks + img16(row, c16)) = x;
+    *reinterpret_cast<u32x4*>(Vs + img16(row, c16)) = y;
+  }
+
+  const bf16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
+  const bf16_t* dob = a.dout + b * a.do_sb + h * a.do_sh;
+  const bf16_t* ob = a.o + b * a.o_sb + h * a.o_sh;
+  const float* lse = a.lse + ((long)b * a.H + h) * a.Sq;
+  const int nqt = (a.Sq + BLK - 1) / BLK;
+
+  TileRegs1 tq, tdo, to;
+  float lse_v = 0.f;
+  auto fetch = [&](int q0) {
+    tq.load(qb, a.q_ss, q0, a.Sq, tid);
+    tdo.load(dob, a.do_ss, q0, a.Sq, tid);
+    to.load(ob, a.o_ss, q0, a.Sq, tid);
+    if (tid < BLK) lse_v = q0 + tid < a.Sq ? lse[q0 + tid] : INFINITY;
+  };
+  auto stage = [&](int buf) {
+    tq.store(QO + buf * BLK * D, tid);
+    tdo.store(QO + (2 + buf) * BLK * D, tid);
+    float s = dot_bf16x8(to.v, tdo.v);  // 8 threads per query row
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if ((tid & 7) == 0) rowc[buf][1][tid >> 3] = s;
+    if (tid < BLK) rowc[buf][0][tid] = lse_v;
+  };
+  if (nqt > 0) {
+    fetch(0);
+    stage(0);
+  }
+  __syncthreads();
+
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dk[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  const int qt = wave & 3, dt0 = 2 * (wave >> 2);
+  for (int it = 0; it < nqt; ++it) {
+    const int cur = it & 1;
+    const int q0 = it * BLK;
+    const bool more = it + 1 < nqt;
+    if (more) fetch(q0 + BLK);
+    const bf16_t* Qt = QO + cur * BLK * D;
+    const bf16_t* Ot = QO + (2 + cur) * BLK * D;
+    if (active) {
+      const bool need_mask = q0 + BLK > a.Sq || key0 + 32 > a.Sk || (a.causal && key0 + 31 > q0 + a.q_offset);
+      if (need_mask) fused_tile<true>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, Ks, Vs, dk, dv, q0, key0, lane);
+      else fused_tile<false>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, Ks, Vs, dk, dv, q0, key0, lane);
+    }
+    __syncthreads();
+    // dQ^T (d tiles dt0, dt0+1) x queries 16qt..16qt+15 = K^T dS^T over all keys
+    f32x4 dq[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int s2 = 0; s2 < nk32; ++s2) {
+      bf16x8 sb = frag_tr(dSt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * qt, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        bf16x8 ka = frag_tr(Ks, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * (dt0 + i), lane);
+        dq[i] = mfma16x16x32(ka, sb, dq[i]);
+      }
+    }
+    const int qrow = q0 + 16 * qt + (lane & 15);
+    if (qrow < a.Sq) {
+      bf16_t* rowp = a.out3 + b * a.out3_sb + (long)qrow * a.out3_ss + h * a.out3_sh;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        u32x2 w;
+        w[0] = pack_bf16x2(dq[i][0] * a.scale, dq[i][1] * a.scale);
+        w[1] = pack_bf16x2(dq[i][2] * a.scale, dq[i][3] * a.scale);
+        *reinterpret_cast<u32x2*>(rowp + 16 * (dt0 + i) + 4 * g) = w;
+      }
+    }
+    if (more) stage(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int key = key0 + 16 * j + (lane & 15);
+    if (key < a.Sk) {
+      store_row_T(a.out + b * a.out_sb + (long)key * a.out_ss + h * a.out_sh, dk[j], a.scale, lane);
+      store_row_T(a.out2 + b * a.out2_sb + (long)key * a.out2_ss + h * a.out2_sh, dv[j], 1.f, lane);
+    }
+  }
+}
+
 }  // namespace
 
 // strides are in elements, ordered (batch, seq, head); head_dim must be 64 and contiguous.
@@ -503,6 +707,11 @@ LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, v
   return (int)hipGetLastError();
 }
 
+// backward implementation for Sk <= 256: 1 = fused single-pass kernel (default), 0 = split
+// dQ + dK/dV kernels; -1 = read LJS_ATTN_BWD_FUSED at the next call
+static int g_bwd_fused = -1;
+LJS_API void ljs_attn_set_bwd_fused(int v) { g_bwd_fused = v; }
+
 // dq/dk/dv outputs get their own strides; delta is a [B][H][Sq] f32 workspace
 LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                          const void* lse, void* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H,
@@ -521,6 +730,18 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
   a.Sq = Sq; a.Sk = Sk; a.H = H;
   a.scale = scale; a.scale_log2 = scale * LOG2E;
   a.causal = causal; a.q_offset = q_offset;
+  if (g_bwd_fused < 0) {
+    const char* e = getenv("LJS_ATTN_BWD_FUSED");
+    g_bwd_fused = e ? atoi(e) : 1;
+  }
+  if (g_bwd_fused && Sk <= FK) {
+    AttnArgs f = a;
+    f.out = (bf16_t*)dk; f.out_sb = dks[0]; f.out_ss = dks[1]; f.out_sh = dks[2];
+    f.out2 = (bf16_t*)dv; f.out2_sb = dvs[0]; f.out2_ss = dvs[1]; f.out2_sh = dvs[2];
+    f.out3 = (bf16_t*)dq; f.out3_sb = dqs[0]; f.out3_ss = dqs[1]; f.out3_sh = dqs[2];
+    hipLaunchKernelGGL(attn_bwd_fused_kernel, dim3(H, B), dim3(FT), 0, stream, f);
+    return (int)hipGetLastError();
+  }
   // dQ first: it also computes delta, which the dK/dV kernel consumes (stream order)
   AttnArgs c = a;
   c.out = (bf16_t*)dq; c.out_sb = dqs[0]; c.out_ss = dqs[1]; c.out_sh = dqs[2];

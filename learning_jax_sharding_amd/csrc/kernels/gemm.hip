@@ -391,21 +391,27 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
   ta.init(p.lda, wave, lane);
   tb.init(p.ldb, wave, lane);
 
-  // issue-side cursor: the item whose K-tiles are being fetched (advanced incrementally)
+  // issue-side cursor: the item whose K-tiles are being fetched, advanced incrementally with
+  // 32-bit scalar offsets (the launcher guarantees operand extents < 2^30 bytes)
   int is_item = 0, is_kt = 0;
   __amdgpu_buffer_rsrc_t ra, rb;
-  long a_org = 0, b_org = 0;
+  int a_off = 0, b_off = 0;
+  const int a_step = (int)a_kt, b_step = (int)b_kt;
   auto load_item = [&](int k) {
     const WorkItem w = decode_item(p, slot + G * k, ntm, ntn);
     ra = make_rsrc(p.A + (long)w.b * p.sA, a_bytes);
     rb = make_rsrc(p.B + (long)w.b * p.sB, b_bytes);
-    a_org = (A_KC ? (long)w.m0 * BM * p.lda : (long)w.m0 * BM) * 2 + w.kt0 * a_kt;
-    b_org = (B_KC ? (long)w.n0 * BN * p.ldb : (long)w.n0 * BN) * 2 + w.kt0 * b_kt;
+    a_off = __builtin_amdgcn_readfirstlane(
+        (int)((A_KC ? (long)w.m0 * BM * p.lda : (long)w.m0 * BM) * 2 + w.kt0 * a_kt));
+    b_off = __builtin_amdgcn_readfirstlane(
+        (int)((B_KC ? (long)w.n0 * BN * p.ldb : (long)w.n0 * BN) * 2 + w.kt0 * b_kt));
   };
   auto issue_next = [&](int st) {
     if (is_kt == 0) load_item(is_item);
-    ta.issue(ra, smem + st * STAGE, __builtin_amdgcn_readfirstlane((int)(a_org + is_kt * a_kt)), wave);
-    tb.issue(rb, smem + st * STAGE + A_TILE, __builtin_amdgcn_readfirstlane((int)(b_org + is_kt * b_kt)), wave);
+    ta.issue(ra, smem + st * STAGE, a_off, wave);
+    tb.issue(rb, smem + st * STAGE + A_TILE, b_off, wave);
+    a_off += a_step;
+    b_off += b_step;
     if (++is_kt == nk) { is_kt = 0; ++is_item; }
   };
 
@@ -546,7 +552,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
           acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // drain before the next item's counted waits; after the block's last item the wave just
+      // ends (its atomics complete on their own and the CU is free for the next block sooner)
+      if (it + 1 < my_items) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
 }
@@ -564,6 +572,14 @@ LJS_DMA_INST_LAYOUTS(2)
 LJS_DMA_INST_LAYOUTS(4)
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, false)
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, true)
+// 128x128 with 8 waves (2 x 4, 64x32 each): two waves per SIMD at one block per CU, so a
+// deep (3-4 stage) ring does not cost MFMA/LDS overlap
+#define LJS_DMA_INST_8W(NST)                                                                                \
+  LJS_DMA_INST(128, 128, 2, 4, NST, false, false, true) LJS_DMA_INST(128, 128, 2, 4, NST, true, true, false) \
+  LJS_DMA_INST(128, 128, 2, 4, NST, true, true, true)
+LJS_DMA_INST_8W(3)
+LJS_DMA_INST_8W(4)
+#undef LJS_DMA_INST_8W
 #undef LJS_DMA_INST_LAYOUTS
 #undef LJS_DMA_INST
 
@@ -654,9 +670,23 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
                                         (((uintptr_t)C) & 15) == 0);
   if (tile > 1000 && !(dma_ok && dma_store_ok)) tile = 128;
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
+  if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;
   if (tile == 2561) {
     if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);
     else e = launch_dma<256, 128, 4, 2, 3, true, true, false>(a, stream, 0);
+  } else if (tile == 12883 || tile == 12884) {
+    // 128x128, 8 waves, 3 / 4 stages (weight-grad MN x MN f32, or k-contiguous operands)
+    const bool d4 = tile == 12884;
+    if (!a_kc) {
+      if (d4) e = launch_dma<128, 128, 2, 4, 4, false, false, true>(a, stream, 0);
+      else e = launch_dma<128, 128, 2, 4, 3, false, false, true>(a, stream, 0);
+    } else if (out_f32) {
+      if (d4) e = launch_dma<128, 128, 2, 4, 4, true, true, true>(a, stream, 0);
+      else e = launch_dma<128, 128, 2, 4, 3, true, true, true>(a, stream, 0);
+    } else {
+      if (d4) e = launch_dma<128, 128, 2, 4, 4, true, true, false>(a, stream, 0);
+      else e = launch_dma<128, 128, 2, 4, 3, true, true, false>(a, stream, 0);
+    }
   } else if (tile == 1284 || tile == 1282) {
     // (plain if/else, not ?: -- see the explicit-instantiation note above)
 #define LJS_DMA(AK, BK_, OF)                                                              \

@@ -71,6 +71,15 @@ def lib():
     return _LIB
 
 
+def set_attention_bwd_fused(enabled: bool):
+    """Select the attention backward for key lengths <= 256: the single-pass fused kernel
+    (default) or the split dQ + dK/dV kernels (always used above 256 keys)."""
+    fn = lib().ljs_attn_set_bwd_fused
+    fn.argtypes = [c_int]
+    fn.restype = None
+    fn(1 if enabled else 0)
+
+
 def available() -> bool:
     try:
         lib()

@@ -20,6 +20,9 @@ q1, k1, v1 = (t.detach().requires_grad_() for t in (q, k, v))
 o = hip.attention(q1, k1, v1, scale)
 g = torch.randn_like(o)
 res["fwd+bwd"] = timeit(lambda: torch.autograd.grad(hip.attention(q1, k1, v1, scale), (q1, k1, v1), g))
+hip.set_attention_bwd_fused(False)
+res["fwd+bwd split"] = timeit(lambda: torch.autograd.grad(hip.attention(q1, k1, v1, scale), (q1, k1, v1), g))
+hip.set_attention_bwd_fused(True)
 fl = 4 * B * H * S * S * D
 res["fwd TFLOPS"] = fl / res["fwd"] / 1e6
 res["fwd+bwd TFLOPS"] = 3.5 * fl / res["fwd+bwd"] / 1e6

@@ -33,7 +33,7 @@ def _stored(mat, kc_rowmajor: bool):
 
 @pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (0, 0), (1, 0), (0, 1)])
 @pytest.mark.parametrize("out_f32", [0, 1])
-@pytest.mark.parametrize("tile", [64, 128, 2561, 1284, 1282])
+@pytest.mark.parametrize("tile", [64, 128, 2561, 1284, 1282, 12883, 12884])
 @pytest.mark.parametrize("M,N,K", [(256, 192, 320), (136, 72, 40), (512, 1536, 640), (304, 136, 128)])
 def test_gemm_layouts(hip, a_kc, b_kc, out_f32, tile, M, N, K):
     A = _rand(M, K, seed=1)
@@ -48,7 +48,7 @@ def test_gemm_layouts(hip, a_kc, b_kc, out_f32, tile, M, N, K):
     torch.testing.assert_close(C.float(), ref, rtol=tol, atol=tol * math.sqrt(K))
 
 
-@pytest.mark.parametrize("tile", [1284, 1282, 2561])
+@pytest.mark.parametrize("tile", [1284, 1282, 2561, 12883, 12884])
 def test_gemm_dma_splitk_batched_broadcast(hip, tile):
     """LDS-DMA kernels: weight-grad layout (both operands m/n-contiguous) with split-K atomics
     into a zeroed f32 C, batched column blocks, and a broadcast (ld = 0) k-contiguous row."""
@@ -127,9 +127,16 @@ def _attn_ref(q, k, v, scale, causal=False, q_offset=0):
     return attention_reference(q, k, v, scale, causal, q_offset)
 
 
-@pytest.mark.parametrize("B,S,H", [(2, 256, 8), (1, 200, 4), (3, 64, 2)])
+@pytest.fixture(params=["fused", "split"])
+def attn_bwd_impl(request, hip):
+    hip.set_attention_bwd_fused(request.param == "fused")
+    yield request.param
+    hip.set_attention_bwd_fused(True)
+
+
+@pytest.mark.parametrize("B,S,H", [(2, 256, 8), (1, 200, 4), (3, 64, 2), (1, 40, 3), (1, 320, 2)])
 @pytest.mark.parametrize("causal", [False, True])
-def test_attention_fwd_bwd(hip, B, S, H, causal):
+def test_attention_fwd_bwd(hip, attn_bwd_impl, B, S, H, causal):
     D = 64
     # q/k/v as column slices of one fused QKV buffer, exactly as the model produces them
     qkv = _rand(B, S, 3 * H * D, seed=7).reshape(B, S, 3, H, D)
@@ -152,6 +159,23 @@ def test_attention_fwd_bwd(hip, B, S, H, causal):
     for a, b_, name in ((q1.grad, qr.grad, "dq"), (k1.grad, kr.grad, "dk"), (v1.grad, vr.grad, "dv")):
         err = (a.float() - b_).abs().max().item()
         assert err <= 3e-2 * max(1.0, b_.abs().max().item()), (name, err)
+
+
+@pytest.mark.parametrize("Sq,Sk,causal,q_offset", [(192, 128, False, 0), (130, 256, True, 64), (64, 100, True, 0)])
+def test_attention_bwd_block_fused_matches_split(hip, Sq, Sk, causal, q_offset):
+    """Block backward (ring attention's kernel: external O / lse, Sq != Sk, causal offset):
+    the fused single-pass kernel == the split dQ + dK/dV kernels."""
+    B, H, D = 2, 3, 64
+    q, do = _rand(B, Sq, H, D, seed=1), _rand(B, Sq, H, D, seed=2)
+    k, v = _rand(B, Sk, H, D, seed=3), _rand(B, Sk, H, D, seed=4)
+    o, lse = hip.attn_fwd_lse(q, k, v, D ** -0.5, causal, q_offset)
+    outs = {}
+    for fused in (True, False):
+        hip.set_attention_bwd_fused(fused)
+        outs[fused] = hip.attn_bwd_block(q, k, v, o, do, lse, D ** -0.5, causal, q_offset)
+    hip.set_attention_bwd_fused(True)
+    for a, b_ in zip(outs[True], outs[False]):
+        torch.testing.assert_close(a.float(), b_.float(), rtol=2e-2, atol=2e-2)
 
 
 def test_attention_online_softmax_rescale(hip):
