@@ -65,6 +65,24 @@ class LocalComm:
 
     def __init__(self):
         self._native = None
+        self._p2p_groups = {}
+
+    def _p2p(self, g, xs, chunked=False):
+        """Direct peer-memory collectives (comm/p2p.py) for small GPU messages when enabled."""
+        from . import p2p
+        if len(g) < 2 or not p2p.enabled():
+            return None
+        ts = [xs[d] for d in g]
+        if not all(t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) for t in ts):
+            return None
+        nbytes = ts[0].numel() * ts[0].element_size()
+        if nbytes > p2p.max_bytes():
+            return None
+        key = tuple(t.device.index for t in ts)
+        grp = self._p2p_groups.get(key)
+        if grp is None:
+            grp = self._p2p_groups[key] = p2p.P2PGroup([t.device for t in ts], p2p.max_bytes())
+        return grp if grp.fits(nbytes, chunked) else None
 
     def _rccl(self, g, xs):
         from . import native
@@ -78,10 +96,15 @@ class LocalComm:
     def all_gather(self, xs: Dict[int, torch.Tensor], groups: Groups, dim: int) -> Dict[int, torch.Tensor]:
         out = {}
         for g in groups:
-            nat = self._rccl(g, xs)
-            if nat is not None:
+            grp = self._p2p(g, xs)
+            nat = self._rccl(g, xs) if grp is None else None
+            if grp is not None or nat is not None:
                 n = len(g)
-                gathered = nat.all_gather([xs[d].contiguous() for d in g])
+                if grp is not None:
+                    res = grp.all_gather({i: xs[d].contiguous() for i, d in enumerate(g)})
+                    gathered = [res[i] for i in range(n)]
+                else:
+                    gathered = nat.all_gather([xs[d].contiguous() for d in g])
                 for d, buf in zip(g, gathered):
                     x = xs[d]
                     out[d] = buf.movedim(0, dim).reshape(x.shape[:dim] + (n * x.shape[dim],) +
@@ -99,15 +122,21 @@ class LocalComm:
             if len(g) == 1:
                 out[g[0]] = xs[g[0]].clone()
                 continue
-            nat = self._rccl(g, xs)
-            if nat is not None:
+            grp = self._p2p(g, xs, chunked=True)
+            nat = self._rccl(g, xs) if grp is None else None
+            if grp is not None or nat is not None:
                 n = len(g)
                 ins = []
                 for d in g:
                     x = xs[d]
                     s = x.shape[dim] // n
                     ins.append(x.reshape(x.shape[:dim] + (n, s) + x.shape[dim + 1:]).movedim(dim, 0).contiguous())
-                for d, r in zip(g, nat.reduce_scatter(ins)):
+                if grp is not None:
+                    res = grp.reduce_scatter(dict(enumerate(ins)))
+                    outs = [res[i] for i in range(n)]
+                else:
+                    outs = nat.reduce_scatter(ins)
+                for d, r in zip(g, outs):
                     out[d] = r
                 continue
             dev0 = xs[g[0]].device
@@ -130,6 +159,13 @@ class LocalComm:
         for g in groups:
             if len(g) == 1:
                 out[g[0]] = xs[g[0]]
+                continue
+            grp = self._p2p(g, xs)
+            if grp is not None:
+                ts = [xs[d].contiguous() for d in g]
+                grp.all_reduce(dict(enumerate(ts)), out=dict(enumerate(ts)))
+                for d, t in zip(g, ts):
+                    out[d] = t
                 continue
             nat = self._rccl(g, xs)
             if nat is not None:
@@ -156,11 +192,17 @@ class LocalComm:
             n = len(g)
             perm = perms[gi] if perms is not None else list(range(n))
             chunks = {d: xs[d].chunk(n, split_dim) for d in g}
-            nat = self._rccl(g, xs) if n > 1 else None
-            if nat is not None:
+            grp = self._p2p(g, xs, chunked=True)
+            nat = self._rccl(g, xs) if n > 1 and grp is None else None
+            if grp is not None or nat is not None:
                 # member i sends chunk perm[r] to member r; receives member-major
                 sends = [torch.stack([chunks[d][perm[r]] for r in range(n)]).contiguous() for d in g]
-                for d, recv in zip(g, nat.all_to_all(sends)):
+                if grp is not None:
+                    res = grp.all_to_all(dict(enumerate(sends)))
+                    recvs = [res[i] for i in range(n)]
+                else:
+                    recvs = nat.all_to_all(sends)
+                for d, recv in zip(g, recvs):
                     out[d] = torch.cat(list(recv.unbind(0)), concat_dim).contiguous()
                 continue
             for i, d in enumerate(g):
@@ -193,6 +235,24 @@ class DistComm:
         self.me = local_devices()[0].id
         self._pgs: Dict[Tuple[Tuple[int, ...], ...], Dict[Tuple[int, ...], object]] = {}
         self._lock = threading.Lock()
+        self._p2p_groups = {}
+
+    def _p2p(self, g, pg, x, chunked=False):
+        """Direct peer-memory collective group over IPC buffers (comm/p2p.py), members in
+        sorted-rank order like the process group; None when disabled or not applicable.  The
+        decision depends only on values every member shares, so members agree on it."""
+        from . import p2p
+        if pg is None or not p2p.enabled() or not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16):
+            return None
+        nbytes = x.numel() * x.element_size()
+        if nbytes > p2p.max_bytes():
+            return None
+        srt = tuple(sorted(g))
+        grp = self._p2p_groups.get(srt)
+        if grp is None:
+            devs = [x.device if r == self.me else torch.device("cuda", 0) for r in srt]
+            grp = self._p2p_groups[srt] = p2p.P2PGroup(devs, p2p.max_bytes(), rank=srt.index(self.me), pg=pg)
+        return grp if grp.fits(nbytes, chunked) else None
 
     def _group_of(self, groups: Groups) -> Tuple[Tuple[int, ...], object]:
         key = tuple(tuple(int(x) for x in g) for g in groups)
@@ -226,8 +286,13 @@ class DistComm:
         if pg is None:
             return {self.me: x.clone()}
         n = len(g)
-        buf = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-        dist.all_gather_into_tensor(buf.view((n * x.shape[0],) + tuple(x.shape[1:])) if x.dim() else buf.view(n), x, group=pg)
+        grp = self._p2p(g, pg, x)
+        if grp is not None:
+            buf = grp.all_gather({grp.rank: x})[grp.rank]
+        else:
+            buf = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+            dist.all_gather_into_tensor(buf.view((n * x.shape[0],) + tuple(x.shape[1:])) if x.dim() else buf.view(n),
+                                        x, group=pg)
         if not self._member_order_ok(g):
             order = [sorted(g).index(d) for d in g]
             buf = buf[order]
@@ -247,6 +312,9 @@ class DistComm:
             srt = sorted(g)
             xt = xt[[g.index(d) for d in srt]]
         xt = xt.contiguous()
+        grp = self._p2p(g, pg, xt, chunked=True)
+        if grp is not None:
+            return {self.me: grp.reduce_scatter({grp.rank: xt})[grp.rank]}
         out = torch.empty(xt.shape[1:], dtype=x.dtype, device=x.device)
         dist.reduce_scatter_tensor(out.view(-1), xt.view(-1), group=pg)
         return {self.me: out}
@@ -259,7 +327,11 @@ class DistComm:
         g, pg = self._group_of(groups)
         x = xs[self.me]
         if pg is not None:
-            dist.all_reduce(x, group=pg)
+            grp = self._p2p(g, pg, x)
+            if grp is not None:
+                grp.all_reduce({grp.rank: x}, out={grp.rank: x})
+            else:
+                dist.all_reduce(x, group=pg)
         return {self.me: x}
 
     def all_to_all(self, xs, groups, split_dim, concat_dim, perms=None):
@@ -275,8 +347,12 @@ class DistComm:
         chunks = x.reshape(x.shape[:split_dim] + (n, s) + x.shape[split_dim + 1:]).movedim(split_dim, 0)
         # the chunk sent to group member at tile position i is chunk perm[i]; order sends by sorted rank
         send = chunks[[perm[g.index(r)] for r in srt]].contiguous()
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv.view(n, -1), send.view(n, -1), group=pg)
+        grp = self._p2p(g, pg, send, chunked=True)
+        if grp is not None:
+            recv = grp.all_to_all({grp.rank: send})[grp.rank]
+        else:
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv.view(n, -1), send.view(n, -1), group=pg)
         # recv[k] came from sorted rank srt[k]; concatenate in member (tile) order
         recv = recv[[srt.index(d) for d in g]]
         out = recv.movedim(0, concat_dim)

@@ -49,6 +49,10 @@ def runtime():
                                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(_VP)],
                     "ljs_comm_all_to_all": [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.c_size_t, ctypes.c_int,
                                             ctypes.POINTER(_VP)],
+                    "ljs_comm_split": [_VP, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                       ctypes.POINTER(_VP)],
+                    "ljs_comm_async_error": [_VP],
+                    "ljs_comm_abort": [_VP],
                 }
                 for name, argt in sig.items():
                     fn = getattr(L, name)
@@ -101,16 +105,63 @@ class NativeRccl:
 
     def __init__(self):
         self._comms: Dict[Tuple[int, ...], int] = {}
+        self._world: Optional[Tuple[int, ...]] = None
+
+    def _init_all(self, gpus: Tuple[int, ...]) -> int:
+        arr = (ctypes.c_int * len(gpus))(*gpus)
+        out = _VP()
+        self._check(runtime().ljs_comm_init(len(gpus), arr, ctypes.byref(out)), "ncclCommInitAll")
+        return out.value
 
     def comm(self, gpus: Tuple[int, ...]) -> int:
+        """Communicator of an ordered group of distinct GPUs.  The first one covers every
+        visible GPU (the "world"); mesh-axis subgroups are then carved out of it with
+        ncclCommSplit, falling back to a fresh ncclCommInitAll."""
         h = self._comms.get(gpus)
-        if h is None:
-            arr = (ctypes.c_int * len(gpus))(*gpus)
-            out = _VP()
-            rc = runtime().ljs_comm_init(len(gpus), arr, ctypes.byref(out))
-            self._check(rc, "ncclCommInitAll")
-            h = self._comms[gpus] = out.value
+        if h is not None:
+            return h
+        if self._world is None:
+            world = tuple(range(torch.cuda.device_count()))
+            if set(gpus) <= set(world) and len(world) > len(gpus):
+                self._world = world
+                self._comms[world] = self._init_all(world)
+        world = self._world
+        if world is not None and gpus != world and set(gpus) <= set(world):
+            colors = (ctypes.c_int * len(world))(*[0 if g in gpus else -1 for g in world])
+            keys = (ctypes.c_int * len(world))(*[gpus.index(g) if g in gpus else 0 for g in world])
+            out = (_VP * 1)()
+            if runtime().ljs_comm_split(self._comms[world], colors, keys, 1, out) == 0:
+                h = self._comms[gpus] = out[0]
+                return h
+        h = self._comms[gpus] = self._init_all(gpus)
         return h
+
+    def check(self) -> None:
+        """Failure detection: raise on the first asynchronous RCCL error of any
+        cached communicator (ncclCommGetAsyncError)."""
+        for gpus, h in self._comms.items():
+            rc = runtime().ljs_comm_async_error(h)
+            if rc:
+                raise RuntimeError(f"RCCL communicator {gpus} failed: {runtime().ljs_comm_error_string(rc).decode()}")
+
+    def wait(self, ts: Sequence[torch.Tensor], timeout_s: float = 60.0) -> None:
+        """Wait for the members' streams with a deadline, polling RCCL's async error state; on
+        timeout every communicator is aborted and an error raised instead of hanging."""
+        import time
+        evs = []
+        for t in ts:
+            e = torch.cuda.Event()
+            e.record(torch.cuda.current_stream(t.device))
+            evs.append(e)
+        t0 = time.time()
+        while not all(e.query() for e in evs):
+            self.check()
+            if time.time() - t0 > timeout_s:
+                for h in self._comms.values():
+                    runtime().ljs_comm_abort(h)
+                self._comms.clear()
+                raise TimeoutError(f"collective did not complete within {timeout_s} s; communicators aborted")
+            time.sleep(1e-4)
 
     @staticmethod
     def _check(rc, what):

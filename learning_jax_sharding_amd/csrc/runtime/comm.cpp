@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -155,3 +156,98 @@ LJS_RT_API int ljs_comm_permute(void* handle, int npairs, const int* src, const 
 }
 
 LJS_RT_API const char* ljs_comm_error_string(int code) { return ncclGetErrorString((ncclResult_t)code); }
+
+// Sub-communicators by ncclCommSplit of an existing communicator (all members call it inside
+// one group): members with the same colour form one new communicator, ranked by key; colour
+// < 0 (NCCL_SPLIT_NOCOLOR) leaves a member out.  out_handles[c] receives the communicator of
+// colour c (ncolors of them), its members ordered by key.
+LJS_RT_API int ljs_comm_split(void* parent, const int* colors, const int* keys, int ncolors, void** out_handles) {
+  Comm* p = static_cast<Comm*>(parent);
+  const int n = (int)p->comms.size();
+  std::vector<ncclComm_t> news(n, nullptr);
+  ncclGroupStart();
+  for (int i = 0; i < n; ++i) {
+    ncclCommSplit(p->comms[i], colors[i] < 0 ? NCCL_SPLIT_NOCOLOR : colors[i], keys[i], &news[i], nullptr);
+  }
+  ncclResult_t r = ncclGroupEnd();
+  if (r != ncclSuccess) return (int)r;
+  for (int c = 0; c < ncolors; ++c) {
+    Comm* cc = new Comm();
+    std::vector<std::pair<int, int>> mem;  // (key, member)
+    for (int i = 0; i < n; ++i)
+      if (colors[i] == c) mem.push_back({keys[i], i});
+    std::sort(mem.begin(), mem.end());
+    for (auto& km : mem) {
+      cc->comms.push_back(news[km.second]);
+      cc->devs.push_back(p->devs[km.second]);
+    }
+    out_handles[c] = cc;
+  }
+  return 0;
+}
+
+// Failure detection: first asynchronous error of any member communicator
+// (ncclCommGetAsyncError), 0 when healthy.  ljs_comm_abort tears a wedged communicator down
+// so the caller can raise instead of hanging.
+LJS_RT_API int ljs_comm_async_error(void* handle) {
+  Comm* c = static_cast<Comm*>(handle);
+  for (auto& cm : c->comms) {
+    ncclResult_t e = ncclSuccess;
+    ncclResult_t r = ncclCommGetAsyncError(cm, &e);
+    if (r != ncclSuccess) return (int)r;
+    if (e != ncclSuccess && e != ncclInProgress) return (int)e;
+  }
+  return 0;
+}
+
+LJS_RT_API int ljs_comm_abort(void* handle) {
+  Comm* c = static_cast<Comm*>(handle);
+  for (auto& cm : c->comms) ncclCommAbort(cm);
+  c->comms.clear();
+  return 0;
+}
+
+// ---- peer-memory staging buffers for the direct P2P collectives (kernels/p2p.hip)
+// fine-grained uncached device memory, zero-filled, with an IPC handle for other processes
+LJS_RT_API int ljs_p2p_alloc(int dev, size_t bytes, void** ptr, void* ipc_handle /* 64 bytes or null */) {
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return (int)e;
+  e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*ptr, 0, bytes);
+  if (e != hipSuccess) return (int)e;
+  if (ipc_handle) {
+    hipIpcMemHandle_t h;
+    e = hipIpcGetMemHandle(&h, *ptr);
+    if (e != hipSuccess) return (int)e;
+    static_assert(sizeof(h) <= 64, "ipc handle size");
+    std::memcpy(ipc_handle, &h, sizeof(h));
+  }
+  return (int)hipDeviceSynchronize();
+}
+
+LJS_RT_API int ljs_p2p_free(void* ptr) { return (int)hipFree(ptr); }
+
+LJS_RT_API int ljs_p2p_open(int dev, const void* ipc_handle, void** ptr) {
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return (int)e;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, ipc_handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+LJS_RT_API int ljs_p2p_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+LJS_RT_API int ljs_p2p_enable_peer(int dev, int peer) {
+  if (dev == peer) return 0;
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return (int)e;
+  e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (int)e;
+}
+
+LJS_RT_API int ljs_rt_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
