@@ -355,7 +355,7 @@ __global__ void adam_kernel(const float* __restrict__ p, const G* __restrict__ g
 // copy and the transposed [C][R] copy (staged through LDS so both writes are coalesced).  This
 // removes every per-step f32->bf16 weight cast kernel from the training step.
 struct AdamTensor {
-  long p, g, m, v, st, sn, R, C, g_bf16, tiles_c;
+  long p, g, m, v, st, sn, R, C, g_bf16, tiles_c, vec;  // vec: 4-wide path allowed (C % 4, alignment)
 };
 constexpr int kAdamMax = 32;
 struct AdamBatch {
@@ -384,6 +384,80 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
   float* Vv = reinterpret_cast<float*>(T.v);
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int col = tc_i * 64 + tx;
+  if (T.vec && (tc_i + 1) * 64 <= T.C) {
+    // full-width column block, 16-byte aligned rows: each thread owns 4 consecutive columns of
+    // 4 rows (all 16 loads issued up front), vector p/m/v/g loads and stores, 8-byte bf16
+    // shadow stores; the transposed shadow leaves as 8-byte stores from the LDS transpose
+    const int c4 = (threadIdx.x & 15) * 4, r0 = threadIdx.x >> 4;
+    const long cbase = (long)tc_i * 64 + c4;
+    f32x4 gv[4], mv[4], vv[4], pv[4];
+    bool ok[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = tr_i * 64 + r0 + 16 * q;
+      ok[q] = row < T.R;
+      const long i = ok[q] ? (long)row * T.C + cbase : cbase;
+      if (T.g_bf16) {
+        const u32x2 raw = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(T.g) + i);
+        gv[q] = f32x4{__uint_as_float(raw[0] << 16), __uint_as_float(raw[0] & 0xffff0000u),
+                      __uint_as_float(raw[1] << 16), __uint_as_float(raw[1] & 0xffff0000u)};
+      } else {
+        gv[q] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(T.g) + i);
+      }
+      mv[q] = *reinterpret_cast<const f32x4*>(Mm + i);
+      vv[q] = *reinterpret_cast<const f32x4*>(Vv + i);
+      pv[q] = *reinterpret_cast<const f32x4*>(P + i);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = r0 + 16 * q;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g = gv[q][e];
+        const float m = b1 * mv[q][e] + (1.f - b1) * g;
+        const float v = b2 * vv[q][e] + (1.f - b2) * g * g;
+        const float p = pv[q][e];
+        mv[q][e] = m;
+        vv[q][e] = v;
+        pv[q][e] = p - lr * ((m * inv_bc1) / (sqrtf(v) * inv_sqrt_bc2 + eps) + wd * p);
+        tr[rl][c4 + e] = pv[q][e];
+      }
+      if (ok[q]) {
+        const long i = (long)(tr_i * 64 + rl) * T.C + cbase;
+        *reinterpret_cast<f32x4*>(P + i) = pv[q];
+        *reinterpret_cast<f32x4*>(Mm + i) = mv[q];
+        *reinterpret_cast<f32x4*>(Vv + i) = vv[q];
+        if (T.sn)
+          *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(T.sn) + i) =
+              u32x2{pack_bf16x2(pv[q][0], pv[q][1]), pack_bf16x2(pv[q][2], pv[q][3])};
+      }
+    }
+    if (T.st) {
+      __syncthreads();
+      // shadow_t[c][r]: thread -> 4 consecutive rows r4..r4+3 of output row c (bank-conflict
+      // free: tr's row stride is 65 words)
+      const int r4 = (threadIdx.x & 15) * 4, cl0 = threadIdx.x >> 4;
+      const int orow0 = tc_i * 64, ocol = tr_i * 64 + r4;
+      const bool rows_vec = (T.R & 3) == 0 && ocol + 4 <= T.R;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cl = cl0 + 16 * q, c = orow0 + cl;
+        bf16_t* dst = reinterpret_cast<bf16_t*>(T.st) + (long)c * T.R + ocol;
+        if (rows_vec) {
+          *reinterpret_cast<u32x2*>(dst) = u32x2{pack_bf16x2(tr[r4][cl], tr[r4 + 1][cl]),
+                                                 pack_bf16x2(tr[r4 + 2][cl], tr[r4 + 3][cl])};
+        } else {
+          for (int k = 0; k < 4 && ocol + k < T.R; ++k) dst[k] = f2bf(tr[r4 + k][cl]);
+        }
+      }
+    }
+    if (ticket) {
+      __syncthreads();
+      if (threadIdx.x == 0 && ticket_last(ticket, gridDim.x))
+        __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
 #pragma unroll 4
   for (int rr = 0; rr < 16; ++rr) {
     const int rl = ty + 4 * rr, row = tr_i * 64 + rl;
@@ -630,6 +704,9 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
     t.p = r[0]; t.g = r[1]; t.m = r[2]; t.v = r[3]; t.st = r[4]; t.sn = r[5]; t.R = r[6]; t.C = r[7];
     t.g_bf16 = r[8];
     t.tiles_c = (t.C + 63) / 64;
+    auto al = [](long ptr, long a) { return ptr % a == 0; };
+    t.vec = t.C % 4 == 0 && al(t.p, 16) && al(t.m, 16) && al(t.v, 16) && al(t.g, t.g_bf16 ? 8 : 16) &&
+            al(t.sn, 8) && al(t.st, 8);
     b.tile_start[i] = tiles;
     tiles += (int)(((t.R + 63) / 64) * t.tiles_c);
   }

@@ -341,6 +341,22 @@ def _cast_raw(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return out
 
 
+def cast_into(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """dst[...] = src converted to dst.dtype (f32 <-> bf16 on the HIP kernel; both contiguous)."""
+    assert src.numel() == dst.numel() and dst.is_contiguous(), (src.shape, dst.shape)
+    if src.dtype == dst.dtype:
+        dst.copy_(src)
+        return dst
+    if not supports_cast(src.dtype, dst.dtype) or not src.is_contiguous() or not dst.is_cuda:
+        dst.copy_(src.reshape(dst.shape))
+        return dst
+    n = src.numel()
+    if n:
+        fn = lib().ljs_cast_f32_bf16 if src.dtype == torch.float32 else lib().ljs_cast_bf16_f32
+        _ck(fn(_p(src), _p(dst), n, _stream(dst)), "cast")
+    return dst
+
+
 def cast(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     if t.requires_grad and torch.is_grad_enabled():
         return _Cast.apply(t, dtype)

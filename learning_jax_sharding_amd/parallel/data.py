@@ -6,16 +6,23 @@ sharded over ``data`` (``case6_attention.py:161,184,212``).  Here the partitione
 gradient convention leaves every replica of a parameter tile with a partial gradient, and
 this module sums them over each tile's replica group:
 
-* **buckets** are filled in the order gradients become ready (autograd tensor hooks), and a
-  bucket is all-reduced as soon as it holds ``bucket_bytes``.  On MI355X the whole case6
-  parameter set (5.25 MB) would fit one bucket, which could never overlap; the default
-  ~1 MiB cap instead launches the out-projection's gradients while the attention backward
-  and the QKV weight-gradient GEMM are still running.  xGMI rings are per-link bound, so a
-  few MB per collective is already past the latency knee;
+* **producer groups**: gradients that one kernel wrote as views of ONE buffer (the batched
+  Q/K/V weight-gradient GEMM writes dWq, dWk, dWv into one ``[3, K, N]`` tensor) are held back
+  until the whole buffer has arrived and then reduced as that buffer, in place - no
+  concatenation, one collective instead of three;
+* **buckets** are filled in the order producer groups complete (autograd tensor hooks) and
+  launched as soon as one holds ``bucket_bytes`` (default 1 MiB): the output projection's
+  gradients leave while the attention backward and the QKV weight-gradient GEMM still run;
+* **wire dtype**: gradients of bf16-computed layers travel as **bf16** (``LJS_GRAD_COMM_DTYPE``,
+  default ``bf16``; ``fp32`` keeps them f32).  This is the reference's own semantics: under
+  ``dtype=bfloat16`` the weight-gradient ``dot_general`` produces bf16 partial sums and the
+  all-reduce GSPMD inserts for the batch-sharded contraction runs on them, before the convert
+  to the f32 parameter dtype [JAX-internal, SURVEY §2.7 case-6 bwd].  Half the bytes on
+  point-to-point xGMI rings, where the gradient tail is exposed;
 * each bucket's all-reduce runs on a side comm stream (RCCL over xGMI), joined only before
-  the optimizer consumes the gradients; under ``jit(capture=True)`` the collective becomes
-  an asynchronous cut point of the segmented HIP-graph capture (``spmd/graphs.py``), so the
-  overlap is replayed every step.
+  the optimizer consumes the gradients; under ``jit(capture=True)`` the collective becomes an
+  asynchronous cut point of the segmented HIP-graph capture (``spmd/graphs.py``) while the
+  casts on either side of it stay inside the captured segments.
 
 Single-process runs (host / virtual / multi-GPU in one process) use the synchronous
 bucketed path of :func:`learning_jax_sharding_amd.spmd.api.reduce_replica_grads`.
@@ -29,11 +36,21 @@ import torch
 
 from ..array import ShardedArray
 
-__all__ = ["GradReducer", "default_bucket_bytes", "bucket_plan"]
+__all__ = ["GradReducer", "default_bucket_bytes", "bucket_plan", "comm_dtype"]
 
 
 def default_bucket_bytes() -> int:
     return int(float(os.environ.get("LJS_GRAD_BUCKET_MB", "1")) * (1 << 20))
+
+
+def comm_dtype() -> Optional[torch.dtype]:
+    """Wire dtype of f32 gradient buckets (None = as computed)."""
+    v = os.environ.get("LJS_GRAD_COMM_DTYPE", "bf16").lower()
+    if v in ("bf16", "bfloat16"):
+        return torch.bfloat16
+    if v in ("fp32", "f32", "float32", "none", ""):
+        return None
+    raise ValueError(f"LJS_GRAD_COMM_DTYPE={v!r}: expected bf16 or fp32")
 
 
 def bucket_plan(sizes: Sequence[int], bucket_bytes: int) -> List[List[int]]:
@@ -50,31 +67,56 @@ def bucket_plan(sizes: Sequence[int], bucket_bytes: int) -> List[List[int]]:
     return out
 
 
+def _storage_key(g: torch.Tensor) -> Tuple[int, int]:
+    st = g.untyped_storage()
+    return st.data_ptr(), st.nbytes()
+
+
+def _covering_flat(grads: List[torch.Tensor]) -> Optional[torch.Tensor]:
+    """A flat view over the storage if ``grads`` are contiguous views that tile it exactly, in
+    order (a producer group); else None."""
+    st_ptr, st_bytes = _storage_key(grads[0])
+    off = 0
+    for g in grads:
+        if not g.is_contiguous() or _storage_key(g)[0] != st_ptr or g.storage_offset() != off:
+            return None
+        off += g.numel()
+    if off * grads[0].element_size() != st_bytes:
+        return None
+    return grads[0].new_empty(0).set_(grads[0].untyped_storage(), 0, (off,), (1,))
+
+
 class GradReducer:
     """Overlapped, bucketed replica-group gradient all-reduce for one backward pass.
 
     ``leaves`` are the differentiated parameter arrays; ``inputs[i]`` the local torch
     leaf of ``leaves[i]`` (one local device per process in distributed runs)."""
 
-    def __init__(self, leaves: Sequence[ShardedArray], bucket_bytes: Optional[int] = None):
+    def __init__(self, leaves: Sequence[ShardedArray], bucket_bytes: Optional[int] = None,
+                 wire_dtype: Optional[torch.dtype] = "env"):
         self.leaves = list(leaves)
         self.bucket_bytes = bucket_bytes or default_bucket_bytes()
+        self.wire_dtype = comm_dtype() if wire_dtype == "env" else wire_dtype
         self.groups = []
         for p in self.leaves:
             ta = p.tile
             self.groups.append(tuple(tuple(ta.holders(t)) for t in sorted(set(ta.coords.values())))
-            if ta.num_replicas > 1 else None)
+                               if ta.num_replicas > 1 else None)
         self.ready: Dict[int, torch.Tensor] = {}
+        self.pending: Dict[Tuple, List[int]] = {}     # producer groups waiting for their buffer
         self.open: Dict[Tuple, List[int]] = {}
         self.open_bytes: Dict[Tuple, int] = {}
-        self.launched: List[Tuple[List[int], Tuple, torch.Tensor, object]] = []
+        self.launched: List[Tuple[List[int], torch.Tensor, Optional[torch.Tensor], object]] = []
 
     @staticmethod
     def wanted(leaves: Sequence[ShardedArray]) -> bool:
         from ..comm.backend import get_comm
-        if get_comm().kind != "dist" or os.environ.get("LJS_OVERLAP_GRAD_REDUCE", "1") == "0":
+        mode = os.environ.get("LJS_OVERLAP_GRAD_REDUCE", "1")
+        if get_comm().kind != "dist" or mode == "0":
             return False
-        return any(p.tile.num_replicas > 1 and any(t.is_cuda for t in p.local.values()) for p in leaves)
+        # "force": also for host tensors (exercises this path in the CPU multi-process tests)
+        return any(p.tile.num_replicas > 1 and (mode == "force" or any(t.is_cuda for t in p.local.values()))
+                   for p in leaves)
 
     # ------------------------------------------------------------------ hooks
     def attach(self, inputs: Sequence[torch.Tensor]) -> List:
@@ -87,11 +129,19 @@ class GradReducer:
 
     def _on_grad(self, i: int, g: torch.Tensor):
         self.ready[i] = g
-        key = (self.groups[i], g.dtype)
-        self.open.setdefault(key, []).append(i)
-        self.open_bytes[key] = self.open_bytes.get(key, 0) + g.numel() * g.element_size()
-        if self.open_bytes[key] >= self.bucket_bytes:
-            self._launch(key)
+        skey = _storage_key(g)
+        pkey = (self.groups[i], g.dtype, skey)
+        members = self.pending.setdefault(pkey, [])
+        members.append(i)
+        seen = sum(self.ready[j].numel() * self.ready[j].element_size() for j in members)
+        if seen >= skey[1]:
+            # the producing buffer is complete: its views join the bucket together
+            del self.pending[pkey]
+            key = (self.groups[i], g.dtype)
+            self.open.setdefault(key, []).extend(sorted(members, key=lambda j: self.ready[j].storage_offset()))
+            self.open_bytes[key] = self.open_bytes.get(key, 0) + seen
+            if self.open_bytes[key] >= self.bucket_bytes:
+                self._launch(key)
         return None
 
     def _launch(self, key):
@@ -104,31 +154,49 @@ class GradReducer:
         from ..comm.backend import get_comm
         from ..spmd import graphs
         me = next(iter(self.leaves[idxs[0]].local))
+        flat32 = _covering_flat(grads)
+        if flat32 is None:
+            flat32 = torch.cat([g.reshape(-1) for g in grads])
+        wire = None
+        if self.wire_dtype is not None and flat32.dtype == torch.float32 and self.wire_dtype != flat32.dtype:
+            from ..ops.hip import cast as _cast
+            wire = _cast(flat32, self.wire_dtype) if flat32.is_cuda else flat32.to(self.wire_dtype)
+        buf = wire if wire is not None else flat32
 
-        def fn(grads=grads, groups=groups, me=me):
-            flat = torch.cat([g.reshape(-1) for g in grads])
-            return get_comm().all_reduce_({me: flat}, [tuple(g) for g in groups])[me]
+        def fn(buf=buf, groups=groups, me=me):
+            return get_comm().all_reduce_({me: buf}, [tuple(g) for g in groups])[me]
 
         from ..spmd import plan as _plan
-        _plan.record("all_reduce", groups=tuple(groups), note="grad.bucket", bytes_in=sum(
-            g.numel() * g.element_size() for g in grads), overlapped=True)
-        flat, handle = graphs.run_collective(fn, async_=True)
-        self.launched.append((idxs, groups, flat, handle))
+        _plan.record("all_reduce", groups=tuple(groups), note="grad.bucket", dtype=str(buf.dtype).replace("torch.", ""),
+                     bytes_in=buf.numel() * buf.element_size(), overlapped=True)
+        _, handle = graphs.run_collective(fn, async_=True)
+        self.launched.append((idxs, flat32, wire, handle))
 
     # ------------------------------------------------------------------ result
     def finish(self, grads: Dict[int, Dict[int, torch.Tensor]]) -> Dict[int, Dict[int, torch.Tensor]]:
         """Launch what is left, join every bucket, return {leaf index: {dev: reduced grad}}.
         ``grads`` holds the unreduced per-leaf gradients (replica-free leaves pass through)."""
+        for pkey in list(self.pending):
+            members = self.pending.pop(pkey)
+            key = (pkey[0], pkey[1])
+            self.open.setdefault(key, []).extend(members)
         for key in list(self.open):
             self._launch(key)
         from ..spmd import graphs
         out = dict(grads)
-        for idxs, groups, flat, handle in self.launched:
+        for idxs, flat32, wire, handle in self.launched:
             graphs.join(handle)
+            if wire is not None:
+                # back to the gradients' dtype inside the captured segment after the join
+                from ..ops.hip import cast_into as _cast_into
+                if flat32.is_cuda:
+                    _cast_into(wire, flat32)
+                else:
+                    flat32.copy_(wire)
             off = 0
             for i in idxs:
                 d, g = next(iter(grads[i].items()))
                 n = g.numel()
-                out[i] = {d: flat[off:off + n].view(g.shape)}
+                out[i] = {d: flat32[off:off + n].view(g.shape)}
                 off += n
         return out

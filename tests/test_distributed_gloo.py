@@ -78,6 +78,27 @@ def job_train(ljs):
     return res
 
 
+def job_train_overlap_fp32(ljs):
+    os.environ.update({"LJS_OVERLAP_GRAD_REDUCE": "force", "LJS_GRAD_COMM_DTYPE": "fp32"})
+    return _overlap_train(ljs)
+
+
+def job_train_overlap_bf16(ljs):
+    os.environ.update({"LJS_OVERLAP_GRAD_REDUCE": "force", "LJS_GRAD_COMM_DTYPE": "bf16"})
+    return _overlap_train(ljs)
+
+
+def _overlap_train(ljs):
+    """The overlapped bucketed reducer (parallel/data.py) on host tensors: producer groups,
+    buckets and the wire dtype, with the collectives recorded in the plan."""
+    from learning_jax_sharding_amd.spmd import plan as _plan
+    with _plan.record_plan() as rec:
+        res = job_train(ljs)
+    res["buckets"] = [(s.info.get("dtype"), s.info.get("bytes_in")) for s in rec.steps
+                      if s.info.get("note") == "grad.bucket"]
+    return res
+
+
 def _run(job, world=2):
     port = 29500 + (os.getpid() % 1000)
     with tempfile.TemporaryDirectory() as d:
@@ -114,3 +135,22 @@ def test_dist_train_matches_single_process(host_devices):
             assert abs(l - lref) <= 1e-2 * max(1, abs(lref)), (shape, l, lref)
             for k in pref:
                 np.testing.assert_allclose(p[k], pref[k], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_dist_train_overlapped_reducer(host_devices, wire):
+    r0, r1 = _run(f"job_train_overlap_{wire}")
+    host_devices(2)
+    import learning_jax_sharding_amd as ljs
+    ref = job_train(ljs)
+    # (2,1): DP over 2 ranks -> bucketed grad all-reduce; the out-projection bucket and the
+    # Q/K/V producer group (one [3,K,N] buffer, reduced in place) per step
+    assert r0["buckets"] and all(dt == ("bfloat16" if wire == "bf16" else "float32") for dt, _ in r0["buckets"])
+    tol = dict(rtol=1e-4, atol=1e-5) if wire == "fp32" else dict(rtol=2e-2, atol=2e-4)
+    for shape in ref:
+        lref, pref = ref[shape]
+        for r in (r0, r1):
+            l, p = r[shape]
+            assert abs(l - lref) <= 1e-2 * max(1, abs(lref)), (shape, l, lref)
+            for k in pref:
+                np.testing.assert_allclose(p[k], pref[k], **tol)

@@ -18,9 +18,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCRIPT = os.path.join(ROOT, "scripts", "dp_check.py")
 
 
-def _run(tmp_path, world, capture, steps=3, port=29517):
-    out = str(tmp_path / f"w{world}_c{capture}.npz")
-    env = dict(os.environ, PYTHONPATH=ROOT, LJS_PLATFORM="gpu", LJS_DIST_BACKEND="gloo")
+def _run(tmp_path, world, capture, steps=3, port=29517, wire="bf16"):
+    out = str(tmp_path / f"w{world}_c{capture}_{wire}.npz")
+    env = dict(os.environ, PYTHONPATH=ROOT, LJS_PLATFORM="gpu", LJS_DIST_BACKEND="gloo", LJS_GRAD_COMM_DTYPE=wire)
     env.pop("LJS_NUM_DEVICES", None)
     if world == 1:
         cmd = [sys.executable, SCRIPT, out, str(steps), str(int(capture))]
@@ -33,13 +33,23 @@ def _run(tmp_path, world, capture, steps=3, port=29517):
     return np.load(out)
 
 
-def test_dp2_graph_matches_single_process(tmp_path):
-    ref = _run(tmp_path, 1, False)
-    eager = _run(tmp_path, 2, False)
-    graph = _run(tmp_path, 2, True)
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_dp2_graph_matches_single_process(tmp_path, wire):
+    """fp32 wire: DP == single process to f32 reassociation.  bf16 wire (the default; the
+    reference's own bf16 gradient all-reduce): Adam's first steps move each weight by ~lr times
+    the SIGN of its gradient, so a near-zero gradient whose bf16-rounded sum flips sign moves
+    that weight by up to 2 lr per step - a handful of elements, bounded by 3 steps x 2 lr."""
+    ref = _run(tmp_path, 1, False, wire=wire)
+    eager = _run(tmp_path, 2, False, port=29537 if wire == "bf16" else 29517, wire=wire)
+    graph = _run(tmp_path, 2, True, port=29537 if wire == "bf16" else 29517, wire=wire)
     assert int(graph["step"]) == 3 and int(eager["step"]) == 3
     for k in ref.files:
         if k == "step":
             continue
-        np.testing.assert_allclose(eager[k], ref[k], rtol=2e-3, atol=2e-4, err_msg=f"eager {k}")
+        if wire == "fp32":
+            np.testing.assert_allclose(eager[k], ref[k], rtol=2e-3, atol=2e-4, err_msg=f"eager {k}")
+        else:
+            diff = np.abs(eager[k] - ref[k])
+            assert diff.max() <= 6e-3 + 1e-6, (k, diff.max())
+            assert np.mean(diff > 2e-4 + 2e-3 * np.abs(ref[k])) < 5e-3, (k, np.mean(diff > 2e-4))
         np.testing.assert_allclose(graph[k], eager[k], rtol=1e-5, atol=1e-6, err_msg=f"graph {k}")

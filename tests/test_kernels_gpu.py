@@ -313,6 +313,34 @@ def test_adam_multi_and_shadows(hip):
     torch.testing.assert_close(shadow.entry(ws[1], create=False).bufs["N"], ws[1].bfloat16())
 
 
+@pytest.mark.parametrize("R,C", [(640, 512), (200, 132), (96, 100), (70, 66), (33, 7)])
+@pytest.mark.parametrize("g_bf16", [False, True])
+def test_adam_multi_vector_and_edges(hip, R, C, g_bf16):
+    """Adam's 4-wide path (C % 4 == 0, aligned; ragged row/column tiles fall back per tile) and the
+    scalar path agree with torch.optim.Adam, bf16 gradients included, and both bf16 shadows
+    (plain and transposed) equal the updated weights."""
+    from learning_jax_sharding_amd.ops import shadow
+    w = torch.randn(R, C, device=dev)
+    g = torch.randn(R, C, device=dev)
+    if g_bf16:
+        g = g.bfloat16()
+    m, v = torch.zeros_like(w), torch.zeros_like(w)
+    ref = w.clone().requires_grad_()
+    opt = torch.optim.Adam([ref], lr=1e-3)
+    shadow.get(w, "T")
+    shadow.get(w, "N")
+    step = torch.zeros((), dtype=torch.int32, device=dev)
+    for _ in range(3):
+        step += 1
+        hip.adam_multi([(w, g, m, v)], step, 1e-3, 0.9, 0.999, 1e-8, 0.0)
+        ref.grad = g.float().clone()
+        opt.step()
+    torch.testing.assert_close(w, ref.detach(), rtol=1e-5, atol=1e-6)
+    e = shadow.entry(w, create=False)
+    torch.testing.assert_close(e.bufs["T"], w.t().bfloat16())
+    torch.testing.assert_close(e.bufs["N"], w.bfloat16())
+
+
 def test_linear_broadcast_grad_and_strided(hip):
     """dY that repeats one row (cotangent of y.sum()) is read with ld=0, not materialised."""
     x = _rand(128, 256, dtype=torch.float32, seed=1)
