@@ -144,6 +144,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
+    segs = None
+    if capture:
+        caps = list(step._graphs.values())
+        if caps:
+            segs = sum(1 for it in caps[-1].graph.items if it[0] == "graph")
     if args.model == "layer":
         flops = transformer_layer_flops(B, S, M, args.heads, args.dim_head, args.ff_dim, train=args.mode == "train")
     else:
@@ -173,7 +178,7 @@ def main():
                                 (f"attention+FF transformer layer (M={M}, heads={args.heads}x{args.dim_head}, "
                                  f"ff={args.ff_dim}, FF GEMMs {'MX-fp8' if args.fp8 else 'bf16'}, f32 params, Adam)"),
                        "global_batch": B, "seq_len": S, "parallelism": par, "mode": args.mode,
-                       "hip_graph": capture},
+                       "hip_graph": capture, "graph_segments": segs},
         }
         print(json.dumps(rec), flush=True)
     if dist_on:

@@ -236,6 +236,32 @@ class DistComm:
         self._pgs: Dict[Tuple[Tuple[int, ...], ...], Dict[Tuple[int, ...], object]] = {}
         self._lock = threading.Lock()
         self._p2p_groups = {}
+        self._fake = dist.get_backend() == "fake"
+        # native RCCL rank communicators (comm/native.py RankRccl): collectives issued on the
+        # current stream, so they are captured into HIP graphs instead of cutting them
+        self._native = None
+        from . import native as _nat
+        if _nat.rank_eligible():
+            dev = local_devices()[0]
+            self._native = _nat.RankRccl(dist.get_rank(), dist.get_world_size(), dev.torch_device.index)
+
+    _GRAPH_KINDS = ("all_gather", "reduce_scatter", "all_reduce", "all_to_all")
+
+    def graph_safe(self, kind: str, x: Optional[torch.Tensor] = None) -> bool:
+        """Whether this collective can be captured inside a HIP graph (no capture cut): native
+        RCCL rank communicators, or the rehearsal backend ('fake': collectives move nothing)."""
+        from . import p2p
+        if kind not in self._GRAPH_KINDS or p2p.enabled():
+            return False
+        if self._fake:
+            return True
+        return self._native is not None and (x is None or self._native.supports(x))
+
+    def _nat(self, groups, x) -> Optional[int]:
+        if self._native is None or not self._native.supports(x):
+            return None
+        key = tuple(tuple(int(v) for v in g) for g in groups)
+        return self._native.partition(key)
 
     def _p2p(self, g, pg, x, chunked=False):
         """Direct peer-memory collective group over IPC buffers (comm/p2p.py), members in
@@ -287,8 +313,12 @@ class DistComm:
             return {self.me: x.clone()}
         n = len(g)
         grp = self._p2p(g, pg, x)
+        nh = None if grp is not None else self._nat(groups, x)
         if grp is not None:
             buf = grp.all_gather({grp.rank: x})[grp.rank]
+        elif nh is not None:
+            buf = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+            self._native.all_gather(nh, x, buf)
         else:
             buf = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
             dist.all_gather_into_tensor(buf.view((n * x.shape[0],) + tuple(x.shape[1:])) if x.dim() else buf.view(n),
@@ -316,6 +346,10 @@ class DistComm:
         if grp is not None:
             return {self.me: grp.reduce_scatter({grp.rank: xt})[grp.rank]}
         out = torch.empty(xt.shape[1:], dtype=x.dtype, device=x.device)
+        nh = self._nat(groups, xt)
+        if nh is not None:
+            self._native.reduce_scatter(nh, xt, out)
+            return {self.me: out}
         dist.reduce_scatter_tensor(out.view(-1), xt.view(-1), group=pg)
         return {self.me: out}
 
@@ -328,8 +362,11 @@ class DistComm:
         x = xs[self.me]
         if pg is not None:
             grp = self._p2p(g, pg, x)
+            nh = None if grp is not None else self._nat(groups, x)
             if grp is not None:
                 grp.all_reduce({grp.rank: x}, out={grp.rank: x})
+            elif nh is not None:
+                self._native.all_reduce_(nh, x)
             else:
                 dist.all_reduce(x, group=pg)
         return {self.me: x}
@@ -348,8 +385,11 @@ class DistComm:
         # the chunk sent to group member at tile position i is chunk perm[i]; order sends by sorted rank
         send = chunks[[perm[g.index(r)] for r in srt]].contiguous()
         grp = self._p2p(g, pg, send, chunked=True)
+        nh = None if grp is not None else self._nat(groups, send)
         if grp is not None:
             recv = grp.all_to_all({grp.rank: send})[grp.rank]
+        elif nh is not None:
+            recv = self._native.all_to_all(nh, send, torch.empty_like(send), n)
         else:
             recv = torch.empty_like(send)
             dist.all_to_all_single(recv.view(n, -1), send.view(n, -1), group=pg)

@@ -58,9 +58,11 @@ def _run(spec: _Spec, xs: Dict[int, torch.Tensor]) -> Dict[int, torch.Tensor]:
     comm = get_comm()
     out = None
     if comm.kind == "dist" and any(t.is_cuda for t in xs.values()):
-        # cross-process (RCCL) collectives are cut points of a segmented HIP-graph capture
+        # cross-process collectives through torch process groups are cut points of a segmented
+        # HIP-graph capture; native RCCL ones are captured like kernels
         from ..spmd import graphs
-        if graphs.current() is not None:
+        x0 = next(iter(xs.values()))
+        if graphs.current() is not None and not comm.graph_safe(spec.kind, x0):
             out = graphs.run_collective(lambda: _run_local(comm, spec, xs))[0]
     if out is None:
         out = _run_local(comm, spec, xs)

@@ -17,7 +17,7 @@ from typing import Dict, Optional, Sequence, Tuple
 
 import torch
 
-__all__ = ["available", "runtime", "device_info", "eligible", "NativeRccl"]
+__all__ = ["available", "runtime", "device_info", "eligible", "NativeRccl", "RankRccl", "rank_eligible"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIBPATH = os.path.join(os.path.dirname(_HERE), "_lib", "libljs_runtime.so")
@@ -53,6 +53,12 @@ def runtime():
                                        ctypes.POINTER(_VP)],
                     "ljs_comm_async_error": [_VP],
                     "ljs_comm_abort": [_VP],
+                    "ljs_comm_unique_id_size": [],
+                    "ljs_comm_get_unique_id": [ctypes.c_char_p],
+                    "ljs_comm_init_rank": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(_VP)],
+                    "ljs_comm_split_rank": [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_VP)],
+                    "ljs_comm_nranks": [_VP],
                 }
                 for name, argt in sig.items():
                     fn = getattr(L, name)
@@ -205,3 +211,113 @@ class NativeRccl:
         for h in self._comms.values():
             runtime().ljs_comm_destroy(h)
         self._comms.clear()
+
+
+# ============================================================================ one process per GPU
+def rank_eligible() -> bool:
+    """Native rank communicators for torchrun jobs: RCCL (``nccl``) process group, a GPU, the
+    runtime library, and not disabled with ``LJS_NATIVE_RCCL=0``."""
+    import torch.distributed as dist
+    if os.environ.get("LJS_NATIVE_RCCL", "1") == "0" or not torch.cuda.is_available():
+        return False
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_backend() != "nccl":
+        return False
+    return available()
+
+
+class RankRccl:
+    """RCCL communicators of a one-process-per-GPU job, driven through the native runtime.
+
+    The world communicator is created with ``ncclCommInitRank`` from a unique id that rank 0
+    publishes in the torch.distributed store; the communicator of every device group of a
+    partition is carved out of it with ONE collective ``ncclCommSplit`` per partition (colour
+    = the group's index, key = rank order inside the group, so communicator ranks follow sorted
+    global ranks like torch process groups).  Every rank must create partitions in the same
+    order - the SPMD program guarantees it, as it does for ``dist.new_group``.
+
+    Collectives are plain RCCL calls on the caller's current HIP stream: inside a HIP-graph
+    capture they become graph nodes, so a training step with its gradient all-reduces replays
+    as ONE graph (no capture cuts, no per-collective Python)."""
+
+    _SEQ = [0]
+
+    def __init__(self, rank: int, world: int, device: int):
+        self.rank, self.world, self.device = rank, world, device
+        self._world_h = self._init_world()
+        self._parts: Dict[Tuple[Tuple[int, ...], ...], Optional[int]] = {}
+
+    def _init_world(self) -> int:
+        import torch.distributed as dist
+        store = dist.distributed_c10d._get_default_store()
+        RankRccl._SEQ[0] += 1
+        key = f"ljs/rccl_uid/{RankRccl._SEQ[0]}"
+        n = runtime().ljs_comm_unique_id_size()
+        if self.rank == 0:
+            buf = ctypes.create_string_buffer(n)
+            NativeRccl._check(runtime().ljs_comm_get_unique_id(buf), "ncclGetUniqueId")
+            store.set(key, buf.raw)
+            uid = buf.raw
+        else:
+            uid = store.get(key)
+        out = _VP()
+        NativeRccl._check(runtime().ljs_comm_init_rank(uid, self.world, self.rank, self.device, ctypes.byref(out)),
+                          "ncclCommInitRank")
+        return out.value
+
+    def partition(self, groups: Tuple[Tuple[int, ...], ...]) -> Optional[int]:
+        """Handle of this rank's communicator in a partition of the ranks into groups (None
+        when this rank's group is a singleton).  Collective over every rank on first use."""
+        if groups in self._parts:
+            return self._parts[groups]
+        mine = next((g for g in groups if self.rank in g), None)
+        if mine is not None and sorted(mine) == list(range(self.world)):
+            h = self._world_h
+        else:
+            color, key = -1, 0
+            if mine is not None and len(mine) > 1:
+                color = [g for g in groups if len(g) > 1].index(mine)
+                key = sorted(mine).index(self.rank)
+            out = _VP()
+            NativeRccl._check(runtime().ljs_comm_split_rank(self._world_h, color, key, ctypes.byref(out)),
+                              "ncclCommSplit")
+            h = out.value if color >= 0 else None
+        self._parts[groups] = h
+        return h
+
+    @staticmethod
+    def supports(t: torch.Tensor) -> bool:
+        return t.is_cuda and t.dtype in _DT and t.is_contiguous()
+
+    def _one(self, t):
+        return (_VP * 1)(t.data_ptr())
+
+    def _stream(self, t):
+        return (_VP * 1)(torch.cuda.current_stream(t.device).cuda_stream)
+
+    def all_reduce_(self, h: int, x: torch.Tensor) -> torch.Tensor:
+        NativeRccl._check(runtime().ljs_comm_all_reduce(h, self._one(x), self._one(x), x.numel(), _DT[x.dtype], 0,
+                                                        self._stream(x)), "all_reduce")
+        return x
+
+    def all_gather(self, h: int, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """out: [n * x.numel()] elements, rank-major."""
+        NativeRccl._check(runtime().ljs_comm_all_gather(h, self._one(x), self._one(out), x.numel(), _DT[x.dtype],
+                                                        self._stream(x)), "all_gather")
+        return out
+
+    def reduce_scatter(self, h: int, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """x: n chunks of out.numel() elements (chunk r to rank r)."""
+        NativeRccl._check(runtime().ljs_comm_reduce_scatter(h, self._one(x), self._one(out), out.numel(),
+                                                            _DT[x.dtype], 0, self._stream(x)), "reduce_scatter")
+        return out
+
+    def all_to_all(self, h: int, send: torch.Tensor, recv: torch.Tensor, n: int) -> torch.Tensor:
+        NativeRccl._check(runtime().ljs_comm_all_to_all(h, self._one(send), self._one(recv), send.numel() // n,
+                                                        _DT[send.dtype], self._stream(send)), "all_to_all")
+        return recv
+
+    def check(self) -> None:
+        for h in [self._world_h] + [v for v in self._parts.values() if v]:
+            rc = runtime().ljs_comm_async_error(h)
+            if rc:
+                raise RuntimeError(f"RCCL communicator failed: {runtime().ljs_comm_error_string(rc).decode()}")

@@ -21,8 +21,10 @@
 namespace {
 
 struct Comm {
-  std::vector<ncclComm_t> comms;  // one per member, rank = member index
+  std::vector<ncclComm_t> comms;  // one per LOCAL member
   std::vector<int> devs;
+  std::vector<int> ranks;         // communicator rank of each local member
+  int nranks = 0;                 // ranks in the communicator (all processes)
 };
 
 ncclDataType_t to_nccl(int dt) {
@@ -83,9 +85,70 @@ LJS_RT_API int ljs_comm_init(int n, const int* devs, void** handle) {
     delete c;
     return (int)r;
   }
+  for (int i = 0; i < n; ++i) c->ranks.push_back(i);
+  c->nranks = n;
   *handle = c;
   return 0;
 }
+
+// ---- one process per GPU (torchrun): a communicator with ONE local member, created from a
+// unique id that rank 0 publishes through the torch.distributed store.  Collectives are plain
+// RCCL calls on the caller's HIP stream, so they are captured into HIP graphs like kernels
+// (the training step replays as one graph with its gradient all-reduces inside).
+LJS_RT_API int ljs_comm_unique_id_size() { return (int)sizeof(ncclUniqueId); }
+
+LJS_RT_API int ljs_comm_get_unique_id(void* out) {
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return (int)r;
+  std::memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+LJS_RT_API int ljs_comm_init_rank(const void* unique_id, int nranks, int rank, int dev, void** handle) {
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return (int)e;
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof(id));
+  Comm* c = new Comm();
+  c->comms.resize(1);
+  ncclResult_t r = ncclCommInitRank(&c->comms[0], nranks, id, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return (int)r;
+  }
+  c->devs.push_back(dev);
+  c->ranks.push_back(rank);
+  c->nranks = nranks;
+  *handle = c;
+  return 0;
+}
+
+// collective over the parent (every rank calls it): ranks with the same colour form one new
+// communicator ordered by key; colour < 0 leaves this rank out (*handle = null)
+LJS_RT_API int ljs_comm_split_rank(void* parent, int color, int key, void** handle) {
+  Comm* p = static_cast<Comm*>(parent);
+  if (p->comms.size() != 1) return (int)ncclInvalidUsage;
+  ncclComm_t nc = nullptr;
+  ncclResult_t r = ncclCommSplit(p->comms[0], color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &nc, nullptr);
+  if (r != ncclSuccess) return (int)r;
+  if (color < 0 || nc == nullptr) {
+    *handle = nullptr;
+    return 0;
+  }
+  Comm* c = new Comm();
+  c->comms.push_back(nc);
+  c->devs.push_back(p->devs[0]);
+  int rk = 0, n = 0;
+  ncclCommUserRank(nc, &rk);
+  ncclCommCount(nc, &n);
+  c->ranks.push_back(rk);
+  c->nranks = n;
+  *handle = c;
+  return 0;
+}
+
+LJS_RT_API int ljs_comm_nranks(void* handle) { return static_cast<Comm*>(handle)->nranks; }
 
 LJS_RT_API int ljs_comm_destroy(void* handle) {
   Comm* c = static_cast<Comm*>(handle);
@@ -125,14 +188,14 @@ LJS_RT_API int ljs_comm_reduce_scatter(void* handle, void* const* sendbufs, void
   return (int)ncclGroupEnd();
 }
 
-// all-to-all of n equal chunks of `count` elements: chunk r of member i lands as chunk i of member r
+// all-to-all of nranks equal chunks of `count` elements: chunk r of rank i lands as chunk i of rank r
 LJS_RT_API int ljs_comm_all_to_all(void* handle, void* const* sendbufs, void* const* recvbufs, size_t count, int dt,
                                    void* const* streams) {
   Comm* c = static_cast<Comm*>(handle);
-  const size_t n = c->comms.size();
+  const size_t n = (size_t)c->nranks;
   const size_t bytes = count * dt_size(dt);
   ncclGroupStart();
-  for (size_t i = 0; i < n; ++i) {
+  for (size_t i = 0; i < c->comms.size(); ++i) {
     for (size_t r = 0; r < n; ++r) {
       ncclSend(static_cast<const char*>(sendbufs[i]) + r * bytes, count, to_nccl(dt), (int)r, c->comms[i],
                (hipStream_t)streams[i]);
@@ -180,7 +243,9 @@ LJS_RT_API int ljs_comm_split(void* parent, const int* colors, const int* keys, 
     for (auto& km : mem) {
       cc->comms.push_back(news[km.second]);
       cc->devs.push_back(p->devs[km.second]);
+      cc->ranks.push_back((int)cc->ranks.size());
     }
+    cc->nranks = (int)cc->comms.size();
     out_handles[c] = cc;
   }
   return 0;

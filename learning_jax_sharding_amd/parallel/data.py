@@ -20,9 +20,11 @@ this module sums them over each tile's replica group:
   to the f32 parameter dtype [JAX-internal, SURVEY §2.7 case-6 bwd].  Half the bytes on
   point-to-point xGMI rings, where the gradient tail is exposed;
 * each bucket's all-reduce runs on a side comm stream (RCCL over xGMI), joined only before
-  the optimizer consumes the gradients; under ``jit(capture=True)`` the collective becomes an
-  asynchronous cut point of the segmented HIP-graph capture (``spmd/graphs.py``) while the
-  casts on either side of it stay inside the captured segments.
+  the optimizer consumes the gradients.  Under ``jit(capture=True)`` a native-RCCL all-reduce
+  is captured INTO the step's HIP graph (forked onto the side stream inside the capture), so
+  the whole step replays as one graph; a torch-process-group one (gloo) becomes an
+  asynchronous cut point of the segmented capture (``spmd/graphs.py``).  The casts on either
+  side stay inside the captured graph either way.
 
 Single-process runs (host / virtual / multi-GPU in one process) use the synchronous
 bucketed path of :func:`learning_jax_sharding_amd.spmd.api.reduce_replica_grads`.
@@ -169,7 +171,8 @@ class GradReducer:
         from ..spmd import plan as _plan
         _plan.record("all_reduce", groups=tuple(groups), note="grad.bucket", dtype=str(buf.dtype).replace("torch.", ""),
                      bytes_in=buf.numel() * buf.element_size(), overlapped=True)
-        _, handle = graphs.run_collective(fn, async_=True)
+        comm = get_comm()
+        _, handle = graphs.run_collective(fn, async_=True, capturable=comm.graph_safe("all_reduce", buf))
         self.launched.append((idxs, flat32, wire, handle))
 
     # ------------------------------------------------------------------ result

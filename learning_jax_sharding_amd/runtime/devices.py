@@ -177,6 +177,13 @@ def initialize_distributed(backend: Optional[str] = None) -> None:
         torch.cuda.set_device(_local_gpu())
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", _local_gpu())
+    if backend == "fake":
+        # rehearsal: ONE process plays rank RANK of WORLD_SIZE and every collective completes
+        # at once without moving data - the whole multi-rank code path (process groups, grad
+        # buckets, segmented graphs, side-stream joins) runs, so its overhead is measurable on
+        # one GPU with the network taken out (numerics are NOT those of a real run)
+        from torch.testing._internal.distributed.fake_pg import FakeStore
+        kwargs.update(store=FakeStore(), rank=int(os.environ.get("RANK", "0")), world_size=world)
     dist.init_process_group(backend=backend, **kwargs)
     with _LOCK:
         _BACKEND = None

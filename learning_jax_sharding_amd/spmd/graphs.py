@@ -14,6 +14,12 @@ re-issued on the same stream order, its fresh result copied into the static outp
 A collective may also be issued ASYNCHRONOUSLY (data-parallel gradient buckets): it then
 runs on a side comm stream, concurrent with the following graph segments, and the
 consumer joins it with :func:`join` (an event wait, also replayed in order).
+
+Collectives of the native RCCL rank communicators (``comm/native.py`` ``RankRccl``) are plain
+RCCL calls on the current stream and are NOT cut points: they are captured with the kernels
+(asynchronous ones forked onto a side stream inside the capture), so a data-parallel train step
+replays as a single graph.  The cut path remains for torch process-group collectives (gloo, or
+``LJS_NATIVE_RCCL=0``).
 """
 from __future__ import annotations
 
@@ -110,6 +116,12 @@ class SegmentedGraph:
         self._begin()
         return out, handle
 
+    def side_stream(self) -> torch.cuda.Stream:
+        """Stream for collectives forked inside the capture (joined before the capture ends)."""
+        if self.comm_stream is None:
+            self.comm_stream = torch.cuda.Stream()
+        return self.comm_stream
+
     def join(self, ev: torch.cuda.Event):
         self._cut()
         torch.cuda.current_stream().wait_event(ev)
@@ -135,10 +147,31 @@ class SegmentedGraph:
                 cur.wait_event(it[1])
 
 
-def run_collective(fn: Callable[[], Any], async_: bool = False):
-    """Issue a cross-process collective: directly (eager), or as a cut point of the active
-    segmented capture.  Returns (outputs, join handle or None)."""
+class _Fork:
+    """Join handle of a collective forked onto a side stream INSIDE a capture (no cut)."""
+    __slots__ = ("ev",)
+
+    def __init__(self, ev):
+        self.ev = ev
+
+
+def run_collective(fn: Callable[[], Any], async_: bool = False, capturable: bool = False):
+    """Issue a cross-process collective: directly (eager), as a cut point of the active
+    segmented capture, or - when ``capturable`` (native RCCL on the current stream) - as part
+    of the capture itself, forked onto a side stream when ``async_`` so it overlaps the rest of
+    the captured step.  Returns (outputs, join handle or None)."""
     seg = current()
+    if seg is not None and capturable:
+        if not async_:
+            return fn(), None
+        cur = torch.cuda.current_stream()
+        cs = seg.side_stream()
+        cs.wait_stream(cur)
+        with torch.cuda.stream(cs):
+            out = fn()
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        return out, _Fork(ev)
     if seg is None:
         if async_ and torch.cuda.is_available():
             cs = _side_stream()
@@ -155,6 +188,9 @@ def run_collective(fn: Callable[[], Any], async_: bool = False):
 def join(handle) -> None:
     """Make the current stream wait for an asynchronous collective."""
     if handle is None:
+        return
+    if isinstance(handle, _Fork):
+        torch.cuda.current_stream().wait_event(handle.ev)
         return
     seg = current()
     if seg is not None:
