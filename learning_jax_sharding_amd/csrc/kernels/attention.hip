@@ -47,6 +47,21 @@ struct AttnArgs {
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// XCD-aware 3-D tile index of a 1-D grid of nx * H * B blocks: blocks sharing an XCD (dealt
+// round-robin by block id) take CONSECUTIVE tiles, so the query blocks of one (batch, head)
+// run on one XCD and re-read that head's K/V from its L2 instead of from HBM/MALL once per XCD.
+struct Tile3 {
+  int x, h, b;
+};
+__device__ __forceinline__ Tile3 tile3(int nx, int H) {
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  Tile3 r;
+  r.x = t % nx;
+  r.h = (t / nx) % H;
+  r.b = t / (nx * H);
+  return r;
+}
+
 // ---- LDS image: [64 rows][64 d] bf16, 128-byte rows.  16-byte chunk XOR 2*((row>>1)&3):
 // bank-conflict free for BOTH the ds_read_b128 row reads (MFMA operand rows) and the
 // ds_read_b64_tr_b16 transposed reads (found by exhaustive bank simulation of both patterns).
@@ -182,7 +197,8 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const Tile3 tl = tile3((a.Sq + BLK - 1) / BLK, a.H);
+  const int qb = tl.x, h = tl.h, b = tl.b;
   const int qrow0 = qb * BLK + wave * 16;
   const int qrow = qrow0 + (lane & 15);
   const bool qok = qrow < a.Sq;
@@ -311,7 +327,8 @@ __device__ __forceinline__ void dkv_tile(const AttnArgs& a, const bf16_t* Qt, co
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int kblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const Tile3 tl = tile3((a.Sk + BLK - 1) / BLK, a.H);
+  const int kblk = tl.x, h = tl.h, b = tl.b;
   const int key0 = kblk * BLK + wave * 16;
   const int key = key0 + (lane & 15);
   const bool kok = key < a.Sk;
@@ -413,7 +430,8 @@ __device__ __forceinline__ void dq_tile(const AttnArgs& a, const bf16_t* Kt, con
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const Tile3 tl = tile3((a.Sq + BLK - 1) / BLK, a.H);
+  const int qb = tl.x, h = tl.h, b = tl.b;
   const int qrow0 = qb * BLK + wave * 16;
   const int qrow = qrow0 + (lane & 15);
   const bool qok = qrow < a.Sq;
@@ -702,8 +720,7 @@ LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, v
   a.Sq = Sq; a.Sk = Sk; a.H = H;
   a.scale = scale; a.scale_log2 = scale * LOG2E;
   a.causal = causal; a.q_offset = q_offset;
-  dim3 grid((Sq + BLK - 1) / BLK, H, B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((Sq + BLK - 1) / BLK * H * B), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -745,10 +762,10 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
   // dQ first: it also computes delta, which the dK/dV kernel consumes (stream order)
   AttnArgs c = a;
   c.out = (bf16_t*)dq; c.out_sb = dqs[0]; c.out_ss = dqs[1]; c.out_sh = dqs[2];
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Sq + BLK - 1) / BLK, H, B), dim3(256), 0, stream, c);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Sq + BLK - 1) / BLK * H * B), dim3(256), 0, stream, c);
   AttnArgs b = a;
   b.out = (bf16_t*)dk; b.out_sb = dks[0]; b.out_ss = dks[1]; b.out_sh = dks[2];
   b.out2 = (bf16_t*)dv; b.out2_sb = dvs[0]; b.out2_ss = dvs[1]; b.out2_sh = dvs[2];
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((Sk + BLK - 1) / BLK, H, B), dim3(256), 0, stream, b);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((Sk + BLK - 1) / BLK * H * B), dim3(256), 0, stream, b);
   return (int)hipGetLastError();
 }

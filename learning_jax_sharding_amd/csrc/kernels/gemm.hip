@@ -31,17 +31,8 @@ struct GemmArgs {
   int M, N, K;
   int batch, splitk, kt_per_split;
   float alpha;
-  int flags;  // 1 relu, 2 bias, 4 bias f32, 8 accumulate into C (f32 out), 32 split-K slab combine
-  // split-K slab combine (flag 32, LDS-DMA kernel, f32 out): each split writes its partial tile
-  // to its own slab of `ws` (write-through), the last arriver per output tile (ticket) sums them
-  // and stores C once -- no memset of C and no f32 atomics (those run at ~1.3 TB/s chip-wide)
-  float* ws;
-  unsigned* tickets;
-  long ws_bytes;
+  int flags;  // 1 relu, 2 bias, 4 bias f32, 8 accumulate into C (f32 out)
 };
-
-constexpr int kGemmTickets = 16384;            // ticket words at the head of the workspace
-constexpr long kGemmTicketBytes = kGemmTickets * 4L;
 
 // swizzled 8-byte-chunk index for the m/n-contiguous image (rows of R bf16)
 template <int R>
@@ -378,7 +369,6 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
   constexpr int S_EPI = TM * TN / 2;
   static_assert(L * (NST - 1) + S_EPI <= 63, "vmcnt immediate range");
   __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
-  __shared__ int s_last;  // split-K slab combine: this block arrived last for its tile
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -537,50 +527,6 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
       }
       after_epi = true;
     } else {
-      const bool slab = (p.flags & 32) && p.splitk > 1;
-      if (slab) {
-        // publish this split's partial tile (write-through 16-B stores, lane-major so the combine
-        // reads it back with the same addressing), drain, one ticket add per block; the block
-        // whose add comes last sums the other splits' slabs into its registers
-        constexpr int NT = NW * 64;
-        const int tile_id = (w.b * ntm + w.m0) * ntn + w.n0;
-        const int split = w.kt0 / p.kt_per_split;
-        const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws, p.ws_bytes);
-        const int tile_bytes = BM * BN * 4;
-        const int mine = (tile_id * p.splitk + split) * tile_bytes + tid * 16;
-#pragma unroll
-        for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[ii][j]), rw,
-                                                   mine + (ii * TN + j) * NT * 16, 0, 16 /* sc1 */);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) s_last = ticket_last(p.tickets + tile_id, (unsigned)p.splitk) ? 1 : 0;
-        __syncthreads();
-        if (!s_last) {
-#pragma unroll
-          for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          continue;
-        }
-        const int t0 = tile_id * p.splitk * tile_bytes + tid * 16;
-        for (int s = 0; s < p.splitk; ++s) {
-          if (s == split) continue;
-          u32x4 part[TM][TN];
-#pragma unroll
-          for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              part[ii][j] = __builtin_amdgcn_raw_buffer_load_b128(rw, t0 + s * tile_bytes + (ii * TN + j) * NT * 16,
-                                                                  0, 16 /* sc1 */);
-#pragma unroll
-          for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[ii][j] += __builtin_bit_cast(f32x4, part[ii][j]);
-        }
-      }
       // lane holds C[16 ii + 4 g + r][16 j + (lane & 15)]
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -600,7 +546,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
             if (relu) v = fmaxf(v, 0.f);
             if (row >= p.M || col >= p.N) continue;
             float* C = reinterpret_cast<float*>(p.C) + (long)w.b * p.sC + (long)row * p.ldc + col;
-            if (p.splitk > 1 && !slab) atomicAdd(C, v);
+            if (p.splitk > 1) atomicAdd(C, v);
             else *C = accumulate ? *C + v : v;
           }
           acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -685,7 +631,7 @@ hipError_t dispatch_layout(const GemmArgs& a, int a_kc, int b_kc, int out_f32, h
 LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
                           long lda, long ldb, long ldc, long sA, long sB, long sC, long sBias, int batch,
                           int a_kc, int b_kc, int out_f32, int flags, float alpha, int splitk, int tile,
-                          void* ws, long ws_bytes, hipStream_t stream) {
+                          hipStream_t stream) {
   if (K % 8 || (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
   if (splitk > 1 && !out_f32) return (int)hipErrorInvalidValue;
   GemmArgs a;
@@ -704,6 +650,14 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if (splitk > nkt) splitk = nkt;
   a.kt_per_split = (nkt + splitk - 1) / splitk;
   a.splitk = (nkt + a.kt_per_split - 1) / a.kt_per_split;
+  if (flags & 16) {  // zero C first (split-K accumulates with atomics); C must be one dense block
+    if (batch > 1 && sC != (long)M * ldc) return (int)hipErrorInvalidValue;
+    size_t es = out_f32 ? 4 : 2;
+    size_t bytes = ((size_t)(batch - 1) * sC + (size_t)(M - 1) * ldc + N) * es;
+    hipError_t me = hipMemsetAsync(C, 0, bytes, stream);
+    if (me != hipSuccess) return (int)me;
+  }
+  hipError_t e;
   // Persistent LDS-DMA kernels (tile codes): 2561 = 256x128, 8 waves, 3 stages, 1 block/CU
   // (k-contiguous operands only); 1284 = 128x128, 4 waves, 4 stages, 1 block/CU; 1282 =
   // 128x128, 4 waves, 2 stages, 2 blocks/CU.  They need K % 64 == 0, a split that divides the
@@ -717,33 +671,6 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if (tile > 1000 && !(dma_ok && dma_store_ok)) tile = 128;
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
   if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;
-  a.ws = nullptr;
-  a.tickets = nullptr;
-  a.ws_bytes = 0;
-  a.flags &= ~32;
-  {
-    // split-K slab combine: LDS-DMA 128x128 kernels with f32 out (the weight-gradient GEMMs)
-    const bool dma_tile = tile == 1282 || tile == 1284 || tile == 12883 || tile == 12884;
-    const long tiles = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
-    const long need = kGemmTicketBytes + tiles * a.splitk * 128L * 128 * 4;
-    if (ws && out_f32 && a.splitk > 1 && dma_tile && tiles <= kGemmTickets &&
-        need <= ws_bytes && need < (1L << 31)) {
-      a.flags |= 32;
-      if (flags & 16) a.flags &= ~8;  // zero + accumulate == store
-      a.tickets = (unsigned*)ws;
-      a.ws = (float*)((char*)ws + kGemmTicketBytes);
-      a.ws_bytes = need - kGemmTicketBytes;
-      flags &= ~16;  // the combine stores C once: nothing to zero
-    }
-  }
-  if (flags & 16) {  // zero C first (split-K accumulates with atomics); C must be one dense block
-    if (batch > 1 && sC != (long)M * ldc) return (int)hipErrorInvalidValue;
-    size_t es = out_f32 ? 4 : 2;
-    size_t bytes = ((size_t)(batch - 1) * sC + (size_t)(M - 1) * ldc + N) * es;
-    hipError_t me = hipMemsetAsync(C, 0, bytes, stream);
-    if (me != hipSuccess) return (int)me;
-  }
-  hipError_t e;
   if (tile == 2561) {
     if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);
     else e = launch_dma<256, 128, 4, 2, 3, true, true, false>(a, stream, 0);

@@ -29,8 +29,7 @@ _LP = ctypes.POINTER(ctypes.c_long)
 
 _SIGS = {
     "ljs_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
-                      c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
-                      c_long, c_void_p],
+                      c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p],
     "ljs_gemm_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long,
                      c_long, c_long, c_long, c_int, c_void_p],
     "ljs_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, _LP, _LP, _LP, _LP,
@@ -134,16 +133,6 @@ def _longs(vals) -> ctypes.Array:
 
 
 # ============================================================================ GEMM
-# Split-K weight-gradient GEMMs combine their partial tiles through per-split slabs and an
-# in-launch last-arriver ticket (no memset of C, no f32 atomics); workspace = 64 KiB of tickets
-# + 64 MiB of slabs (a 128x128 f32 tile per (tile, split)); larger requests fall back to atomics.
-# Measured at the bench shapes (scripts/gemm_study.py): the combine is read by ONE block at
-# ~100 GB/s, so past 8 splits its serial tail costs more than the memset + atomics it replaces.
-_SLAB_MAX_SPLIT = 8
-_GEMM_WS_BYTES = (64 << 20) + (64 << 10)
-_SPLITK_SLABS = os.environ.get("LJS_SPLITK_SLABS", "1") == "1"
-
-
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldc: int,
          a_kc: bool, b_kc: bool, batch: int = 1, sA: int = 0, sB: int = 0, sC: int = 0,
          bias: Optional[torch.Tensor] = None, sBias: int = 0, relu: bool = False, alpha: float = 1.0,
@@ -162,14 +151,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     if tile is None:
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc)
     eA = A.element_size()
-    ws, ws_bytes = None, 0
-    if out_f32 and 1 < splitk <= _SLAB_MAX_SPLIT and _SPLITK_SLABS:
-        w = _workspace(C.device, "gemm_splitk", _GEMM_WS_BYTES)
-        ws, ws_bytes = _p(w), w.numel() * 4
     rc = lib().ljs_gemm_bf16(ctypes.c_void_p(A.data_ptr() + a_off * eA), ctypes.c_void_p(B.data_ptr() + b_off * eA),
                              ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb,
                              ldc, sA, sB, sC, sBias, batch, int(a_kc), int(b_kc), int(out_f32), flags, alpha,
-                             splitk, tile, ws, ws_bytes, _stream(C))
+                             splitk, tile, _stream(C))
     _ck(rc, "ljs_gemm_bf16")
 
 

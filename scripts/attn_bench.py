@@ -23,6 +23,18 @@ res["fwd+bwd"] = timeit(lambda: torch.autograd.grad(hip.attention(q1, k1, v1, sc
 hip.set_attention_bwd_fused(False)
 res["fwd+bwd split"] = timeit(lambda: torch.autograd.grad(hip.attention(q1, k1, v1, scale), (q1, k1, v1), g))
 hip.set_attention_bwd_fused(True)
+# torch SDPA (ROCm flash / efficient backends) on the same problem, (B, H, S, D) layout
+import torch.nn.functional as F
+qt, kt, vt = (t.transpose(1, 2).contiguous() for t in (q, k, v))
+try:
+    res["torch sdpa fwd"] = timeit(lambda: F.scaled_dot_product_attention(qt, kt, vt, scale=scale))
+    qt1, kt1, vt1 = (t.detach().requires_grad_() for t in (qt, kt, vt))
+    ot = F.scaled_dot_product_attention(qt1, kt1, vt1, scale=scale)
+    gt = torch.randn_like(ot)
+    res["torch sdpa fwd+bwd"] = timeit(lambda: torch.autograd.grad(
+        F.scaled_dot_product_attention(qt1, kt1, vt1, scale=scale), (qt1, kt1, vt1), gt))
+except Exception as e:  # noqa: BLE001
+    print("sdpa failed:", e)
 fl = 4 * B * H * S * S * D
 res["fwd TFLOPS"] = fl / res["fwd"] / 1e6
 res["fwd+bwd TFLOPS"] = 3.5 * fl / res["fwd+bwd"] / 1e6

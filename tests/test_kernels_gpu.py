@@ -67,36 +67,6 @@ def test_gemm_dma_splitk_batched_broadcast(hip, tile):
     torch.testing.assert_close(out.float(), (row.float() @ W.float().t()).expand(500, 320), rtol=2e-2, atol=5e-2)
 
 
-@pytest.mark.parametrize("tile", [1282, 1284, 12883])
-@pytest.mark.parametrize("splitk", [2, 4, 8])
-def test_gemm_splitk_slab_combine(hip, tile, splitk):
-    """Split-K through per-split slabs + last-arriver ticket: repeated launches (the tickets re-arm
-    themselves), accumulate mode, ragged tile edges, and bit-agreement with the atomic path's sum
-    up to f32 reassociation."""
-    T, M, N, nb = 4096, 200, 136, 2
-    X = _rand(T, M, seed=11)
-    dY = _rand(T, nb * N, seed=12)
-    ref = torch.stack([X.float().t() @ dY[:, i * N:(i + 1) * N].float() for i in range(nb)])
-    for rep in range(3):
-        dW = torch.full((nb, M, N), float("nan"), dtype=torch.float32, device=dev)
-        hip.gemm(X, dY, dW, M, N, T, M, nb * N, N, False, False, batch=nb, sA=0, sB=N, sC=M * N, splitk=splitk,
-                 tile=tile, zero_c=True)
-        torch.testing.assert_close(dW, ref, rtol=1e-3, atol=5e-2, msg=f"rep {rep}")
-    acc = ref.clone()
-    hip.gemm(X, dY, acc, M, N, T, M, nb * N, N, False, False, batch=nb, sA=0, sB=N, sC=M * N, splitk=splitk,
-             tile=tile, accumulate=True)
-    torch.testing.assert_close(acc, 2 * ref, rtol=1e-3, atol=1e-1)
-    old = hip._SPLITK_SLABS
-    try:
-        hip._SPLITK_SLABS = False
-        dA = torch.full((nb, M, N), float("nan"), dtype=torch.float32, device=dev)
-        hip.gemm(X, dY, dA, M, N, T, M, nb * N, N, False, False, batch=nb, sA=0, sB=N, sC=M * N, splitk=splitk,
-                 tile=tile, zero_c=True)
-    finally:
-        hip._SPLITK_SLABS = old
-    torch.testing.assert_close(dW, dA, rtol=1e-5, atol=1e-3)
-
-
 def test_gemm_identity_asymmetric(hip):
     """A = I with an asymmetric B catches a transposed C write."""
     n = 64
