@@ -1,4 +1,4 @@
-// LJS_HIPCC_FLAGS: -mllvm -amdgpu-mfma-vgpr-form
+// LJS_HIPCC_FLAGS: -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans
 // Fused multi-head attention for gfx950 (head_dim 64), forward and backward.
 //
 // Semantics (case6_attention.py:120-133): scores = f32(q) . f32(k) * scale, f32 softmax over
@@ -163,8 +163,7 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
 #pragma unroll
   for (int jt = 1; jt < 4; ++jt)
     tmax = fmaxf(tmax, fmaxf(fmaxf(s[jt][0], s[jt][1]), fmaxf(s[jt][2], s[jt][3])));
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+  tmax = row4_max(tmax);
   // scores are compared raw (scale > 0 preserves order); the scale is applied in one FMA below
   const float m_new = fmaxf(st.m, tmax * a.scale_log2);
   float m_use = m_new;
@@ -194,29 +193,38 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
   }
 }
 
+// Block = 4 waves x NSUB sub-tiles of 16 queries (64 NSUB queries of one head).  Each K/V tile
+// staged through LDS serves all NSUB sub-tiles of every wave (NSUB x fewer K/V loads per
+// query).  Sub-tile s of wave w holds queries 16 (4 s + w) + lane,
+// interleaved so causal work stays balanced across waves.
+template <int NSUB>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
+  constexpr int QB = BLK * NSUB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const Tile3 tl = tile3((a.Sq + BLK - 1) / BLK, a.H);
+  const Tile3 tl = tile3((a.Sq + QB - 1) / QB, a.H);
   const int qb = tl.x, h = tl.h, b = tl.b;
-  const int qrow0 = qb * BLK + wave * 16;
-  const int qrow = qrow0 + (lane & 15);
-  const bool qok = qrow < a.Sq;
 
-  const bf16_t* qp = a.q + b * a.q_sb + (long)qrow * a.q_ss + h * a.q_sh;
-  bf16x8 qf[2] = {load_row_frag(qp, qok, 0, lane), load_row_frag(qp, qok, 1, lane)};
+  bf16x8 qf[NSUB][2];
+  FwdState st[NSUB];
+#pragma unroll
+  for (int sb = 0; sb < NSUB; ++sb) {
+    const int qrow = qb * QB + 16 * (4 * sb + wave) + (lane & 15);
+    const bool qok = qrow < a.Sq;
+    const bf16_t* qp = a.q + b * a.q_sb + (long)qrow * a.q_ss + h * a.q_sh;
+    qf[sb][0] = load_row_frag(qp, qok, 0, lane);
+    qf[sb][1] = load_row_frag(qp, qok, 1, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[sb].o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    st[sb].m = -INFINITY;
+    st[sb].l = 0.f;
+  }
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
 
   int kend = a.Sk;
-  if (a.causal) kend = min(a.Sk, a.q_offset + (qb + 1) * BLK);
+  if (a.causal) kend = min(a.Sk, a.q_offset + (qb + 1) * QB);
   const int nkt = (kend + BLK - 1) / BLK;
-
-  FwdState st;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) st.o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  st.m = -INFINITY;
-  st.l = 0.f;
 
   TileRegs tk, tv;
   if (nkt > 0) {
@@ -237,24 +245,33 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     const bf16_t* Kt = smem + cur * BLK * D;
     const bf16_t* Vt = smem + (2 + cur) * BLK * D;
     const int kbase = kt * BLK;
-    // wave-uniform: does any key of this tile need masking for any of this wave's queries?
-    const bool need_mask = kbase + BLK > a.Sk || (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
-    if (need_mask) fwd_tile<true>(a, st, Kt, Vt, qf, kbase, qrow, lane);
-    else fwd_tile<false>(a, st, Kt, Vt, qf, kbase, qrow, lane);
+#pragma unroll
+    for (int sb = 0; sb < NSUB; ++sb) {
+      const int qrow0 = qb * QB + 16 * (4 * sb + wave);
+      // wave-uniform: tile entirely in this sub-tile's causal future -> nothing to do
+      if (a.causal && kbase > qrow0 + 15 + a.q_offset) continue;
+      const bool need_mask = kbase + BLK > a.Sk || (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
+      if (need_mask) fwd_tile<true>(a, st[sb], Kt, Vt, qf[sb], kbase, qrow0 + (lane & 15), lane);
+      else fwd_tile<false>(a, st[sb], Kt, Vt, qf[sb], kbase, qrow0 + (lane & 15), lane);
+    }
     if (more) {
       tk.store(smem + (cur ^ 1) * BLK * D, tid);
       tv.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
     }
     __syncthreads();
   }
-  float lt = st.l;
-  lt += __shfl_xor(lt, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
-  if (qok) {
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    bf16_t* op = a.out + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
-    store_row_T(op, st.o, inv, lane);
-    if ((lane >> 4) == 0 && a.lse) a.lse[((long)b * a.H + h) * a.Sq + qrow] = lt > 0.f ? st.m + __log2f(lt) : INFINITY;
+#pragma unroll
+  for (int sb = 0; sb < NSUB; ++sb) {
+    const int qrow = qb * QB + 16 * (4 * sb + wave) + (lane & 15);
+    float lt = st[sb].l;
+    lt = row4_sum(lt);
+    if (qrow < a.Sq) {
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      bf16_t* op = a.out + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
+      store_row_T(op, st[sb].o, inv, lane);
+      if ((lane >> 4) == 0 && a.lse)
+        a.lse[((long)b * a.H + h) * a.Sq + qrow] = lt > 0.f ? st[sb].m + __log2f(lt) : INFINITY;
+    }
   }
 }
 
@@ -456,8 +473,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
         s = fmaf(__uint_as_float(x[k] & 0xffff0000u), __uint_as_float(y[k] & 0xffff0000u), s);
       }
     }
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    s = row4_sum(s);
     dl_q = s;
     if (qok && (lane >> 4) == 0) const_cast<float*>(a.delta)[((long)b * a.H + h) * a.Sq + qrow] = s;
   }
@@ -706,6 +722,10 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
 
 }  // namespace
 
+// forward sub-tiles per wave: 1 or 2 forces it; 0 = automatic; -1 = read LJS_ATTN_FWD_NSUB
+static int g_fwd_nsub = -1;
+LJS_API void ljs_attn_set_fwd_nsub(int v) { g_fwd_nsub = v; }
+
 // strides are in elements, ordered (batch, seq, head); head_dim must be 64 and contiguous.
 LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Sq, int Sk,
                          int H, const long* qs, const long* ks, const long* vs, const long* os, float scale,
@@ -720,7 +740,18 @@ LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, v
   a.Sq = Sq; a.Sk = Sk; a.H = H;
   a.scale = scale; a.scale_log2 = scale * LOG2E;
   a.causal = causal; a.q_offset = q_offset;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((Sq + BLK - 1) / BLK * H * B), dim3(256), 0, stream, a);
+  // queries per block: as many sub-tiles per wave as keep >= ~2 blocks per CU resident
+  if (g_fwd_nsub < 0) {
+    const char* e = getenv("LJS_ATTN_FWD_NSUB");
+    g_fwd_nsub = e ? atoi(e) : 0;
+  }
+  // NSUB = 1 measured fastest at the bench shape (26.4 vs 28.5 us for 2; 4 spills past 2 waves
+  // per SIMD), so 2 is opt-in
+  int nsub = g_fwd_nsub;
+  if (nsub != 1 && nsub != 2) nsub = 1;
+  const int nqb = (Sq + BLK * nsub - 1) / (BLK * nsub);
+  if (nsub == 2) hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(nqb * H * B), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3(nqb * H * B), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 

@@ -27,8 +27,30 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&b);
 }
 
+// two f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE); building the pair from two scalar
+// conversions costs a cvt each plus a shift and an SDWA or
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+  bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, v);
+}
+
+// Cross-row reductions with the gfx950 lane-swap instructions (no LDS round trip, no index
+// math): v_permlane16_swap exchanges odd 16-lane rows of one operand with even rows of the
+// other, v_permlane32_swap the upper half with the lower; with both operands = v each lane
+// ends up holding its own value and its partner's, so max/sum over lanes l, l^16, l^32,
+// l^48 (the four 16-lane rows) take two swaps and two ops.
+__device__ __forceinline__ float row4_max(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float row4_sum(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 
 __device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {

@@ -80,6 +80,14 @@ def set_attention_bwd_fused(enabled: bool):
     fn(1 if enabled else 0)
 
 
+def set_attention_fwd_nsub(nsub: int):
+    """Forward query sub-tiles per wave (1 or 2; 0 = default)."""
+    fn = lib().ljs_attn_set_fwd_nsub
+    fn.argtypes = [c_int]
+    fn.restype = None
+    fn(int(nsub))
+
+
 def available() -> bool:
     try:
         lib()
@@ -165,7 +173,7 @@ def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f3
     whenever K is a multiple of 64, else the register-staged 128/64 tiles."""
     tiles128 = -(-M // 128) * -(-N // 128) * batch * max(1, splitk)
     if K % 64 == 0 and tiles128 >= 96 and (out_f32 or (N % 8 == 0 and ldc % 8 == 0)):
-        if a_kc and b_kc and not out_f32 and M >= 4096 and N >= 1024 and N % 128 == 0:
+        if a_kc and b_kc and not out_f32 and M >= 4096 and N * batch >= 1024 and N % 128 == 0:
             return 2561
         return 1282
     return 128 if tiles128 >= 160 else 64

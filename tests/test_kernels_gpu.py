@@ -134,9 +134,16 @@ def attn_bwd_impl(request, hip):
     hip.set_attention_bwd_fused(True)
 
 
+@pytest.fixture(params=[1, 2])
+def attn_fwd_nsub(request, hip):
+    hip.set_attention_fwd_nsub(request.param)
+    yield request.param
+    hip.set_attention_fwd_nsub(0)
+
+
 @pytest.mark.parametrize("B,S,H", [(2, 256, 8), (1, 200, 4), (3, 64, 2), (1, 40, 3), (1, 320, 2)])
 @pytest.mark.parametrize("causal", [False, True])
-def test_attention_fwd_bwd(hip, attn_bwd_impl, B, S, H, causal):
+def test_attention_fwd_bwd(hip, attn_bwd_impl, attn_fwd_nsub, B, S, H, causal):
     D = 64
     # q/k/v as column slices of one fused QKV buffer, exactly as the model produces them
     qkv = _rand(B, S, 3 * H * D, seed=7).reshape(B, S, 3, H, D)
@@ -162,7 +169,7 @@ def test_attention_fwd_bwd(hip, attn_bwd_impl, B, S, H, causal):
 
 
 @pytest.mark.parametrize("Sq,Sk,causal,q_offset", [(192, 128, False, 0), (130, 256, True, 64), (64, 100, True, 0)])
-def test_attention_bwd_block_fused_matches_split(hip, Sq, Sk, causal, q_offset):
+def test_attention_bwd_block_fused_matches_split(hip, attn_fwd_nsub, Sq, Sk, causal, q_offset):
     """Block backward (ring attention's kernel: external O / lse, Sq != Sk, causal offset):
     the fused single-pass kernel == the split dQ + dK/dV kernels."""
     B, H, D = 2, 3, 64
