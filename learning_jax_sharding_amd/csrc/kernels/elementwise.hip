@@ -124,6 +124,8 @@ __global__ void sum_all_vec_kernel(const T* __restrict__ in, long n, float* __re
   }
 }
 
+constexpr int kGroup = 32, kMaxSumBlocks = 1024;  // sum_all: ticket group size, max grid
+
 // Whole-array sum with the in-launch last-arriver reduction: no memset, no second kernel, and
 // the result is written directly in the output dtype (f32 or bf16).
 template <typename T>
@@ -160,6 +162,11 @@ __global__ void sum_all_ticket_kernel(const T* __restrict__ in, long n, float* _
   if (lane == 0) part[w] = s;
   __syncthreads();
   if (w == 0) {
+    // two-level last-arriver: one ticket word per group of kGroup blocks, then one top ticket
+    // over the groups (a single word retires only ~88 arrivals/us, so 1024 arrivals on one
+    // word would serialise for ~12 us)
+    const int G = (int)gridDim.x, grp = blockIdx.x / kGroup, ngrp = (G + kGroup - 1) / kGroup;
+    const int in_grp = min(kGroup, G - grp * kGroup);
     if (lane == 0) {
       float t = 0.f;
       for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += part[k];
@@ -167,16 +174,22 @@ __global__ void sum_all_ticket_kernel(const T* __restrict__ in, long n, float* _
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int last = 0;
-    if (lane == 0) last = ticket_last(ticket, gridDim.x);
+    if (lane == 0) last = ticket_last(ticket + 1 + grp, in_grp);
     last = __shfl(last, 0, 64);
-    if (last) {
-      float v = 0.f;
-      for (int i = lane; i < (int)gridDim.x; i += 64) v += sc1_load(partials + i);
-      v = warp_sum64(v);
-      if (lane == 0) {
-        if (out_bf16) *reinterpret_cast<bf16_t*>(out) = f2bf(v);
-        else *reinterpret_cast<float*>(out) = v;
-      }
+    if (!last) return;
+    float v = lane < in_grp ? sc1_load(partials + grp * kGroup + lane) : 0.f;
+    v = warp_sum64(v);
+    if (lane == 0) sc1_store(partials + kMaxSumBlocks + grp, v);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = 0;
+    if (lane == 0) last = ticket_last(ticket, ngrp);
+    last = __shfl(last, 0, 64);
+    if (!last) return;
+    v = lane < ngrp ? sc1_load(partials + kMaxSumBlocks + lane) : 0.f;
+    v = warp_sum64(v);
+    if (lane == 0) {
+      if (out_bf16) *reinterpret_cast<bf16_t*>(out) = f2bf(v);
+      else *reinterpret_cast<float*>(out) = v;
     }
   }
 }
@@ -236,6 +249,35 @@ __global__ void colsum_bcast_kernel(const void* __restrict__ in, int is_bf16, in
   if (c >= C) return;
   const float v = is_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(in)[c]) : reinterpret_cast<const float*>(in)[c];
   out[c] = (accumulate ? out[c] : 0.f) + v * (float)R;
+}
+
+// Split-K combine for the weight-gradient GEMMs: the GEMM writes each K-chunk's f32 partial
+// [R][C] tile set to its own slab with plain 16-byte stores (no f32 atomics, which the chip
+// retires at ~1.3 TB/s, and no memset of the output), and this kernel sums the S slabs once,
+// reading each slab as one streaming pass.  The output's columns may be split into column
+// blocks of width cb stored as separate [R][cb] matrices (out_bs apart): the fused dW[q|k|v]
+// GEMM produces [640][1536] slabs whose column blocks are dWq, dWk, dWv.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slabs, int S, long slab_stride,
+                                                          int R, int C, float* __restrict__ out, int cb,
+                                                          long out_bs, int accumulate) {
+  const long n4 = (long)R * C / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long e = 4 * i;
+    f32x4 acc = *reinterpret_cast<const f32x4*>(slabs + e);
+    int s = 1;
+    for (; s + 3 < S; s += 4) {  // 4 independent slab loads in flight
+      f32x4 v0 = *reinterpret_cast<const f32x4*>(slabs + s * slab_stride + e);
+      f32x4 v1 = *reinterpret_cast<const f32x4*>(slabs + (s + 1) * slab_stride + e);
+      f32x4 v2 = *reinterpret_cast<const f32x4*>(slabs + (s + 2) * slab_stride + e);
+      f32x4 v3 = *reinterpret_cast<const f32x4*>(slabs + (s + 3) * slab_stride + e);
+      acc += (v0 + v1) + (v2 + v3);
+    }
+    for (; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(slabs + s * slab_stride + e);
+    const int r = (int)(e / C), c = (int)(e % C);
+    float* dst = out + (long)(c / cb) * out_bs + (long)r * cb + (c % cb);
+    if (accumulate) acc += *reinterpret_cast<const f32x4*>(dst);
+    *reinterpret_cast<f32x4*>(dst) = acc;
+  }
 }
 
 // out[0..n) = (bf16) *g: materialises the broadcast row of a scalar cotangent (e.g. of y.sum())
@@ -569,15 +611,17 @@ LJS_API int ljs_cast_transpose_f32_bf16(const void* in, void* out, int R, int C,
 }
 
 // out (scalar, f32 or bf16 per out_bf16) = sum(in); in is f32 (is_bf16=0) or bf16.
-// ws: persistent workspace of >= 257 floats whose last word (the ticket) is zero at rest.
+// ws: persistent workspace of >= 1089 floats whose ticket words are zero at rest.
 LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, int out_bf16, void* ws, hipStream_t s) {
+  // ws layout: [partials: kMaxSumBlocks][group partials: 32][top ticket][group tickets: 32]
   float* partials = (float*)ws;
-  unsigned* ticket = (unsigned*)ws + 256;
+  unsigned* ticket = (unsigned*)ws + kMaxSumBlocks + 32;
   const bool aligned = (((uintptr_t)in) & 15) == 0;
   if (aligned) {
-    long per = 256L * (is_bf16 ? 8 : 4) * 4;  // ~4 vector loads per thread
+    // ~4 blocks per CU with 4 independent 16-byte loads per thread keep >= 4 MiB in flight
+    long per = 256L * (is_bf16 ? 8 : 4) * 4;
     int g = grid_for(n, (int)per);
-    if (g > 256) g = 256;
+    if (g > kMaxSumBlocks) g = kMaxSumBlocks;
     if (is_bf16)
       hipLaunchKernelGGL(sum_all_ticket_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, partials,
                          ticket, out, out_bf16);
@@ -635,6 +679,22 @@ LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void*
     hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)in, R, C, ld, (float*)out);
   else
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)in, R, C, ld, (float*)out);
+  return (int)hipGetLastError();
+}
+
+// out (column blocks of width cb, out_bs floats apart) = sum of S f32 [R][C] slabs (slab_stride
+// floats apart).  Requires C % 4 == 0, cb % 4 == 0, C % cb == 0 and 16-byte aligned buffers.
+LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, int C, void* out, int cb, long out_bs,
+                            int accumulate, hipStream_t s) {
+  if (C % 4 || cb % 4 || C % cb || slab_stride % 4 || out_bs % 4 || S < 1 || (((uintptr_t)slabs) & 15) ||
+      (((uintptr_t)out) & 15))
+    return (int)hipErrorInvalidValue;
+  const long n4 = (long)R * C / 4;
+  int grid = (int)((n4 + 255) / 256);
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, s, (const float*)slabs, S, slab_stride, R, C,
+                     (float*)out, cb, out_bs, accumulate);
   return (int)hipGetLastError();
 }
 

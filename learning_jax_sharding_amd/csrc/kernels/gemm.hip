@@ -352,6 +352,8 @@ __device__ __forceinline__ WorkItem decode_item(const GemmArgs& p, int item, int
   return w;
 }
 
+constexpr int kSC1 = 16;  // buffer-instruction cache policy bit: sc1 (gfx940-family CPol::SC1)
+
 template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
   constexpr int NW = WM * WN;
@@ -360,12 +362,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
   using TA = DmaTile<BM, A_KC, NW>;
   using TB = DmaTile<BN, B_KC, NW>;
   constexpr int L = TA::PER_WAVE + TB::PER_WAVE;  // DMA instructions per wave per K-tile
-  // bf16 output: C^T blocks (operands swapped), lanes pair up into 16-byte row chunks and
-  // leave through exactly S_EPI buffer stores per lane (masked lanes get an out-of-range
-  // offset, so the count is exact and the next K-step's counted vmcnt stays valid).
-  // f32 output (split-K atomics / weight grads): plain orientation, full drain after it.
-  constexpr bool SWAP = !OUT_F32;
-  static_assert(!SWAP || TN % 2 == 0, "column blocks pair up for 16-byte stores");
+  // Operands swapped (C^T = B^T A^T per 16x16 block): each lane ends with 4 CONSECUTIVE
+  // columns of one output row.  bf16 output: lanes pair up into 16-byte row chunks and leave
+  // through exactly S_EPI buffer stores per lane (masked lanes get an out-of-range offset, so
+  // the count is exact and the next K-step's counted vmcnt stays valid).  f32 output (split-K
+  // slabs / atomics, weight grads): one 16-byte store (or 4 atomics) per block, full drain after.
+  constexpr bool SWAP = true;
+  static_assert(OUT_F32 || TN % 2 == 0, "column blocks pair up for 16-byte stores");
   constexpr int S_EPI = TM * TN / 2;
   static_assert(L * (NST - 1) + S_EPI <= 63, "vmcnt immediate range");
   __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
@@ -429,6 +432,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
   const bool has_bias = (p.flags & 2) && p.splitk == 1;
   const bool bias_f32 = p.flags & 4;
   const bool accumulate = p.flags & 8;
+  // flags & 32: output stores with sc1, which drop the written lines from the XCD's L2 (plain
+  // stores keep them) so the output stream does not evict the operand panels other blocks reuse
+  const bool st_sc1 = p.flags & 32;
   const __amdgpu_buffer_rsrc_t rc =
       make_rsrc(p.C, (OUT_F32 ? 4 : 2) * ((long)(p.batch - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
   bool after_epi = false;
@@ -475,7 +481,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
     const WorkItem w = decode_item(p, slot + G * it, ntm, ntn);
     const int m0 = w.m0 * BM + wr * (BM / WM), n0 = w.n0 * BN + wc * (BN / WN);
     const int g = lane >> 4;
-    if constexpr (SWAP) {
+    if constexpr (!OUT_F32) {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]; lanes g, g^1 trade halves so
       // even g owns cols 16 j0 + 4 g .. +7 and odd g owns 16 j1 + 4 (g - 1) .. +7
       const bool even = (g & 1) == 0;
@@ -522,38 +528,58 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
           const int row = m0 + ii * 16 + (lane & 15);
           const bool ok = row < p.M && col < p.N;  // N % 8 == 0 (launcher): chunks are whole
           const int off = ok ? (int)(((long)w.b * p.sC + (long)row * p.ldc + col) * 2) : 0x7ffffff0;
-          __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, 0);
+          if (st_sc1) __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, kSC1);
+          else __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, 0);
         }
       }
       after_epi = true;
     } else {
-      // lane holds C[16 ii + 4 g + r][16 j + (lane & 15)]
+      // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]
+      const bool vec = (p.ldc & 3) == 0 && (p.sC & 3) == 0 && ((((uintptr_t)p.C) & 15) == 0);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = n0 + j * 16 + (lane & 15);
-        float bv = 0.f;
-        if (has_bias && col < p.N) {
-          const long bo = (long)w.b * p.sBias + col;
-          bv = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo]
-                        : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo]);
+        const int col = n0 + j * 16 + 4 * g;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (has_bias) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (col + e >= p.N) continue;
+            const long bo = (long)w.b * p.sBias + col + e;
+            bv[e] = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo]
+                             : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo]);
+          }
         }
 #pragma unroll
         for (int ii = 0; ii < TM; ++ii) {
+          const int row = m0 + ii * 16 + (lane & 15);
+          f32x4 v;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = m0 + ii * 16 + 4 * g + r;
-            float v = acc[ii][j][r] * p.alpha + bv;
-            if (relu) v = fmaxf(v, 0.f);
-            if (row >= p.M || col >= p.N) continue;
-            float* C = reinterpret_cast<float*>(p.C) + (long)w.b * p.sC + (long)row * p.ldc + col;
-            if (p.splitk > 1) atomicAdd(C, v);
-            else *C = accumulate ? *C + v : v;
+          for (int e = 0; e < 4; ++e) {
+            v[e] = acc[ii][j][e] * p.alpha + bv[e];
+            if (relu) v[e] = fmaxf(v[e], 0.f);
           }
           acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (row >= p.M || col >= p.N) continue;
+          float* C = reinterpret_cast<float*>(p.C) + (long)w.b * p.sC + (long)row * p.ldc + col;
+          if (p.splitk > 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (col + e < p.N) atomicAdd(C + e, v[e]);
+          } else if (vec && col + 4 <= p.N) {
+            if (accumulate) v += *reinterpret_cast<const f32x4*>(C);
+            const int off = (int)(((long)w.b * p.sC + (long)row * p.ldc + col) * 4);
+            const u32x4 bits = __builtin_bit_cast(u32x4, v);
+            if (st_sc1) __builtin_amdgcn_raw_buffer_store_b128(bits, rc, off, 0, kSC1);
+            else __builtin_amdgcn_raw_buffer_store_b128(bits, rc, off, 0, 0);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (col + e < p.N) C[e] = accumulate ? C[e] + v[e] : v[e];
+          }
         }
       }
       // drain before the next item's counted waits; after the block's last item the wave just
-      // ends (its atomics complete on their own and the CU is free for the next block sooner)
+      // ends (its stores complete on their own and the CU is free for the next block sooner)
       if (it + 1 < my_items) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }

@@ -43,6 +43,7 @@ _SIGS = {
     "ljs_sum_all": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_fill_row_bf16": [c_void_p, c_int, c_void_p, c_long, c_void_p],
+    "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ljs_adam_f32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
@@ -141,6 +142,11 @@ def _longs(vals) -> ctypes.Array:
 
 
 # ============================================================================ GEMM
+# output stores with sc1 (drop the written lines from L2 so the output stream does not evict the
+# operand panels that neighbouring blocks re-read)
+_GEMM_SC1 = os.environ.get("LJS_GEMM_SC1", "1") == "1"
+
+
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldc: int,
          a_kc: bool, b_kc: bool, batch: int = 1, sA: int = 0, sB: int = 0, sC: int = 0,
          bias: Optional[torch.Tensor] = None, sBias: int = 0, relu: bool = False, alpha: float = 1.0,
@@ -155,7 +161,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     out_f32 = C.dtype == torch.float32
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
-        (16 if zero_c else 0)
+        (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0)
     if tile is None:
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc)
     eA = A.element_size()
@@ -372,7 +378,7 @@ def _sum_all_raw(t: torch.Tensor, out_dtype: torch.dtype = torch.float32) -> tor
     t = t.contiguous()
     out_bf16 = out_dtype == torch.bfloat16 and t.data_ptr() % 16 == 0
     out = torch.empty((), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=t.device)
-    ws = _workspace(t.device, "sum_all", 257 * 4)
+    ws = _workspace(t.device, "sum_all", 1089 * 4)
     rc = lib().ljs_sum_all(_p(t), int(t.dtype == torch.bfloat16), t.numel(), _p(out), int(out_bf16), _p(ws),
                            _stream(t))
     _ck(rc, "sum_all")
@@ -460,6 +466,15 @@ def _torch_linear(x, w, b, compute_dtype, relu, out_dtype):
     if relu:
         y = torch.relu(y)
     return y.to(out_dtype)
+
+
+def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, accumulate: bool = False) -> None:
+    """out = sum over the leading dim of f32 ``slabs`` [S][R][C], written as C/cb column blocks of
+    width ``cb`` stored ``out_bs`` floats apart (the split-K combine of the weight-grad GEMMs)."""
+    S, R, C = slabs.shape
+    assert slabs.dtype == torch.float32 and out.dtype == torch.float32 and slabs.is_contiguous()
+    rc = lib().ljs_slab_reduce(_p(slabs), S, R * C, R, C, _p(out), cb, out_bs, int(accumulate), _stream(out))
+    _ck(rc, "slab_reduce")
 
 
 def colsum_ld(t: torch.Tensor, R: int, C: int, ld: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -18,6 +18,7 @@ leading dimension instead of being materialised.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -34,6 +35,24 @@ def _splitk(M: int, N: int, K: int, batch: int, tile: int) -> int:
         return 1
     s = max(1, min(16, round(400 / tiles), K // 1024))
     return s
+
+
+_DW_SPLIT = int(os.environ.get("LJS_DW_SPLIT", "0"))  # tuning override of the K-chunk count
+
+
+def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: int, out: torch.Tensor, cb: int,
+              out_bs: int) -> None:
+    """out (column blocks of width cb, out_bs apart) = xb^T @ dy for xb [T][K], dy [T][Nt] (row
+    stride ld, 0 = broadcast row): S K-chunks of the token dim run as one batched LDS-DMA GEMM
+    into f32 slabs [S][K][Nt], combined by one streaming reduction."""
+    S = _DW_SPLIT or hip.pick_splitk_dma(K, Nt, T, 1)
+    if T % (64 * S):
+        S = hip.pick_splitk_dma(K, Nt, T, 1)
+    kc = T // S
+    slabs = torch.empty((S, K, Nt), dtype=torch.float32, device=xb.device)
+    hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
+             tile=1282)
+    hip.slab_reduce(slabs, out, cb, out_bs)
 
 
 def _row_view(dy: torch.Tensor, M: int, N: int) -> Tuple[torch.Tensor, int]:
@@ -129,21 +148,37 @@ class _Linear(torch.autograd.Function):
             batched = (len(want) == nw and nw > 1 and ld0 > 0 and all(
                 mats[i][1] == ld0 and mats[i][0].data_ptr() == t0.data_ptr() + i * N * 2 for i in want))
             dma = M % 64 == 0
-            tile = 1282 if dma else (128 if (K >= 256 and N >= 256) else 64)
-            if batched:
-                dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
-                sk = hip.pick_splitk_dma(K, N, M, nw) if dma else _splitk(K, N, M, nw, tile)
-                hip.gemm(xb, t0, dW, K, N, M, K, ld0, N, False, False, batch=nw, sA=0, sB=N, sC=K * N,
-                         splitk=sk, tile=tile, zero_c=True)
-                for i in want:
-                    dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
+            if dma:
+                # split-K as a batch over K-chunks writing per-chunk f32 slabs, then one combine
+                # pass (no atomics, no memset): the column blocks of a fused [K][nw*N] product are
+                # the nw weight gradients
+                if batched:
+                    dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
+                    _dw_slabs(xb, t0, ld0, M, K, nw * N, dW, N, K * N)
+                    for i in want:
+                        dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
+                else:
+                    for i in want:
+                        t, ld = mats[i]
+                        dW = torch.empty((K, N), dtype=torch.float32, device=dev)
+                        _dw_slabs(xb, t, ld, M, K, N, dW, N, 0)
+                        dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
             else:
-                for i in want:
-                    t, ld = mats[i]
-                    dW = torch.empty((K, N), dtype=torch.float32, device=dev)
-                    sk = hip.pick_splitk_dma(K, N, M, 1) if dma else _splitk(K, N, M, 1, tile)
-                    hip.gemm(xb, t, dW, K, N, M, K, ld, N, False, False, splitk=sk, tile=tile, zero_c=True)
-                    dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
+                tile = 128 if (K >= 256 and N >= 256) else 64
+                if batched:
+                    dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
+                    sk = _splitk(K, N, M, nw, tile)
+                    hip.gemm(xb, t0, dW, K, N, M, K, ld0, N, False, False, batch=nw, sA=0, sB=N, sC=K * N,
+                             splitk=sk, tile=tile, zero_c=True)
+                    for i in want:
+                        dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
+                else:
+                    for i in want:
+                        t, ld = mats[i]
+                        dW = torch.empty((K, N), dtype=torch.float32, device=dev)
+                        sk = _splitk(K, N, M, 1, tile)
+                        hip.gemm(xb, t, dW, K, N, M, K, ld, N, False, False, splitk=sk, tile=tile, zero_c=True)
+                        dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
         # ---- db
         if has_b and ctx.needs_input_grad[1] and live:
             tot = None

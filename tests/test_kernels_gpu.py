@@ -354,6 +354,41 @@ def test_ticket_reductions_rearm(hip):
     torch.testing.assert_close(got, row.float() * 1000, rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("S,R,C,cb", [(8, 640, 1536, 512), (16, 512, 640, 640), (3, 40, 24, 8)])
+def test_slab_reduce(hip, S, R, C, cb):
+    slabs = _rand(S, R, C, dtype=torch.float32, seed=400 + S)
+    nb = C // cb
+    out = torch.empty((nb, R, cb), dtype=torch.float32, device=dev)
+    hip.slab_reduce(slabs, out, cb, R * cb)
+    ref = slabs.sum(0).reshape(R, nb, cb).permute(1, 0, 2)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+    hip.slab_reduce(slabs, out, cb, R * cb, accumulate=True)
+    torch.testing.assert_close(out, 2 * ref, rtol=1e-5, atol=2e-4)
+
+
+@pytest.mark.parametrize("T", [16384, 4096, 192])
+def test_linear_weight_grad_slabs(hip, T):
+    """dW of the fused QKV dense (3 kernels, one [T][1536] cotangent) and of a single dense with a
+    broadcast-row cotangent, through the K-chunk slab GEMM + combine, vs fp32 torch."""
+    x = _rand(T, 640, seed=11)
+    ws = [(_rand(640, 512, dtype=torch.float32, seed=12 + i) * 0.05).requires_grad_() for i in range(3)]
+    ys = hip.linear(x, ws, None, torch.bfloat16, False, torch.bfloat16)
+    big = _rand(T, 1536, seed=20)
+    for dys in ([big[:, 512 * i:512 * (i + 1)] for i in range(3)],      # column blocks: one batched GEMM
+                [_rand(T, 512, seed=21 + i) for i in range(3)]):        # separate buffers
+        grads = torch.autograd.grad(ys, ws, dys, retain_graph=True)
+        for g, dy in zip(grads, dys):
+            ref = x.float().t() @ dy.float()
+            torch.testing.assert_close(g, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
+    w = (_rand(512, 640, dtype=torch.float32, seed=30) * 0.05).requires_grad_()
+    xo = _rand(T, 512, seed=31)
+    (y,) = hip.linear(xo, [w], None, torch.bfloat16, False, torch.bfloat16)
+    row = _rand(640, seed=32)
+    (g,) = torch.autograd.grad([y], [w], [row.expand(T, 640)])
+    ref = xo.float().sum(0)[:, None] * row.float()[None, :]
+    torch.testing.assert_close(g, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
+
+
 def test_sum_backward_broadcast_row(hip):
     x = _rand(8, 16, 96, seed=5).requires_grad_()
     s = hip.sum_all(x, torch.bfloat16)
