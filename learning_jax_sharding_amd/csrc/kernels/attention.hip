@@ -517,6 +517,34 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   if (qok) store_row_T(a.out + b * a.out_sb + (long)qrow * a.out_ss + h * a.out_sh, dq, a.scale, lane);
 }
 
+// ---- LDS-DMA from inline asm.  The compiler's waitcnt pass treats a builtin LDS-DMA as a
+// possible writer of EVERY LDS location and puts vmcnt waits in front of all later ds_read /
+// ds_write, which serialises a prefetch behind the math it should overlap.  Issued as asm the
+// DMA is invisible to that pass; the kernel waits for it explicitly (vmcnt(0) + barrier).
+// Extra untracked vector-memory ops can only make the compiler's own counted waits wait longer
+// (the counter retires in order), never shorter.
+__device__ __forceinline__ u32x4 rsrc_u4(const void* base, long bytes) {
+  const unsigned long long b = (unsigned long long)base;
+  u32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((unsigned)b);
+  r[1] = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) & 0xffffu;  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes));
+  r[3] = 0x00020000u;
+  return r;
+}
+// 64 lanes x 16 B from rsrc + voff (per lane) to LDS [lds, lds + 1 KiB), lane-contiguous
+__device__ __forceinline__ void dma_lds_x4(const u32x4& rs, int voff, const void* lds) {
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LDS_PTR(const void))lds);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :: "v"(voff), "s"(rs), "s"(m) : "memory", "m0");
+}
+// 64 lanes x 4 B to LDS [lds, lds + 256 B)
+__device__ __forceinline__ void dma_lds_x1(const u32x4& rs, int voff, const void* lds) {
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LDS_PTR(const void))lds);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds"
+               :: "v"(voff), "s"(rs), "s"(m) : "memory", "m0");
+}
+
 // ---------------------------------------------------------------- fused short-key backward
 // Sk <= 256: ONE workgroup (8 waves) per (batch, head) keeps K and V in LDS (each wave
 // owns 32 keys for dK / dV), then sweeps the query blocks once.  S and dP are computed
@@ -559,7 +587,9 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
   // two 32-query halves: P / dS of a half feed the dK/dV MFMAs right away (register pressure)
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
-    f32x4 p[2][2], ds[2][2];
+    // P and dS leave the softmax already packed to bf16 pairs (the MFMA B-operand layout of
+    // frag_acc): 16 live VGPRs instead of 32 f32, which keeps the kernel out of scratch
+    u32x4 pbu[2], sbu[2];
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
       const int t = 2 * s2 + tt;
@@ -574,29 +604,31 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
         s = mfma16x16x32(q1f, frag_rows(Ks, key0 + 16 * j, 1, lane), s);
         dp = mfma16x16x32(o0f, frag_rows(Vs, key0 + 16 * j, 0, lane), dp);
         dp = mfma16x16x32(o1f, frag_rows(Vs, key0 + 16 * j, 1, lane), dp);
+        float pv[4], dsv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float pv = fast_exp2(fmaf(s[r], a.scale_log2, -lse[r]));
+          pv[r] = fast_exp2(fmaf(s[r], a.scale_log2, -lse[r]));
           if constexpr (MASK) {
             int q = q0 + 16 * t + 4 * g + r, key = key0 + 16 * j + (lane & 15);
             bool ok = q < a.Sq && key < a.Sk && !(a.causal && key > q + a.q_offset);
-            pv = ok ? pv : 0.f;
+            pv[r] = ok ? pv[r] : 0.f;
           }
-          p[j][tt][r] = pv;
-          ds[j][tt][r] = pv * (dp[r] - dl[r]);
+          dsv[r] = pv[r] * (dp[r] - dl[r]);
         }
+        pbu[j][2 * tt] = pack_bf16x2(pv[0], pv[1]);
+        pbu[j][2 * tt + 1] = pack_bf16x2(pv[2], pv[3]);
+        sbu[j][2 * tt] = pack_bf16x2(dsv[0], dsv[1]);
+        sbu[j][2 * tt + 1] = pack_bf16x2(dsv[2], dsv[3]);
         // dS^T row (this lane's key), queries 16t + 4g .. +3
-        u32x2 w;
-        w[0] = pack_bf16x2(ds[j][tt][0], ds[j][tt][1]);
-        w[1] = pack_bf16x2(ds[j][tt][2], ds[j][tt][3]);
-        *reinterpret_cast<u32x2*>(dSt + img8(key0 + 16 * j + (lane & 15), 4 * t + g)) = w;
+        *reinterpret_cast<u32x2*>(dSt + img8(key0 + 16 * j + (lane & 15), 4 * t + g)) =
+            u32x2{sbu[j][2 * tt], sbu[j][2 * tt + 1]};
       }
     }
     bf16x8 pb[2], sb[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      pb[j] = frag_acc(p[j][0], p[j][1]);
-      sb[j] = frag_acc(ds[j][0], ds[j][1]);
+      pb[j] = __builtin_bit_cast(bf16x8, pbu[j]);
+      sb[j] = __builtin_bit_cast(bf16x8, sbu[j]);
     }
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
@@ -616,6 +648,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Vs[FK * D];
   __shared__ __attribute__((aligned(16))) bf16_t dSt[FK * BLK];
   __shared__ __attribute__((aligned(16))) bf16_t QO[4 * BLK * D];  // Q[2], dO[2]
+  __shared__ __attribute__((aligned(16))) bf16_t Os[BLK * D];      // next block's O (delta only)
   __shared__ __attribute__((aligned(16))) float rowc[2][2][BLK];    // [buf][lse, delta][query]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int h = blockIdx.x, b = blockIdx.y;
@@ -640,28 +673,44 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   const float* lse = a.lse + ((long)b * a.H + h) * a.Sq;
   const int nqt = (a.Sq + BLK - 1) / BLK;
 
-  TileRegs1 tq, tdo, to;
-  float lse_v = 0.f;
-  auto fetch = [&](int q0) {
-    tq.load(qb, a.q_ss, q0, a.Sq, tid);
-    tdo.load(dob, a.do_ss, q0, a.Sq, tid);
-    to.load(ob, a.o_ss, q0, a.Sq, tid);
-    if (tid < BLK) lse_v = q0 + tid < a.Sq ? lse[q0 + tid] : INFINITY;
+  // Next query block's Q / dO / O (and its log-sum-exp) arrive by LDS-DMA (buffer_load ... lds,
+  // issued from inline asm -- see dma_lds_x4):
+  // no staging VGPRs (those spilled the kernel to scratch, and every scratch reload's vmcnt(0)
+  // waited for the whole prefetch), one 1 KiB piece per wave per tile.  The img16 swizzle is
+  // applied on the SOURCE address (a wave's DMA fills 1 KiB of LDS contiguously); rows past Sq
+  // get an out-of-range offset and read as zeros.
+  const u32x4 rq = rsrc_u4(qb, 2 * ((long)(a.Sq - 1) * a.q_ss + D));
+  const u32x4 rdo = rsrc_u4(dob, 2 * ((long)(a.Sq - 1) * a.do_ss + D));
+  const u32x4 ro = rsrc_u4(ob, 2 * ((long)(a.Sq - 1) * a.o_ss + D));
+  const u32x4 rl = rsrc_u4(lse, 4L * a.Sq);
+  const int drow = 8 * wave + (lane >> 3);
+  const int dchunk = ((lane & 7) ^ (((drow >> 1) & 3) << 1)) * 8;  // element offset in the row
+  auto issue = [&](int q0, int buf) {
+    const int r = q0 + drow;
+    const bool ok = r < a.Sq;
+    const int oq = ok ? (int)(((long)r * a.q_ss + dchunk) * 2) : 0x7ffffff0;
+    const int odo = ok ? (int)(((long)r * a.do_ss + dchunk) * 2) : 0x7ffffff0;
+    const int oo = ok ? (int)(((long)r * a.o_ss + dchunk) * 2) : 0x7ffffff0;
+    dma_lds_x4(rq, oq, QO + buf * BLK * D + wave * 512);
+    dma_lds_x4(rdo, odo, QO + (2 + buf) * BLK * D + wave * 512);
+    dma_lds_x4(ro, oo, Os + wave * 512);
+    if (wave == 0) dma_lds_x1(rl, q0 + lane < a.Sq ? (q0 + lane) * 4 : 0x7ffffff0, &rowc[buf][0][0]);
   };
-  auto stage = [&](int buf) {
-    tq.store(QO + buf * BLK * D, tid);
-    tdo.store(QO + (2 + buf) * BLK * D, tid);
-    float s = dot_bf16x8(to.v, tdo.v);  // 8 threads per query row
+  // after every wave's DMA of `buf` landed (vmcnt(0) + barrier): delta = rowsum(dO o O)
+  auto finish = [&](int buf) {
+    const int row = tid >> 3, c16 = tid & 7;  // 8 threads per query row
+    const u32x4 o = *reinterpret_cast<const u32x4*>(Os + img16(row, c16));
+    const u32x4 d = *reinterpret_cast<const u32x4*>(QO + (2 + buf) * BLK * D + img16(row, c16));
+    float s = dot_bf16x8(o, d);
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
-    if ((tid & 7) == 0) rowc[buf][1][tid >> 3] = s;
-    if (tid < BLK) rowc[buf][0][tid] = lse_v;
+    if (c16 == 0) rowc[buf][1][row] = s;
   };
-  if (nqt > 0) {
-    fetch(0);
-    stage(0);
-  }
+  if (nqt > 0) issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nqt > 0) finish(0);
   __syncthreads();
 
   f32x4 dk[2][4], dv[2][4];
@@ -677,7 +726,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
     const int cur = it & 1;
     const int q0 = it * BLK;
     const bool more = it + 1 < nqt;
-    if (more) fetch(q0 + BLK);
+    if (more) issue(q0 + BLK, cur ^ 1);
     const bf16_t* Qt = QO + cur * BLK * D;
     const bf16_t* Ot = QO + (2 + cur) * BLK * D;
     if (active) {
@@ -696,6 +745,9 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
         dq[i] = mfma16x16x32(ka, sb, dq[i]);
       }
     }
+    // this wave's DMA pieces of the next block landed (waited here, before the dQ stores join
+    // the vmcnt queue); the barrier below publishes everyone's
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int qrow = q0 + 16 * qt + (lane & 15);
     if (qrow < a.Sq) {
       bf16_t* rowp = a.out3 + b * a.out3_sb + (long)qrow * a.out3_ss + h * a.out3_sh;
@@ -707,8 +759,11 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
         *reinterpret_cast<u32x2*>(rowp + 16 * (dt0 + i) + 4 * g) = w;
       }
     }
-    if (more) stage(cur ^ 1);
     __syncthreads();
+    if (more) {
+      finish(cur ^ 1);
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {

@@ -83,6 +83,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + idx;
 }
 
+// raw buffer resource over [base, base + bytes): out-of-range offsets read 0 and drop stores.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long bytes) {
+  // readfirstlane the inputs so the compiler can prove the descriptor wave-uniform (no waterfall)
+  const unsigned long long b = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes));
+  void* p = (void*)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, nb, 0x00020000);
+}
+
 // ---- in-launch "last arriver" hand-off (cdna_hip_programming.md §6 Guideline 16, valid form:
 // write-through (sc1) payload stores by ONE wave, that wave's vmcnt(0), one lane's agent-scope
 // atomic ticket add; the block whose add returns n-1 reads every payload with sc1 loads and

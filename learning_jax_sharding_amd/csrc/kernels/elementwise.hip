@@ -2,6 +2,7 @@
 // Philox RNG.  All vectorised to 16 bytes per lane (CDNA Guideline 13); grid-stride loops
 // capped at 2048 workgroups so one launch fills the 256 CUs without oversubscription.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -621,7 +622,9 @@ LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, int out_
     // ~4 blocks per CU with 4 independent 16-byte loads per thread keep >= 4 MiB in flight
     long per = 256L * (is_bf16 ? 8 : 4) * 4;
     int g = grid_for(n, (int)per);
-    if (g > kMaxSumBlocks) g = kMaxSumBlocks;
+    static const int cap_env = getenv("LJS_SUM_BLOCKS") ? atoi(getenv("LJS_SUM_BLOCKS")) : 0;  // tuning
+    const int cap = cap_env > 0 && cap_env <= kMaxSumBlocks ? cap_env : 256;
+    if (g > cap) g = cap;
     if (is_bf16)
       hipLaunchKernelGGL(sum_all_ticket_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, partials,
                          ticket, out, out_bf16);

@@ -286,15 +286,6 @@ __device__ __forceinline__ int swz_mn16(int krow) {
   else return ((((krow >> 1) & 1)) | (((krow >> 3) & 1) << 1)) << 1;
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long bytes) {
-  // readfirstlane the inputs so the compiler can prove the descriptor wave-uniform (no waterfall)
-  const unsigned long long b = (unsigned long long)base;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
-  const int nb = __builtin_amdgcn_readfirstlane((int)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes));
-  void* p = (void*)(((unsigned long long)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(p, 0, nb, 0x00020000);
-}
 
 // One operand tile (R rows x BK) of one K-tile: its 1 KiB DMA pieces, split over NW waves.
 // Per-lane offsets are relative to (row 0, k 0); the tile origin goes in the scalar offset.
