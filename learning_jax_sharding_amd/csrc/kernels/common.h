@@ -115,6 +115,17 @@ __device__ __forceinline__ bool ticket_last(unsigned* ticket, unsigned n) {
   return false;
 }
 
+// Two-level arrival over n blocks (block id bid): one ticket word per group of 32 blocks
+// (t[1 + group]) and one top word (t[0]) drawn by each group's last arriver.  One word retires
+// only ~88 arrivals/us, so a few hundred blocks on a single word serialise for microseconds.
+// Returns true in exactly one block; t needs 1 + ceil(n / 32) words, zero at rest (re-armed).
+__device__ __forceinline__ bool ticket_last_2lvl(unsigned* t, unsigned bid, unsigned n) {
+  const unsigned grp = bid >> 5, ngrp = (n + 31) >> 5;
+  const unsigned in_grp = n - (grp << 5) < 32u ? n - (grp << 5) : 32u;
+  if (!ticket_last(t + 1 + grp, in_grp)) return false;
+  return ticket_last(t, ngrp);
+}
+
 __device__ __forceinline__ float warp_max64(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;

@@ -133,7 +133,8 @@ template <typename T>
 __global__ void sum_all_ticket_kernel(const T* __restrict__ in, long n, float* __restrict__ partials,
                                       unsigned* __restrict__ ticket, void* __restrict__ out, int out_bf16) {
   constexpr int V = 16 / sizeof(T);
-  constexpr int U = 4;  // independent 16-byte loads in flight per thread
+  constexpr int U = 16;  // independent 16-byte loads in flight per thread (Little's law: the
+                        // launcher sizes the grid so the whole array is ~one batch in flight)
   float s = 0.f;
   const long nv = n / V;
   const long stride = (long)gridDim.x * blockDim.x;
@@ -496,7 +497,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
     }
     if (ticket) {
       __syncthreads();
-      if (threadIdx.x == 0 && ticket_last(ticket, gridDim.x))
+      if (threadIdx.x == 0 && ticket_last_2lvl(ticket, blockIdx.x, gridDim.x))
         __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
   if (ticket) {
     // every thread of this block has consumed its read of *step before the ticket is drawn
     __syncthreads();
-    if (threadIdx.x == 0 && ticket_last(ticket, gridDim.x))
+    if (threadIdx.x == 0 && ticket_last_2lvl(ticket, blockIdx.x, gridDim.x))
       __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -619,11 +620,12 @@ LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, int out_
   unsigned* ticket = (unsigned*)ws + kMaxSumBlocks + 32;
   const bool aligned = (((uintptr_t)in) & 15) == 0;
   if (aligned) {
-    // ~4 blocks per CU with 4 independent 16-byte loads per thread keep >= 4 MiB in flight
-    long per = 256L * (is_bf16 ? 8 : 4) * 4;
+    // one batch of U = 16 independent 16-byte loads per thread covers the array (21 MB of the
+    // bench's bf16 output in flight at once: an HBM-latency-bound read otherwise)
+    long per = 256L * (is_bf16 ? 8 : 4) * 16;
     int g = grid_for(n, (int)per);
     static const int cap_env = getenv("LJS_SUM_BLOCKS") ? atoi(getenv("LJS_SUM_BLOCKS")) : 0;  // tuning
-    const int cap = cap_env > 0 && cap_env <= kMaxSumBlocks ? cap_env : 256;
+    const int cap = cap_env > 0 && cap_env <= kMaxSumBlocks ? cap_env : kMaxSumBlocks;
     if (g > cap) g = cap;
     if (is_bf16)
       hipLaunchKernelGGL(sum_all_ticket_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, partials,
@@ -775,6 +777,7 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   }
   b.tile_start[n] = tiles;
   b.n = n;
+  if (ticket && 1 + (tiles + 31) / 32 > (64 << 10) / 4) return (int)hipErrorInvalidValue;  // ticket words
   hipLaunchKernelGGL(adam_multi_kernel, dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset, (unsigned*)ticket,
                      lr, b1, b2, eps, wd);
   return (int)hipGetLastError();

@@ -625,7 +625,7 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
     if increment_step:
         assert step.dtype == torch.int32 and step.is_contiguous()
     step_i = step if step.dtype == torch.int32 else step.to(torch.int32)
-    ticket = _workspace(step_i.device, "adam_ticket", 16) if increment_step else None
+    ticket = _workspace(step_i.device, "adam_ticket", 64 << 10) if increment_step else None  # two-level tickets
     for i in range(0, len(rows), 32):
         chunk = rows[i:i + 32]
         tab = np.asarray([r[0] for r in chunk], dtype=np.int64).reshape(-1)
