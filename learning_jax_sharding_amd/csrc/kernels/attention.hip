@@ -30,6 +30,7 @@ namespace {
 constexpr int D = 64;      // head dim
 constexpr int BLK = 64;    // queries / keys per tile
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr int FKR = 256;   // max keys of the K/V-resident forward
 
 struct AttnArgs {
   const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* o; const bf16_t* dout;
@@ -190,6 +191,68 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
       bf16x8 va = frag_tr(Vt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
       st.o[dt] = mfma16x16x32(va, pb, st.o[dt]);
     }
+  }
+}
+
+// K/V-resident forward for Sk <= 256: the whole K and V of the (batch, head) -- at most 2 x
+// 32 KB -- go to LDS in ONE burst of LDS-DMA pieces (issued from asm, swizzle on the source
+// address), so a block pays the HBM latency once instead of once per 64-key tile behind a
+// one-tile register prefetch; the key loop then runs from LDS with no barriers.  NW waves x 16
+// queries per block; K/V traffic per query falls with NW.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[FKR * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[FKR * D];
+  constexpr int QB = 16 * NW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Tile3 tl = tile3((a.Sq + QB - 1) / QB, a.H);
+  const int qb = tl.x, h = tl.h, b = tl.b;
+  const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
+  const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
+
+  int kend = a.Sk;
+  if (a.causal) kend = min(a.Sk, a.q_offset + (qb + 1) * QB);
+  const int nkt = (kend + BLK - 1) / BLK;
+  {
+    const u32x4 rk = rsrc_u4(kb, 2 * ((long)(a.Sk - 1) * a.k_ss + D));
+    const u32x4 rv = rsrc_u4(vb, 2 * ((long)(a.Sk - 1) * a.v_ss + D));
+    const int npieces = nkt * (BLK / 8);  // 8 rows x 128 B per 1 KiB piece
+    for (int pc = wave; pc < npieces; pc += NW) {
+      const int row = 8 * pc + (lane >> 3);
+      const int c = ((lane & 7) ^ (((row >> 1) & 3) << 1)) * 8;
+      const bool ok = row < a.Sk;
+      dma_lds_x4(rk, ok ? (int)(((long)row * a.k_ss + c) * 2) : 0x7ffffff0, Ks + pc * 512);
+      dma_lds_x4(rv, ok ? (int)(((long)row * a.v_ss + c) * 2) : 0x7ffffff0, Vs + pc * 512);
+    }
+  }
+  const int qrow = qb * QB + 16 * wave + (lane & 15);
+  const bool qok = qrow < a.Sq;
+  const bf16_t* qp = a.q + b * a.q_sb + (long)qrow * a.q_ss + h * a.q_sh;
+  bf16x8 qf[2];
+  qf[0] = load_row_frag(qp, qok, 0, lane);
+  qf[1] = load_row_frag(qp, qok, 1, lane);
+  FwdState st;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) st.o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  st.m = -INFINITY;
+  st.l = 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int qrow0 = qb * QB + 16 * wave;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int kbase = kt * BLK;
+    if (a.causal && kbase > qrow0 + 15 + a.q_offset) break;
+    const bool need_mask = kbase + BLK > a.Sk || (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
+    if (need_mask) fwd_tile<true>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kbase, qrow, lane);
+    else fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kbase, qrow, lane);
+  }
+  float lt = row4_sum(st.l);
+  if (qok) {
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    bf16_t* op = a.out + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
+    store_row_T(op, st.o, inv, lane);
+    if ((lane >> 4) == 0 && a.lse)
+      a.lse[((long)b * a.H + h) * a.Sq + qrow] = lt > 0.f ? st.m + __log2f(lt) : INFINITY;
   }
 }
 
@@ -517,34 +580,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   if (qok) store_row_T(a.out + b * a.out_sb + (long)qrow * a.out_ss + h * a.out_sh, dq, a.scale, lane);
 }
 
-// ---- LDS-DMA from inline asm.  The compiler's waitcnt pass treats a builtin LDS-DMA as a
-// possible writer of EVERY LDS location and puts vmcnt waits in front of all later ds_read /
-// ds_write, which serialises a prefetch behind the math it should overlap.  Issued as asm the
-// DMA is invisible to that pass; the kernel waits for it explicitly (vmcnt(0) + barrier).
-// Extra untracked vector-memory ops can only make the compiler's own counted waits wait longer
-// (the counter retires in order), never shorter.
-__device__ __forceinline__ u32x4 rsrc_u4(const void* base, long bytes) {
-  const unsigned long long b = (unsigned long long)base;
-  u32x4 r;
-  r[0] = __builtin_amdgcn_readfirstlane((unsigned)b);
-  r[1] = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) & 0xffffu;  // stride 0
-  r[2] = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes));
-  r[3] = 0x00020000u;
-  return r;
-}
-// 64 lanes x 16 B from rsrc + voff (per lane) to LDS [lds, lds + 1 KiB), lane-contiguous
-__device__ __forceinline__ void dma_lds_x4(const u32x4& rs, int voff, const void* lds) {
-  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LDS_PTR(const void))lds);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
-               :: "v"(voff), "s"(rs), "s"(m) : "memory", "m0");
-}
-// 64 lanes x 4 B to LDS [lds, lds + 256 B)
-__device__ __forceinline__ void dma_lds_x1(const u32x4& rs, int voff, const void* lds) {
-  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LDS_PTR(const void))lds);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds"
-               :: "v"(voff), "s"(rs), "s"(m) : "memory", "m0");
-}
-
 // ---------------------------------------------------------------- fused short-key backward
 // Sk <= 256: ONE workgroup (8 waves) per (batch, head) keeps K and V in LDS (each wave
 // owns 32 keys for dK / dV), then sweeps the query blocks once.  S and dP are computed
@@ -779,6 +814,9 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
 
 // forward sub-tiles per wave: 1 or 2 forces it; 0 = automatic; -1 = read LJS_ATTN_FWD_NSUB
 static int g_fwd_nsub = -1;
+// K/V-resident forward (Sk <= 256): 0 off, 4 / 8 waves per block; -1 = read LJS_ATTN_FWD_RES
+static int g_fwd_res = -1;
+LJS_API void ljs_attn_set_fwd_res(int v) { g_fwd_res = v; }
 LJS_API void ljs_attn_set_fwd_nsub(int v) { g_fwd_nsub = v; }
 
 // strides are in elements, ordered (batch, seq, head); head_dim must be 64 and contiguous.
@@ -802,6 +840,17 @@ LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, v
   }
   // NSUB = 1 measured fastest at the bench shape (26.4 vs 28.5 us for 2; 4 spills past 2 waves
   // per SIMD), so 2 is opt-in
+  if (g_fwd_res < 0) {
+    const char* e = getenv("LJS_ATTN_FWD_RES");
+    g_fwd_res = e ? atoi(e) : 8;
+  }
+  if (g_fwd_res > 0 && Sk <= FKR && (long)(Sk - 1) * (ks[1] > vs[1] ? ks[1] : vs[1]) * 2 + 128 < (1L << 31)) {
+    const int nw = g_fwd_res == 8 ? 8 : 4;
+    const int nqb = (Sq + 16 * nw - 1) / (16 * nw);
+    if (nw == 8) hipLaunchKernelGGL(attn_fwd_res_kernel<8>, dim3(nqb * H * B), dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL(attn_fwd_res_kernel<4>, dim3(nqb * H * B), dim3(256), 0, stream, a);
+    return (int)hipGetLastError();
+  }
   int nsub = g_fwd_nsub;
   if (nsub != 1 && nsub != 2) nsub = 1;
   const int nqb = (Sq + BLK * nsub - 1) / (BLK * nsub);

@@ -94,6 +94,34 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, nb, 0x00020000);
 }
 
+// ---- LDS-DMA from inline asm.  The compiler's waitcnt pass treats a builtin LDS-DMA as a
+// possible writer of EVERY LDS location and puts vmcnt waits in front of all later ds_read /
+// ds_write, which serialises a prefetch behind the math it should overlap.  Issued as asm the
+// DMA is invisible to that pass; the kernel waits for it explicitly (vmcnt(0) + barrier).
+// Extra untracked vector-memory ops can only make the compiler's own counted waits wait longer
+// (the counter retires in order), never shorter.
+__device__ __forceinline__ u32x4 rsrc_u4(const void* base, long bytes) {
+  const unsigned long long b = (unsigned long long)base;
+  u32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((unsigned)b);
+  r[1] = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) & 0xffffu;  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes));
+  r[3] = 0x00020000u;
+  return r;
+}
+// 64 lanes x 16 B from rsrc + voff (per lane) to LDS [lds, lds + 1 KiB), lane-contiguous
+__device__ __forceinline__ void dma_lds_x4(const u32x4& rs, int voff, const void* lds) {
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LDS_PTR(const void))lds);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :: "v"(voff), "s"(rs), "s"(m) : "memory", "m0");
+}
+// 64 lanes x 4 B to LDS [lds, lds + 256 B)
+__device__ __forceinline__ void dma_lds_x1(const u32x4& rs, int voff, const void* lds) {
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LDS_PTR(const void))lds);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds"
+               :: "v"(voff), "s"(rs), "s"(m) : "memory", "m0");
+}
+
 // ---- in-launch "last arriver" hand-off (cdna_hip_programming.md §6 Guideline 16, valid form:
 // write-through (sc1) payload stores by ONE wave, that wave's vmcnt(0), one lane's agent-scope
 // atomic ticket add; the block whose add returns n-1 reads every payload with sc1 loads and

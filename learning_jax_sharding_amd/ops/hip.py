@@ -72,6 +72,15 @@ def lib():
     return _LIB
 
 
+def set_attention_fwd_resident(waves: int):
+    """Forward kernel for key lengths <= 256: 0 = tiled (K/V tiles through registers), 4 or 8 =
+    K/V-resident (whole K/V of a head in LDS by one LDS-DMA burst; waves x 16 queries per block)."""
+    fn = lib().ljs_attn_set_fwd_res
+    fn.argtypes = [c_int]
+    fn.restype = None
+    fn(int(waves))
+
+
 def set_attention_bwd_fused(enabled: bool):
     """Select the attention backward for key lengths <= 256: the single-pass fused kernel
     (default) or the split dQ + dK/dV kernels (always used above 256 keys)."""

@@ -134,11 +134,16 @@ def attn_bwd_impl(request, hip):
     hip.set_attention_bwd_fused(True)
 
 
-@pytest.fixture(params=[1, 2])
+@pytest.fixture(params=[(1, 0), (2, 0), (1, 4), (1, 8)], ids=["tiled1", "tiled2", "res4", "res8"])
 def attn_fwd_nsub(request, hip):
-    hip.set_attention_fwd_nsub(request.param)
+    """Forward kernel variant: tiled with 1 / 2 query sub-tiles per wave, or K/V-resident with
+    4 / 8 waves per block (Sk <= 256; longer keys fall back to the tiled kernel)."""
+    nsub, res = request.param
+    hip.set_attention_fwd_nsub(nsub)
+    hip.set_attention_fwd_resident(res)
     yield request.param
     hip.set_attention_fwd_nsub(0)
+    hip.set_attention_fwd_resident(-1)
 
 
 @pytest.mark.parametrize("B,S,H", [(2, 256, 8), (1, 200, 4), (3, 64, 2), (1, 40, 3), (1, 320, 2)])
