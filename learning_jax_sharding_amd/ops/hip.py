@@ -181,6 +181,11 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     _ck(rc, "ljs_gemm_bf16")
 
 
+# 256x128 tile for large k-contiguous bf16 GEMMs (off: the 128x128 x 2/CU kernel on a persistent
+# grid measured faster at the bench's QKV projection, 39.9 vs 45.5 us)
+_TILE_2561 = os.environ.get("LJS_GEMM_TILE2561", "0") == "1"
+
+
 def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f32: bool, splitk: int = 1,
               ldc: int = 0) -> int:
     """Kernel/tile choice (measured on MI355X at the bench shapes, ``scripts/gemm_one.py``):
@@ -188,7 +193,7 @@ def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f3
     whenever K is a multiple of 64, else the register-staged 128/64 tiles."""
     tiles128 = -(-M // 128) * -(-N // 128) * batch * max(1, splitk)
     if K % 64 == 0 and tiles128 >= 96 and (out_f32 or (N % 8 == 0 and ldc % 8 == 0)):
-        if a_kc and b_kc and not out_f32 and M >= 4096 and N * batch >= 1024 and N % 128 == 0:
+        if _TILE_2561 and a_kc and b_kc and not out_f32 and M >= 4096 and N * batch >= 1024 and N % 128 == 0:
             return 2561
         return 1282
     return 128 if tiles128 >= 160 else 64
