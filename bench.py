@@ -136,6 +136,7 @@ def main():
         barrier_sync()
         t0 = time.perf_counter()
         run(args.steps)
+        th = time.perf_counter()  # host side done enqueuing (diagnostic: host- vs device-bound)
         barrier_sync()
         t1 = time.perf_counter()
     elapsed = t1 - t0
@@ -168,6 +169,7 @@ def main():
             "ms_per_step": round(ms, 4),
             "tflops_per_gpu": round(tflops_total / n, 3),
             "tokens_per_s": round(tokens_per_s, 1),
+            "host_ms_per_step": round((th - t0) / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
