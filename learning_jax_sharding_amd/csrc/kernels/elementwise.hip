@@ -282,6 +282,19 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   }
 }
 
+// The cotangent of y.sum() reaching a dense layer is ONE scalar g broadcast over [R][C]: write
+// the bf16 row the GEMMs read with ld = 0 and, in the same launch, the bias gradient (the
+// column sums of that broadcast, R * bf16(g) per column) -- one kernel instead of two.
+__global__ void bcast_scalar_kernel(const void* __restrict__ g, int g_bf16, int C, float R, bf16_t* __restrict__ row,
+                                    float* __restrict__ db) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float v = g_bf16 ? bf2f(*reinterpret_cast<const bf16_t*>(g)) : *reinterpret_cast<const float*>(g);
+  const bf16_t b = f2bf(v);
+  row[c] = b;
+  if (db) db[c] = bf2f(b) * R;
+}
+
 // out[0..n) = (bf16) *g: materialises the broadcast row of a scalar cotangent (e.g. of y.sum())
 __global__ void fill_row_kernel(const void* __restrict__ g, int g_bf16, bf16_t* __restrict__ out, long n) {
   const float v = g_bf16 ? bf2f(*reinterpret_cast<const bf16_t*>(g)) : *reinterpret_cast<const float*>(g);
@@ -700,6 +713,12 @@ LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, i
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, s, (const float*)slabs, S, slab_stride, R, C,
                      (float*)out, cb, out_bs, accumulate);
+  return (int)hipGetLastError();
+}
+
+LJS_API int ljs_bcast_scalar(const void* g, int g_bf16, int C, float R, void* row, void* db, hipStream_t s) {
+  hipLaunchKernelGGL(bcast_scalar_kernel, dim3((C + 255) / 256), dim3(256), 0, s, g, g_bf16, C, R, (bf16_t*)row,
+                     (float*)db);
   return (int)hipGetLastError();
 }
 

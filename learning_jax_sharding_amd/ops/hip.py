@@ -43,6 +43,7 @@ _SIGS = {
     "ljs_sum_all": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_fill_row_bf16": [c_void_p, c_int, c_void_p, c_long, c_void_p],
+    "ljs_bcast_scalar": [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p],
     "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ljs_adam_f32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
@@ -408,6 +409,11 @@ class _SumAll(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.dtype == torch.bfloat16 and g.dtype == torch.bfloat16 and g.is_cuda and g.numel() == 1 \
+                and len(ctx.shape) >= 1:
+            # the scalar itself, broadcast with all strides 0 (no kernel): a dense layer's backward
+            # turns it into its bf16 row + bias gradient in one launch (bcast_scalar)
+            return g.reshape(()).expand(ctx.shape), None
         if ctx.dtype == torch.bfloat16 and g.dtype in (torch.float32, torch.bfloat16) and g.is_cuda \
                 and len(ctx.shape) >= 1:
             # one bf16 row holding g, broadcast (stride 0) over every leading dim: the consumers
@@ -489,6 +495,16 @@ def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, ac
     assert slabs.dtype == torch.float32 and out.dtype == torch.float32 and slabs.is_contiguous()
     rc = lib().ljs_slab_reduce(_p(slabs), S, R * C, R, C, _p(out), cb, out_bs, int(accumulate), _stream(out))
     _ck(rc, "slab_reduce")
+
+
+def bcast_scalar(g: torch.Tensor, C: int, R: int, want_db: bool):
+    """(bf16 row [C] filled with bf16(g), f32 [C] = R * bf16(g) or None) from the 1-element
+    tensor ``g`` (f32 or bf16), in one launch."""
+    row = torch.empty((C,), dtype=torch.bfloat16, device=g.device)
+    db = torch.empty((C,), dtype=torch.float32, device=g.device) if want_db else None
+    rc = lib().ljs_bcast_scalar(_p(g), int(g.dtype == torch.bfloat16), C, float(R), _p(row), _p(db), _stream(row))
+    _ck(rc, "bcast_scalar")
+    return row, db
 
 
 def colsum_ld(t: torch.Tensor, R: int, C: int, ld: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:

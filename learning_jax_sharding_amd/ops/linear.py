@@ -122,12 +122,20 @@ class _Linear(torch.autograd.Function):
         ys = saved[2 + nw:] if relu else None
         dev = xb.device
         mats: List[Optional[Tuple[torch.Tensor, int]]] = []
+        db_bcast: List[Optional[torch.Tensor]] = [None] * nw
+        want_db = has_b and ctx.needs_input_grad[1]
         for i, dy in enumerate(dys):
             if dy is None:
                 mats.append(None)
                 continue
             if relu:
                 dy = (dy * (ys[i] > 0)).reshape(M, N)
+            elif dy.is_cuda and dy.numel() > 0 and all(st == 0 for st in dy.stride()):
+                # one scalar broadcast (the cotangent of y.sum()): its bf16 row and the bias
+                # gradient come out of one kernel; the GEMMs read the row with ld = 0
+                row, db_bcast[i] = hip.bcast_scalar(dy.as_strided((1,), (1,)), N, M, want_db)
+                mats.append((row.unsqueeze(0).expand(M, N), 0))
+                continue
             mats.append(_row_view(dy, M, N))
         dx = db = None
         dws = [None] * nw
@@ -180,9 +188,12 @@ class _Linear(torch.autograd.Function):
                         hip.gemm(xb, t, dW, K, N, M, K, ld, N, False, False, splitk=sk, tile=tile, zero_c=True)
                         dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
         # ---- db
-        if has_b and ctx.needs_input_grad[1] and live:
+        if want_db and live:
             tot = None
             for i in live:
+                if db_bcast[i] is not None:
+                    tot = db_bcast[i] if tot is None else tot + db_bcast[i]
+                    continue
                 t, ld = mats[i]
                 tot = hip.colsum_ld(t, M, N, ld, tot)
             db = tot.to(b.dtype)

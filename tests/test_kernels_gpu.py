@@ -338,6 +338,24 @@ def test_linear_broadcast_grad_and_strided(hip):
                                rtol=2e-2, atol=5e-2)
 
 
+def test_linear_scalar_broadcast_grad(hip):
+    """The cotangent of the bf16 sum_all is the seed scalar broadcast with all strides 0: the
+    dense backward turns it into its bf16 row + bias gradient in one kernel (bcast_scalar)."""
+    x = _rand(256, 256, dtype=torch.float32, seed=3)
+    w = (_rand(256, 320, dtype=torch.float32, seed=4) * 0.05).requires_grad_()
+    b = torch.zeros(320, device=dev, requires_grad=True)
+    xr = x.clone().requires_grad_()
+    (y,) = hip.linear(xr, [w], b, torch.bfloat16, False, torch.bfloat16)
+    s = hip.sum_all(y, torch.bfloat16)
+    seed = torch.tensor(0.5, dtype=torch.bfloat16, device=dev)
+    gw, gb, gx = torch.autograd.grad(s, [w, b, xr], seed)
+    xf = x.bfloat16().float()
+    torch.testing.assert_close(gw, 0.5 * xf.sum(0)[:, None].expand(256, 320), rtol=1e-2, atol=1e-1)
+    torch.testing.assert_close(gb, torch.full((320,), 128.0, device=dev))
+    torch.testing.assert_close(gx, 0.5 * w.detach().bfloat16().float().sum(1)[None, :].expand(256, 256),
+                               rtol=2e-2, atol=5e-2)
+
+
 def test_ticket_reductions_rearm(hip):
     """Last-arriver reductions (sum_all, colsum) re-arm their tickets: repeated calls with
     different data and grid sizes stay exact, and sum_all writes bf16 directly."""
