@@ -295,6 +295,22 @@ __global__ void bcast_scalar_kernel(const void* __restrict__ g, int g_bf16, int 
   if (db) db[c] = bf2f(b) * R;
 }
 
+// sum of n f32 partials (a producer's fused per-wave output sums) -> scalar, one block
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ p, int n, void* __restrict__ out,
+                                                          int out_bf16) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += p[i];
+  s = warp_sum64(s);
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float v = (part[0] + part[1]) + (part[2] + part[3]);
+    if (out_bf16) *reinterpret_cast<bf16_t*>(out) = f2bf(v);
+    else *reinterpret_cast<float*>(out) = v;
+  }
+}
+
 // out[0..n) = (bf16) *g: materialises the broadcast row of a scalar cotangent (e.g. of y.sum())
 __global__ void fill_row_kernel(const void* __restrict__ g, int g_bf16, bf16_t* __restrict__ out, long n) {
   const float v = g_bf16 ? bf2f(*reinterpret_cast<const bf16_t*>(g)) : *reinterpret_cast<const float*>(g);
@@ -719,6 +735,11 @@ LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, i
 LJS_API int ljs_bcast_scalar(const void* g, int g_bf16, int C, float R, void* row, void* db, hipStream_t s) {
   hipLaunchKernelGGL(bcast_scalar_kernel, dim3((C + 255) / 256), dim3(256), 0, s, g, g_bf16, C, R, (bf16_t*)row,
                      (float*)db);
+  return (int)hipGetLastError();
+}
+
+LJS_API int ljs_sum_partials(const void* p, int n, void* out, int out_bf16, hipStream_t s) {
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, (const float*)p, n, out, out_bf16);
   return (int)hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ struct GemmArgs {
   int batch, splitk, kt_per_split;
   float alpha;
   int flags;  // 1 relu, 2 bias, 4 bias f32, 8 accumulate into C (f32 out)
+  float* psum;  // LDS-DMA kernels, bf16 out: per (item, wave) sums of the stored values, or null
 };
 
 // swizzled 8-byte-chunk index for the m/n-contiguous image (rows of R bf16)
@@ -361,7 +362,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
   constexpr bool SWAP = true;
   static_assert(OUT_F32 || TN % 2 == 0, "column blocks pair up for 16-byte stores");
   constexpr int S_EPI = TM * TN / 2;
-  static_assert(L * (NST - 1) + S_EPI <= 63, "vmcnt immediate range");
+  static_assert(L * (NST - 1) + S_EPI + 1 <= 63, "vmcnt immediate range");
   __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -426,6 +427,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
   // flags & 32: output stores with sc1, which drop the written lines from the XCD's L2 (plain
   // stores keep them) so the output stream does not evict the operand panels other blocks reuse
   const bool st_sc1 = p.flags & 32;
+  const bool psum_on = !OUT_F32 && p.psum != nullptr;
+  float tsum = 0.f;
   const __amdgpu_buffer_rsrc_t rc =
       make_rsrc(p.C, (OUT_F32 ? 4 : 2) * ((long)(p.batch - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
   bool after_epi = false;
@@ -437,10 +440,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
     const bool tail = f + NST - 2 >= total;
     if constexpr (NST >= 3) {
       if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (SWAP && after_epi && psum_on)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2) + S_EPI + 1) : "memory");
       else if (SWAP && after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2) + S_EPI) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");
     } else {
-      if (SWAP && after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI) : "memory");
+      if (SWAP && after_epi && psum_on) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI + 1) : "memory");
+      else if (SWAP && after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     after_epi = false;
@@ -521,7 +527,18 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
           const int off = ok ? (int)(((long)w.b * p.sC + (long)row * p.ldc + col) * 2) : 0x7ffffff0;
           if (st_sc1) __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, kSC1);
           else __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, 0);
+          if (psum_on && ok) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) tsum += __uint_as_float(pk[e] << 16) + __uint_as_float(pk[e] & 0xffff0000u);
+          }
         }
+      }
+      if (psum_on) {
+        // fused loss reduction: this wave's share of sum(C) -- of the bf16 values just stored --
+        // to its own slot (one store per wave, counted in the next K-step's vmcnt)
+        tsum = warp_sum64(tsum);
+        if (lane == 0) p.psum[(long)(slot + G * it) * NW + wave] = tsum;
+        tsum = 0.f;
       }
       after_epi = true;
     } else {
@@ -655,7 +672,7 @@ hipError_t dispatch_layout(const GemmArgs& a, int a_kc, int b_kc, int out_f32, h
 LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
                           long lda, long ldb, long ldc, long sA, long sB, long sC, long sBias, int batch,
                           int a_kc, int b_kc, int out_f32, int flags, float alpha, int splitk, int tile,
-                          hipStream_t stream) {
+                          void* psum, int* psum_count, hipStream_t stream) {
   if (K % 8 || (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
   if (splitk > 1 && !out_f32) return (int)hipErrorInvalidValue;
   GemmArgs a;
@@ -669,6 +686,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   a.batch = batch;
   a.alpha = alpha;
   a.flags = flags;
+  a.psum = nullptr;
+  if (psum_count) *psum_count = 0;
   int nkt = (K + BK - 1) / BK;
   if (splitk < 1) splitk = 1;
   if (splitk > nkt) splitk = nkt;
@@ -695,6 +714,12 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if (tile > 1000 && !(dma_ok && dma_store_ok)) tile = 128;
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
   if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;
+  // fused output sum (psum): LDS-DMA kernels with bf16 output only; one float per (item, wave)
+  if (psum && !out_f32 && tile > 1000) {
+    const int bm = tile == 2561 ? 256 : 128, nw = (tile == 2561 || tile == 12883 || tile == 12884) ? 8 : 4;
+    a.psum = (float*)psum;
+    if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + 127) / 128) * batch * a.splitk * nw;
+  }
   if (tile == 2561) {
     if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);
     else e = launch_dma<256, 128, 4, 2, 3, true, true, false>(a, stream, 0);

@@ -29,7 +29,9 @@ _LP = ctypes.POINTER(ctypes.c_long)
 
 _SIGS = {
     "ljs_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
-                      c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p],
+                      c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
+                      ctypes.POINTER(c_int), c_void_p],
+    "ljs_sum_partials": [c_void_p, c_int, c_void_p, c_int, c_void_p],
     "ljs_gemm_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long,
                      c_long, c_long, c_long, c_int, c_void_p],
     "ljs_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, _LP, _LP, _LP, _LP,
@@ -161,11 +163,14 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
          a_kc: bool, b_kc: bool, batch: int = 1, sA: int = 0, sB: int = 0, sC: int = 0,
          bias: Optional[torch.Tensor] = None, sBias: int = 0, relu: bool = False, alpha: float = 1.0,
          accumulate: bool = False, splitk: int = 1, tile: Optional[int] = None, a_off: int = 0, b_off: int = 0,
-         c_off: int = 0, zero_c: bool = False) -> None:
+         c_off: int = 0, zero_c: bool = False, psum: Optional[torch.Tensor] = None) -> int:
     """Raw launcher.  A/B bf16; C bf16 or f32 (split-K/accumulate need f32 C).
 
     ``lda``/``ldb`` may be 0 for an operand that repeats one row (a broadcast gradient).
     ``zero_c`` zeroes C inside the launch sequence (needed before split-K accumulation).
+    ``psum`` (f32, >= :func:`psum_slots` floats): the LDS-DMA kernels with bf16 output also write
+    per-(tile, wave) sums of the stored values there.  Returns the number of partials written
+    (0 when the chosen kernel does not produce them).
     """
     assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
     out_f32 = C.dtype == torch.float32
@@ -175,11 +180,45 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     if tile is None:
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc)
     eA = A.element_size()
+    cnt = c_int(0)
     rc = lib().ljs_gemm_bf16(ctypes.c_void_p(A.data_ptr() + a_off * eA), ctypes.c_void_p(B.data_ptr() + b_off * eA),
                              ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb,
                              ldc, sA, sB, sC, sBias, batch, int(a_kc), int(b_kc), int(out_f32), flags, alpha,
-                             splitk, tile, _stream(C))
+                             splitk, tile, _p(psum), ctypes.byref(cnt), _stream(C))
     _ck(rc, "ljs_gemm_bf16")
+    return cnt.value
+
+
+def psum_slots(M: int, N: int, batch: int = 1) -> int:
+    """Upper bound on the fused output-sum partials of one bf16 GEMM (128-row tiles, 8 waves)."""
+    return -(-M // 128) * -(-N // 128) * batch * 8
+
+
+# Fused output sums: a bf16 GEMM output registered here (weakly) carries the per-wave sums of
+# its values computed in the GEMM epilogue, so a following whole-array sum (the loss y.sum())
+# reduces a few thousand partials in one tiny kernel instead of re-reading the output.  The
+# entry is used only while the output tensor is alive, unmodified (version counter) and
+# summed whole (same storage, numel, contiguous).
+_PSUM = {}
+
+
+def _register_psum(y: torch.Tensor, partials: torch.Tensor, count: int) -> None:
+    import weakref
+    key = y.data_ptr()
+    ref = weakref.ref(y, lambda _r, k=key: _PSUM.pop(k, None) if _PSUM.get(k, (None,))[0] is _r else None)
+    _PSUM[key] = (ref, y._version, partials, count, y.numel())
+
+
+def _psum_for(t: torch.Tensor):
+    ent = _PSUM.get(t.data_ptr())
+    if ent is None:
+        return None
+    ref, ver, partials, count, numel = ent
+    y = ref()
+    if y is None or count <= 0 or t.numel() != numel or not t.is_contiguous() or t._version != ver \
+            or y.data_ptr() != t.data_ptr():
+        return None
+    return partials, count
 
 
 # 256x128 tile for large k-contiguous bf16 GEMMs (off: the 128x128 x 2/CU kernel on a persistent
@@ -393,6 +432,11 @@ def _sum_all_raw(t: torch.Tensor, out_dtype: torch.dtype = torch.float32) -> tor
     t = t.contiguous()
     out_bf16 = out_dtype == torch.bfloat16 and t.data_ptr() % 16 == 0
     out = torch.empty((), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=t.device)
+    ps = _psum_for(t)
+    if ps is not None:  # the producing GEMM already summed its output tile by tile
+        rc = lib().ljs_sum_partials(_p(ps[0]), ps[1], _p(out), int(out_bf16), _stream(t))
+        _ck(rc, "sum_partials")
+        return out
     ws = _workspace(t.device, "sum_all", 1089 * 4)
     rc = lib().ljs_sum_all(_p(t), int(t.dtype == torch.bfloat16), t.numel(), _p(out), int(out_bf16), _p(ws),
                            _stream(t))

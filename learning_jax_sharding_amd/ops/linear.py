@@ -37,7 +37,9 @@ def _splitk(M: int, N: int, K: int, batch: int, tile: int) -> int:
     return s
 
 
-_DW_SPLIT = int(os.environ.get("LJS_DW_SPLIT", "0"))  # tuning override of the K-chunk count
+_DW_SPLIT = int(os.environ.get("LJS_DW_SPLIT", "0"))
+# large bf16 dense outputs also carry their fused per-tile sums (see hip._PSUM): y.sum() is free
+_FUSED_SUM = os.environ.get("LJS_FUSED_SUM", "1") == "1"  # tuning override of the K-chunk count
 
 
 def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: int, out: torch.Tensor, cb: int,
@@ -104,9 +106,14 @@ class _Linear(torch.autograd.Function):
         bias = None
         if b is not None:
             bias = (b if b.dtype in (torch.float32, torch.bfloat16) else b.float()).contiguous()
-        hip.gemm(xb, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=sB, sC=N,
-                 bias=bias, sBias=0, relu=relu)
+        partials = None
+        if _FUSED_SUM and nw == 1 and od == torch.bfloat16 and M * N >= (1 << 20):
+            partials = torch.empty((hip.psum_slots(M, N),), dtype=torch.float32, device=x.device)
+        cnt = hip.gemm(xb, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=sB, sC=N,
+                       bias=bias, sBias=0, relu=relu, psum=partials)
         ys = [out[:, i * N:(i + 1) * N].view(tuple(lead) + (N,)) for i in range(nw)]
+        if partials is not None and cnt > 0 and od == out_dtype:
+            hip._register_psum(ys[0], partials, cnt)
         if od != out_dtype:
             ys = [y.to(out_dtype) for y in ys]
         ctx.save_for_backward(xb, b, *ws, *(ys if relu else []))

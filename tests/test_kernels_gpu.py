@@ -356,6 +356,30 @@ def test_linear_scalar_broadcast_grad(hip):
                                rtol=2e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("T,N", [(16384, 640), (4096, 512), (1000, 1152)])
+def test_fused_output_sum(hip, T, N):
+    """A large bf16 dense output carries its per-tile sums from the GEMM epilogue; sum_all of it
+    reduces those partials (== the sum of the stored bf16 values), and falls back to reading
+    the array once the output was modified in place or only part of it is summed."""
+    x = _rand(T, 640, dtype=torch.float32, seed=5)
+    w = _rand(640, N, dtype=torch.float32, seed=6) * 0.05
+    b = _rand(N, dtype=torch.float32, seed=7)
+    (y,) = hip.linear(x, [w], b, torch.bfloat16, False, torch.bfloat16)
+    fused = hip._psum_for(y) is not None
+    ref = y.float().sum()
+    got = hip.sum_all(y, torch.bfloat16)
+    torch.testing.assert_close(got.float(), ref, rtol=1e-2, atol=1.0)
+    got32 = hip.sum_all(y, torch.float32)
+    torch.testing.assert_close(got32, ref, rtol=1e-4, atol=1e-1)
+    if T * N >= (1 << 20) and T % 64 == 0:
+        assert fused, "expected the DMA GEMM to produce fused partial sums"
+    y.mul_(2.0)
+    assert hip._psum_for(y) is None
+    torch.testing.assert_close(hip.sum_all(y, torch.float32), 2 * ref, rtol=1e-4, atol=2e-1)
+    half = y[: T // 2]
+    torch.testing.assert_close(hip.sum_all(half, torch.float32), half.float().sum(), rtol=1e-4, atol=1e-1)
+
+
 def test_ticket_reductions_rearm(hip):
     """Last-arriver reductions (sum_all, colsum) re-arm their tickets: repeated calls with
     different data and grid sizes stay exact, and sum_all writes bf16 directly."""
