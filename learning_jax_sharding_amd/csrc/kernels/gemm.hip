@@ -409,6 +409,18 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
     b_off += b_step;
     if (++is_kt == nk) { is_kt = 0; ++is_item; }
   };
+  // the same in two halves (A pieces, then B pieces + cursor advance)
+  auto issue_half = [&](int st, bool second) {
+    if (!second) {
+      if (is_kt == 0) load_item(is_item);
+      ta.issue(ra, smem + st * STAGE, a_off, wave);
+      a_off += a_step;
+    } else {
+      tb.issue(rb, smem + st * STAGE + A_TILE, b_off, wave);
+      b_off += b_step;
+      if (++is_kt == nk) { is_kt = 0; ++is_item; }
+    }
+  };
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -454,7 +466,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
     // arrives; every wave's pieces of step f are in LDS once all have arrived
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (f + NST - 1 < total) issue_next((f + NST - 1) % NST);
+    const bool more = f + NST - 1 < total;
+    const int nst = (f + NST - 1) % NST;
     const bf16_t* As_ = smem + (f % NST) * STAGE;
     const bf16_t* Bs_ = As_ + A_TILE;
 #pragma unroll
@@ -464,6 +477,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
       for (int ii = 0; ii < TM; ++ii) af[ii] = frag<BM, A_KC>(As_, wr * (BM / WM) + ii * 16, ks, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, B_KC>(Bs_, wc * (BN / WN) + j * 16, ks, lane);
+      // the next stage's DMA pieces are issued AFTER this k-step's fragment reads, half per
+      // k-step: their issue time (60-185 cycles per piece) then overlaps the LDS latency and
+      // the MFMAs instead of delaying the first fragment read behind all L pieces
+      if (more) {
+        if (ks == 0) issue_half(nst, false);
+        if (ks == BK / 32 - 1) issue_half(nst, true);
+      }
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii)
 #pragma unroll
