@@ -814,7 +814,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
 
 // forward sub-tiles per wave: 1 or 2 forces it; 0 = automatic; -1 = read LJS_ATTN_FWD_NSUB
 static int g_fwd_nsub = -1;
-// K/V-resident forward (Sk <= 256): 0 off, 4 / 8 waves per block; -1 = read LJS_ATTN_FWD_RES
+// K/V-resident forward (Sk <= 256): 0 off, 4 / 8 / 16 waves per block; -1 = read LJS_ATTN_FWD_RES
 static int g_fwd_res = -1;
 LJS_API void ljs_attn_set_fwd_res(int v) { g_fwd_res = v; }
 LJS_API void ljs_attn_set_fwd_nsub(int v) { g_fwd_nsub = v; }
@@ -845,9 +845,10 @@ LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, v
     g_fwd_res = e ? atoi(e) : 8;
   }
   if (g_fwd_res > 0 && Sk <= FKR && (long)(Sk - 1) * (ks[1] > vs[1] ? ks[1] : vs[1]) * 2 + 128 < (1L << 31)) {
-    const int nw = g_fwd_res == 8 ? 8 : 4;
+    const int nw = g_fwd_res == 16 ? 16 : g_fwd_res == 8 ? 8 : 4;
     const int nqb = (Sq + 16 * nw - 1) / (16 * nw);
-    if (nw == 8) hipLaunchKernelGGL(attn_fwd_res_kernel<8>, dim3(nqb * H * B), dim3(512), 0, stream, a);
+    if (nw == 16) hipLaunchKernelGGL(attn_fwd_res_kernel<16>, dim3(nqb * H * B), dim3(1024), 0, stream, a);
+    else if (nw == 8) hipLaunchKernelGGL(attn_fwd_res_kernel<8>, dim3(nqb * H * B), dim3(512), 0, stream, a);
     else hipLaunchKernelGGL(attn_fwd_res_kernel<4>, dim3(nqb * H * B), dim3(256), 0, stream, a);
     return (int)hipGetLastError();
   }
