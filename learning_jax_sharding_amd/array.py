@@ -60,6 +60,59 @@ class Shard:
         return f"Shard(device={self.device!r}, index={self.index}, replica_id={self.replica_id})"
 
 
+class LazyLocal(dict):
+    """Per-device tensors computed on first use: ``thunk()`` returns the {device: tensor} dict.
+
+    Used for values a training step usually never reads -- the all-reduced scalar loss of
+    ``grad`` (its gradient is seeded on the pre-reduction partial sums): the collective that
+    would produce it runs only if something reads the value, the way XLA drops the primal
+    output of ``jax.grad``.  Every dict access materialises it."""
+
+    def __init__(self, thunk):
+        super().__init__()
+        self._thunk = thunk
+
+    def _force(self):
+        if self._thunk is not None:
+            th, self._thunk = self._thunk, None
+            super().update(th())
+        return self
+
+    @property
+    def pending(self) -> bool:
+        return self._thunk is not None
+
+    def __getitem__(self, k):
+        return dict.__getitem__(self._force(), k)
+
+    def __iter__(self):
+        return dict.__iter__(self._force())
+
+    def __len__(self):
+        return dict.__len__(self._force())
+
+    def __contains__(self, k):
+        return dict.__contains__(self._force(), k)
+
+    def keys(self):
+        return dict.keys(self._force())
+
+    def values(self):
+        return dict.values(self._force())
+
+    def items(self):
+        return dict.items(self._force())
+
+    def get(self, k, default=None):
+        return dict.get(self._force(), k, default)
+
+    def copy(self):
+        return dict(self._force())
+
+    def __repr__(self):
+        return "LazyLocal(<pending>)" if self._thunk is not None else dict.__repr__(self)
+
+
 class ShardedArray:
     __array_priority__ = 100
 
@@ -67,7 +120,7 @@ class ShardedArray:
         self.shape = tuple(int(s) for s in shape)
         self.dtype = _dt.canonicalize(dtype)
         self.sharding = sharding
-        self.local = dict(local)
+        self.local = local if isinstance(local, LazyLocal) and local.pending else dict(local)
         self._tile: Optional[TileAssignment] = None
 
     # ------------------------------------------------------------------ metadata

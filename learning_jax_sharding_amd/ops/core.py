@@ -17,6 +17,7 @@ sums that are all-reduced over the contraction groups.
 from __future__ import annotations
 
 import math
+import os
 import re
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -24,7 +25,7 @@ import numpy as np
 import torch
 
 from .. import dtypes as _dt
-from ..array import ShardedArray
+from ..array import LazyLocal, ShardedArray
 from ..comm import collectives as C
 from ..sharding.shardings import Sharding, sharding_from_tile
 from ..sharding.tile import TileAssignment
@@ -308,6 +309,9 @@ def with_sharding_constraint(x, sharding: Sharding):
 
 
 # ----------------------------------------------------------------------------- reductions
+_LAZY_SCALAR_SUMS = os.environ.get("LJS_LAZY_SCALAR_SUMS", "1") == "1"
+
+
 def _reduce(x: ShardedArray, axis, keepdims: bool, local_fn, combine: str, dtype=None) -> ShardedArray:
     axes = _norm_axes(axis, x.ndim)
     sharded = [a for a in axes if x.tile.tile_shape[a] > 1]
@@ -317,14 +321,28 @@ def _reduce(x: ShardedArray, axis, keepdims: bool, local_fn, combine: str, dtype
     acc = torch.float32 if out_dtype in (torch.bfloat16, torch.float16) and combine == "sum" and sharded \
         else out_dtype
     loc = _map(x, lambda t: local_fn(t, axes, keepdims, acc))
+    partials = None
+    scalar = all(i in axes for i in range(x.ndim)) or x.ndim == 0
     if sharded:
         groups = x.tile.groups_along(sharded)
         if combine == "sum":
-            loc = C.all_reduce(loc, groups, note="reduce")
+            partials = (loc, len(groups[0]))
+            if scalar and _LAZY_SCALAR_SUMS:
+                # the all-reduce (and the cast) run only if the scalar's value is read:
+                # grad() seeds the partials and never reads the loss value (LazyLocal)
+                pre = loc
+
+                def thunk(pre=pre, groups=groups):
+                    red = C.all_reduce(pre, groups, note="reduce")
+                    return {d: (t if t.dtype == out_dtype else t.to(out_dtype)) for d, t in red.items()}
+                loc = LazyLocal(thunk)
+            else:
+                loc = C.all_reduce(loc, groups, note="reduce")
         else:
             gathered = C.all_gather({d: t.unsqueeze(0) for d, t in loc.items()}, groups, 0, note="reduce")
             loc = {d: (t.amax(0) if combine == "max" else t.amin(0)) for d, t in gathered.items()}
-    loc = {d: (t if t.dtype == out_dtype else t.to(out_dtype)) for d, t in loc.items()}
+    if not isinstance(loc, LazyLocal):
+        loc = {d: (t if t.dtype == out_dtype else t.to(out_dtype)) for d, t in loc.items()}
     if keepdims:
         tile = x.tile.unshard(axes)
         shape = tuple(1 if i in axes else s for i, s in enumerate(x.shape))
@@ -332,7 +350,13 @@ def _reduce(x: ShardedArray, axis, keepdims: bool, local_fn, combine: str, dtype
         kept = [i for i in range(x.ndim) if i not in axes]
         tile = x.tile.project(kept)
         shape = tuple(x.shape[i] for i in kept)
-    return ShardedArray(shape, out_dtype, sharding_from_tile(tile, like=[x.sharding]), loc)
+    res = ShardedArray(shape, out_dtype, sharding_from_tile(tile, like=[x.sharding]), loc)
+    if partials is not None and res.size == 1:
+        # a scalar that is the all-reduced sum of per-shard partial sums: grad() seeds the partials
+        # directly (d sum / d partial = 1) instead of back-propagating through the all-reduce,
+        # so a data-parallel loss needs no collective in the backward pass
+        res._sum_partials = partials
+    return res
 
 
 def reduce_sum(x: ShardedArray, axis=None, keepdims=False, dtype=None) -> ShardedArray:

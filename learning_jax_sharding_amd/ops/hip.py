@@ -453,11 +453,13 @@ class _SumAll(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        if ctx.dtype == torch.bfloat16 and g.dtype == torch.bfloat16 and g.is_cuda and g.numel() == 1 \
-                and len(ctx.shape) >= 1:
-            # the scalar itself, broadcast with all strides 0 (no kernel): a dense layer's backward
-            # turns it into its bf16 row + bias gradient in one launch (bcast_scalar)
-            return g.reshape(()).expand(ctx.shape), None
+        if ctx.dtype == torch.bfloat16 and g.dtype in (torch.bfloat16, torch.float32) and g.is_cuda \
+                and g.numel() == 1 and len(ctx.shape) >= 1:
+            # the scalar itself, broadcast with all strides 0: a dense layer's backward turns it
+            # into its bf16 row + bias gradient in one launch (bcast_scalar).  An f32 seed (the
+            # f32 partial sum of a sharded loss) is rounded to bf16 first (one 1-element cast).
+            gb = g.reshape(()) if g.dtype == torch.bfloat16 else _cast_raw(g.reshape(1), torch.bfloat16).reshape(())
+            return gb.expand(ctx.shape), None
         if ctx.dtype == torch.bfloat16 and g.dtype in (torch.float32, torch.bfloat16) and g.is_cuda \
                 and len(ctx.shape) >= 1:
             # one bf16 row holding g, broadcast (stride 0) over every leading dim: the consumers

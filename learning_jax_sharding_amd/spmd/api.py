@@ -26,7 +26,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from ..array import ShapeDtypeStruct, ShardedArray, device_put
+from ..array import LazyLocal, ShapeDtypeStruct, ShardedArray, device_put
 from ..comm import collectives as C
 from ..sharding.shardings import Sharding, SingleDeviceSharding
 from ..sharding.tile import TileAssignment
@@ -324,6 +324,11 @@ def reduce_replica_grads(pairs: List[Tuple[ShardedArray, Dict[int, torch.Tensor]
 _SEEDS: Dict[Tuple, torch.Tensor] = {}
 
 
+# debugging switch: back-propagate a sharded scalar sum through its all-reduce (the generic
+# transpose) instead of seeding the pre-reduction partial sums
+_SEED_THROUGH_ALLREDUCE = os.environ.get("LJS_SEED_THROUGH_ALLREDUCE", "0") == "1"
+
+
 def _seed(t: torch.Tensor, value: float) -> torch.Tensor:
     """Constant cotangent seed, cached per (device, dtype, shape, value): autograd only reads
     it, so a captured train step replays without a fill kernel."""
@@ -357,10 +362,21 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
         ta = out.tile
         n_holders = ta.num_devices
         outs, seeds = [], []
-        for d, t in out.local.items():
-            if t.requires_grad:
-                outs.append(t)
-                seeds.append(_seed(t, 1.0 / n_holders))
+        partials = getattr(out, "_sum_partials", None)
+        if partials is not None and not _SEED_THROUGH_ALLREDUCE:
+            # out = all_reduce(partials) over groups of size G (replicated over n_holders / G
+            # groups): seeding each partial with G / n_holders is exactly what the all-reduce's
+            # transpose would deliver to it from the 1 / n_holders seeds below
+            loc, gsize = partials
+            for d, t in loc.items():
+                if t.requires_grad:
+                    outs.append(t)
+                    seeds.append(_seed(t, gsize / n_holders))
+        else:
+            for d, t in out.local.items():
+                if t.requires_grad:
+                    outs.append(t)
+                    seeds.append(_seed(t, 1.0 / n_holders))
         grads_per_arg = []
         all_leaves = [l for ls in diff_leaves for l in ls]
         inputs = [t for l in all_leaves for t in l.local.values() if t.requires_grad]
@@ -412,7 +428,12 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
                 return x
             grads_per_arg.append(T.tree_map(mk, args[a], is_leaf=_leaf_is_array))
         g = tuple(grads_per_arg) if multi else grads_per_arg[0]
-        val = ShardedArray(out.shape, out.dtype, out.sharding, {d: t.detach() for d, t in out.local.items()})
+        if isinstance(out.local, LazyLocal) and out.local.pending:
+            # the value of a lazily all-reduced scalar stays lazy: grad() drops it unread
+            val = ShardedArray(out.shape, out.dtype, out.sharding,
+                               LazyLocal(lambda o=out: {d: t.detach() for d, t in o.local.items()}))
+        else:
+            val = ShardedArray(out.shape, out.dtype, out.sharding, {d: t.detach() for d, t in out.local.items()})
         if has_aux:
             return (val, aux), g
         return val, g

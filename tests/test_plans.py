@@ -158,3 +158,36 @@ def test_plan_case6_backward(host_devices):
     data_groups = ((0, 2), (1, 3))
     ar = [s for s in plan.collectives if s.kind == "all_reduce"]
     assert ar and all(_groups(s) in (data_groups, ((0, 1, 2, 3),)) for s in ar), plan.as_text()
+
+
+def test_plan_dp_loss_needs_no_scalar_collectives(host_devices):
+    """grad() of a data-parallel loss: the gradient is seeded on the per-shard partial sums,
+    so neither the forward all-reduce of the scalar loss nor its transpose runs; the only
+    collectives are the gradient replica sums.  value_and_grad() still returns the exact
+    all-reduced value (computed when read)."""
+    host_devices(4)
+    from learning_jax_sharding_amd import nn
+    from learning_jax_sharding_amd.models import MultiHeadAttention
+    mesh = Mesh(create_device_mesh((4, 1)), ("data", "model"))
+    rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
+    model = MultiHeadAttention(64, heads=4, dim_head=16)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (4, 32, 64))
+    params = model.init(ljs.random.PRNGKey(1), x)["params"]
+    params = ljs.device_put(params, nn.logical_to_mesh_sharding(nn.get_partition_spec(params), mesh, rules))
+    xs = ljs.device_put(x, NamedSharding(mesh, P("data", "model")))
+
+    def loss(p):
+        return model.apply({"params": p}, xs).sum()
+
+    with mesh, nn.axis_rules(rules), record_plan() as plan:
+        g = ljs.grad(loss)(params)
+    notes = [(s.kind, s.info.get("note")) for s in plan.collectives]
+    assert all(n == "grad.replica_sum" for _, n in notes), plan.as_text()
+    with mesh, nn.axis_rules(rules):
+        val, g2 = ljs.value_and_grad(loss)(params)
+        ref = float(np.asarray(model.apply({"params": params}, xs).astype(jnp.float32).sum()))
+    assert abs(float(np.asarray(val)) - ref) <= 2e-2 * max(1.0, abs(ref))
+    for k in ("to_q", "to_out_0"):
+        a = np.asarray(nn.unbox(g)[k]["kernel"])
+        b = np.asarray(nn.unbox(g2)[k]["kernel"])
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5)
