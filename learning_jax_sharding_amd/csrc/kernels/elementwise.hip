@@ -261,7 +261,8 @@ __global__ void colsum_bcast_kernel(const void* __restrict__ in, int is_bf16, in
 // GEMM produces [640][1536] slabs whose column blocks are dWq, dWk, dWv.
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slabs, int S, long slab_stride,
                                                           int R, int C, float* __restrict__ out, int cb,
-                                                          long out_bs, int accumulate) {
+                                                          long out_bs, int accumulate,
+                                                          bf16_t* __restrict__ out_bf16) {
   const long n4 = (long)R * C / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const long e = 4 * i;
@@ -279,6 +280,8 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
     float* dst = out + (long)(c / cb) * out_bs + (long)r * cb + (c % cb);
     if (accumulate) acc += *reinterpret_cast<const f32x4*>(dst);
     *reinterpret_cast<f32x4*>(dst) = acc;
+    if (out_bf16)  // bf16 twin (same layout): the data-parallel all-reduce's wire buffer
+      *reinterpret_cast<u32x2*>(out_bf16 + (dst - out)) = u32x2{pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3])};
   }
 }
 
@@ -719,7 +722,7 @@ LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void*
 // out (column blocks of width cb, out_bs floats apart) = sum of S f32 [R][C] slabs (slab_stride
 // floats apart).  Requires C % 4 == 0, cb % 4 == 0, C % cb == 0 and 16-byte aligned buffers.
 LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, int C, void* out, int cb, long out_bs,
-                            int accumulate, hipStream_t s) {
+                            int accumulate, void* out_bf16, hipStream_t s) {
   if (C % 4 || cb % 4 || C % cb || slab_stride % 4 || out_bs % 4 || S < 1 || (((uintptr_t)slabs) & 15) ||
       (((uintptr_t)out) & 15))
     return (int)hipErrorInvalidValue;
@@ -727,8 +730,9 @@ LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, i
   int grid = (int)((n4 + 255) / 256);
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
+  if (out_bf16 && (((uintptr_t)out_bf16) & 7)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, s, (const float*)slabs, S, slab_stride, R, C,
-                     (float*)out, cb, out_bs, accumulate);
+                     (float*)out, cb, out_bs, accumulate, (bf16_t*)out_bf16);
   return (int)hipGetLastError();
 }
 

@@ -46,7 +46,7 @@ _SIGS = {
     "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_fill_row_bf16": [c_void_p, c_int, c_void_p, c_long, c_void_p],
     "ljs_bcast_scalar": [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p],
-    "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p],
+    "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ljs_adam_f32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
@@ -534,12 +534,16 @@ def _torch_linear(x, w, b, compute_dtype, relu, out_dtype):
     return y.to(out_dtype)
 
 
-def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, accumulate: bool = False) -> None:
+def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, accumulate: bool = False,
+                out_bf16: Optional[torch.Tensor] = None) -> None:
     """out = sum over the leading dim of f32 ``slabs`` [S][R][C], written as C/cb column blocks of
-    width ``cb`` stored ``out_bs`` floats apart (the split-K combine of the weight-grad GEMMs)."""
+    width ``cb`` stored ``out_bs`` floats apart (the split-K combine of the weight-grad GEMMs).
+    ``out_bf16`` (same layout as ``out``) also receives the sums rounded to bf16."""
     S, R, C = slabs.shape
     assert slabs.dtype == torch.float32 and out.dtype == torch.float32 and slabs.is_contiguous()
-    rc = lib().ljs_slab_reduce(_p(slabs), S, R * C, R, C, _p(out), cb, out_bs, int(accumulate), _stream(out))
+    assert out_bf16 is None or (out_bf16.dtype == torch.bfloat16 and out_bf16.numel() == out.numel())
+    rc = lib().ljs_slab_reduce(_p(slabs), S, R * C, R, C, _p(out), cb, out_bs, int(accumulate), _p(out_bf16),
+                               _stream(out))
     _ck(rc, "slab_reduce")
 
 

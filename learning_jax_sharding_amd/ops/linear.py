@@ -43,7 +43,7 @@ _FUSED_SUM = os.environ.get("LJS_FUSED_SUM", "1") == "1"  # tuning override of t
 
 
 def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: int, out: torch.Tensor, cb: int,
-              out_bs: int) -> None:
+              out_bs: int, twin: Optional[torch.Tensor] = None) -> None:
     """out (column blocks of width cb, out_bs apart) = xb^T @ dy for xb [T][K], dy [T][Nt] (row
     stride ld, 0 = broadcast row): S K-chunks of the token dim run as one batched LDS-DMA GEMM
     into f32 slabs [S][K][Nt], combined by one streaming reduction."""
@@ -54,7 +54,7 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
     slabs = torch.empty((S, K, Nt), dtype=torch.float32, device=xb.device)
     hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
              tile=1282)
-    hip.slab_reduce(slabs, out, cb, out_bs)
+    hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
 
 
 def _row_view(dy: torch.Tensor, M: int, N: int) -> Tuple[torch.Tensor, int]:
@@ -167,16 +167,26 @@ class _Linear(torch.autograd.Function):
                 # split-K as a batch over K-chunks writing per-chunk f32 slabs, then one combine
                 # pass (no atomics, no memset): the column blocks of a fused [K][nw*N] product are
                 # the nw weight gradients
+                # under a data-parallel backward with a bf16 gradient wire, the combine also writes
+                # the bf16 twin the all-reduce sends (no separate cast kernel; parallel/data.py)
+                from ..parallel import data as _dp
+                wire = _dp.active_wire_dtype() == torch.bfloat16
                 if batched:
                     dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
-                    _dw_slabs(xb, t0, ld0, M, K, nw * N, dW, N, K * N)
+                    twin = torch.empty((nw, K, N), dtype=torch.bfloat16, device=dev) if wire else None
+                    _dw_slabs(xb, t0, ld0, M, K, nw * N, dW, N, K * N, twin)
+                    if twin is not None:
+                        _dp.register_wire_twin(dW, twin)
                     for i in want:
                         dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
                 else:
                     for i in want:
                         t, ld = mats[i]
                         dW = torch.empty((K, N), dtype=torch.float32, device=dev)
-                        _dw_slabs(xb, t, ld, M, K, N, dW, N, 0)
+                        twin = torch.empty((K, N), dtype=torch.bfloat16, device=dev) if wire else None
+                        _dw_slabs(xb, t, ld, M, K, N, dW, N, 0, twin)
+                        if twin is not None:
+                            _dp.register_wire_twin(dW, twin)
                         dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
             else:
                 tile = 128 if (K >= 256 and N >= 256) else 64

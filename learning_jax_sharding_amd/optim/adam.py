@@ -174,6 +174,16 @@ class _Adam:
         return params2, (ScaleByAdamState(new_count, mu, nu), empty)
 
 
+def _grad_local(g: ShardedArray, d: int) -> torch.Tensor:
+    """Gradient shard for the fused kernel: a data-parallel gradient still in its bf16 wire
+    buffer is read there (the kernel converts on load) instead of being cast back to f32."""
+    loc = g.local
+    raw = getattr(loc, "raw", None)
+    if raw is not None and getattr(loc, "pending", False) and d in raw:
+        return raw[d]
+    return loc[d]
+
+
 def _adam_multi_apply(self, pl, gl, ml, vl, count, inplace):
     """MI355X path: every local shard of every param in ONE multi-tensor kernel per device
     (it also refreshes the params' bf16 GEMM shadows).  Returns None to use the per-leaf path."""
@@ -197,7 +207,7 @@ def _adam_multi_apply(self, pl, gl, ml, vl, count, inplace):
             else:
                 tp, tm, tv = pt.clone(), mt.clone(), vt.clone()
             new_loc[i][0][d], new_loc[i][1][d], new_loc[i][2][d] = tp, tm, tv
-            by_dev.setdefault(d, []).append((tp, g.local[d], tm, tv))
+            by_dev.setdefault(d, []).append((tp, _grad_local(g, d), tm, tv))
     fold = inplace and all(t.dtype == torch.int32 and t.is_cuda for t in count.local.values()) \
         and set(count.local) == set(by_dev)
     if fold:

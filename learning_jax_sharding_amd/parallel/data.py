@@ -41,6 +41,37 @@ from ..array import ShardedArray
 __all__ = ["GradReducer", "default_bucket_bytes", "bucket_plan", "comm_dtype"]
 
 
+# reduced bf16 buckets are handed to the optimizer without the cast back to f32 (see finish())
+_LAZY_WIRE_GRADS = os.environ.get("LJS_LAZY_WIRE_GRADS", "1") == "1"
+
+
+# wire dtype of the data-parallel backward in progress (None outside one): producers of whole
+# gradient buffers (the weight-grad slab combine) then also write the buffer's bf16 "twin",
+# which the bucket sends instead of casting the f32 buffer itself
+_ACTIVE_WIRE: Optional[torch.dtype] = None
+_TWINS: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+
+
+def active_wire_dtype() -> Optional[torch.dtype]:
+    return _ACTIVE_WIRE
+
+
+def register_wire_twin(buf: torch.Tensor, twin: torch.Tensor) -> None:
+    """``twin`` holds ``buf``'s values in the wire dtype (same element order)."""
+    _TWINS[buf.untyped_storage().data_ptr()] = (buf, twin)
+
+
+def _take_twin(flat: torch.Tensor, dtype: torch.dtype) -> Optional[torch.Tensor]:
+    ent = _TWINS.pop(flat.untyped_storage().data_ptr(), None)
+    if ent is None:
+        return None
+    buf, twin = ent
+    if (twin.dtype != dtype or twin.numel() != flat.numel() or flat.storage_offset() != 0
+            or buf.untyped_storage().data_ptr() != flat.untyped_storage().data_ptr()):
+        return None
+    return twin.reshape(-1)
+
+
 def default_bucket_bytes() -> int:
     return int(float(os.environ.get("LJS_GRAD_BUCKET_MB", "1")) * (1 << 20))
 
@@ -122,6 +153,9 @@ class GradReducer:
 
     # ------------------------------------------------------------------ hooks
     def attach(self, inputs: Sequence[torch.Tensor]) -> List:
+        global _ACTIVE_WIRE
+        _ACTIVE_WIRE = self.wire_dtype
+        _TWINS.clear()
         handles = []
         for i, t in enumerate(inputs):
             if self.groups[i] is None:
@@ -161,8 +195,10 @@ class GradReducer:
             flat32 = torch.cat([g.reshape(-1) for g in grads])
         wire = None
         if self.wire_dtype is not None and flat32.dtype == torch.float32 and self.wire_dtype != flat32.dtype:
-            from ..ops.hip import cast as _cast
-            wire = _cast(flat32, self.wire_dtype) if flat32.is_cuda else flat32.to(self.wire_dtype)
+            wire = _take_twin(flat32, self.wire_dtype)
+            if wire is None:
+                from ..ops.hip import cast as _cast
+                wire = _cast(flat32, self.wire_dtype) if flat32.is_cuda else flat32.to(self.wire_dtype)
         buf = wire if wire is not None else flat32
 
         def fn(buf=buf, groups=groups, me=me):
@@ -179,27 +215,50 @@ class GradReducer:
     def finish(self, grads: Dict[int, Dict[int, torch.Tensor]]) -> Dict[int, Dict[int, torch.Tensor]]:
         """Launch what is left, join every bucket, return {leaf index: {dev: reduced grad}}.
         ``grads`` holds the unreduced per-leaf gradients (replica-free leaves pass through)."""
+        global _ACTIVE_WIRE
+        _ACTIVE_WIRE = None
         for pkey in list(self.pending):
             members = self.pending.pop(pkey)
             key = (pkey[0], pkey[1])
             self.open.setdefault(key, []).extend(members)
         for key in list(self.open):
             self._launch(key)
+        _TWINS.clear()
         from ..spmd import graphs
+        from ..array import LazyLocal
         out = dict(grads)
         for idxs, flat32, wire, handle in self.launched:
             graphs.join(handle)
-            if wire is not None:
+            lazy = wire is not None and flat32.is_cuda and _LAZY_WIRE_GRADS
+            if wire is not None and not lazy:
                 # back to the gradients' dtype inside the captured segment after the join
                 from ..ops.hip import cast_into as _cast_into
                 if flat32.is_cuda:
                     _cast_into(wire, flat32)
                 else:
                     flat32.copy_(wire)
+            cast_once = None
+            if lazy:
+                # the reduced bucket stays in the wire dtype: the fused Adam reads bf16 gradients
+                # directly (LazyLocal.raw), and the f32 view is produced -- by one cast of the whole
+                # bucket -- only if something else reads the gradient values
+                done = []
+
+                def cast_once(wire=wire, flat32=flat32, done=done):
+                    if not done:
+                        from ..ops.hip import cast_into as _cast_into
+                        _cast_into(wire, flat32)
+                        done.append(True)
             off = 0
             for i in idxs:
                 d, g = next(iter(grads[i].items()))
                 n = g.numel()
-                out[i] = {d: flat32[off:off + n].view(g.shape)}
+                if lazy:
+                    ll = LazyLocal(lambda d=d, o=off, n=n, sh=g.shape, c=cast_once, f=flat32:
+                                   (c(), {d: f[o:o + n].view(sh)})[1])
+                    ll.raw = {d: wire[off:off + n].view(g.shape)}
+                    out[i] = ll
+                else:
+                    out[i] = {d: flat32[off:off + n].view(g.shape)}
                 off += n
         return out

@@ -423,8 +423,14 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
                 if isinstance(x, ShardedArray):
                     i = next(it)
                     p = all_leaves[i]
-                    return ShardedArray(p.shape, p.dtype, p.sharding,
-                                        {d: t.detach() for d, t in reduced[i].items()})
+                    r = reduced[i]
+                    if isinstance(r, LazyLocal) and r.pending:
+                        # keep a reduced-in-wire-dtype gradient lazy (the optimizer reads .raw)
+                        loc = LazyLocal(lambda r=r: {d: t.detach() for d, t in r.items()})
+                        loc.raw = {d: t.detach() for d, t in r.raw.items()}
+                    else:
+                        loc = {d: t.detach() for d, t in r.items()}
+                    return ShardedArray(p.shape, p.dtype, p.sharding, loc)
                 return x
             grads_per_arg.append(T.tree_map(mk, args[a], is_leaf=_leaf_is_array))
         g = tuple(grads_per_arg) if multi else grads_per_arg[0]
