@@ -289,13 +289,14 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // the bf16 row the GEMMs read with ld = 0 and, in the same launch, the bias gradient (the
 // column sums of that broadcast, R * bf16(g) per column) -- one kernel instead of two.
 __global__ void bcast_scalar_kernel(const void* __restrict__ g, int g_bf16, int C, float R, bf16_t* __restrict__ row,
-                                    float* __restrict__ db) {
+                                    float* __restrict__ db, bf16_t* __restrict__ db_bf16) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const float v = g_bf16 ? bf2f(*reinterpret_cast<const bf16_t*>(g)) : *reinterpret_cast<const float*>(g);
   const bf16_t b = f2bf(v);
   row[c] = b;
   if (db) db[c] = bf2f(b) * R;
+  if (db_bf16) db_bf16[c] = f2bf(bf2f(b) * R);  // the bias gradient's bf16 wire twin
 }
 
 // sum of n f32 partials (a producer's fused per-wave output sums) -> scalar, one block
@@ -736,9 +737,10 @@ LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, i
   return (int)hipGetLastError();
 }
 
-LJS_API int ljs_bcast_scalar(const void* g, int g_bf16, int C, float R, void* row, void* db, hipStream_t s) {
+LJS_API int ljs_bcast_scalar(const void* g, int g_bf16, int C, float R, void* row, void* db, void* db_bf16,
+                             hipStream_t s) {
   hipLaunchKernelGGL(bcast_scalar_kernel, dim3((C + 255) / 256), dim3(256), 0, s, g, g_bf16, C, R, (bf16_t*)row,
-                     (float*)db);
+                     (float*)db, (bf16_t*)db_bf16);
   return (int)hipGetLastError();
 }
 

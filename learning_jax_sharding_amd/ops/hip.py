@@ -45,7 +45,7 @@ _SIGS = {
     "ljs_sum_all": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_fill_row_bf16": [c_void_p, c_int, c_void_p, c_long, c_void_p],
-    "ljs_bcast_scalar": [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p],
+    "ljs_bcast_scalar": [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ljs_adam_f32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
@@ -547,12 +547,16 @@ def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, ac
     _ck(rc, "slab_reduce")
 
 
-def bcast_scalar(g: torch.Tensor, C: int, R: int, want_db: bool):
+def bcast_scalar(g: torch.Tensor, C: int, R: int, want_db: bool, db_out: Optional[torch.Tensor] = None,
+                 db_bf16: Optional[torch.Tensor] = None):
     """(bf16 row [C] filled with bf16(g), f32 [C] = R * bf16(g) or None) from the 1-element
-    tensor ``g`` (f32 or bf16), in one launch."""
+    tensor ``g`` (f32 or bf16), in one launch (``db_out``: where to write the f32 result;
+    ``db_bf16``: also write it rounded to bf16)."""
     row = torch.empty((C,), dtype=torch.bfloat16, device=g.device)
-    db = torch.empty((C,), dtype=torch.float32, device=g.device) if want_db else None
-    rc = lib().ljs_bcast_scalar(_p(g), int(g.dtype == torch.bfloat16), C, float(R), _p(row), _p(db), _stream(row))
+    db = (db_out if db_out is not None else torch.empty((C,), dtype=torch.float32, device=g.device)) \
+        if want_db else None
+    rc = lib().ljs_bcast_scalar(_p(g), int(g.dtype == torch.bfloat16), C, float(R), _p(row), _p(db),
+                                _p(db_bf16 if want_db else None), _stream(row))
     _ck(rc, "bcast_scalar")
     return row, db
 

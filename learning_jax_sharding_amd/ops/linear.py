@@ -131,6 +131,18 @@ class _Linear(torch.autograd.Function):
         mats: List[Optional[Tuple[torch.Tensor, int]]] = []
         db_bcast: List[Optional[torch.Tensor]] = [None] * nw
         want_db = has_b and ctx.needs_input_grad[1]
+        # one dense with a bias whose cotangent is a scalar broadcast (a loss sum), both gradients
+        # wanted: dW and db share ONE f32 buffer [K*N + N]
+        # (and, under a bf16 data-parallel wire, one bf16 twin) so the gradient all-reduce sends
+        # them as one producer group -- no concatenation, no cast kernel (parallel/data.py)
+        from ..parallel import data as _dp
+        wire = _dp.active_wire_dtype() == torch.bfloat16
+        joint = joint_bf16 = None
+        if (nw == 1 and want_db and ctx.needs_input_grad[4] and dys[0] is not None and M % 64 == 0 and not relu
+                and b.dtype == torch.float32 and ws[0].dtype == torch.float32 and dys[0].is_cuda
+                and dys[0].numel() > 0 and all(st == 0 for st in dys[0].stride())):
+            joint = torch.empty((K * N + N,), dtype=torch.float32, device=dev)
+            joint_bf16 = torch.empty((K * N + N,), dtype=torch.bfloat16, device=dev) if wire else None
         for i, dy in enumerate(dys):
             if dy is None:
                 mats.append(None)
@@ -140,7 +152,10 @@ class _Linear(torch.autograd.Function):
             elif dy.is_cuda and dy.numel() > 0 and all(st == 0 for st in dy.stride()):
                 # one scalar broadcast (the cotangent of y.sum()): its bf16 row and the bias
                 # gradient come out of one kernel; the GEMMs read the row with ld = 0
-                row, db_bcast[i] = hip.bcast_scalar(dy.as_strided((1,), (1,)), N, M, want_db)
+                row, db_bcast[i] = hip.bcast_scalar(
+                    dy.as_strided((1,), (1,)), N, M, want_db,
+                    db_out=joint[K * N:] if joint is not None else None,
+                    db_bf16=joint_bf16[K * N:] if joint_bf16 is not None else None)
                 mats.append((row.unsqueeze(0).expand(M, N), 0))
                 continue
             mats.append(_row_view(dy, M, N))
@@ -169,9 +184,13 @@ class _Linear(torch.autograd.Function):
                 # the nw weight gradients
                 # under a data-parallel backward with a bf16 gradient wire, the combine also writes
                 # the bf16 twin the all-reduce sends (no separate cast kernel; parallel/data.py)
-                from ..parallel import data as _dp
-                wire = _dp.active_wire_dtype() == torch.bfloat16
-                if batched:
+                if joint is not None:
+                    t, ld = mats[0]
+                    dW = joint[:K * N].view(K, N)
+                    _dw_slabs(xb, t, ld, M, K, N, dW, N, 0,
+                              joint_bf16[:K * N].view(K, N) if joint_bf16 is not None else None)
+                    dws[0] = dW
+                elif batched:
                     dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
                     twin = torch.empty((nw, K, N), dtype=torch.bfloat16, device=dev) if wire else None
                     _dw_slabs(xb, t0, ld0, M, K, nw * N, dW, N, K * N, twin)
@@ -214,6 +233,11 @@ class _Linear(torch.autograd.Function):
                 t, ld = mats[i]
                 tot = hip.colsum_ld(t, M, N, ld, tot)
             db = tot.to(b.dtype)
+        if joint is not None:
+            if dws[0] is None or db is None or db.data_ptr() != joint[K * N:].data_ptr():
+                joint_bf16 = None  # the two gradients did not both land in the joint buffer
+            if joint_bf16 is not None:
+                _dp.register_wire_twin(joint, joint_bf16)
         return (dx, db, None, None, *dws)
 
 
