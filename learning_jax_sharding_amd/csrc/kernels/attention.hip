@@ -769,7 +769,11 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       if (need_mask) fused_tile<true>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, Ks, Vs, dk, dv, q0, key0, lane);
       else fused_tile<false>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, Ks, Vs, dk, dv, q0, key0, lane);
     }
+    // this wave's DMA pieces of the next block landed; after the barrier everyone's have, so the
+    // next block's delta is formed inside the dQ phase (two barriers per query block, not three)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (more) finish(cur ^ 1);
     // dQ^T (d tiles dt0, dt0+1) x queries 16qt..16qt+15 = K^T dS^T over all keys
     f32x4 dq[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     for (int s2 = 0; s2 < nk32; ++s2) {
@@ -780,9 +784,6 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
         dq[i] = mfma16x16x32(ka, sb, dq[i]);
       }
     }
-    // this wave's DMA pieces of the next block landed (waited here, before the dQ stores join
-    // the vmcnt queue); the barrier below publishes everyone's
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int qrow = q0 + 16 * qt + (lane & 15);
     if (qrow < a.Sq) {
       bf16_t* rowp = a.out3 + b * a.out3_sb + (long)qrow * a.out3_ss + h * a.out3_sh;
@@ -795,10 +796,6 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       }
     }
     __syncthreads();
-    if (more) {
-      finish(cur ^ 1);
-      __syncthreads();
-    }
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {

@@ -444,6 +444,22 @@ def _sum_all_raw(t: torch.Tensor, out_dtype: torch.dtype = torch.float32) -> tor
     return out
 
 
+# constant f32 gradient seeds (spmd.api._seed) -> their bf16 rounding, so the backward of a bf16
+# sum fed by a cached seed needs no cast kernel
+_SEEDS_BF16 = {}
+
+
+def register_seed_bf16(seed: torch.Tensor, seed_bf16: torch.Tensor) -> None:
+    _SEEDS_BF16[seed.data_ptr()] = (seed, seed_bf16)
+
+
+def _seed_bf16(g: torch.Tensor) -> torch.Tensor:
+    ent = _SEEDS_BF16.get(g.data_ptr())
+    if ent is not None and ent[0].data_ptr() == g.data_ptr() and ent[0].numel() == 1:
+        return ent[1].reshape(())
+    return _cast_raw(g.reshape(1), torch.bfloat16).reshape(())
+
+
 class _SumAll(torch.autograd.Function):
     @staticmethod
     def forward(ctx, t, acc_dtype):
@@ -458,7 +474,7 @@ class _SumAll(torch.autograd.Function):
             # the scalar itself, broadcast with all strides 0: a dense layer's backward turns it
             # into its bf16 row + bias gradient in one launch (bcast_scalar).  An f32 seed (the
             # f32 partial sum of a sharded loss) is rounded to bf16 first (one 1-element cast).
-            gb = g.reshape(()) if g.dtype == torch.bfloat16 else _cast_raw(g.reshape(1), torch.bfloat16).reshape(())
+            gb = g.reshape(()) if g.dtype == torch.bfloat16 else _seed_bf16(g)
             return gb.expand(ctx.shape), None
         if ctx.dtype == torch.bfloat16 and g.dtype in (torch.float32, torch.bfloat16) and g.is_cuda \
                 and len(ctx.shape) >= 1:

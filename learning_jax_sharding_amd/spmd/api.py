@@ -339,6 +339,10 @@ def _seed(t: torch.Tensor, value: float) -> torch.Tensor:
         if t.device.type == "meta" or (t.is_cuda and torch.cuda.is_current_stream_capturing()):
             return s
         _SEEDS[key] = s
+        if t.is_cuda and t.dtype == torch.float32 and s.numel() == 1:
+            # its bf16 rounding, for a bf16 sum's backward fed by this f32 seed (no cast kernel)
+            from ..ops import hip as _hip
+            _hip.register_seed_bf16(s, s.to(torch.bfloat16))
     return s
 
 
