@@ -197,9 +197,26 @@ __global__ void sum_all_ticket_kernel(const T* __restrict__ in, long n, float* _
 }
 
 // column sums of a bf16 [R][C] matrix, partial slabs + last-arriver per column block (no memset)
+// Optional fused ReLU backward (mask != null): in *= (mask > 0) element-wise -- mask is the
+// ReLU's bf16 output, same [R][C] layout with row stride ld -- and the masked values are also
+// written to masked_out (row stride C).  One pass then yields both the masked gradient the
+// GEMMs read and its column sums (the bias gradient).
+__device__ __forceinline__ u32x4 relu_mask_bf16x8(const u32x4& v, const u32x4& m) {
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // a bf16 is > 0 iff its sign bit is clear and it is not +0: keep each half where that holds
+    const unsigned lo = (m[k] & 0x8000u) == 0 && (m[k] & 0x7fffu) != 0 ? 0x0000ffffu : 0u;
+    const unsigned hi = (m[k] & 0x80000000u) == 0 && (m[k] & 0x7fff0000u) != 0 ? 0xffff0000u : 0u;
+    o[k] = v[k] & (lo | hi);
+  }
+  return o;
+}
+
 __global__ void colsum_ticket_kernel(const bf16_t* __restrict__ in, int R, int C, long ld, int rows_per_block,
                                      float* __restrict__ partials, unsigned* __restrict__ tickets,
-                                     float* __restrict__ out, int accumulate) {
+                                     float* __restrict__ out, int accumulate, const bf16_t* __restrict__ mask,
+                                     long mld, bf16_t* __restrict__ masked_out) {
   const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
   const int c0 = blockIdx.x * 64 + cl * 8;
   const int r0 = blockIdx.y * rows_per_block, r1 = min(R, r0 + rows_per_block);
@@ -211,7 +228,29 @@ __global__ void colsum_ticket_kernel(const bf16_t* __restrict__ in, int R, int C
       acc[2 * k + 1] += __uint_as_float(v[k] & 0xffff0000u);
     }
   };
-  if (c0 < C) {
+  if (c0 < C && mask) {
+    int r = r0 + rl;
+    for (; r + 96 < r1; r += 128) {  // 4 independent row loads (+ 4 mask loads) in flight
+      u32x4 v[4], m[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = *reinterpret_cast<const u32x4*>(in + (long)(r + 32 * u) * ld + c0);
+        m[u] = *reinterpret_cast<const u32x4*>(mask + (long)(r + 32 * u) * mld + c0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const u32x4 o = relu_mask_bf16x8(v[u], m[u]);
+        *reinterpret_cast<u32x4*>(masked_out + (long)(r + 32 * u) * C + c0) = o;
+        add(o);
+      }
+    }
+    for (; r < r1; r += 32) {
+      const u32x4 o = relu_mask_bf16x8(*reinterpret_cast<const u32x4*>(in + (long)r * ld + c0),
+                                       *reinterpret_cast<const u32x4*>(mask + (long)r * mld + c0));
+      *reinterpret_cast<u32x4*>(masked_out + (long)r * C + c0) = o;
+      add(o);
+    }
+  } else if (c0 < C) {
     int r = r0 + rl;
     for (; r + 96 < r1; r += 128) {  // 4 independent row loads in flight
       u32x4 v[4];
@@ -700,7 +739,8 @@ LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void*
     // workspace layout: [tickets: 4096 words][partials: gy * C floats]
     if (ws && cb <= 4096 && (long)gy * C + 4096 <= kColsumWsFloats) {
       hipLaunchKernelGGL(colsum_ticket_kernel, dim3(cb, gy), dim3(256), 0, s, (const bf16_t*)in, R, C, ld, rpb,
-                         (float*)ws + 4096, (unsigned*)ws, (float*)out, accumulate);
+                         (float*)ws + 4096, (unsigned*)ws, (float*)out, accumulate, (const bf16_t*)nullptr, 0L,
+                         (bf16_t*)nullptr);
       return (int)hipGetLastError();
     }
     if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * C, s);
@@ -746,6 +786,25 @@ LJS_API int ljs_bcast_scalar(const void* g, int g_bf16, int C, float R, void* ro
 
 LJS_API int ljs_sum_partials(const void* p, int n, void* out, int out_bf16, hipStream_t s) {
   hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, (const float*)p, n, out, out_bf16);
+  return (int)hipGetLastError();
+}
+
+// masked_out[R][C] = in * (mask > 0) and out[C] (f32) = its column sums, in one pass (fused ReLU
+// backward + bias gradient).  bf16 in / mask with row stride ld, C % 8 == 0, 16-byte aligned.
+LJS_API int ljs_relu_bwd_colsum(const void* in, const void* mask, int R, int C, long ld, long mld, void* masked_out,
+                                void* out, void* ws, hipStream_t s) {
+  if (C % 8 || ld % 8 || mld % 8 || (((uintptr_t)in) & 15) || (((uintptr_t)mask) & 15) || (((uintptr_t)masked_out) & 15) || !ws)
+    return (int)hipErrorInvalidValue;
+  int cb = (C + 63) / 64;
+  int want = 512 / cb;
+  int gy = want < 1 ? 1 : want;
+  int rpb = (R + gy - 1) / gy;
+  if (rpb < 32) rpb = 32;
+  gy = (R + rpb - 1) / rpb;
+  if (cb > 4096 || (long)gy * C + 4096 > kColsumWsFloats) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(colsum_ticket_kernel, dim3(cb, gy), dim3(256), 0, s, (const bf16_t*)in, R, C, ld, rpb,
+                     (float*)ws + 4096, (unsigned*)ws, (float*)out, 0, (const bf16_t*)mask, mld,
+                     (bf16_t*)masked_out);
   return (int)hipGetLastError();
 }
 

@@ -45,6 +45,7 @@ _SIGS = {
     "ljs_sum_all": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_fill_row_bf16": [c_void_p, c_int, c_void_p, c_long, c_void_p],
+    "ljs_relu_bwd_colsum": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_bcast_scalar": [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
@@ -575,6 +576,19 @@ def bcast_scalar(g: torch.Tensor, C: int, R: int, want_db: bool, db_out: Optiona
                                 _p(db_bf16 if want_db else None), _stream(row))
     _ck(rc, "bcast_scalar")
     return row, db
+
+
+def relu_bwd_colsum(dy: torch.Tensor, y: torch.Tensor, R: int, C: int):
+    """(dy * (y > 0) as a new bf16 [R][C], its f32 column sums [C]) in one pass: the fused ReLU
+    backward + bias gradient of a dense layer.  dy / y: bf16 [R][C] views with unit column
+    stride (row strides may differ)."""
+    masked = torch.empty((R, C), dtype=torch.bfloat16, device=dy.device)
+    out = torch.empty((C,), dtype=torch.float32, device=dy.device)
+    ws = _workspace(dy.device, "colsum", _COLSUM_WS_BYTES)
+    rc = lib().ljs_relu_bwd_colsum(_p(dy), _p(y), R, C, dy.stride(0), y.stride(0), _p(masked), _p(out), _p(ws),
+                                   _stream(dy))
+    _ck(rc, "relu_bwd_colsum")
+    return masked, out
 
 
 def colsum_ld(t: torch.Tensor, R: int, C: int, ld: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:

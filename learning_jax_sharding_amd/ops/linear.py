@@ -148,6 +148,15 @@ class _Linear(torch.autograd.Function):
                 mats.append(None)
                 continue
             if relu:
+                d2, y2 = dy.reshape(M, N), ys[i].reshape(M, N)
+                if (d2.is_cuda and d2.dtype == torch.bfloat16 and y2.dtype == torch.bfloat16 and N % 8 == 0
+                        and d2.stride(1) == 1 and y2.stride(1) == 1 and d2.stride(0) % 8 == 0
+                        and y2.stride(0) % 8 == 0 and d2.data_ptr() % 16 == 0 and y2.data_ptr() % 16 == 0):
+                    # fused ReLU backward: the masked gradient and its column sums (the bias
+                    # gradient) in one pass over dy and y
+                    masked, db_bcast[i] = hip.relu_bwd_colsum(d2, y2, M, N)
+                    mats.append((masked, N))
+                    continue
                 dy = (dy * (ys[i] > 0)).reshape(M, N)
             elif dy.is_cuda and dy.numel() > 0 and all(st == 0 for st in dy.stride()):
                 # one scalar broadcast (the cotangent of y.sum()): its bf16 row and the bias

@@ -380,6 +380,20 @@ def test_fused_output_sum(hip, T, N):
     torch.testing.assert_close(hip.sum_all(half, torch.float32), half.float().sum(), rtol=1e-4, atol=1e-1)
 
 
+@pytest.mark.parametrize("R,C,yld", [(16384, 2560, 2560), (300, 72, 72), (256, 64, 192)])
+def test_relu_bwd_colsum(hip, R, C, yld):
+    """Fused ReLU backward + bias gradient: masked = dy * (y > 0), db = colsum(masked), vs torch;
+    y may be a column slice of a wider buffer (row stride != C); -0.0 and +0.0 are masked."""
+    dy = _rand(R, C, seed=50)
+    ybuf = _rand(R, yld, seed=51)
+    ybuf[0, :4] = torch.tensor([0.0, -0.0, 1e-30, -1e-30], dtype=torch.bfloat16)
+    y = ybuf[:, :C]
+    masked, db = hip.relu_bwd_colsum(dy, y, R, C)
+    ref = dy.float() * (y.float() > 0).float()
+    torch.testing.assert_close(masked.float(), ref, rtol=0, atol=0)
+    torch.testing.assert_close(db, ref.sum(0), rtol=1e-4, atol=1e-2)
+
+
 def test_ticket_reductions_rearm(hip):
     """Last-arriver reductions (sum_all, colsum) re-arm their tickets: repeated calls with
     different data and grid sizes stay exact, and sum_all writes bf16 directly."""
