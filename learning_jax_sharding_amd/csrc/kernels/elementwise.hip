@@ -474,6 +474,9 @@ struct AdamTensor {
   long p, g, m, v, st, sn, R, C, g_bf16, tiles_c, vec;  // vec: 4-wide path allowed (C % 4, alignment)
 };
 constexpr int kAdamMax = 32;
+// rows per Adam tile (x 64 columns): 32-row tiles give twice the workgroups of 64-row ones, so
+// each CU overlaps more load / store / transpose phases (the update is latency-bound)
+constexpr int kAdamRows = 32;
 struct AdamBatch {
   AdamTensor t[kAdamMax];
   int tile_start[kAdamMax + 1];
@@ -485,7 +488,7 @@ struct AdamBatch {
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* __restrict__ step, int step_offset,
                                                          unsigned* __restrict__ ticket, float lr, float b1, float b2,
                                                          float eps, float wd) {
-  __shared__ float tr[64][65];
+  __shared__ float tr[kAdamRows][65];
   const int id = blockIdx.x;
   int ti = 0;
   while (ti + 1 < batch.n && id >= batch.tile_start[ti + 1]) ++ti;
@@ -506,11 +509,12 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
     // shadow stores; the transposed shadow leaves as 8-byte stores from the LDS transpose
     const int c4 = (threadIdx.x & 15) * 4, r0 = threadIdx.x >> 4;
     const long cbase = (long)tc_i * 64 + c4;
-    f32x4 gv[4], mv[4], vv[4], pv[4];
-    bool ok[4];
+    constexpr int NQ = kAdamRows / 16;
+    f32x4 gv[NQ], mv[NQ], vv[NQ], pv[NQ];
+    bool ok[NQ];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = tr_i * 64 + r0 + 16 * q;
+    for (int q = 0; q < NQ; ++q) {
+      const int row = tr_i * kAdamRows + r0 + 16 * q;
       ok[q] = row < T.R;
       const long i = ok[q] ? (long)row * T.C + cbase : cbase;
       if (T.g_bf16) {
@@ -525,7 +529,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
       pv[q] = *reinterpret_cast<const f32x4*>(P + i);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const int rl = r0 + 16 * q;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -539,7 +543,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
         tr[rl][c4 + e] = pv[q][e];
       }
       if (ok[q]) {
-        const long i = (long)(tr_i * 64 + rl) * T.C + cbase;
+        const long i = (long)(tr_i * kAdamRows + rl) * T.C + cbase;
         *reinterpret_cast<f32x4*>(P + i) = pv[q];
         *reinterpret_cast<f32x4*>(Mm + i) = mv[q];
         *reinterpret_cast<f32x4*>(Vv + i) = vv[q];
@@ -552,12 +556,13 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
       __syncthreads();
       // shadow_t[c][r]: thread -> 4 consecutive rows r4..r4+3 of output row c (bank-conflict
       // free: tr's row stride is 65 words)
-      const int r4 = (threadIdx.x & 15) * 4, cl0 = threadIdx.x >> 4;
-      const int orow0 = tc_i * 64, ocol = tr_i * 64 + r4;
+      constexpr int RL = kAdamRows / 4;            // lanes across the tile's rows
+      const int r4 = (threadIdx.x % RL) * 4, cl0 = threadIdx.x / RL;
+      const int orow0 = tc_i * 64, ocol = tr_i * kAdamRows + r4;
       const bool rows_vec = (T.R & 3) == 0 && ocol + 4 <= T.R;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int cl = cl0 + 16 * q, c = orow0 + cl;
+      for (int q = 0; q < 64 / (256 / RL); ++q) {
+        const int cl = cl0 + (256 / RL) * q, c = orow0 + cl;
         bf16_t* dst = reinterpret_cast<bf16_t*>(T.st) + (long)c * T.R + ocol;
         if (rows_vec) {
           *reinterpret_cast<u32x2*>(dst) = u32x2{pack_bf16x2(tr[r4][cl], tr[r4 + 1][cl]),
@@ -575,8 +580,8 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
     return;
   }
 #pragma unroll 4
-  for (int rr = 0; rr < 16; ++rr) {
-    const int rl = ty + 4 * rr, row = tr_i * 64 + rl;
+  for (int rr = 0; rr < kAdamRows / 4; ++rr) {
+    const int rl = ty + 4 * rr, row = tr_i * kAdamRows + rl;
     float newp = 0.f;
     if (row < T.R && col < T.C) {
       const long i = (long)row * T.C + col;
@@ -594,11 +599,10 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
   }
   if (T.st) {
     __syncthreads();
-    const int orow0 = tc_i * 64, ocol = tr_i * 64 + tx;  // shadow_t[c][r]
-#pragma unroll 4
-    for (int rr = 0; rr < 16; ++rr) {
-      const int cl = ty + 4 * rr, c = orow0 + cl;
-      if (c < T.C && ocol < T.R) reinterpret_cast<bf16_t*>(T.st)[(long)c * T.R + ocol] = f2bf(tr[tx][cl]);
+    const int orow0 = tc_i * 64;  // shadow_t[c][r]
+    for (int idx = threadIdx.x; idx < kAdamRows * 64; idx += 256) {
+      const int r = idx % kAdamRows, cl = idx / kAdamRows, c = orow0 + cl, ocol = tr_i * kAdamRows + r;
+      if (c < T.C && ocol < T.R) reinterpret_cast<bf16_t*>(T.st)[(long)c * T.R + ocol] = f2bf(tr[r][cl]);
     }
   }
   if (ticket) {
@@ -878,7 +882,7 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
     t.vec = t.C % 4 == 0 && al(t.p, 16) && al(t.m, 16) && al(t.v, 16) && al(t.g, t.g_bf16 ? 8 : 16) &&
             al(t.sn, 8) && al(t.st, 8);
     b.tile_start[i] = tiles;
-    tiles += (int)(((t.R + 63) / 64) * t.tiles_c);
+    tiles += (int)(((t.R + kAdamRows - 1) / kAdamRows) * t.tiles_c);
   }
   b.tile_start[n] = tiles;
   b.n = n;

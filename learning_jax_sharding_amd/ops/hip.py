@@ -85,13 +85,14 @@ def set_attention_fwd_resident(waves: int):
     fn(int(waves))
 
 
-def set_attention_bwd_fused(enabled: bool):
+def set_attention_bwd_fused(enabled: Optional[bool]):
     """Select the attention backward for key lengths <= 256: the single-pass fused kernel
-    (default) or the split dQ + dK/dV kernels (always used above 256 keys)."""
+    (True), the split dQ + dK/dV kernels (False; always used above 256 keys), or None for the
+    automatic choice by grid size (the default)."""
     fn = lib().ljs_attn_set_bwd_fused
     fn.argtypes = [c_int]
     fn.restype = None
-    fn(1 if enabled else 0)
+    fn(2 if enabled is None else (1 if enabled else 0))
 
 
 def set_attention_fwd_nsub(nsub: int):

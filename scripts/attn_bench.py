@@ -22,7 +22,7 @@ g = torch.randn_like(o)
 res["fwd+bwd"] = timeit(lambda: torch.autograd.grad(hip.attention(q1, k1, v1, scale), (q1, k1, v1), g))
 hip.set_attention_bwd_fused(False)
 res["fwd+bwd split"] = timeit(lambda: torch.autograd.grad(hip.attention(q1, k1, v1, scale), (q1, k1, v1), g))
-hip.set_attention_bwd_fused(True)
+hip.set_attention_bwd_fused(None)
 # torch SDPA (ROCm flash / efficient backends) on the same problem, (B, H, S, D) layout
 import torch.nn.functional as F
 qt, kt, vt = (t.transpose(1, 2).contiguous() for t in (q, k, v))

@@ -131,7 +131,7 @@ def _attn_ref(q, k, v, scale, causal=False, q_offset=0):
 def attn_bwd_impl(request, hip):
     hip.set_attention_bwd_fused(request.param == "fused")
     yield request.param
-    hip.set_attention_bwd_fused(True)
+    hip.set_attention_bwd_fused(None)
 
 
 @pytest.fixture(params=[(1, 0), (2, 0), (1, 4), (1, 8), (1, 16)], ids=["tiled1", "tiled2", "res4", "res8", "res16"])
@@ -185,7 +185,7 @@ def test_attention_bwd_block_fused_matches_split(hip, attn_fwd_nsub, Sq, Sk, cau
     for fused in (True, False):
         hip.set_attention_bwd_fused(fused)
         outs[fused] = hip.attn_bwd_block(q, k, v, o, do, lse, D ** -0.5, causal, q_offset)
-    hip.set_attention_bwd_fused(True)
+    hip.set_attention_bwd_fused(None)
     for a, b_ in zip(outs[True], outs[False]):
         torch.testing.assert_close(a.float(), b_.float(), rtol=2e-2, atol=2e-2)
 
