@@ -243,7 +243,13 @@ class DistComm:
         from . import native as _nat
         if _nat.rank_eligible():
             dev = local_devices()[0]
-            self._native = _nat.RankRccl(dist.get_rank(), dist.get_world_size(), dev.torch_device.index)
+            try:
+                self._native = _nat.RankRccl(dist.get_rank(), dist.get_world_size(), dev.torch_device.index)
+            except RuntimeError as e:  # pragma: no cover - depends on the node's RCCL
+                # keep the job running on torch's process groups (segmented graph capture)
+                import warnings
+                warnings.warn(f"native RCCL communicators unavailable ({e}); using torch.distributed groups")
+                self._native = None
 
     _GRAPH_KINDS = ("all_gather", "reduce_scatter", "all_reduce", "all_to_all")
 
