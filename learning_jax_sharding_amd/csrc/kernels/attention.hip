@@ -256,6 +256,96 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
   }
 }
 
+// Persistent K/V-resident forward (Sk <= 256): one workgroup per CU walks work items (query
+// block, head, batch) with K/V double-buffered in LDS -- the next item's K/V burst (LDS-DMA from
+// asm) and Q fragments (registers) are in flight while the current item computes, so only the
+// first item's load latency is exposed.  NW waves x 16 queries per item.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_pers_kernel(AttnArgs a, int items) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2][FKR * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2][FKR * D];
+  constexpr int QB = 16 * NW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nqb = (a.Sq + QB - 1) / QB;
+  const int G = gridDim.x;
+  struct Item {
+    int qb, h, b, nkt;
+  };
+  auto decode = [&](int it) {
+    Item w;
+    w.qb = it % nqb;
+    w.h = (it / nqb) % a.H;
+    w.b = it / (nqb * a.H);
+    int kend = a.Sk;
+    if (a.causal) kend = min(a.Sk, a.q_offset + (w.qb + 1) * QB);
+    w.nkt = (kend + BLK - 1) / BLK;
+    return w;
+  };
+  auto issue_kv = [&](const Item& w, int buf) {
+    const bf16_t* kb = a.k + w.b * a.k_sb + w.h * a.k_sh;
+    const bf16_t* vb = a.v + w.b * a.v_sb + w.h * a.v_sh;
+    const u32x4 rk = rsrc_u4(kb, 2 * ((long)(a.Sk - 1) * a.k_ss + D));
+    const u32x4 rv = rsrc_u4(vb, 2 * ((long)(a.Sk - 1) * a.v_ss + D));
+    const int npieces = w.nkt * (BLK / 8);
+    for (int pc = wave; pc < npieces; pc += NW) {
+      const int row = 8 * pc + (lane >> 3);
+      const int c = ((lane & 7) ^ (((row >> 1) & 3) << 1)) * 8;
+      const bool ok = row < a.Sk;
+      dma_lds_x4(rk, ok ? (int)(((long)row * a.k_ss + c) * 2) : 0x7ffffff0, &Ks[buf][pc * 512]);
+      dma_lds_x4(rv, ok ? (int)(((long)row * a.v_ss + c) * 2) : 0x7ffffff0, &Vs[buf][pc * 512]);
+    }
+  };
+  auto load_q = [&](const Item& w, bf16x8 (&q)[2]) {
+    const int qrow = w.qb * QB + 16 * wave + (lane & 15);
+    const bool qok = qrow < a.Sq;
+    const bf16_t* qp = a.q + w.b * a.q_sb + (long)qrow * a.q_ss + w.h * a.q_sh;
+    q[0] = load_row_frag(qp, qok, 0, lane);
+    q[1] = load_row_frag(qp, qok, 1, lane);
+  };
+  int item = blockIdx.x;
+  if (item >= items) return;
+  Item cur = decode(item);
+  bf16x8 qn[2];
+  load_q(cur, qn);
+  issue_kv(cur, 0);
+  for (int k = 0; item < items; ++k, item += G) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // buffer k&1 landed for every wave; buffer (k+1)&1 is free
+    const int buf = k & 1;
+    const bf16x8 qf[2] = {qn[0], qn[1]};
+    const int nxt = item + G;
+    Item nw = cur;
+    if (nxt < items) {
+      nw = decode(nxt);
+      load_q(nw, qn);
+      issue_kv(nw, buf ^ 1);
+    }
+    FwdState st;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st.o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    st.m = -INFINITY;
+    st.l = 0.f;
+    const int qrow = cur.qb * QB + 16 * wave + (lane & 15);
+    const int qrow0 = cur.qb * QB + 16 * wave;
+    for (int kt = 0; kt < cur.nkt; ++kt) {
+      const int kbase = kt * BLK;
+      if (a.causal && kbase > qrow0 + 15 + a.q_offset) break;
+      const bool need_mask = kbase + BLK > a.Sk || (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
+      if (need_mask) fwd_tile<true>(a, st, &Ks[buf][kt * BLK * D], &Vs[buf][kt * BLK * D], qf, kbase, qrow, lane);
+      else fwd_tile<false>(a, st, &Ks[buf][kt * BLK * D], &Vs[buf][kt * BLK * D], qf, kbase, qrow, lane);
+    }
+    const float lt = row4_sum(st.l);
+    if (qrow < a.Sq) {
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      bf16_t* op = a.out + cur.b * a.o_sb + (long)qrow * a.o_ss + cur.h * a.o_sh;
+      store_row_T(op, st.o, inv, lane);
+      if ((lane >> 4) == 0 && a.lse)
+        a.lse[((long)cur.b * a.H + cur.h) * a.Sq + qrow] = lt > 0.f ? st.m + __log2f(lt) : INFINITY;
+    }
+    cur = nw;
+  }
+}
+
 // Block = 4 waves x NSUB sub-tiles of 16 queries (64 NSUB queries of one head).  Each K/V tile
 // staged through LDS serves all NSUB sub-tiles of every wave (NSUB x fewer K/V loads per
 // query).  Sub-tile s of wave w holds queries 16 (4 s + w) + lane,
@@ -842,6 +932,21 @@ LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, v
     g_fwd_res = e ? atoi(e) : 8;
   }
   if (g_fwd_res > 0 && Sk <= FKR && (long)(Sk - 1) * (ks[1] > vs[1] ? ks[1] : vs[1]) * 2 + 128 < (1L << 31)) {
+    if (g_fwd_res == 108 || g_fwd_res == 116) {  // persistent, double-buffered K/V
+      static int cus = 0;
+      if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+      }
+      const int nwp = g_fwd_res - 100;
+      const int items = (Sq + 16 * nwp - 1) / (16 * nwp) * H * B;
+      const int grid = items < cus ? items : cus;
+      if (nwp == 16) hipLaunchKernelGGL(attn_fwd_pers_kernel<16>, dim3(grid), dim3(1024), 0, stream, a, items);
+      else hipLaunchKernelGGL(attn_fwd_pers_kernel<8>, dim3(grid), dim3(512), 0, stream, a, items);
+      return (int)hipGetLastError();
+    }
     const int nw = g_fwd_res == 16 ? 16 : g_fwd_res == 8 ? 8 : 4;
     const int nqb = (Sq + 16 * nw - 1) / (16 * nw);
     if (nw == 16) hipLaunchKernelGGL(attn_fwd_res_kernel<16>, dim3(nqb * H * B), dim3(1024), 0, stream, a);

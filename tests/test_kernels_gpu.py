@@ -134,10 +134,11 @@ def attn_bwd_impl(request, hip):
     hip.set_attention_bwd_fused(None)
 
 
-@pytest.fixture(params=[(1, 0), (2, 0), (1, 4), (1, 8), (1, 16)], ids=["tiled1", "tiled2", "res4", "res8", "res16"])
+@pytest.fixture(params=[(1, 0), (2, 0), (1, 4), (1, 8), (1, 16), (1, 108), (1, 116)],
+                ids=["tiled1", "tiled2", "res4", "res8", "res16", "pers8", "pers16"])
 def attn_fwd_nsub(request, hip):
     """Forward kernel variant: tiled with 1 / 2 query sub-tiles per wave, or K/V-resident with
-    4 / 8 / 16 waves per block (Sk <= 256; longer keys fall back to the tiled kernel)."""
+    4 / 8 / 16 waves per block, or its persistent double-buffered form (108 / 116: 8 / 16 waves) (Sk <= 256; longer keys fall back to the tiled kernel)."""
     nsub, res = request.param
     hip.set_attention_fwd_nsub(nsub)
     hip.set_attention_fwd_resident(res)
