@@ -44,6 +44,7 @@ struct AttnArgs {
   int Sq, Sk, H;
   float scale, scale_log2;
   int causal, q_offset;
+  int prio_hi_half;  // 8-wave kernels: s_setprio 1 for waves 4-7 (LJS_ATTN_PRIO)
 };
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -228,6 +229,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
   const int qrow = qb * QB + 16 * wave + (lane & 15);
   const bool qok = qrow < a.Sq;
   const bf16_t* qp = a.q + b * a.q_sb + (long)qrow * a.q_ss + h * a.q_sh;
+  if (a.prio_hi_half && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
   bf16x8 qf[2];
   qf[0] = load_row_frag(qp, qok, 0, lane);
   qf[1] = load_row_frag(qp, qok, 1, lane);
@@ -847,6 +849,9 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       dv[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   const int qt = wave & 3, dt0 = 2 * (wave >> 2);
+  // static priority for the second-dispatched half (MI355X_MICROARCH "Two waves per SIMD" item
+  // 4): waves 4-7 lose VALU arbitration to their SIMD partners on every segment otherwise
+  if (a.prio_hi_half && wave >= 4) __builtin_amdgcn_s_setprio(1);
   for (int it = 0; it < nqt; ++it) {
     const int cur = it & 1;
     const int q0 = it * BLK;
@@ -899,6 +904,15 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
 
 }  // namespace
 
+static int attn_prio() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("LJS_ATTN_PRIO");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 // forward sub-tiles per wave: 1 or 2 forces it; 0 = automatic; -1 = read LJS_ATTN_FWD_NSUB
 static int g_fwd_nsub = -1;
 // K/V-resident forward (Sk <= 256): 0 off, 4 / 8 / 16 waves per block; -1 = read LJS_ATTN_FWD_RES
@@ -920,6 +934,7 @@ LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, v
   a.Sq = Sq; a.Sk = Sk; a.H = H;
   a.scale = scale; a.scale_log2 = scale * LOG2E;
   a.causal = causal; a.q_offset = q_offset;
+  a.prio_hi_half = attn_prio();
   // queries per block: as many sub-tiles per wave as keep >= ~2 blocks per CU resident
   if (g_fwd_nsub < 0) {
     const char* e = getenv("LJS_ATTN_FWD_NSUB");
@@ -985,6 +1000,7 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
   a.Sq = Sq; a.Sk = Sk; a.H = H;
   a.scale = scale; a.scale_log2 = scale * LOG2E;
   a.causal = causal; a.q_offset = q_offset;
+  a.prio_hi_half = attn_prio();
   if (g_bwd_fused < 0) {
     const char* e = getenv("LJS_ATTN_BWD_FUSED");
     g_bwd_fused = e ? atoi(e) : 2;
