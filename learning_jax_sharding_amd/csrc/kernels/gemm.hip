@@ -626,6 +626,9 @@ LJS_DMA_INST_LAYOUTS(2)
 LJS_DMA_INST_LAYOUTS(4)
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, false)
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, true)
+// 128x160 with 4 waves stacked along M (32x160 each): N = 640 splits into 4 column tiles, so a
+// [16384, 640] output is exactly 512 items = one round of 2 blocks/CU (128x128: 640 items, 1.25)
+LJS_DMA_INST(128, 160, 4, 1, 2, true, true, false)
 // 128x128 with 8 waves (2 x 4, 64x32 each): two waves per SIMD at one block per CU, so a
 // deep (3-4 stage) ring does not cost MFMA/LDS overlap
 #define LJS_DMA_INST_8W(NST)                                                                                \
@@ -733,14 +736,18 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
                                         (((uintptr_t)C) & 15) == 0);
   if (tile > 1000 && !(dma_ok && dma_store_ok)) tile = 128;
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
+  if (tile == 1602 && !(a_kc && b_kc && !out_f32 && a.splitk == 1)) tile = 1282;
   if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;
   // fused output sum (psum): LDS-DMA kernels with bf16 output only; one float per (item, wave)
   if (psum && !out_f32 && tile > 1000) {
     const int bm = tile == 2561 ? 256 : 128, nw = (tile == 2561 || tile == 12883 || tile == 12884) ? 8 : 4;
+    const int bn = tile == 1602 ? 160 : 128;
     a.psum = (float*)psum;
-    if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + 127) / 128) * batch * a.splitk * nw;
+    if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch * a.splitk * nw;
   }
-  if (tile == 2561) {
+  if (tile == 1602) {
+    e = launch_dma<128, 160, 4, 1, 2, true, true, false>(a, stream, 0);
+  } else if (tile == 2561) {
     if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);
     else e = launch_dma<256, 128, 4, 2, 3, true, true, false>(a, stream, 0);
   } else if (tile == 12883 || tile == 12884) {

@@ -223,9 +223,14 @@ def _psum_for(t: torch.Tensor):
     return partials, count
 
 
-# 256x128 tile for large k-contiguous bf16 GEMMs (off: the 128x128 x 2/CU kernel on a persistent
-# grid measured faster at the bench's QKV projection, 39.9 vs 45.5 us)
-_TILE_2561 = os.environ.get("LJS_GEMM_TILE2561", "0") == "1"
+# 256x128 tile for large k-contiguous bf16 GEMMs: with the DMA pieces issued after each k-step's
+# fragment reads it beats the 128x128 x 2/CU kernel at the QKV projection (37.9 vs 40.4 us) and
+# the FF up-projection (60.7 vs 65.2 us; scripts/gemm_tiles_out.py)
+_TILE_2561 = os.environ.get("LJS_GEMM_TILE2561", "1") == "1"
+
+
+# 128x160 tiles when they (and not 128x128 tiles) fill whole rounds of 512 resident blocks
+_TILE_1602 = os.environ.get("LJS_GEMM_TILE1602", "1") == "1"
 
 
 def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f32: bool, splitk: int = 1,
@@ -234,6 +239,9 @@ def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f3
     the LDS-DMA kernels (codes 2561 = 256x128 8 waves, 1282 = 128x128 4 waves x 2 blocks/CU)
     whenever K is a multiple of 64, else the register-staged 128/64 tiles."""
     tiles128 = -(-M // 128) * -(-N // 128) * batch * max(1, splitk)
+    if (_TILE_1602 and K % 64 == 0 and a_kc and b_kc and not out_f32 and splitk <= 1 and N % 160 == 0
+            and ldc % 8 == 0 and tiles128 % 512 and (-(-M // 128) * (N // 160) * batch) % 512 == 0):
+        return 1602
     if K % 64 == 0 and tiles128 >= 96 and (out_f32 or (N % 8 == 0 and ldc % 8 == 0)):
         if _TILE_2561 and a_kc and b_kc and not out_f32 and M >= 4096 and N * batch >= 1024 and N % 128 == 0:
             return 2561
