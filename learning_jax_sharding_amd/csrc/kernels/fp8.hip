@@ -202,7 +202,6 @@ __global__ __launch_bounds__(256) void gemm_mx_fp8_kernel(F8Args p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
     const unsigned char* As_ = smem + (kt & 1) * F8_STAGE;
     const unsigned char* Bs_ = As_ + F8_TILE;
     const unsigned* Sa = reinterpret_cast<const unsigned*>(As_ + 2 * F8_TILE);
@@ -225,6 +224,9 @@ __global__ __launch_bounds__(256) void gemm_mx_fp8_kernel(F8Args p) {
       bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
       sb[j] = (int)((Sb[row] >> (8 * g)) & 0xff);
     }
+    // next stage's DMA after this K-tile's fragment reads: its issue time overlaps their LDS
+    // latency and the MFMAs (as in the bf16 LDS-DMA GEMM)
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
