@@ -41,9 +41,10 @@ def parse():
                    help="dp: (N,1) data x model; 2d: (N/2, 2); or explicit 'DxM'")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--mode", default="train", choices=["train", "fwd"])
-    p.add_argument("--model", default="attention", choices=["attention", "layer"],
+    p.add_argument("--model", default="attention", choices=["attention", "layer", "ff", "fsdp"],
                    help="attention: the case6 block (headline); layer: attention + FF transformer layer")
     p.add_argument("--ff-dim", type=int, default=2560)
+    p.add_argument("--layers", type=int, default=4, help="fsdp: number of dim x dim Dense layers")
     p.add_argument("--fp8", action="store_true", help="layer: MX-fp8 FF GEMMs (CDNA4 block-scaled MFMA)")
     return p.parse_args()
 
@@ -59,8 +60,10 @@ def main():
     import learning_jax_sharding_amd as ljs
     from learning_jax_sharding_amd import nn, optim
     from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
-    from learning_jax_sharding_amd.models import (MultiHeadAttention, TransformerLayer, attention_block_flops,
+    from learning_jax_sharding_amd.models import (DenseStack, MultiHeadAttention, TransformerLayer,
+                                                  attention_block_flops, dense_stack_flops, feed_forward_flops,
                                                   transformer_layer_flops)
+    from learning_jax_sharding_amd.parallel import fsdp
     from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
     from learning_jax_sharding_amd.training import TrainState
 
@@ -78,6 +81,10 @@ def main():
     S, M = args.seq, args.dim
     if args.model == "layer":
         model = TransformerLayer(M, heads=args.heads, dim_head=args.dim_head, ff_dim=args.ff_dim, fp8=args.fp8)
+    elif args.model == "ff":
+        model = nn.FeedForward(args.ff_dim, fp8=args.fp8)
+    elif args.model == "fsdp":
+        model = DenseStack(M, layers=args.layers)
     else:
         model = MultiHeadAttention(M, heads=args.heads, dim_head=args.dim_head)
     x_sharding = NamedSharding(mesh, P("data", "model"))
@@ -88,7 +95,11 @@ def main():
         return TrainState.create(apply_fn=model.apply, params=params, tx=optim.adam(1e-3))
 
     abstract = ljs.eval_shape(init_fn, ljs.random.PRNGKey(1), x)
-    state_sharding = nn.logical_to_mesh_sharding(nn.get_partition_spec(abstract), mesh, rules)
+    if args.model == "fsdp":
+        # case3 at scale: every parameter (and its Adam moments) sharded over 'data'
+        state_sharding = fsdp.fsdp_shardings(abstract, mesh, "data")
+    else:
+        state_sharding = nn.logical_to_mesh_sharding(nn.get_partition_spec(abstract), mesh, rules)
     state = ljs.jit(init_fn, out_shardings=state_sharding)(ljs.random.PRNGKey(1), x)
 
     def train_step(state, x):
@@ -150,7 +161,11 @@ def main():
         caps = list(step._graphs.values())
         if caps:
             segs = sum(1 for it in caps[-1].graph.items if it[0] == "graph")
-    if args.model == "layer":
+    if args.model == "ff":
+        flops = feed_forward_flops(B, S, M, args.ff_dim, train=args.mode == "train")
+    elif args.model == "fsdp":
+        flops = dense_stack_flops(B, S, M, args.layers, train=args.mode == "train")
+    elif args.model == "layer":
         flops = transformer_layer_flops(B, S, M, args.heads, args.dim_head, args.ff_dim, train=args.mode == "train")
     else:
         flops = attention_block_flops(B, S, M, args.heads, args.dim_head, train=args.mode == "train")
@@ -159,8 +174,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     if rank == 0:
         par = f"dp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
+        if args.model == "fsdp":
+            par = f"fsdp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
+        gemm = "MX-fp8" if args.fp8 else "bf16"
+        model_desc = {
+            "attention": f"case6 attention block (M={M}, heads={args.heads}x{args.dim_head}, bf16 compute, "
+                         f"f32 params, Adam)",
+            "layer": f"attention+FF transformer layer (M={M}, heads={args.heads}x{args.dim_head}, "
+                     f"ff={args.ff_dim}, FF GEMMs {gemm}, f32 params, Adam)",
+            "ff": f"case4 GSPMD feed-forward relu(x Win) Wout (M={M}, ff={args.ff_dim}, {gemm} GEMMs, "
+                  f"f32 params, Adam)",
+            "fsdp": f"case3 fully-sharded matmul chain ({args.layers} x Dense {M}x{M}, relu, bf16 compute, "
+                    f"f32 params FSDP-sharded over data, Adam)",
+        }[args.model]
         rec = {
-            "metric": METRIC,
+            "metric": METRIC if args.model == "attention" else f"step-time ms + TFLOPS/GPU, {args.model} train step",
             "value": round(tflops_total, 3),
             "unit": "TFLOPS (whole job, matmul FLOPs of fwd+bwd)",
             "n_gpus": n,
@@ -175,10 +203,7 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (random normal x, random-init weights)",
-            "config": {"model": (f"case6 attention block (M={M}, heads={args.heads}x{args.dim_head}, "
-                                 f"bf16 compute, f32 params, Adam)") if args.model == "attention" else
-                                (f"attention+FF transformer layer (M={M}, heads={args.heads}x{args.dim_head}, "
-                                 f"ff={args.ff_dim}, FF GEMMs {'MX-fp8' if args.fp8 else 'bf16'}, f32 params, Adam)"),
+            "config": {"model": model_desc,
                        "global_batch": B, "seq_len": S, "parallelism": par, "mode": args.mode,
                        "hip_graph": capture, "graph_segments": segs},
         }

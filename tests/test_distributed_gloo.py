@@ -154,3 +154,53 @@ def test_dist_train_overlapped_reducer(host_devices, wire):
             assert abs(l - lref) <= 1e-2 * max(1, abs(lref)), (shape, l, lref)
             for k in pref:
                 np.testing.assert_allclose(p[k], pref[k], **tol)
+
+
+def job_train_fsdp(ljs):
+    """case3 at scale (bench.py --model fsdp): every weight and Adam moment sharded over
+    'data'; the partitioner gathers weights at use and reduce-scatters their gradients."""
+    from learning_jax_sharding_amd import nn, optim
+    from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
+    from learning_jax_sharding_amd.models import DenseStack
+    from learning_jax_sharding_amd.parallel import fsdp
+    from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
+    from learning_jax_sharding_amd.spmd import plan as _plan
+    from learning_jax_sharding_amd.training import TrainState
+    mesh = Mesh(create_device_mesh((2, 1)), ("data", "model"))
+    model = DenseStack(64, layers=3, dtype=torch.float32)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (4, 16, 64))
+
+    def init_fn(k, x):
+        return TrainState.create(apply_fn=model.apply, params=model.init(k, x)["params"], tx=optim.adam(1e-3))
+
+    abstract = ljs.eval_shape(init_fn, ljs.random.PRNGKey(1), x)
+    shard = fsdp.fsdp_shardings(abstract, mesh, "data")
+    state = ljs.jit(init_fn, out_shardings=shard)(ljs.random.PRNGKey(1), x)
+    x = ljs.device_put(x, NamedSharding(mesh, P("data")))
+
+    def step(state, x):
+        def loss(p):
+            return model.apply({"params": p}, x).sum()
+        l, g = ljs.value_and_grad(loss)(state.params)
+        return state.apply_gradients(grads=g), l
+
+    with mesh, _plan.record_plan() as rec:
+        for _ in range(2):
+            state, l = step(state, x)
+    ker = {k: v["kernel"] for k, v in state.params.items()}
+    return (float(np.asarray(l)), {k: np.asarray(v) for k, v in ker.items()},
+            {k: tuple(v.tile.tile_shape) for k, v in ker.items()}, rec.collective_kinds())
+
+
+def test_dist_train_fsdp(host_devices):
+    r0, r1 = _run("job_train_fsdp")
+    host_devices(2)
+    import learning_jax_sharding_amd as ljs
+    lref, pref, tiles, kinds = job_train_fsdp(ljs)
+    print(kinds)
+    assert any("gather" in k for k in kinds) and any("reduce_scatter" in k for k in kinds), kinds
+    for l, p, t, _ in (r0, r1):
+        assert abs(l - lref) <= 1e-3 * max(1, abs(lref)), (l, lref)
+        assert all(2 in ts for ts in t.values()), t  # weights stay sharded over 'data'
+        for k in pref:
+            np.testing.assert_allclose(p[k], pref[k], rtol=1e-4, atol=1e-5)
