@@ -812,6 +812,35 @@ LJS_API int ljs_relu_bwd_colsum(const void* in, const void* mask, int R, int C, 
   return (int)hipGetLastError();
 }
 
+// masked_out[R][C] = in * (mask > 0) without column sums (the ReLU backward of a bias-free dense):
+// a flat grid over 8-element vectors fills the chip, where the column-sum kernel is limited to
+// ~512 workgroups by its per-column-block reduction.  Same layout requirements as above.
+__global__ void __launch_bounds__(256) relu_bwd_kernel(const bf16_t* __restrict__ in, const bf16_t* __restrict__ mask,
+                                                       int C8, long n8, long ld, long mld,
+                                                       bf16_t* __restrict__ masked_out) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const long r = i / C8;
+    const int c = (int)(i - r * C8) * 8;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(in + r * ld + c);
+    const u32x4 m = *reinterpret_cast<const u32x4*>(mask + r * mld + c);
+    *reinterpret_cast<u32x4*>(masked_out + i * 8) = relu_mask_bf16x8(v, m);
+  }
+}
+
+LJS_API int ljs_relu_bwd(const void* in, const void* mask, int R, int C, long ld, long mld, void* masked_out,
+                         hipStream_t s) {
+  if (C % 8 || ld % 8 || mld % 8 || (((uintptr_t)in) & 15) || (((uintptr_t)mask) & 15) || (((uintptr_t)masked_out) & 15))
+    return (int)hipErrorInvalidValue;
+  const long n8 = (long)R * (C / 8);
+  long grid = (n8 + 255) / 256;
+  if (grid > 8192) grid = 8192;  // 32 workgroups per CU, then grid-stride
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)in, (const bf16_t*)mask,
+                     C / 8, n8, ld, mld, (bf16_t*)masked_out);
+  return (int)hipGetLastError();
+}
+
 LJS_API int ljs_fill_row_bf16(const void* g, int g_bf16, void* out, long n, hipStream_t s) {
   int grid = grid_for(n, 256);
   if (grid > 1024) grid = 1024;

@@ -46,6 +46,7 @@ _SIGS = {
     "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_fill_row_bf16": [c_void_p, c_int, c_void_p, c_long, c_void_p],
     "ljs_relu_bwd_colsum": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p],
+    "ljs_relu_bwd": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p, c_void_p],
     "ljs_bcast_scalar": [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
@@ -598,6 +599,15 @@ def relu_bwd_colsum(dy: torch.Tensor, y: torch.Tensor, R: int, C: int):
                                    _stream(dy))
     _ck(rc, "relu_bwd_colsum")
     return masked, out
+
+
+def relu_bwd(dy: torch.Tensor, y: torch.Tensor, R: int, C: int) -> torch.Tensor:
+    """dy * (y > 0) as a new bf16 [R][C] (the ReLU backward of a bias-free dense; same view
+    requirements as :func:`relu_bwd_colsum`)."""
+    masked = torch.empty((R, C), dtype=torch.bfloat16, device=dy.device)
+    rc = lib().ljs_relu_bwd(_p(dy), _p(y), R, C, dy.stride(0), y.stride(0), _p(masked), _stream(dy))
+    _ck(rc, "relu_bwd")
+    return masked
 
 
 def colsum_ld(t: torch.Tensor, R: int, C: int, ld: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:

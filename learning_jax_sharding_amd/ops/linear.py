@@ -154,7 +154,10 @@ class _Linear(torch.autograd.Function):
                         and y2.stride(0) % 8 == 0 and d2.data_ptr() % 16 == 0 and y2.data_ptr() % 16 == 0):
                     # fused ReLU backward: the masked gradient and its column sums (the bias
                     # gradient) in one pass over dy and y
-                    masked, db_bcast[i] = hip.relu_bwd_colsum(d2, y2, M, N)
+                    if want_db:
+                        masked, db_bcast[i] = hip.relu_bwd_colsum(d2, y2, M, N)
+                    else:  # no bias gradient wanted: a flat full-chip pass, no column sums
+                        masked = hip.relu_bwd(d2, y2, M, N)
                     mats.append((masked, N))
                     continue
                 dy = (dy * (ys[i] > 0)).reshape(M, N)

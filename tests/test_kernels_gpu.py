@@ -393,6 +393,8 @@ def test_relu_bwd_colsum(hip, R, C, yld):
     ref = dy.float() * (y.float() > 0).float()
     torch.testing.assert_close(masked.float(), ref, rtol=0, atol=0)
     torch.testing.assert_close(db, ref.sum(0), rtol=1e-4, atol=1e-2)
+    # the bias-free form (flat full-chip grid, no column sums) gives the same masked gradient
+    torch.testing.assert_close(hip.relu_bwd(dy, y, R, C).float(), ref, rtol=0, atol=0)
 
 
 def test_ticket_reductions_rearm(hip):
