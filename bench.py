@@ -5,12 +5,28 @@ MI355X".  The model is the reference's FlaxAttention (``case6_attention.py:42-14
 M=640, 8 heads x 64, bf16 compute, f32 params, Adam lr 1e-3) with the reference's
 logical-axis rules; S=256 as in the reference.  Data is synthetic (random normal inputs,
 random-init weights).  Work per GPU is fixed as N grows (weak scaling): the global batch is
-``--batch-per-gpu x N`` sequences.
+``--batch-per-gpu x N`` sequences, and every mesh layout gives each GPU ``batch-per-gpu x S``
+tokens.
 
-Single GPU: ``python bench.py``.  N GPUs: ``torchrun --nproc-per-node N bench.py --gpus N``
-(one process per GPU, RCCL over xGMI).  The step is a jitted, donated, HIP-graph-captured
-function; the timed region is K full steps bracketed by barrier + device synchronize, and
-the reported time is the max over ranks.  Rank 0 prints one JSON line.
+Launch:
+* ``python bench.py`` - one GPU.
+* ``python bench.py --gpus N`` - spawns N rank processes (``torch.distributed.run``, one per
+  GPU, RCCL over xGMI) BEFORE anything touches the GPU and exits with their status; fails if
+  fewer than N GPUs are visible.  Under ``torchrun --nproc-per-node N bench.py --gpus N`` (the
+  driver's launch) the ranks run directly; ``WORLD_SIZE`` must equal ``--gpus``.
+* ``LJS_PLATFORM=cpu python bench.py --gpus N`` - the same N-rank job on gloo host ranks (CPU
+  rehearsal of the multi-GPU code path; tests/test_bench_cpu.py).
+
+``--mesh dp`` (default, (N,1)) or ``--mesh 2d`` ((N/2, 2): the reference's DP x TP layout,
+``case6_attention.py:155-161,183-187``) or ``--mesh DxM``.  DP is the default because on
+point-to-point xGMI the reference's TP layout (sequence over ``model``) moves activation-sized
+K/V/head gathers and an all-to-all every step (~150 MB/GPU at 64x256 tokens), while DP moves
+one 5 MB gradient all-reduce.
+
+The step is a jitted, donated, HIP-graph-captured function; the timed region is K full steps
+bracketed by barrier + device synchronize, and the reported time is the max over ranks.
+Rank 0 prints one JSON line; ``value`` is the whole-job TFLOPS (summed over the N GPUs, the
+driver's aggregate convention) and ``tflops_per_gpu`` the per-GPU rate the metric names.
 """
 from __future__ import annotations
 
@@ -29,7 +45,8 @@ METRIC = "step-time ms + TFLOPS/GPU, case6 sharded attention block at 1/2/4/8 MI
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (= ranks); default: WORLD_SIZE under torchrun, else 1")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("LJS_BENCH_BPG", "64")))
@@ -45,15 +62,45 @@ def parse():
                    help="attention: the case6 block (headline); layer: attention + FF transformer layer")
     p.add_argument("--ff-dim", type=int, default=2560)
     p.add_argument("--layers", type=int, default=4, help="fsdp: number of dim x dim Dense layers")
-    p.add_argument("--fp8", action="store_true", help="layer: MX-fp8 FF GEMMs (CDNA4 block-scaled MFMA)")
+    p.add_argument("--fp8", action="store_true", help="layer / ff: MX-fp8 FF GEMMs (CDNA4 block-scaled MFMA)")
     return p.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _launch_ranks(n: int) -> int:
+    """Run this benchmark as n rank processes (one per GPU) and return their exit status.
+    Called before anything initialises the GPU (device_count() does not, on ROCm torch)."""
+    import subprocess
+    import torch
+    platform = os.environ.get("LJS_PLATFORM", "").lower()
+    if platform != "cpu" and not os.environ.get("LJS_DIST_BACKEND"):
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is None:
+        args.gpus = world
+    if world == 1 and args.gpus > 1:
+        sys.exit(_launch_ranks(args.gpus))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         os.environ.setdefault("LJS_PLATFORM", "gpu")
+        os.environ.pop("LJS_NUM_DEVICES", None)
     else:
         os.environ.setdefault("LJS_NUM_DEVICES", "1")
     import torch
@@ -68,6 +115,12 @@ def main():
     from learning_jax_sharding_amd.training import TrainState
 
     n = ljs.device_count()
+    if world > 1:
+        import torch.distributed as _dist
+        assert _dist.is_initialized() and _dist.get_world_size() == world, "process group not initialised"
+        assert n == world and ljs.local_device_count() == 1, (n, world)
+    if args.model == "fsdp" and args.mesh not in ("dp",) and not args.mesh.endswith("x1"):
+        raise SystemExit("bench.py: --model fsdp shards weights over 'data' only; use --mesh dp or Nx1")
     if args.mesh == "dp":
         mshape = (n, 1)
     elif args.mesh == "2d":
@@ -172,6 +225,13 @@ def main():
     tflops_total = flops / (ms * 1e-3) / 1e12
     tokens_per_s = B * S / (ms * 1e-3)
     rank = int(os.environ.get("RANK", "0"))
+    # physical GPUs doing the work: one per rank, or the one GPU under N virtual devices
+    n_gpus = world if world > 1 else (1 if cuda else 0)
+    comm = "none"
+    if dist_on:
+        from learning_jax_sharding_amd.comm.backend import get_comm
+        c = get_comm()
+        comm = dist.get_backend() + ("+native-rccl" if getattr(c, "_native", None) is not None else "")
     if rank == 0:
         par = f"dp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
         if args.model == "fsdp":
@@ -190,22 +250,24 @@ def main():
         rec = {
             "metric": METRIC if args.model == "attention" else f"step-time ms + TFLOPS/GPU, {args.model} train step",
             "value": round(tflops_total, 3),
-            "unit": "TFLOPS (whole job, matmul FLOPs of fwd+bwd)",
-            "n_gpus": n,
+            "unit": "TFLOPS summed over all GPUs (matmul FLOPs of fwd+bwd); per GPU: tflops_per_gpu",
+            "n_gpus": n_gpus if cuda else n,
+            "n_devices": n,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
-            "tflops_per_gpu": round(tflops_total / n, 3),
+            "tflops_per_gpu": round(tflops_total / max(1, n_gpus if cuda else n), 3),
             "tokens_per_s": round(tokens_per_s, 1),
             "host_ms_per_step": round((th - t0) / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": ("bf16+mx-fp8" if args.model == "layer" else "mx-fp8") if args.fp8 else "bf16",
             "data": "synthetic (random normal x, random-init weights)",
             "config": {"model": model_desc,
                        "global_batch": B, "seq_len": S, "parallelism": par, "mode": args.mode,
-                       "hip_graph": capture, "graph_segments": segs},
+                       "hip_graph": capture, "graph_segments": segs, "mesh": list(mshape),
+                       "comm": comm, "grad_wire": os.environ.get("LJS_GRAD_COMM_DTYPE", "fp32")},
         }
         print(json.dumps(rec), flush=True)
     if dist_on:

@@ -146,6 +146,11 @@ rules = (
   ('embed', 'model'),
   ('hidden', 'model'),
 )
+# LJS_RULES=gspmd2d runs the "2D finalized" layout of the comment above (embed->data,
+# heads->model: Wq_0 is (320, 256)); megatron / fsdp are the other presets
+if os.environ.get("LJS_RULES"):
+  from learning_jax_sharding_amd import parallel
+  rules = parallel.rules(os.environ["LJS_RULES"])
 
 logical_abstract_variables = jax.eval_shape(functools.partial(init_fn, model=attention, optimizer=optimizer), init_rngs, x)
 logical_state_spec = nn.get_partition_spec(logical_abstract_variables)
@@ -178,9 +183,9 @@ def train_step(state, x):
 with mesh, nn_partitioning.axis_rules(rules):
   new_state = train_step(initialized_state, x)
 
-# With these rules x[0] is (4, 128, 640) and Wq[0] is (320, 512): 'heads' has no rule, so the
-# projection's output dim stays replicated (the comment in the reference expects (320, 256),
-# which is the GSPMD-paper 2D layout - embed->data, heads->model - available as rules="gspmd2d").
+# With the reference rules x[0] is (4, 128, 640) and Wq[0] is (320, 512): 'heads' has no rule,
+# so the projection's output dim stays replicated.  The reference's comment expects (320, 256):
+# that is the GSPMD-paper 2D layout (embed->data, heads->model), LJS_RULES=gspmd2d.
 
 @functools.partial(jax.jit, in_shardings=(logical_state_sharding, x_sharding),
                    out_shardings=x_sharding)

@@ -54,7 +54,37 @@ class _Spec:
         self.reorder = reorder
 
 
+def _group_size(spec: _Spec, d: int) -> int:
+    return next(len(g) for g in spec.groups if d in g)
+
+
+def _run_meta(spec: _Spec, xs: Dict[int, torch.Tensor]) -> Dict[int, torch.Tensor]:
+    """Abstract evaluation (``eval_shape`` on meta tensors): output shapes only, no traffic -
+    a process-group backend cannot run collectives on meta tensors, and must not try."""
+    k = spec.kind
+    out = {}
+    if k == "exchange":
+        from ..runtime.devices import local_devices
+        mine = {dv.id for dv in local_devices()}
+        return {d: torch.empty(shape, dtype=dt, device="meta") for d, (shape, dt, _) in spec.out_meta.items()
+                if d in mine or d in xs}
+    for d, x in xs.items():
+        shp = list(x.shape)
+        n = _group_size(spec, d)
+        if k == "all_gather":
+            shp[spec.dim] *= n
+        elif k == "reduce_scatter":
+            shp[spec.dim] //= n
+        elif k == "all_to_all":
+            shp[spec.split_dim] //= n
+            shp[spec.concat_dim] *= n
+        out[d] = torch.empty(shp, dtype=x.dtype, device="meta")
+    return out
+
+
 def _run(spec: _Spec, xs: Dict[int, torch.Tensor]) -> Dict[int, torch.Tensor]:
+    if any(t.device.type == "meta" for t in xs.values()):
+        return _run_meta(spec, xs)
     comm = get_comm()
     out = None
     if comm.kind == "dist" and any(t.is_cuda for t in xs.values()):

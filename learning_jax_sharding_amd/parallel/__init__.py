@@ -3,7 +3,7 @@
 * :mod:`.data` - data parallelism: bucketed, backward-overlapped gradient all-reduce;
 * :mod:`.fsdp` - fully-sharded data parallelism: FSDP shardings, side-stream prefetched
   parameter all-gathers (their transposes are the overlapped gradient reduce-scatters);
-* :mod:`.tensor` - tensor parallelism: rule presets (reference, FSDP, Megatron "gspmd2d")
+* :mod:`.tensor` - tensor parallelism: rule presets (reference, FSDP, GSPMD "2D finalized", Megatron)
   and explicit column/row-parallel dense layers;
 * :mod:`.sequence` - sequence / context parallelism: all-gather-KV and ring attention.
 

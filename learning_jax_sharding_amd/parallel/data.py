@@ -13,12 +13,11 @@ this module sums them over each tile's replica group:
 * **buckets** are filled in the order producer groups complete (autograd tensor hooks) and
   launched as soon as one holds ``bucket_bytes`` (default 1 MiB): the output projection's
   gradients leave while the attention backward and the QKV weight-gradient GEMM still run;
-* **wire dtype**: gradients of bf16-computed layers travel as **bf16** (``LJS_GRAD_COMM_DTYPE``,
-  default ``bf16``; ``fp32`` keeps them f32).  This is the reference's own semantics: under
-  ``dtype=bfloat16`` the weight-gradient ``dot_general`` produces bf16 partial sums and the
-  all-reduce GSPMD inserts for the batch-sharded contraction runs on them, before the convert
-  to the f32 parameter dtype [JAX-internal, SURVEY §2.7 case-6 bwd].  Half the bytes on
-  point-to-point xGMI rings, where the gradient tail is exposed;
+* **wire dtype**: gradients travel in the parameter dtype (**f32**) by default, so a
+  data-parallel step sums exactly what a single device would.  ``LJS_GRAD_COMM_DTYPE=bf16``
+  is the opt-in half-bytes wire: the weight-gradient producers then also write a bf16 "twin"
+  that the bucket sends (no cast kernel) - half the bytes on point-to-point xGMI rings where
+  the gradient tail is exposed, at bf16 rounding of each rank's partial sum;
 * each bucket's all-reduce runs on a side comm stream (RCCL over xGMI), joined only before
   the optimizer consumes the gradients.  Under ``jit(capture=True)`` a native-RCCL all-reduce
   is captured INTO the step's HIP graph (forked onto the side stream inside the capture), so
@@ -78,7 +77,7 @@ def default_bucket_bytes() -> int:
 
 def comm_dtype() -> Optional[torch.dtype]:
     """Wire dtype of f32 gradient buckets (None = as computed)."""
-    v = os.environ.get("LJS_GRAD_COMM_DTYPE", "bf16").lower()
+    v = os.environ.get("LJS_GRAD_COMM_DTYPE", "fp32").lower()
     if v in ("bf16", "bfloat16"):
         return torch.bfloat16
     if v in ("fp32", "f32", "float32", "none", ""):

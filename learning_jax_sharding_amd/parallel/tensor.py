@@ -7,10 +7,17 @@ The reference's "model" axis shards the attention weights on their *contraction*
 gathers the weights before the QKV projections and all-to-alls the out-projection
 (SURVEY §2.7).  That plan is reproduced by the partitioner from ``REFERENCE_RULES``.
 
-``MEGATRON_RULES`` (preset ``"gspmd2d"``) instead shards heads and the FF hidden dim over
-``model`` (column-parallel QKV / W_in, row-parallel W_out / W_o, one all-reduce per block
-in forward and one in backward) - on 8 xGMI-connected MI355X this moves far fewer bytes
-per step than gathering weights and sequence, so it is the preferred TP layout there.
+``GSPMD2D_RULES`` (preset ``"gspmd2d"``) is the GSPMD paper's "2D finalized" attention layout
+the reference's comment names (``case6_attention.py:53-55``: "MND ... Shardings: X,Y,_"):
+``embed -> data``, ``heads -> model``, so Wq/Wk/Wv are split over BOTH mesh axes - (320, 256)
+per device on the 2x2 mesh, the shape the stale comment at ``case6_attention.py:222-227``
+expects.
+
+``MEGATRON_RULES`` (preset ``"megatron"``) shards heads and the FF hidden dim over ``model``
+and keeps ``embed`` replicated (column-parallel QKV / W_in, row-parallel W_out / W_o, one
+all-reduce per block in forward and one in backward) - on 8 xGMI-connected MI355X this
+moves far fewer bytes per step than gathering weights and sequence, so it is the preferred
+TP layout there.
 
 :func:`column_parallel` / :func:`row_parallel` are the explicit Megatron building blocks on
 global-view arrays: they pin the shardings, and the partitioner lowers the matmul with
@@ -25,7 +32,7 @@ from ..mesh import Mesh, current_mesh
 from ..ops import core
 from ..sharding import NamedSharding, PartitionSpec as P
 
-__all__ = ["REFERENCE_RULES", "FSDP_RULES", "MEGATRON_RULES", "DP_RULES", "PRESETS", "rules", "column_parallel",
+__all__ = ["REFERENCE_RULES", "FSDP_RULES", "GSPMD2D_RULES", "MEGATRON_RULES", "DP_RULES", "PRESETS", "rules", "column_parallel",
            "row_parallel"]
 
 Rules = Tuple[Tuple[str, Optional[str]], ...]
@@ -34,6 +41,8 @@ Rules = Tuple[Tuple[str, Optional[str]], ...]
 REFERENCE_RULES: Rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
 # case5_attention_dense.py:109-112: embed on data (FSDP-style weight sharding)
 FSDP_RULES: Rules = (("batch", "data"), ("embed", "data"), ("kv", None), ("hidden", "model"))
+# GSPMD paper "2D finalized" (case6_attention.py:53-55): weights split over data AND model
+GSPMD2D_RULES: Rules = (("batch", "data"), ("embed", "data"), ("heads", "model"), ("hidden", "model"))
 # heads / FF hidden over model, batch over data, embed replicated
 MEGATRON_RULES: Rules = (("batch", "data"), ("heads", "model"), ("hidden", "model"), ("embed", None),
                          ("kv", None), ("length", None))
@@ -41,7 +50,7 @@ MEGATRON_RULES: Rules = (("batch", "data"), ("heads", "model"), ("hidden", "mode
 DP_RULES: Rules = (("batch", "data"),)
 
 PRESETS = {"reference": REFERENCE_RULES, "case6": REFERENCE_RULES, "fsdp": FSDP_RULES, "case5": FSDP_RULES,
-           "gspmd2d": MEGATRON_RULES, "megatron": MEGATRON_RULES, "dp": DP_RULES}
+           "gspmd2d": GSPMD2D_RULES, "megatron": MEGATRON_RULES, "dp": DP_RULES}
 
 
 def rules(name: str) -> Rules:

@@ -15,9 +15,12 @@ def load(path):
     rows = collections.defaultdict(list)
     if path.endswith(".db"):
         c = sqlite3.connect(path)
-        for name, dur, gx, wx, vgpr, agpr, lds in c.execute(
-                "select name, duration, grid_x, workgroup_x, vgpr_count, accum_vgpr_count, lds_size from kernels"):
-            rows[name].append((dur / 1e3, gx // max(1, wx), vgpr, agpr, lds))
+        # workgroups = product over x/y/z of grid / workgroup extents (grid is in work-items)
+        for name, dur, gx, gy, gz, wx, wy, wz, vgpr, agpr, lds in c.execute(
+                "select name, duration, grid_x, grid_y, grid_z, workgroup_x, workgroup_y, workgroup_z, "
+                "vgpr_count, accum_vgpr_count, lds_size from kernels"):
+            wgs = (gx // max(1, wx)) * (max(1, gy) // max(1, wy)) * (max(1, gz) // max(1, wz))
+            rows[name].append((dur / 1e3, wgs, vgpr, agpr, lds))
     else:
         for r in csv.DictReader(open(path)):
             rows[r["Name"]].append((float(r["AverageNs"]) / 1e3, 0, 0, 0, 0))

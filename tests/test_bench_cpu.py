@@ -28,3 +28,42 @@ def test_bench_json_contract(model):
     assert rec["value"] >= 0 and rec["ms_per_step"] > 0  # value is rounded: ~0 TFLOPS on host
     assert rec["config"]["global_batch"] == 2 and rec["config"]["seq_len"] == 32
     assert rec["config"]["parallelism"] == ("fsdp1" if model == "fsdp" else "dp1")
+
+
+@pytest.mark.parametrize("gpus,mesh,par", [(4, "dp", "dp4"), (4, "2d", "dp2xtp2"), (8, "dp", "dp8"),
+                                           (8, "2d", "dp4xtp2")])
+def test_bench_spawns_ranks(gpus, mesh, par):
+    """`bench.py --gpus N` outside torchrun launches N rank processes (gloo host ranks here,
+    RCCL on GPUs) and reports the N-rank job - it never silently runs one device."""
+    env = dict(os.environ, LJS_PLATFORM="cpu")
+    env.pop("LJS_NUM_DEVICES", None)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--mesh", mesh, *TINY],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == gpus and rec["n_devices"] == gpus
+    assert rec["config"]["parallelism"] == par
+    assert rec["config"]["global_batch"] == 2 * gpus  # weak scaling: batch-per-gpu x N
+    assert rec["config"]["comm"].startswith("gloo")
+    assert rec["dtype"] == "bf16"
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, LJS_PLATFORM="cpu", WORLD_SIZE="2", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", *TINY],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
+
+
+def test_bench_fp8_dtype_label():
+    env = dict(os.environ, LJS_NUM_DEVICES="1", LJS_PLATFORM="cpu")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "ff", "--fp8", *TINY],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    if r.returncode != 0 and "fp8" in r.stderr.lower() and "gpu" in r.stderr.lower():
+        pytest.skip("MX-fp8 path needs the GPU")
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["dtype"] == "mx-fp8"

@@ -84,3 +84,22 @@ def test_case6(impl):
     assert any(l.startswith("time for 10 itters:") for l in out)
     # trace-time prints happen once per jit signature (eval_shape, init, train, apply)
     assert sum(1 for l in out if l.startswith("context.shape")) == 4
+
+
+def test_case6_gspmd2d_rules():
+    """The GSPMD-paper "2D finalized" preset gives the (320, 256) Wq shard the reference's
+    comment expects (case6_attention.py:53-55,222-227)."""
+    out = lines(run_case("case6_attention.py", {"LJS_RULES": "gspmd2d"}))
+    assert "Wq shape:  (640, 512)" in out
+    assert "Wq_0 shape:  (320, 256)" in out
+    assert "x[0] shape:  (4, 128, 640)" in out
+
+
+def test_case1a_single_device():
+    """BASELINE config 1: case1a's replicated matmul on a 1-device CPU mesh, no collectives."""
+    out = lines(run_case("case1a_single_device.py"))
+    for exp in ["A_0.shape:  (4, 16)", "Is A_0 equal to A?  True", "B_0.shape:  (16, 4)",
+                "Are A and B the same numbers?  True", "collectives:  []", "C_0.shape:  (4, 4)",
+                "Number of buffers:  1", "Are C_0 and C equal?  True", "Is C == A @ B?  True"]:
+        assert exp in out, exp
+    assert "CPU 0" in " ".join(out)

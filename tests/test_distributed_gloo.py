@@ -14,6 +14,7 @@ def _worker(rank, world, port, out_dir, job):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "LJS_PLATFORM": "cpu"})
     os.environ.pop("LJS_NUM_DEVICES", None)
+    torch.set_num_threads(1)
     import learning_jax_sharding_amd as ljs
     from learning_jax_sharding_amd.runtime.devices import reset_backend
     reset_backend()
@@ -46,18 +47,18 @@ def job_collectives(ljs):
     return out
 
 
-def job_train(ljs):
+def job_train(ljs, shapes=((2, 1), (1, 2)), batch=4, seq=32, dtype=torch.bfloat16):
     from learning_jax_sharding_amd import nn, optim
     from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
     from learning_jax_sharding_amd.models import MultiHeadAttention
     from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
     from learning_jax_sharding_amd.training import TrainState
     res = {}
-    for shape in [(2, 1), (1, 2)]:
+    for shape in shapes:
         mesh = Mesh(create_device_mesh(shape), ("data", "model"))
         rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
-        model = MultiHeadAttention(64, heads=4, dim_head=16)
-        x = ljs.random.normal(ljs.random.PRNGKey(0), (4, 32, 64))
+        model = MultiHeadAttention(64, heads=4, dim_head=16, dtype=dtype)
+        x = ljs.random.normal(ljs.random.PRNGKey(0), (batch, seq, 64))
         params = model.init(ljs.random.PRNGKey(1), x)["params"]
         params = ljs.device_put(params, nn.logical_to_mesh_sharding(nn.get_partition_spec(params), mesh, rules))
         x = ljs.device_put(x, NamedSharding(mesh, P("data", "model")))
@@ -76,6 +77,25 @@ def job_train(ljs):
                            {k: np.asarray(v["kernel"].value if hasattr(v["kernel"], "value") else v["kernel"])
                             for k, v in state.params.items()})
     return res
+
+
+# the reference's meshes: 2x2 (case5/6, 4 devices) and 2x4 (cases 1-4, 8 devices), plus the
+# transposed / 1-D layouts, so every mesh axis has several groups and cross-process
+# all-to-all, exchange (batch_isend_irecv) and per-axis sub-groups all run
+MESHES = {4: ((2, 2), (1, 4), (4, 1)), 8: ((2, 4), (4, 2), (1, 8))}
+
+
+def _job_meshes(ljs, world):
+    return {"f32": job_train(ljs, MESHES[world], batch=8, seq=32, dtype=torch.float32),
+            "bf16": job_train(ljs, MESHES[world], batch=8, seq=32)}
+
+
+def job_train_w4(ljs):
+    return _job_meshes(ljs, 4)
+
+
+def job_train_w8(ljs):
+    return _job_meshes(ljs, 8)
 
 
 def job_train_overlap_fp32(ljs):
@@ -100,7 +120,7 @@ def _overlap_train(ljs):
 
 
 def _run(job, world=2):
-    port = 29500 + (os.getpid() % 1000)
+    port = 29500 + (os.getpid() % 1000) + 7 * world
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, port, d, job), nprocs=world, join=True)
         out = []
@@ -135,6 +155,48 @@ def test_dist_train_matches_single_process(host_devices):
             assert abs(l - lref) <= 1e-2 * max(1, abs(lref)), (shape, l, lref)
             for k in pref:
                 np.testing.assert_allclose(p[k], pref[k], rtol=1e-4, atol=1e-5)
+
+
+def _adam_close(a, b, what):
+    """Parameters after 2 Adam steps from gradients that differ only by rounding: an element
+    whose gradient is ~0 may take the opposite step (|update| <= lr = 1e-3 per step)."""
+    diff = np.abs(a - b)
+    assert diff.max() <= 4.2e-3, (what, diff.max())
+    assert np.mean(diff > 2e-3 + 2e-2 * np.abs(b)) < 1e-2, what
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_dist_train_reference_meshes(host_devices, world):
+    """case6 train steps on the reference's 2x2 / 2x4 meshes (and their transposes / 1-D
+    layouts) with one gloo process per device:
+    * f32 compute == the same SPMD job on in-process host devices to f32 tolerance (same
+      partition, same math; only the collectives' summation order differs);
+    * bf16 compute (the reference dtype) == the in-process job and an unsharded 1x1 run up to
+      bf16 partial-sum rounding (gloo sums bf16 collectives in bf16, the loopback in f32)."""
+    outs = _run(f"job_train_w{world}", world=world)
+    host_devices(world)
+    import learning_jax_sharding_amd as ljs
+    ref32 = job_train(ljs, MESHES[world], batch=8, seq=32, dtype=torch.float32)
+    ref16 = job_train(ljs, MESHES[world], batch=8, seq=32)
+    host_devices(1)
+    one = job_train(ljs, ((1, 1),), batch=8, seq=32)["(1, 1)"]
+    for shape in ref32:
+        lref, pref = ref32[shape]
+        for r in outs:
+            l, p = r["f32"][shape]
+            assert abs(l - lref) <= 1e-4 * max(1, abs(lref)), (shape, l, lref)
+            for k in pref:
+                np.testing.assert_allclose(p[k], pref[k], rtol=1e-4, atol=1e-5, err_msg=f"{shape} {k}")
+        lref, pref = ref16[shape]
+        l1, p1 = one
+        for r in outs:
+            l, p = r["bf16"][shape]
+            assert abs(l - lref) <= 1e-2 * max(1, abs(lref)), (shape, l, lref)
+            for k in pref:
+                _adam_close(p[k], pref[k], (shape, k))
+        assert abs(lref - l1) <= 3e-2 * max(1, abs(l1)), (shape, lref, l1)
+        for k in p1:
+            _adam_close(pref[k], p1[k], (shape, k, "1x1"))
 
 
 @pytest.mark.parametrize("wire", ["fp32", "bf16"])
@@ -197,7 +259,6 @@ def test_dist_train_fsdp(host_devices):
     host_devices(2)
     import learning_jax_sharding_amd as ljs
     lref, pref, tiles, kinds = job_train_fsdp(ljs)
-    print(kinds)
     assert any("gather" in k for k in kinds) and any("reduce_scatter" in k for k in kinds), kinds
     for l, p, t, _ in (r0, r1):
         assert abs(l - lref) <= 1e-3 * max(1, abs(lref)), (l, lref)

@@ -264,9 +264,9 @@ def test_ring_attention_matches_allgather(host_devices, causal, mesh_shape):
         np.testing.assert_allclose(a, b, rtol=3e-2, atol=3e-2 * max(1.0, np.abs(b).max()))
 
 
-@pytest.mark.parametrize("preset", ["gspmd2d", "fsdp"])
+@pytest.mark.parametrize("preset", ["gspmd2d", "megatron", "fsdp"])
 def test_rule_presets_match_unsharded(host_devices, preset):
-    """The attention block under the Megatron ("gspmd2d") and FSDP rule presets == 1 device."""
+    """The attention block under the GSPMD 2D, Megatron and FSDP rule presets == 1 device."""
     host_devices(4)
     from learning_jax_sharding_amd import nn, parallel
     from learning_jax_sharding_amd.models import MultiHeadAttention
