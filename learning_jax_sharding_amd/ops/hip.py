@@ -542,23 +542,84 @@ def softmax_lastdim(x: torch.Tensor) -> torch.Tensor:
 # ============================================================================ dense / linear
 def linear(x: torch.Tensor, ws: List[torch.Tensor], b: Optional[torch.Tensor], compute_dtype: torch.dtype,
            relu: bool, out_dtype: torch.dtype) -> List[torch.Tensor]:
-    """Fused dense layer (see :mod:`.linear`); shapes the MFMA path cannot take use torch."""
+    """Fused dense layer (see :mod:`.linear`).  Every GPU shape runs on a HIP GEMM:
+
+    * bf16 compute, K and N multiples of 8, f32 row-major kernels: the fused MFMA path;
+    * bf16 compute otherwise: the same path on zero-padded operands (rows M, K and N up to the
+      next multiple of 8; zero rows/columns change no sum), result sliced back;
+    * f32 compute: the MFMA ``v_mfma_f32_16x16x4f32`` GEMM (:class:`_MatmulF32`, strided
+      operands, its own backward), bias and ReLU as elementwise epilogues.
+
+    Anything else raises unless ``LJS_ALLOW_TORCH_FALLBACK=1`` (debugging only)."""
     from . import linear as _lin
-    if compute_dtype == torch.bfloat16 and _lin.supported(x, ws, b):
-        return _lin.linear(x, list(ws), b, relu, out_dtype)
-    outs = []
-    for w in ws:
-        outs.append(_torch_linear(x, w, b if len(ws) == 1 else None, compute_dtype, relu, out_dtype))
-    return outs
+    if compute_dtype == torch.bfloat16:
+        if _lin.supported(x, ws, b):
+            return _lin.linear(x, list(ws), b, relu, out_dtype)
+        if all(w.dim() == 2 and w.shape == ws[0].shape and w.dtype == torch.float32 for w in ws) \
+                and (b is None or len(ws) == 1):
+            return _linear_padded(x, ws, b, relu, out_dtype)
+    elif compute_dtype == torch.float32:
+        outs = []
+        for w in ws:
+            lead = x.shape[:-1]
+            y = _MatmulF32.apply(x.reshape(-1, x.shape[-1]).float(), w.float())
+            if b is not None and len(ws) == 1:
+                y = y + b.float()
+            if relu:
+                y = torch.relu(y)
+            outs.append(y.to(out_dtype).reshape(tuple(lead) + (w.shape[-1],)))
+        return outs
+    if os.environ.get("LJS_ALLOW_TORCH_FALLBACK", "0") != "1":
+        raise NotImplementedError(f"no HIP dense path for compute dtype {compute_dtype}, x {tuple(x.shape)}, "
+                                  f"w {[tuple(w.shape) for w in ws]} (LJS_ALLOW_TORCH_FALLBACK=1 to use torch)")
+    return [_torch_linear(x, w, b if len(ws) == 1 else None, compute_dtype, relu, out_dtype) for w in ws]
 
 
-def _torch_linear(x, w, b, compute_dtype, relu, out_dtype):
-    y = x.to(compute_dtype).float() @ w.to(compute_dtype).float()
-    if b is not None:
-        y = y + b.to(compute_dtype).float()
-    if relu:
-        y = torch.relu(y)
-    return y.to(out_dtype)
+def _linear_padded(x, ws, b, relu, out_dtype):
+    """bf16 MFMA dense on operands zero-padded to M, K, N multiples of 8 (autograd flows through
+    the pads and slices, so the gradients of x, w and b are those of the unpadded layer)."""
+    from . import linear as _lin
+    K, N = ws[0].shape
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    pm, pk, pn = (-M) % 8, (-K) % 8, (-N) % 8
+    xp = torch.nn.functional.pad(x2, (0, pk, 0, pm)) if (pk or pm) else x2
+    wps = [torch.nn.functional.pad(w, (0, pn, 0, pk)).contiguous() if (pk or pn) else w.contiguous() for w in ws]
+    bp = torch.nn.functional.pad(b, (0, pn)) if (b is not None and pn) else b
+    outs = _lin.linear(xp, wps, bp, relu, out_dtype)
+    return [o[:M, :N].reshape(tuple(lead) + (N,)) for o in outs]
+
+
+class _MatmulF32(torch.autograd.Function):
+    """``x [M, K] @ w [K, N]`` in f32 on the MFMA f32 GEMM; backward dx = dy w^T, dw = x^T dy on
+    the same kernel through transposed strides (nothing is copied)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        x = x.contiguous()
+        w = w.contiguous()
+        M, K = x.shape
+        N = w.shape[1]
+        ctx.save_for_backward(x, w)
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        _gemm_f32(x, w, y, M, N, K, K, 1, N, 1, N, 0, 0, 0, 1)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous().float()
+        M, K = x.shape
+        N = w.shape[1]
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((M, K), dtype=torch.float32, device=x.device)
+            _gemm_f32(dy, w, dx, M, K, N, N, 1, 1, N, K, 0, 0, 0, 1)       # B[n][k] = w[k][n]
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty((K, N), dtype=torch.float32, device=x.device)
+            _gemm_f32(x, dy, dw, K, N, M, 1, K, N, 1, N, 0, 0, 0, 1)        # A[k][m] = x[m][k]
+        return dx, dw
 
 
 def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, accumulate: bool = False,

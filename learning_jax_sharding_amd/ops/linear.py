@@ -256,7 +256,8 @@ class _Linear(torch.autograd.Function):
 def supported(x: torch.Tensor, ws: Sequence[torch.Tensor], b) -> bool:
     K = x.shape[-1]
     N = ws[0].shape[1]
-    return (K % 8 == 0 and N % 8 == 0 and all(w.shape == ws[0].shape and w.dim() == 2 for w in ws)
+    M = x.numel() // max(1, K)   # the weight-gradient GEMM contracts over the M rows
+    return (K % 8 == 0 and N % 8 == 0 and M % 8 == 0 and all(w.shape == ws[0].shape and w.dim() == 2 for w in ws)
             and all(w.dtype == torch.float32 and w.stride(1) == 1 for w in ws)
             and (b is None or len(ws) == 1))
 

@@ -218,9 +218,10 @@ def test_dist_train_overlapped_reducer(host_devices, wire):
                 np.testing.assert_allclose(p[k], pref[k], **tol)
 
 
-def job_train_fsdp(ljs):
+def job_train_fsdp(ljs, mesh_shape=(2, 1)):
     """case3 at scale (bench.py --model fsdp): every weight and Adam moment sharded over
-    'data'; the partitioner gathers weights at use and reduce-scatters their gradients."""
+    'data'; DenseStack prefetches each layer's gather (parallel.fsdp.Prefetcher) and autograd
+    reduce-scatters the gradients."""
     from learning_jax_sharding_amd import nn, optim
     from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
     from learning_jax_sharding_amd.models import DenseStack
@@ -228,7 +229,7 @@ def job_train_fsdp(ljs):
     from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
     from learning_jax_sharding_amd.spmd import plan as _plan
     from learning_jax_sharding_amd.training import TrainState
-    mesh = Mesh(create_device_mesh((2, 1)), ("data", "model"))
+    mesh = Mesh(create_device_mesh(mesh_shape), ("data", "model"))
     model = DenseStack(64, layers=3, dtype=torch.float32)
     x = ljs.random.normal(ljs.random.PRNGKey(0), (4, 16, 64))
 
@@ -250,8 +251,9 @@ def job_train_fsdp(ljs):
         for _ in range(2):
             state, l = step(state, x)
     ker = {k: v["kernel"] for k, v in state.params.items()}
+    notes = [st.info.get("note") for st in rec.steps]
     return (float(np.asarray(l)), {k: np.asarray(v) for k, v in ker.items()},
-            {k: tuple(v.tile.tile_shape) for k, v in ker.items()}, rec.collective_kinds())
+            {k: tuple(v.tile.tile_shape) for k, v in ker.items()}, rec.collective_kinds() + notes)
 
 
 def test_dist_train_fsdp(host_devices):
@@ -259,9 +261,17 @@ def test_dist_train_fsdp(host_devices):
     host_devices(2)
     import learning_jax_sharding_amd as ljs
     lref, pref, tiles, kinds = job_train_fsdp(ljs)
-    assert any("gather" in k for k in kinds) and any("reduce_scatter" in k for k in kinds), kinds
-    for l, p, t, _ in (r0, r1):
+    assert any("gather" in str(k) for k in kinds) and any("reduce_scatter" in str(k) for k in kinds), kinds
+    assert "fsdp.prefetch" in kinds, kinds  # the gathers come from the prefetcher
+    # and the sharded job equals unsharded training on one device (f32 compute)
+    host_devices(1)
+    l1, p1, _, kinds1 = job_train_fsdp(ljs, (1, 1))
+    assert "fsdp.prefetch" not in kinds1
+    for l, p, t, k_r in (r0, r1):
+        assert "fsdp.prefetch" in k_r
         assert abs(l - lref) <= 1e-3 * max(1, abs(lref)), (l, lref)
+        assert abs(l - l1) <= 1e-3 * max(1, abs(l1)), (l, l1)
         assert all(2 in ts for ts in t.values()), t  # weights stay sharded over 'data'
         for k in pref:
             np.testing.assert_allclose(p[k], pref[k], rtol=1e-4, atol=1e-5)
+            np.testing.assert_allclose(p[k], p1[k], rtol=1e-4, atol=1e-5)
