@@ -320,11 +320,27 @@ def _reduce(x: ShardedArray, axis, keepdims: bool, local_fn, combine: str, dtype
     # materialised when partial sums still have to be all-reduced across shards
     acc = torch.float32 if out_dtype in (torch.bfloat16, torch.float16) and combine == "sum" and sharded \
         else out_dtype
-    loc = _map(x, lambda t: local_fn(t, axes, keepdims, acc))
-    partials = None
     scalar = all(i in axes for i in range(x.ndim)) or x.ndim == 0
-    if sharded:
-        groups = x.tile.groups_along(sharded)
+    # a whole-array sum of an autograd-tracked array (a loss): its value is computed only if read.
+    # grad() seeds the summed array itself with the broadcast cotangent (d sum / d x = 1) - the
+    # gradient _SumAll's backward would produce - so a train step that never reads the loss runs
+    # no reduction kernel at all, the way XLA drops the primal output of jax.grad
+    lazy_sum = (combine == "sum" and scalar and _LAZY_SCALAR_SUMS and x.ndim > 0 and torch.is_grad_enabled()
+                and not isinstance(x.local, LazyLocal) and x.local
+                and all(t.requires_grad and t.device.type != "meta" for t in x.local.values()))
+    groups = x.tile.groups_along(sharded) if sharded else None
+    partials = None
+    if lazy_sum:
+        xs = dict(x.local)
+
+        def thunk(xs=xs, groups=groups):
+            part = {d: local_fn(t, axes, keepdims, acc) for d, t in xs.items()}
+            red = C.all_reduce(part, groups, note="reduce") if groups is not None else part
+            return {d: (t if t.dtype == out_dtype else t.to(out_dtype)) for d, t in red.items()}
+        loc = LazyLocal(thunk)
+    else:
+        loc = _map(x, lambda t: local_fn(t, axes, keepdims, acc))
+    if sharded and not lazy_sum:
         if combine == "sum":
             partials = (loc, len(groups[0]))
             if scalar and _LAZY_SCALAR_SUMS:
@@ -351,6 +367,9 @@ def _reduce(x: ShardedArray, axis, keepdims: bool, local_fn, combine: str, dtype
         tile = x.tile.project(kept)
         shape = tuple(x.shape[i] for i in kept)
     res = ShardedArray(shape, out_dtype, sharding_from_tile(tile, like=[x.sharding]), loc)
+    if lazy_sum:
+        # (summed per-device tensors, replica-group size of the all-reduce of their partial sums)
+        res._sum_inputs = (xs, len(groups[0]) if groups is not None else 1)
     if partials is not None and res.size == 1:
         # a scalar that is the all-reduced sum of per-shard partial sums: grad() seeds the partials
         # directly (d sum / d partial = 1) instead of back-propagating through the all-reduce,

@@ -367,7 +367,16 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
         n_holders = ta.num_devices
         outs, seeds = [], []
         partials = getattr(out, "_sum_partials", None)
-        if partials is not None and not _SEED_THROUGH_ALLREDUCE:
+        sum_inputs = getattr(out, "_sum_inputs", None)
+        if sum_inputs is not None and isinstance(out.local, LazyLocal) and out.local.pending \
+                and not _SEED_THROUGH_ALLREDUCE:
+            # out = sum(x) whose value nobody has read: seed x with the broadcast cotangent
+            # (gsize / n_holders in x's dtype, all strides 0 - what the sum's backward returns)
+            xs, gsize = sum_inputs
+            for d, t in xs.items():
+                outs.append(t)
+                seeds.append(_seed(t.new_empty(()), gsize / n_holders).expand(t.shape))
+        elif partials is not None and not _SEED_THROUGH_ALLREDUCE:
             # out = all_reduce(partials) over groups of size G (replicated over n_holders / G
             # groups): seeding each partial with G / n_holders is exactly what the all-reduce's
             # transpose would deliver to it from the 1 / n_holders seeds below
