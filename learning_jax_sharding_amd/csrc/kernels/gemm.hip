@@ -31,9 +31,42 @@ struct GemmArgs {
   int M, N, K;
   int batch, splitk, kt_per_split;
   float alpha;
-  int flags;  // 1 relu, 2 bias, 4 bias f32, 8 accumulate into C (f32 out)
+  int flags;  // 1 relu, 2 bias, 4 bias f32, 8 accumulate into C (f32 out); epilogue operand R
+              // (bf16 output only): 64 residual add, 128 ReLU mask (keep where R > 0), 256 R is f32
   float* psum;  // LDS-DMA kernels, bf16 out: per (item, wave) sums of the stored values, or null
+  const void* res;  // R[b][row][col] at res + b * sR + row * ldr + col (ldr may be 0: one broadcast row)
+  long ldr, sR;
 };
+
+constexpr int kResAdd = 64, kResMask = 128, kResF32 = 256;
+
+// Epilogue operand R applied to 8 consecutive output values (after bias / ReLU, f32):
+//   residual add: out = bf16(bf16(v) + bf16(R))   (the unfused "y = dense(x); y + R" in bf16:
+//                 both roundings kept, so the fusion is bit-exact)
+//   ReLU mask   : out = R > 0 ? v : 0             (the ReLU backward of a dense whose input R is a
+//                 ReLU output, fused into the dX GEMM producing v)
+// rb holds R's 8 values as bf16 pairs (bf16 R) or rf their f32 values (f32 R).
+__device__ __forceinline__ void apply_res8(float* v, int flags, const u32x4& rb, const u32x4& rf0,
+                                           const u32x4& rf1) {
+  float r[8];
+  if (flags & kResF32) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { r[e] = __uint_as_float(rf0[e]); r[4 + e] = __uint_as_float(rf1[e]); }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      r[2 * e] = __uint_as_float(rb[e] << 16);
+      r[2 * e + 1] = __uint_as_float(rb[e] & 0xffff0000u);
+    }
+  }
+  if (flags & kResAdd) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e])) + bf2f(f2bf(r[e]));
+  } else if (flags & kResMask) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = r[e] > 0.f ? v[e] : 0.f;
+  }
+}
 
 // swizzled 8-byte-chunk index for the m/n-contiguous image (rows of R bf16)
 template <int R>
@@ -218,7 +251,30 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
       if (row >= p.M || col >= p.N) continue;
       const bf16_t* src = ct + rl * LDC + cc * 8;
       bf16_t* dst = Cb + (long)row * p.ldc + col;
-      if (vec_ok && col + 8 <= p.N) {
+      if (p.flags & (kResAdd | kResMask)) {
+        float v[8];
+        u32x4 rb = {0, 0, 0, 0}, rf0 = {0, 0, 0, 0}, rf1 = {0, 0, 0, 0};
+        const long ro = (long)b * p.sR + (long)row * p.ldr + col;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = bf2f(src[e]);
+          if (col + e < p.N) {
+            if (p.flags & kResF32) {
+              const float rv = reinterpret_cast<const float*>(p.res)[ro + e];
+              if (e < 4) rf0[e] = __float_as_uint(rv); else rf1[e - 4] = __float_as_uint(rv);
+            } else {
+              const unsigned rv = reinterpret_cast<const bf16_t*>(p.res)[ro + e];
+              rb[e >> 1] |= (e & 1) ? (rv << 16) : rv;
+            }
+          }
+        }
+        apply_res8(v, p.flags, rb, rf0, rf1);
+        if (vec_ok && col + 8 <= p.N)
+          *reinterpret_cast<u32x4*>(dst) = u32x4{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                 pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7])};
+        else
+          for (int e = 0; e < 8 && col + e < p.N; ++e) dst[e] = f2bf(v[e]);
+      } else if (vec_ok && col + 8 <= p.N) {
         *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
       } else {
         for (int e = 0; e < 8 && col + e < p.N; ++e) dst[e] = src[e];
@@ -346,8 +402,13 @@ __device__ __forceinline__ WorkItem decode_item(const GemmArgs& p, int item, int
 
 constexpr int kSC1 = 16;  // buffer-instruction cache policy bit: sc1 (gfx940-family CPol::SC1)
 
-template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32>
-__global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
+// RES: epilogue operand R (bf16 output only; see apply_res8): 0 none, 1 bf16 R, 2 f32 R.  A
+// template parameter so kernels without it keep their register allocation.
+// (a RES variant is told to keep two 4-wave blocks per CU: its epilogue registers would otherwise
+// push VGPR + AGPR past 256 and halve the resident blocks)
+template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0>
+__global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2) ? 2 : 1) void gemm_dma_kernel(
+    GemmArgs p) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int A_TILE = BM * BK, B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
@@ -502,6 +563,27 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]; lanes g, g^1 trade halves so
       // even g owns cols 16 j0 + 4 g .. +7 and odd g owns 16 j1 + 4 (g - 1) .. +7
       const bool even = (g & 1) == 0;
+      // epilogue operand: one row block (ii) of R chunks in flight at a time (all of an item's
+      // chunks at once cost the second resident block its registers); rows / columns past
+      // M / N read 0 through the buffer range check, and the compiler's counted vmcnt waits
+      // for them at first use
+      u32x4 rv[TN / 2][RES == 2 ? 2 : 1];
+      __amdgpu_buffer_rsrc_t rr;
+      if constexpr (RES != 0)
+        rr = make_rsrc(p.res, (RES == 2 ? 4 : 2) * ((long)(p.batch - 1) * p.sR + (long)(p.M - 1) * p.ldr + p.N));
+      auto load_r = [&](int ii) {
+        if constexpr (RES != 0) {
+#pragma unroll
+          for (int q = 0; q < TN / 2; ++q) {
+            const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
+            const int row = m0 + ii * 16 + (lane & 15);
+            const bool ok = row < p.M && col < p.N;
+            const int off = ok ? (int)(((long)w.b * p.sR + (long)row * p.ldr + col) * (RES == 2 ? 4 : 2)) : 0x7ffffff0;
+            rv[q][0] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+            if constexpr (RES == 2) rv[q][RES == 2 ? 1 : 0] = __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? off + 16 : off, 0, 0);
+          }
+        }
+      };
       float bvs[TN / 2][8];
 #pragma unroll
       for (int q = 0; q < TN / 2; ++q) {
@@ -518,6 +600,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
       }
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) {
+        load_r(ii);
 #pragma unroll
         for (int q = 0; q < TN / 2; ++q) {  // both halves of a row's 128 B back to back
           const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
@@ -537,11 +620,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_dma_kernel(GemmArgs p) {
           }
           u32x4 pk;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float x0 = v[2 * e] + bv[2 * e], x1 = v[2 * e + 1] + bv[2 * e + 1];
-            if (relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
-            pk[e] = pack_bf16x2(x0, x1);
+          for (int e = 0; e < 8; ++e) {
+            v[e] += bv[e];
+            if (relu) v[e] = fmaxf(v[e], 0.f);
           }
+          if constexpr (RES != 0) apply_res8(v, p.flags, rv[q][0], rv[q][0], rv[q][RES == 2 ? 1 : 0]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
           const int row = m0 + ii * 16 + (lane & 15);
           const bool ok = row < p.M && col < p.N;  // N % 8 == 0 (launcher): chunks are whole
           const int off = ok ? (int)(((long)w.b * p.sC + (long)row * p.ldc + col) * 2) : 0x7ffffff0;
@@ -637,12 +722,23 @@ LJS_DMA_INST(128, 160, 4, 1, 2, true, true, false)
 LJS_DMA_INST_8W(3)
 LJS_DMA_INST_8W(4)
 #undef LJS_DMA_INST_8W
+// epilogue-operand variants (bf16 output, k-contiguous operands: forward and dX GEMMs)
+#define LJS_DMA_INST_RES(BM, BN, WM, WN, NST) \
+  template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 1>(GemmArgs); \
+  template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 2>(GemmArgs);
+LJS_DMA_INST_RES(128, 160, 4, 1, 2)
+LJS_DMA_INST_RES(256, 128, 4, 2, 3)
+LJS_DMA_INST_RES(128, 128, 2, 2, 2)
+LJS_DMA_INST_RES(128, 128, 2, 2, 4)
+LJS_DMA_INST_RES(128, 128, 2, 4, 3)
+LJS_DMA_INST_RES(128, 128, 2, 4, 4)
+#undef LJS_DMA_INST_RES
 #undef LJS_DMA_INST_LAYOUTS
 #undef LJS_DMA_INST
 
 int g_cus = 0;
 
-template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF>
+template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF, int RES = 0>
 hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   if (!g_cus) {
     int dev = 0;
@@ -665,8 +761,19 @@ hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   if (bpc == 0 && bpc_env == 0 && items > g_cus * kNatural && items % (g_cus * kNatural) == 0) bpc = kNatural;
   int grid = bpc > 0 ? g_cus * bpc : items;
   if (grid > items) grid = items;
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, NST, AK, BKc, OF>), dim3(grid), dim3(WM * WN * 64), 0, s, a);
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, NST, AK, BKc, OF, RES>), dim3(grid), dim3(WM * WN * 64), 0, s,
+                     a);
   return hipGetLastError();
+}
+
+// bf16-output k-contiguous launch with the epilogue operand variant the flags ask for
+template <int BM, int BN, int WM, int WN, int NST>
+hipError_t launch_dma_kk(const GemmArgs& a, hipStream_t s) {
+  if (a.flags & (kResAdd | kResMask)) {
+    if (a.flags & kResF32) return launch_dma<BM, BN, WM, WN, NST, true, true, false, 2>(a, s, 0);
+    return launch_dma<BM, BN, WM, WN, NST, true, true, false, 1>(a, s, 0);
+  }
+  return launch_dma<BM, BN, WM, WN, NST, true, true, false, 0>(a, s, 0);
 }
 
 template <int BM, int BN, bool AK, bool BKc, bool OF>
@@ -695,9 +802,13 @@ hipError_t dispatch_layout(const GemmArgs& a, int a_kc, int b_kc, int out_f32, h
 LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
                           long lda, long ldb, long ldc, long sA, long sB, long sC, long sBias, int batch,
                           int a_kc, int b_kc, int out_f32, int flags, float alpha, int splitk, int tile,
-                          void* psum, int* psum_count, hipStream_t stream) {
+                          void* psum, int* psum_count, const void* res, long ldr, long sR, hipStream_t stream) {
   if (K % 8 || (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
   if (splitk > 1 && !out_f32) return (int)hipErrorInvalidValue;
+  // the epilogue operand applies to bf16 outputs (its 16-byte loads need aligned 8-column chunks)
+  if ((flags & (kResAdd | kResMask)) &&
+      (out_f32 || !res || (ldr % 8) || (sR % 8) || (N % 8) || (((uintptr_t)res) & 15)))
+    return (int)hipErrorInvalidValue;
   GemmArgs a;
   a.A = (const bf16_t*)A;
   a.B = (const bf16_t*)B;
@@ -710,6 +821,9 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   a.alpha = alpha;
   a.flags = flags;
   a.psum = nullptr;
+  a.res = res;
+  a.ldr = ldr;
+  a.sR = sR;
   if (psum_count) *psum_count = 0;
   int nkt = (K + BK - 1) / BK;
   if (splitk < 1) splitk = 1;
@@ -735,6 +849,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   const bool dma_store_ok = out_f32 || (N % 8 == 0 && ldc % 8 == 0 && (sC % 8 == 0 || batch == 1) &&
                                         (((uintptr_t)C) & 15) == 0);
   if (tile > 1000 && !(dma_ok && dma_store_ok)) tile = 128;
+  // the LDS-DMA kernels carry the epilogue operand in their k-contiguous bf16 variants only
+  if ((flags & (kResAdd | kResMask)) && tile > 1000 && !(a_kc && b_kc)) tile = 128;
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
   if (tile == 1602 && !(a_kc && b_kc && !out_f32 && a.splitk == 1)) tile = 1282;
   if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;
@@ -746,10 +862,10 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch * a.splitk * nw;
   }
   if (tile == 1602) {
-    e = launch_dma<128, 160, 4, 1, 2, true, true, false>(a, stream, 0);
+    e = launch_dma_kk<128, 160, 4, 1, 2>(a, stream);
   } else if (tile == 2561) {
     if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);
-    else e = launch_dma<256, 128, 4, 2, 3, true, true, false>(a, stream, 0);
+    else e = launch_dma_kk<256, 128, 4, 2, 3>(a, stream);
   } else if (tile == 12883 || tile == 12884) {
     // 128x128, 8 waves, 3 / 4 stages (weight-grad MN x MN f32, or k-contiguous operands)
     const bool d4 = tile == 12884;
@@ -760,11 +876,15 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
       if (d4) e = launch_dma<128, 128, 2, 4, 4, true, true, true>(a, stream, 0);
       else e = launch_dma<128, 128, 2, 4, 3, true, true, true>(a, stream, 0);
     } else {
-      if (d4) e = launch_dma<128, 128, 2, 4, 4, true, true, false>(a, stream, 0);
-      else e = launch_dma<128, 128, 2, 4, 3, true, true, false>(a, stream, 0);
+      if (d4) e = launch_dma_kk<128, 128, 2, 4, 4>(a, stream);
+      else e = launch_dma_kk<128, 128, 2, 4, 3>(a, stream);
     }
   } else if (tile == 1284 || tile == 1282) {
     // (plain if/else, not ?: -- see the explicit-instantiation note above)
+    if (a_kc && b_kc && !out_f32) {
+      if (tile == 1284) return (int)launch_dma_kk<128, 128, 2, 2, 4>(a, stream);
+      return (int)launch_dma_kk<128, 128, 2, 2, 2>(a, stream);
+    }
 #define LJS_DMA(AK, BK_, OF)                                                              \
   if (a_kc == AK && b_kc == BK_ && out_f32 == OF) {                                       \
     if (tile == 1284) return (int)launch_dma<128, 128, 2, 2, 4, AK, BK_, OF>(a, stream, 0); \

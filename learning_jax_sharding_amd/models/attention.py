@@ -62,7 +62,10 @@ class MultiHeadAttention(Module):
             print(*a)
 
     def __call__(self, hidden_states: ShardedArray, context: Optional[ShardedArray] = None,
-                 deterministic: bool = True) -> ShardedArray:
+                 deterministic: bool = True, residual: Optional[ShardedArray] = None) -> ShardedArray:
+        """``residual`` (the block's input, for a skip connection): returns
+        ``residual + attention(...)`` in the compute dtype, the add fused into the output
+        projection's GEMM epilogue when dropout is the identity."""
         self_attn = context is None
         context = hidden_states if context is None else context
         self._log("context.shape: ", context.shape)
@@ -105,9 +108,16 @@ class MultiHeadAttention(Module):
             hidden = core.einsum("b n f t, b t n h -> b f n h", probs, v)
         hidden = core.reshape(hidden, (b, -1, self.heads * self.dim_head))
         hidden = with_logical_constraint(hidden, ("batch", "kv", "heads"))
+        drop_id = deterministic or self.dropout == 0.0
+        if residual is not None and drop_id:
+            hidden = self.proj_attn(hidden, residual=residual)
+            return with_logical_constraint(hidden, ("batch", "embed"))
         hidden = self.proj_attn(hidden)
         hidden = with_logical_constraint(hidden, ("batch", "embed"))
-        return self.dropout_layer(hidden, deterministic=deterministic)
+        hidden = self.dropout_layer(hidden, deterministic=deterministic)
+        if residual is not None:
+            hidden = core.binary("add", core.convert(residual, dt), hidden)
+        return hidden
 
 
 def attention_block_flops(batch: int, seq: int, dim: int, heads: int, dim_head: int, train: bool) -> float:

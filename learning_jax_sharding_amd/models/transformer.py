@@ -33,8 +33,10 @@ class TransformerLayer(Module):
         self.ff = FeedForward(self.ff_dim, dtype=self.dtype, fp8=self.fp8, name="ff")
 
     def __call__(self, x):
-        h = core.binary("add", core.convert(x, self.dtype), self.attn(x))
-        return core.binary("add", h, self.ff(h))
+        # h = x + attn(x); y = h + ff(h), both skip connections fused into the output GEMMs'
+        # epilogues (x is read in f32 and rounded to the compute dtype there, as convert(x) would)
+        h = self.attn(x, residual=x)
+        return self.ff(h, residual=h)
 
 
 def transformer_layer_flops(batch, seq, dim, heads, dim_head, ff_dim, train: bool) -> float:

@@ -51,11 +51,13 @@ class Dense(Module):
             return None
         return self.param("bias", self.bias_init, (self.features,), _dt.canonicalize(self.param_dtype))
 
-    def __call__(self, inputs: ShardedArray) -> ShardedArray:
+    def __call__(self, inputs: ShardedArray, residual: Optional[ShardedArray] = None) -> ShardedArray:
+        """``inputs @ kernel (+ bias)``; ``residual`` is added in the compute dtype (fused into the
+        GEMM epilogue on the MFMA path)."""
         kernel = self.kernel_param(inputs.shape[-1])
         bias = self.bias_param()
         dtype = _dt.canonicalize(self.dtype) or _dt.result_type(inputs.dtype, kernel.dtype)
-        return core.dense(inputs, [kernel], bias, compute_dtype=dtype)[0]
+        return core.dense(inputs, [kernel], bias, compute_dtype=dtype, residual=residual)[0]
 
 
 DenseGeneral = Dense
@@ -97,7 +99,9 @@ class FeedForward(Module):
     fp8: bool = False
 
     @compact
-    def __call__(self, x: ShardedArray) -> ShardedArray:
+    def __call__(self, x: ShardedArray, residual: Optional[ShardedArray] = None) -> ShardedArray:
+        """``residual`` (e.g. ``x`` itself for a skip connection) is added to the output in the
+        compute dtype, fused into the down projection's GEMM epilogue."""
         d = x.shape[-1]
         w_in = self.param("w_in", with_logical_partitioning(init.lecun_normal(), ("embed", "hidden")),
                           (d, self.hidden_dim), torch.float32)
@@ -108,10 +112,11 @@ class FeedForward(Module):
             from ..ops.fp8 import fp8_dense
             h = fp8_dense(x, w_in, relu=True, out_dtype=dt)
             h = with_logical_constraint(h, ("batch", "length", "hidden"))
-            return fp8_dense(h, w_out, relu=False, out_dtype=dt)
+            y = fp8_dense(h, w_out, relu=False, out_dtype=dt)
+            return y if residual is None else core.binary("add", core.convert(residual, dt), y)
         h = core.dense(x, [w_in], None, compute_dtype=dt, relu=True)[0]
         h = with_logical_constraint(h, ("batch", "length", "hidden"))
-        return core.dense(h, [w_out], None, compute_dtype=dt)[0]
+        return core.dense(h, [w_out], None, compute_dtype=dt, residual=residual)[0]
 
 
 class Embed(Module):

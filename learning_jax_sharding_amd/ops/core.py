@@ -655,17 +655,22 @@ def dot_product_attention(q: ShardedArray, k: ShardedArray, v: ShardedArray, sca
 
 # ----------------------------------------------------------------------------- fused dense
 def dense(x: ShardedArray, kernels: Sequence[ShardedArray], bias: Optional[ShardedArray] = None,
-          compute_dtype=None, relu: bool = False, fp8: bool = False) -> List[ShardedArray]:
+          compute_dtype=None, relu: bool = False, fp8: bool = False,
+          residual: Optional[ShardedArray] = None) -> List[ShardedArray]:
     """``y_i = x @ W_i (+ b)`` in ``compute_dtype`` for several kernels sharing one sharding.
 
     The kernels are concatenated along the output features on the fly (one
     batched MFMA GEMM launch for Q/K/V).  Returns one array per kernel.  Bias
     and ReLU are fused into the GEMM epilogue when the contraction is local.
-    ``fp8`` runs the local GEMMs in MX-fp8 (:mod:`.fp8`).
+    ``fp8`` runs the local GEMMs in MX-fp8 (:mod:`.fp8`).  ``residual`` (one kernel, the
+    output's shape): ``y + convert(residual, compute_dtype)``, fused into the GEMM epilogue
+    when the contraction is local (the residual is resharded to the output's tiling).
     """
     kernels = list(kernels)
     w0 = kernels[0]
     compute_dtype = _dt.canonicalize(compute_dtype) or _dt.result_type(x.dtype, w0.dtype)
+    if residual is not None and len(kernels) != 1:
+        raise ValueError("dense(residual=...) takes one kernel")
     same = all(k.tile == w0.tile and k.shape == w0.shape for k in kernels)
     if not same or (w0.ndim == 2 and w0.tile.tile_shape[1] > 1 and len(kernels) > 1):
         outs = [dense(x, [k], bias if len(kernels) == 1 else None, compute_dtype, relu, fp8)[0] for k in kernels]
@@ -684,12 +689,18 @@ def dense(x: ShardedArray, kernels: Sequence[ShardedArray], bias: Optional[Shard
         bt = _target_for(p.out_tile, out_shape, bias.shape)
         b2 = reshard_tile(bias, bt, note="dense.bias")
         b_loc = b2.local
+    r_loc = None
+    if residual is not None and not partial:
+        if tuple(residual.shape) != out_shape:
+            raise ValueError(f"residual shape {residual.shape} != output shape {out_shape}")
+        r_loc = reshard_tile(residual, p.out_tile, note="dense.residual").local
     loc_lists = {}
     for d in x2.local:
         loc_lists[d] = K.linear(x2.local[d], [w.local[d] for w in ws],
                                 b_loc[d] if fuse_bias else None, compute_dtype,
                                 relu=relu and not partial,
-                                out_dtype=torch.float32 if partial else compute_dtype, fp8=fp8)
+                                out_dtype=torch.float32 if partial else compute_dtype, fp8=fp8,
+                                residual=r_loc[d] if r_loc is not None else None)
     outs = []
     sh = sharding_from_tile(p.out_tile, like=[x.sharding, w0.sharding])
     for i in range(len(kernels)):
@@ -703,5 +714,7 @@ def dense(x: ShardedArray, kernels: Sequence[ShardedArray], bias: Optional[Shard
                 y = binary("add", y, convert(bias, compute_dtype))
             if relu:
                 y = unary("relu", y)
+            if residual is not None:
+                y = binary("add", y, convert(residual, compute_dtype))
         outs.append(y)
     return outs

@@ -30,7 +30,7 @@ _LP = ctypes.POINTER(ctypes.c_long)
 _SIGS = {
     "ljs_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
                       c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
-                      ctypes.POINTER(c_int), c_void_p],
+                      ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p],
     "ljs_sum_partials": [c_void_p, c_int, c_void_p, c_int, c_void_p],
     "ljs_gemm_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long,
                      c_long, c_long, c_long, c_int, c_void_p],
@@ -166,7 +166,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
          a_kc: bool, b_kc: bool, batch: int = 1, sA: int = 0, sB: int = 0, sC: int = 0,
          bias: Optional[torch.Tensor] = None, sBias: int = 0, relu: bool = False, alpha: float = 1.0,
          accumulate: bool = False, splitk: int = 1, tile: Optional[int] = None, a_off: int = 0, b_off: int = 0,
-         c_off: int = 0, zero_c: bool = False, psum: Optional[torch.Tensor] = None) -> int:
+         c_off: int = 0, zero_c: bool = False, psum: Optional[torch.Tensor] = None,
+         res: Optional[torch.Tensor] = None, res_ld: int = 0, res_mode: str = "add", sR: int = 0) -> int:
     """Raw launcher.  A/B bf16; C bf16 or f32 (split-K/accumulate need f32 C).
 
     ``lda``/``ldb`` may be 0 for an operand that repeats one row (a broadcast gradient).
@@ -174,12 +175,19 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     ``psum`` (f32, >= :func:`psum_slots` floats): the LDS-DMA kernels with bf16 output also write
     per-(tile, wave) sums of the stored values there.  Returns the number of partials written
     (0 when the chosen kernel does not produce them).
+    ``res`` (bf16 or f32, element [row][col] at ``row * res_ld + col``; ``res_ld`` 0 = one
+    broadcast row; bf16 C only) is an epilogue operand: ``res_mode="add"`` adds it as a residual
+    (``bf16(bf16(y) + bf16(res))``, bit-exact with the unfused add), ``"mask"`` keeps the outputs
+    where ``res > 0`` (a ReLU backward fused into the dX GEMM).
     """
     assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
     out_f32 = C.dtype == torch.float32
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
         (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0)
+    if res is not None:
+        assert not out_f32 and res.dtype in (torch.bfloat16, torch.float32), (C.dtype, res.dtype)
+        flags |= (64 if res_mode == "add" else 128) | (256 if res.dtype == torch.float32 else 0)
     if tile is None:
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc)
     eA = A.element_size()
@@ -187,7 +195,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     rc = lib().ljs_gemm_bf16(ctypes.c_void_p(A.data_ptr() + a_off * eA), ctypes.c_void_p(B.data_ptr() + b_off * eA),
                              ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb,
                              ldc, sA, sB, sC, sBias, batch, int(a_kc), int(b_kc), int(out_f32), flags, alpha,
-                             splitk, tile, _p(psum), ctypes.byref(cnt), _stream(C))
+                             splitk, tile, _p(psum), ctypes.byref(cnt), _p(res), res_ld, sR, _stream(C))
     _ck(rc, "ljs_gemm_bf16")
     return cnt.value
 
@@ -541,7 +549,7 @@ def softmax_lastdim(x: torch.Tensor) -> torch.Tensor:
 
 # ============================================================================ dense / linear
 def linear(x: torch.Tensor, ws: List[torch.Tensor], b: Optional[torch.Tensor], compute_dtype: torch.dtype,
-           relu: bool, out_dtype: torch.dtype) -> List[torch.Tensor]:
+           relu: bool, out_dtype: torch.dtype, residual: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
     """Fused dense layer (see :mod:`.linear`).  Every GPU shape runs on a HIP GEMM:
 
     * bf16 compute, K and N multiples of 8, f32 row-major kernels: the fused MFMA path;
@@ -550,11 +558,22 @@ def linear(x: torch.Tensor, ws: List[torch.Tensor], b: Optional[torch.Tensor], c
     * f32 compute: the MFMA ``v_mfma_f32_16x16x4f32`` GEMM (:class:`_MatmulF32`, strided
       operands, its own backward), bias and ReLU as elementwise epilogues.
 
+    ``residual`` (same shape as the output) is added after the activation - in the GEMM
+    epilogue on the fused path.
+
     Anything else raises unless ``LJS_ALLOW_TORCH_FALLBACK=1`` (debugging only)."""
     from . import linear as _lin
+    if compute_dtype == torch.bfloat16 and _lin.supported(x, ws, b):
+        return _lin.linear(x, list(ws), b, relu, out_dtype, residual=residual)
+    outs = _linear_any(x, ws, b, compute_dtype, relu, out_dtype)
+    if residual is not None:
+        outs = [outs[0] + residual.to(outs[0].dtype)] + outs[1:]
+    return outs
+
+
+def _linear_any(x, ws, b, compute_dtype, relu, out_dtype):
+    from . import linear as _lin
     if compute_dtype == torch.bfloat16:
-        if _lin.supported(x, ws, b):
-            return _lin.linear(x, list(ws), b, relu, out_dtype)
         if all(w.dim() == 2 and w.shape == ws[0].shape and w.dtype == torch.float32 for w in ws) \
                 and (b is None or len(ws) == 1):
             return _linear_padded(x, ws, b, relu, out_dtype)

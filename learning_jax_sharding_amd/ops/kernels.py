@@ -83,15 +83,24 @@ def dot_general(a: torch.Tensor, b: torch.Tensor, lc, rc, lb, rb, out_dtype: tor
 
 
 def linear(x: torch.Tensor, ws: Sequence[torch.Tensor], b: Optional[torch.Tensor], compute_dtype: torch.dtype,
-           relu: bool = False, out_dtype: Optional[torch.dtype] = None, fp8: bool = False) -> List[torch.Tensor]:
+           relu: bool = False, out_dtype: Optional[torch.dtype] = None, fp8: bool = False,
+           residual: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
     """``[x @ w (+ b)(relu) for w in ws]`` in ``compute_dtype`` (flax ``Dense`` semantics);
-    ``fp8`` = MX-fp8 forward GEMMs (HIP block-scaled MFMA, exact emulation on CPU)."""
+    ``fp8`` = MX-fp8 forward GEMMs (HIP block-scaled MFMA, exact emulation on CPU).
+    ``residual`` (one kernel): ``out + residual`` in the output dtype, both operands rounded to
+    it first (the GPU fuses the add into the GEMM epilogue)."""
     out_dtype = out_dtype or compute_dtype
     if fp8:
         from . import fp8 as F8
-        return [F8.linear_fp8(x, w, b, relu, out_dtype) for w in ws]
+        outs = [F8.linear_fp8(x, w, b, relu, out_dtype) for w in ws]
+        if residual is not None:
+            outs[0] = outs[0] + residual.to(outs[0].dtype)
+        return outs
     if use_hip(x):
-        return _hip().linear(x, list(ws), b, compute_dtype, relu, out_dtype)
+        return _hip().linear(x, list(ws), b, compute_dtype, relu, out_dtype, residual=residual)
+    if residual is not None:
+        outs = linear(x, ws, b, compute_dtype, relu, out_dtype)
+        return [outs[0] + residual.to(outs[0].dtype)] + outs[1:]
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
     xc = x2.to(compute_dtype)

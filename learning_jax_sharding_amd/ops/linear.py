@@ -15,6 +15,14 @@ Backward:
 * ``db = colsum(dY)``.
 Gradients that are a broadcast row (the cotangent of ``y.sum()``) are consumed with a zero
 leading dimension instead of being materialised.
+
+Epilogue fusions (``hip.gemm``'s operand R):
+* ``residual``: ``y = dense(x) + residual`` in the forward GEMM's epilogue (the transformer
+  layer's skip connections; bit-exact with the separate bf16 add), gradient passed through;
+* ReLU backward in the dX GEMM: when a dense's input is the output of a ReLU dense (recorded
+  in the forward), its dX GEMM writes ``dX * (x > 0)`` directly and marks the result, and the
+  ReLU dense's backward then skips its own mask pass (masking is idempotent, so a gradient
+  that was summed with other contributions on the way is simply masked again).
 """
 from __future__ import annotations
 
@@ -27,6 +35,38 @@ from . import hip
 from . import shadow
 
 __all__ = ["linear"]
+
+import weakref
+
+# bf16 outputs of ReLU denses (data_ptr -> (weakref, version)) and dX gradients already masked by
+# such an output (data_ptr -> (weakref, version, mask data_ptr))
+_RELU_OUT = {}
+_PREMASKED = {}
+
+
+def _register(table, t: torch.Tensor, *extra) -> None:
+    key = t.data_ptr()
+    ref = weakref.ref(t, lambda _r, k=key, tb=table: tb.pop(k, None) if tb.get(k, (None,))[0] is _r else None)
+    table[key] = (ref, t._version) + extra
+
+
+def _lookup(table, t: torch.Tensor):
+    ent = table.get(t.data_ptr())
+    if ent is None:
+        return None
+    y = ent[0]()
+    if y is None or y._version != ent[1] or y.data_ptr() != t.data_ptr() or y.numel() != t.numel():
+        return None
+    return ent
+
+
+def _is_relu_out(t: torch.Tensor) -> bool:
+    return _lookup(_RELU_OUT, t) is not None
+
+
+def _premasked_by(dy: torch.Tensor, y: torch.Tensor) -> bool:
+    ent = _lookup(_PREMASKED, dy)
+    return ent is not None and ent[2] == y.data_ptr() and dy.is_contiguous()
 
 
 def _splitk(M: int, N: int, K: int, batch: int, tile: int) -> int:
@@ -86,7 +126,7 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, b, relu, out_dtype, *ws):
+    def forward(ctx, x, b, res, relu, out_dtype, *ws):
         lead = x.shape[:-1]
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
@@ -109,13 +149,33 @@ class _Linear(torch.autograd.Function):
         partials = None
         if _FUSED_SUM and nw == 1 and od == torch.bfloat16 and M * N >= (1 << 20):
             partials = torch.empty((hip.psum_slots(M, N),), dtype=torch.float32, device=x.device)
+        # residual fused into the epilogue (bf16 output, one kernel, 8-column-aligned operand)
+        r2, r_ld = None, 0
+        if res is not None:
+            r2 = res.reshape(M, N)
+            if r2.dtype not in (torch.bfloat16, torch.float32):
+                r2 = r2.float()
+            if not (r2.stride(1) == 1 and r2.stride(0) % 8 == 0 and r2.data_ptr() % 16 == 0):
+                r2 = r2.contiguous()
+            r_ld = r2.stride(0)
+            if nw != 1 or od != torch.bfloat16 or N % 8:
+                r2 = None
         cnt = hip.gemm(xb, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=sB, sC=N,
-                       bias=bias, sBias=0, relu=relu, psum=partials)
+                       bias=bias, sBias=0, relu=relu, psum=partials, res=r2, res_ld=r_ld)
         ys = [out[:, i * N:(i + 1) * N].view(tuple(lead) + (N,)) for i in range(nw)]
+        if res is not None and r2 is None:
+            ys = [ys[0] + res.to(ys[0].dtype)]
+            partials = None
         if partials is not None and cnt > 0 and od == out_dtype:
             hip._register_psum(ys[0], partials, cnt)
         if od != out_dtype:
             ys = [y.to(out_dtype) for y in ys]
+        if relu and od == torch.bfloat16:
+            for y in ys:
+                _register(_RELU_OUT, y)
+        # this dense's input is a ReLU output: its dX GEMM can apply that ReLU's backward mask
+        ctx.premask = bool(xb.dtype == torch.bfloat16 and K % 8 == 0 and _is_relu_out(xb))
+        ctx.has_res = res is not None
         ctx.save_for_backward(xb, b, *ws, *(ys if relu else []))
         ctx.meta = (lead, K, M, N, nw, relu, x.dtype, b is not None)
         return tuple(ys)
@@ -123,6 +183,8 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *dys):
         lead, K, M, N, nw, relu, xdtype, has_b = ctx.meta
+        # the residual's gradient is the output gradient itself (y = dense(x) + res)
+        dres = dys[0] if (ctx.has_res and ctx.needs_input_grad[2]) else None
         saved = ctx.saved_tensors
         xb, b = saved[0], saved[1]
         ws = saved[2:2 + nw]
@@ -138,7 +200,7 @@ class _Linear(torch.autograd.Function):
         from ..parallel import data as _dp
         wire = _dp.active_wire_dtype() == torch.bfloat16
         joint = joint_bf16 = None
-        if (nw == 1 and want_db and ctx.needs_input_grad[4] and dys[0] is not None and M % 64 == 0 and not relu
+        if (nw == 1 and want_db and ctx.needs_input_grad[5] and dys[0] is not None and M % 64 == 0 and not relu
                 and b.dtype == torch.float32 and ws[0].dtype == torch.float32 and dys[0].is_cuda
                 and dys[0].numel() > 0 and all(st == 0 for st in dys[0].stride())):
             joint = torch.empty((K * N + N,), dtype=torch.float32, device=dev)
@@ -146,6 +208,10 @@ class _Linear(torch.autograd.Function):
         for i, dy in enumerate(dys):
             if dy is None:
                 mats.append(None)
+                continue
+            if relu and _premasked_by(dy, ys[i]):
+                # the consumer's dX GEMM already applied this ReLU's mask
+                mats.append(_row_view(dy, M, N))
                 continue
             if relu:
                 d2, y2 = dy.reshape(M, N), ys[i].reshape(M, N)
@@ -178,13 +244,17 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0] and live:
             out_dt = torch.bfloat16 if (xdtype == torch.bfloat16 and len(live) == 1) else torch.float32
             dx = torch.empty((M, K), dtype=out_dt, device=dev)
+            premask = ctx.premask and out_dt == torch.bfloat16
             for j, i in enumerate(live):
                 t, ld = mats[i]
                 wn = shadow.get(ws[i], "N")                  # [K][N]: B[k=n][n'=k], k-contiguous
-                hip.gemm(t, wn, dx, M, K, N, ld, N, K, True, True, accumulate=j > 0)
+                hip.gemm(t, wn, dx, M, K, N, ld, N, K, True, True, accumulate=j > 0,
+                         res=xb if premask else None, res_ld=K, res_mode="mask")
             dx = dx.to(xdtype).view(tuple(lead) + (K,))
+            if premask:
+                _register(_PREMASKED, dx, xb.data_ptr())
         # ---- dW (MN-contiguous operands: X^T and dY read in place)
-        want = [i for i in live if ctx.needs_input_grad[4 + i]]
+        want = [i for i in live if ctx.needs_input_grad[5 + i]]
         if want:
             t0, ld0 = mats[want[0]]
             batched = (len(want) == nw and nw > 1 and ld0 > 0 and all(
@@ -250,7 +320,7 @@ class _Linear(torch.autograd.Function):
                 joint_bf16 = None  # the two gradients did not both land in the joint buffer
             if joint_bf16 is not None:
                 _dp.register_wire_twin(joint, joint_bf16)
-        return (dx, db, None, None, *dws)
+        return (dx, db, dres, None, None, *dws)
 
 
 def supported(x: torch.Tensor, ws: Sequence[torch.Tensor], b) -> bool:
@@ -263,5 +333,10 @@ def supported(x: torch.Tensor, ws: Sequence[torch.Tensor], b) -> bool:
 
 
 def linear(x: torch.Tensor, ws: List[torch.Tensor], b: Optional[torch.Tensor], relu: bool,
-           out_dtype: torch.dtype) -> List[torch.Tensor]:
-    return list(_Linear.apply(x, b, relu, out_dtype, *ws))
+           out_dtype: torch.dtype, residual: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
+    if residual is not None and (relu or len(ws) != 1):
+        # the epilogue adds the residual after the activation; a ReLU dense keeps its own output
+        # for the backward mask, so that combination adds separately
+        ys = list(_Linear.apply(x, b, None, relu, out_dtype, *ws))
+        return [ys[0] + residual.to(ys[0].dtype)] + ys[1:]
+    return list(_Linear.apply(x, b, residual, relu, out_dtype, *ws))
