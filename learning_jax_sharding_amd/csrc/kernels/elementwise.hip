@@ -265,21 +265,38 @@ __global__ void colsum_ticket_kernel(const bf16_t* __restrict__ in, int R, int C
 #pragma unroll
   for (int k = 0; k < 8; ++k) red[rl][cl * 8 + k] = acc[k];
   __syncthreads();
+  __shared__ int last_s;
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
     float s = 0.f;
     for (int r = 0; r < 32; ++r) s += red[r][lane];
-    const int c = blockIdx.x * 64 + lane;
     if (c < C) sc1_store(partials + (long)blockIdx.y * C + c, s);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int last = 0;
-    if (lane == 0) last = ticket_last(tickets + blockIdx.x, gridDim.y);
-    last = __shfl(last, 0, 64);
-    if (last && c < C) {
-      float v = 0.f;
-      for (int y = 0; y < (int)gridDim.y; ++y) v += sc1_load(partials + (long)y * C + c);
-      out[c] = accumulate ? out[c] + v : v;
+    if (lane == 0) last_s = ticket_last(tickets + blockIdx.x, gridDim.y);
+  }
+  __syncthreads();
+  if (!last_s) return;
+  // the last block of this column block sums the gy partial rows: 4 row slices x 64 columns,
+  // 8 independent loads in flight per thread (a dependent chain of gy loads took ~20 us)
+  const int gy = gridDim.y;
+  float v = 0.f;
+  if (c < C) {
+    int y = sl;
+    for (; y + 28 < gy; y += 32) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = sc1_load(partials + (long)(y + 4 * u) * C + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += t[u];
     }
+    for (; y < gy; y += 4) v += sc1_load(partials + (long)y * C + c);
+  }
+  red[sl][lane] = v;
+  __syncthreads();
+  if (threadIdx.x < 64 && c < C) {
+    const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    out[c] = accumulate ? out[c] + s : s;
   }
 }
 

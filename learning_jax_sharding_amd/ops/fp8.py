@@ -150,10 +150,11 @@ def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: torch.Tensor, bias: Opt
 
 
 class _Fp8Linear(torch.autograd.Function):
-    """Forward on MX-fp8 MFMA; backward = :class:`.linear._Linear`'s bf16 backward (same ctx)."""
+    """Forward on MX-fp8 MFMA; backward = :class:`.linear._Linear`'s bf16 backward (same ctx and
+    input layout: ``res`` is always None here)."""
 
     @staticmethod
-    def forward(ctx, x, b, relu, out_dtype, w):
+    def forward(ctx, x, b, res, relu, out_dtype, w):
         lead = x.shape[:-1]
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
@@ -170,6 +171,8 @@ class _Fp8Linear(torch.autograd.Function):
         xb = _bf16(x2 if x2.is_contiguous() else x2.contiguous())
         ctx.save_for_backward(xb, b, w, *([y] if relu else []))
         ctx.meta = (lead, K, M, N, 1, relu, x.dtype, b is not None)
+        ctx.has_res = False
+        ctx.premask = False
         return y
 
     @staticmethod
@@ -214,7 +217,7 @@ def linear_fp8(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], relu
     if x.is_cuda:
         if not supported(x, w):
             raise ValueError(f"fp8 dense needs K % 128 == 0 and N % 8 == 0, got x {tuple(x.shape)} w {tuple(w.shape)}")
-        return _Fp8Linear.apply(x, b, relu, out_dtype, w)
+        return _Fp8Linear.apply(x, b, None, relu, out_dtype, w)
     return _Fp8LinearRef.apply(x, b, relu, out_dtype, w)
 
 
