@@ -962,7 +962,10 @@ LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, v
       else hipLaunchKernelGGL(attn_fwd_pers_kernel<8>, dim3(grid), dim3(512), 0, stream, a, items);
       return (int)hipGetLastError();
     }
-    const int nw = g_fwd_res == 16 ? 16 : g_fwd_res == 8 ? 8 : 4;
+    int nw = g_fwd_res == 16 ? 16 : g_fwd_res == 8 ? 8 : 4;
+    // 8 waves x 16 queries per block leave CUs idle below 256 blocks (B*H = 64 at the
+    // reference shape): 4-wave blocks there (B=8: step 0.1069 -> 0.1057 ms)
+    if (nw == 8 && (Sq + 127) / 128 * H * B < 256) nw = 4;
     const int nqb = (Sq + 16 * nw - 1) / (16 * nw);
     if (nw == 16) hipLaunchKernelGGL(attn_fwd_res_kernel<16>, dim3(nqb * H * B), dim3(1024), 0, stream, a);
     else if (nw == 8) hipLaunchKernelGGL(attn_fwd_res_kernel<8>, dim3(nqb * H * B), dim3(512), 0, stream, a);

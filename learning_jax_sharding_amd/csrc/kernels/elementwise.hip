@@ -491,9 +491,8 @@ struct AdamTensor {
   long p, g, m, v, st, sn, R, C, g_bf16, tiles_c, vec;  // vec: 4-wide path allowed (C % 4, alignment)
 };
 constexpr int kAdamMax = 32;
-// rows per Adam tile (x 64 columns); 32 (twice the workgroups) measured 8.1 vs 8.5 us alone but
-// no better inside the train step, so 64 stays
-constexpr int kAdamRows = 64;
+// rows per Adam tile (x 64 columns): a template parameter (LJS_ADAM_ROWS = 16 / 32 / 64); smaller
+// tiles give more, shorter workgroups (a ragged last round of 64-row tiles idles most CUs)
 struct AdamBatch {
   AdamTensor t[kAdamMax];
   int tile_start[kAdamMax + 1];
@@ -502,6 +501,7 @@ struct AdamBatch {
 
 // `step_offset`/`ticket`: with a ticket the kernel uses t = *step + step_offset and its last
 // arriving block stores *step + 1 (the optimizer's count increment, folded in: no extra launch).
+template <int kAdamRows>
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* __restrict__ step, int step_offset,
                                                          unsigned* __restrict__ ticket, float lr, float b1, float b2,
                                                          float eps, float wd) {
@@ -917,6 +917,8 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
                            float b2, float eps, float wd, hipStream_t s) {
   if (n < 1 || n > kAdamMax) return (int)hipErrorInvalidValue;
   AdamBatch b;
+  static const int rows = getenv("LJS_ADAM_ROWS") ? atoi(getenv("LJS_ADAM_ROWS")) : 64;
+  const int kAdamRows = rows == 16 || rows == 32 ? rows : 64;
   int tiles = 0;
   for (int i = 0; i < n; ++i) {
     const long* r = table + 10 * i;
@@ -933,7 +935,14 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   b.tile_start[n] = tiles;
   b.n = n;
   if (ticket && 1 + (tiles + 31) / 32 > (64 << 10) / 4) return (int)hipErrorInvalidValue;  // ticket words
-  hipLaunchKernelGGL(adam_multi_kernel, dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset, (unsigned*)ticket,
-                     lr, b1, b2, eps, wd);
+  if (kAdamRows == 16)
+    hipLaunchKernelGGL(adam_multi_kernel<16>, dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, lr, b1, b2, eps, wd);
+  else if (kAdamRows == 32)
+    hipLaunchKernelGGL(adam_multi_kernel<32>, dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, lr, b1, b2, eps, wd);
+  else
+    hipLaunchKernelGGL(adam_multi_kernel<64>, dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, lr, b1, b2, eps, wd);
   return (int)hipGetLastError();
 }

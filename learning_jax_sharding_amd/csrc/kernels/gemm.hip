@@ -709,6 +709,16 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
   LJS_DMA_INST(128, 128, 2, 2, NST, false, true, false) LJS_DMA_INST(128, 128, 2, 2, NST, false, true, true)
 LJS_DMA_INST_LAYOUTS(2)
 LJS_DMA_INST_LAYOUTS(4)
+// 64x64 tiles (4 waves of 32x32, 3 or 4 stages): the small-M GEMMs of the reference shape
+// (2048 tokens), where 128x128 tiles leave most CUs idle
+#define LJS_DMA_INST_64(NST)                                                                               \
+  LJS_DMA_INST(64, 64, 2, 2, NST, true, true, false) LJS_DMA_INST(64, 64, 2, 2, NST, true, true, true)     \
+  LJS_DMA_INST(64, 64, 2, 2, NST, false, false, false) LJS_DMA_INST(64, 64, 2, 2, NST, false, false, true) \
+  LJS_DMA_INST(64, 64, 2, 2, NST, true, false, false) LJS_DMA_INST(64, 64, 2, 2, NST, true, false, true)   \
+  LJS_DMA_INST(64, 64, 2, 2, NST, false, true, false) LJS_DMA_INST(64, 64, 2, 2, NST, false, true, true)
+LJS_DMA_INST_64(3)
+LJS_DMA_INST_64(4)
+#undef LJS_DMA_INST_64
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, false)
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, true)
 // 128x160 with 4 waves stacked along M (32x160 each): N = 640 splits into 4 column tiles, so a
@@ -851,6 +861,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if (tile > 1000 && !(dma_ok && dma_store_ok)) tile = 128;
   // the LDS-DMA kernels carry the epilogue operand in their k-contiguous bf16 variants only
   if ((flags & (kResAdd | kResMask)) && tile > 1000 && !(a_kc && b_kc)) tile = 128;
+  if ((flags & (kResAdd | kResMask)) && (tile == 643 || tile == 644)) tile = 64;
+  if ((tile == 643 || tile == 644) && !(dma_ok && dma_store_ok)) tile = 64;
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
   if (tile == 1602 && !(a_kc && b_kc && !out_f32 && a.splitk == 1)) tile = 1282;
   if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;
@@ -878,6 +890,20 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     } else {
       if (d4) e = launch_dma_kk<128, 128, 2, 4, 4>(a, stream);
       else e = launch_dma_kk<128, 128, 2, 4, 3>(a, stream);
+    }
+  } else if (tile == 643 || tile == 644) {
+    if (a_kc && b_kc && !out_f32 && (flags & (kResAdd | kResMask))) {
+      e = hipErrorInvalidValue;  // no epilogue-operand variant at 64x64: use the register-staged tile
+    } else {
+#define LJS_DMA(AK, BK_, OF)                                                                   \
+  if (a_kc == AK && b_kc == BK_ && out_f32 == OF) {                                            \
+    if (tile == 644) return (int)launch_dma<64, 64, 2, 2, 4, AK, BK_, OF>(a, stream, 0);       \
+    return (int)launch_dma<64, 64, 2, 2, 3, AK, BK_, OF>(a, stream, 0);                        \
+  }
+      LJS_DMA(1, 1, 0) LJS_DMA(1, 1, 1) LJS_DMA(0, 0, 0) LJS_DMA(0, 0, 1)
+      LJS_DMA(1, 0, 0) LJS_DMA(1, 0, 1) LJS_DMA(0, 1, 0) LJS_DMA(0, 1, 1)
+#undef LJS_DMA
+      e = hipErrorInvalidValue;
     }
   } else if (tile == 1284 || tile == 1282) {
     // (plain if/else, not ?: -- see the explicit-instantiation note above)

@@ -255,7 +255,26 @@ def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f3
         if _TILE_2561 and a_kc and b_kc and not out_f32 and M >= 4096 and N * batch >= 1024 and N % 128 == 0:
             return 2561
         return 1282
+    if K % 64 == 0 and a_kc and b_kc and (out_f32 or (N % 8 == 0 and ldc % 8 == 0)):
+        # few 128x128 tiles (the 2048-token reference shape): the 64x64 LDS-DMA tile, 4 stages
+        # (out-projection 7.8 -> 7.0 us, its dX 8.0 -> 6.3 us vs the register-staged 64x64 tile;
+        # scripts/gemm_small.py)
+        return 644
     return 128 if tiles128 >= 160 else 64
+
+
+def pick_dw_slabs(K: int, N: int, T: int):
+    """(tile, K-chunks) of a weight-gradient slab GEMM [K, N] = X^T dY over T tokens: 128x128 tiles
+    with ~512 work items at large T; at T <= 4096 the 64x64 tile with the largest power-of-two
+    split keeping <= 512 items and >= 512 tokens per chunk (dWo at 2048 tokens: 14.8 -> 11.5 us,
+    dW[q|k|v] 25.6 -> 19.1 us with the combine; scripts/gemm_small.py)."""
+    if T > 4096 or K % 64 or N % 64:
+        return 1282, pick_splitk_dma(K, N, T, 1)
+    tiles = (K // 64) * (N // 64)
+    s = 1
+    while tiles * s * 2 <= 512 and T % (64 * s * 2) == 0 and T // (s * 2) >= 512:
+        s *= 2
+    return 644, s
 
 
 def pick_splitk_dma(M: int, N: int, K: int, batch: int) -> int:

@@ -33,7 +33,7 @@ def _stored(mat, kc_rowmajor: bool):
 
 @pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (0, 0), (1, 0), (0, 1)])
 @pytest.mark.parametrize("out_f32", [0, 1])
-@pytest.mark.parametrize("tile", [64, 128, 2561, 1284, 1282, 12883, 12884, 1602])
+@pytest.mark.parametrize("tile", [64, 128, 2561, 1284, 1282, 12883, 12884, 1602, 643, 644])
 @pytest.mark.parametrize("M,N,K", [(256, 192, 320), (136, 72, 40), (512, 1536, 640), (304, 136, 128), (384, 640, 512)])
 def test_gemm_layouts(hip, a_kc, b_kc, out_f32, tile, M, N, K):
     A = _rand(M, K, seed=1)
