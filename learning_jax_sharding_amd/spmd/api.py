@@ -177,7 +177,7 @@ class Jitted:
             return cap.out_tree
         dyn, static = self._split(args)
         sig = self._signature(dyn, static)
-        if not self.capture or kwargs or not torch.cuda.is_available():
+        if not self.capture or kwargs or not torch.cuda.is_available() or _spans_gpus():
             # Python side effects (print) run once per signature, as at JAX trace time
             n = self._calls.get(sig, 0)
             self._calls[sig] = n + 1
@@ -319,6 +319,14 @@ def reduce_replica_grads(pairs: List[Tuple[ShardedArray, Dict[int, torch.Tensor]
                     out[i][d] = red[d][off:off + n].view(t.shape)
                     off += n
     return out  # type: ignore
+
+
+def _spans_gpus() -> bool:
+    """Single-controller run over several physical GPUs: one HIP graph captures one device's
+    stream only, so such a step runs eagerly (its collectives are grouped RCCL calls across the
+    GPUs, comm/native.py).  One process per GPU (torchrun) captures each rank's step."""
+    from ..runtime.devices import local_devices
+    return len({d.torch_device.index for d in local_devices() if d.platform == "gpu"}) > 1
 
 
 _SEEDS: Dict[Tuple, torch.Tensor] = {}
