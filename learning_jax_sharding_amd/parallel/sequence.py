@@ -18,6 +18,8 @@ Two schedules are provided on (batch, seq, heads, head_dim) arrays whose seq dim
 
 Memory per device is O(S/n) for K/V instead of O(S), the stepping stone to long-context
 training on 288 GB parts; on xGMI the hop is a point-to-point neighbour transfer, one link.
+Each hop's K/V transfer is issued on a side HIP stream before the current block's flash
+kernel and joined after it, so the transfer overlaps the attention compute.
 """
 from __future__ import annotations
 
@@ -62,6 +64,46 @@ def _rotate(xs: Dict[int, torch.Tensor], nxt: Dict[int, int]) -> Dict[int, torch
     return C._run(C._Spec("exchange", transfers=transfers, out_meta=meta), xs)
 
 
+_SIDE: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _rotate_async(bufs: List[Dict[int, torch.Tensor]], nxt: Dict[int, int]):
+    """Start the next ring hop of every dict in ``bufs`` on a side HIP stream per GPU (after the
+    current stream's producers), so the hop overlaps the attention block computed meanwhile on
+    the compute stream.  Returns a thunk that makes the compute stream wait for the hop and
+    hands back the rotated dicts (host devices: the hop simply runs)."""
+    t0 = next(iter(bufs[0].values()))
+    if not t0.is_cuda:
+        out = [_rotate(b, nxt) for b in bufs]
+        return lambda: out
+    gpus = sorted({t.device.index for b in bufs for t in b.values()})
+    events = []
+    for g in gpus:
+        side = _SIDE.get(g)
+        if side is None:
+            side = _SIDE[g] = torch.cuda.Stream(device=g)
+        side.wait_stream(torch.cuda.current_stream(g))
+    streams = [_SIDE[g] for g in gpus]
+    # one process drives each GPU's side stream in turn; a single-GPU run (virtual devices or
+    # one rank per GPU) has exactly one
+    with torch.cuda.stream(streams[0]):
+        out = [_rotate(b, nxt) for b in bufs]
+        for g, st in zip(gpus, streams):
+            ev = torch.cuda.Event()
+            ev.record(st)
+            events.append((g, ev))
+
+    def join():
+        for g, ev in events:
+            cur = torch.cuda.current_stream(g)
+            cur.wait_event(ev)
+        for b in out:
+            for t in b.values():
+                t.record_stream(torch.cuda.current_stream(t.device))
+        return out
+    return join
+
+
 def _merge(o, lse, o_s, lse_s):
     """Merge two partial attention results (o normalised per part, lse in log2)."""
     neg = torch.full_like(lse, float("-inf"))
@@ -91,6 +133,8 @@ class _RingAttention(torch.autograd.Function):
         lse = {d: None for d in devs}
         kb, vb = dict(kk), dict(vv)
         for s in range(n):
+            # hop s+1's K/V transfer runs on the side stream while block s computes
+            pending = _rotate_async([kb, vb], nxt) if s + 1 < n else None
             for d in devs:
                 j = (pos[d] - s) % n                       # global block index of the kv in hand
                 if causal and j > pos[d]:
@@ -100,8 +144,8 @@ class _RingAttention(torch.autograd.Function):
                     o[d], lse[d] = o_s.float(), l_s
                 else:
                     o[d], lse[d] = _merge(o[d], lse[d], o_s, l_s)
-            if s + 1 < n:
-                kb, vb = _rotate(kb, nxt), _rotate(vb, nxt)
+            if pending is not None:
+                kb, vb = pending()
         outs = []
         for d in devs:
             if o[d] is None:                                # only possible for n == 0
@@ -130,6 +174,9 @@ class _RingAttention(torch.autograd.Function):
         dk = {d: torch.zeros(kb[d].shape, dtype=torch.float32, device=kb[d].device) for d in devs}
         dv = {d: torch.zeros(vb[d].shape, dtype=torch.float32, device=vb[d].device) for d in devs}
         for s in range(n):
+            # the next K/V blocks travel on the side stream during this block's backward; the
+            # gradient accumulators follow once this block has added to them
+            pending = _rotate_async([kb, vb], nxt) if s + 1 < n else None
             for d in devs:
                 j = (pos[d] - s) % n
                 if causal and j > pos[d]:
@@ -142,8 +189,8 @@ class _RingAttention(torch.autograd.Function):
             # the kv blocks and their gradient accumulators travel together; n hops bring
             # every accumulator back to the block's owner
             dk, dv = _rotate(dk, nxt), _rotate(dv, nxt)
-            if s + 1 < n:
-                kb, vb = _rotate(kb, nxt), _rotate(vb, nxt)
+            if pending is not None:
+                kb, vb = pending()
         grads = [dq[d].to(q[d].dtype) for d in devs] + [dk[d].to(kb[d].dtype) for d in devs] + \
             [dv[d].to(vb[d].dtype) for d in devs]
         return (None, None) + tuple(grads)
