@@ -127,7 +127,12 @@ struct F8Args {
   const void* bias;
   long ldc;
   int M, N, K;
-  int flags;  // 1 relu, 2 bias, 4 bias f32, 32 f32 output
+  int flags;  // 1 relu, 2 bias, 4 bias f32, 32 f32 output, 64 residual add, 128 ReLU mask (R > 0),
+              // 256 quantized output copy (QC / SC)
+  const bf16_t* R;      // epilogue operand [M][N] bf16, row stride ldr (ldr 0: one broadcast row)
+  long ldr;
+  unsigned char* QC;    // MX-fp8 copy of the (bf16-rounded) output: QC[M][N] e4m3, SC[M][N/32] e8m0
+  unsigned char* SC;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t f8_rsrc(const void* base, long bytes) {
@@ -141,17 +146,34 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t f8_rsrc(const void* base, long
 // 16-byte chunk c of a 128-byte LDS row, XOR-swizzled (conflict-free row reads)
 __device__ __forceinline__ int f8_swz(int row, int c) { return c ^ ((row >> 1) & 7); }
 
-constexpr int F8_TILE = 128 * F8_BK;           // bytes of one operand tile
-constexpr int F8_STAGE = 2 * F8_TILE + 2 * 512;  // A, B tiles + A, B scale words (128 rows x 4 B)
+// device-only wrappers of the gfx950 builtins (called from a kernel TEMPLATE, whose body the host
+// pass also instantiates)
+__device__ __forceinline__ void f8_dma(__amdgpu_buffer_rsrc_t rs, void* lds, int bytes, int voff, int soff) {
+  if (bytes == 16) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_PTR(void))lds, 16, voff, soff, 0, 0);
+  else __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_PTR(void))lds, 4, voff, soff, 0, 0);
+}
+__device__ __forceinline__ f32x4 f8_mfma(const i32x8& a, const i32x8& b, const f32x4& c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+}
 
-__global__ __launch_bounds__(256) void gemm_mx_fp8_kernel(F8Args p) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * F8_STAGE];
+// BM x 128 output tile, BM / 64 x 2 waves of 64 x 64 (BM = 128: 4 waves; 256: 8 waves, two per
+// SIMD), BK = 128 (one MFMA K step per K-tile), an NST-deep ring of LDS-DMA stages (A and B
+// tiles + the per-row scale words), counted vmcnt, one raw barrier per K-tile.
+template <int BM, int NST>
+__global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
+  constexpr int NW = BM / 32;                      // waves (BM / 64 rows x 2 cols)
+  constexpr int A_TILE = BM * F8_BK, B_TILE = 128 * F8_BK;
+  constexpr int STAGE = A_TILE + B_TILE + BM * 4 + 128 * 4;
+  constexpr int PA = BM / 8 / NW, PB = 16 / NW;    // 1 KiB data pieces per wave (A, B)
+  constexpr int L = PA + PB + 1;                   // DMA instructions per wave per K-tile (+1 scale)
+  static_assert(PA >= 1 && PB >= 1 && L * (NST - 1) <= 63, "piece split");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NST * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
   const int ntn = (p.N + 127) / 128;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (tile / ntn) * 128, n0 = (tile % ntn) * 128;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * 128;
   if (m0 >= p.M) return;
   const int KB = p.K / 32;  // scale bytes per row
   const int nk = p.K / F8_BK;
@@ -161,34 +183,40 @@ __global__ __launch_bounds__(256) void gemm_mx_fp8_kernel(F8Args p) {
   const __amdgpu_buffer_rsrc_t rsa = f8_rsrc(p.SA, (long)p.M * KB);
   const __amdgpu_buffer_rsrc_t rsb = f8_rsrc(p.SB, (long)p.N * KB);
 
-  // data pieces: 16 per operand tile (8 rows x 128 B each), 4 per wave per operand
-  int voa[4], vob[4];
+  int voa[PA], vob[PB];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = wave + 4 * i;
+  for (int i = 0; i < PA; ++i) {
+    const int q = wave + NW * i;
     const int row = 8 * q + (lane >> 3), slot = lane & 7;
-    const int c = f8_swz(row, slot);
-    voa[i] = (m0 + row) * p.K + 16 * c;
-    vob[i] = (n0 + row) * p.K + 16 * c;
+    voa[i] = (m0 + row) * p.K + 16 * f8_swz(row, slot);
   }
-  // scale pieces (4 B per lane, 64 rows per instruction): wave 0,1 -> A rows 0-63,64-127;
-  // wave 2,3 -> B rows
-  const int srow = 64 * (wave & 1) + lane;
-  const int vos = ((wave < 2 ? m0 : n0) + srow) * KB;
-  const __amdgpu_buffer_rsrc_t rs = wave < 2 ? rsa : rsb;
-
-  auto issue = [&](int kt, int st) {
-    unsigned char* base = smem + st * F8_STAGE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = wave + 4 * i;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_PTR(void))(base + q * 1024), 16, voa[i], kt * F8_BK, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_PTR(void))(base + F8_TILE + q * 1024), 16, vob[i],
-                                               kt * F8_BK, 0, 0);
-    }
-    unsigned char* sbase = base + 2 * F8_TILE + (wave < 2 ? 0 : 512) + 256 * (wave & 1);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_PTR(void))sbase, 4, vos, kt * 4, 0, 0);
-  };
+  for (int i = 0; i < PB; ++i) {
+    const int q = wave + NW * i;
+    const int row = 8 * q + (lane >> 3), slot = lane & 7;
+    vob[i] = (n0 + row) * p.K + 16 * f8_swz(row, slot);
+  }
+  // scale words (4 B per lane = one row's 4 scale bytes of a K-tile, 64 rows per instruction):
+  // the first BM / 64 waves load A's, the next two B's, any further waves repeat B's (same
+  // bytes to the same place) so every wave issues exactly one and vmcnt counts stay uniform
+  const int sw = wave < BM / 64 ? wave : (BM / 64 + ((wave - BM / 64) & 1));
+  const bool s_is_a = sw < BM / 64;
+  const int s_row = 64 * (s_is_a ? sw : sw - BM / 64) + lane;
+  const int vos = ((s_is_a ? m0 : n0) + s_row) * KB;
+  const __amdgpu_buffer_rsrc_t rs = s_is_a ? rsa : rsb;
+  const int s_dst = s_is_a ? 64 * 4 * sw : BM * 4 + 64 * 4 * (sw - BM / 64);
+
+  // (a macro, not a lambda: a lambda in a kernel template is also instantiated for the host,
+  // where the LDS-DMA builtin does not exist)
+#define F8_ISSUE(KT, ST)                                                                           \
+  do {                                                                                             \
+    unsigned char* base_ = smem + (ST) * STAGE;                                                    \
+    _Pragma("unroll") for (int i_ = 0; i_ < PA; ++i_)                                              \
+        f8_dma(ra, base_ + (wave + NW * i_) * 1024, 16, voa[i_], (KT) * F8_BK);                    \
+    _Pragma("unroll") for (int i_ = 0; i_ < PB; ++i_)                                              \
+        f8_dma(rb, base_ + A_TILE + (wave + NW * i_) * 1024, 16, vob[i_], (KT) * F8_BK);           \
+    f8_dma(rs, base_ + A_TILE + B_TILE + s_dst, 4, vos, (KT) * 4);                                 \
+  } while (0)
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -196,16 +224,24 @@ __global__ __launch_bounds__(256) void gemm_mx_fp8_kernel(F8Args p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) F8_ISSUE(s, s);
   const int g = lane >> 4, r16 = lane & 15;
   for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // K-tile kt landed (this wave's pieces); the younger stages may stay in flight
+    if constexpr (NST >= 3) {
+      if (kt + NST - 2 >= nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const unsigned char* As_ = smem + (kt & 1) * F8_STAGE;
-    const unsigned char* Bs_ = As_ + F8_TILE;
-    const unsigned* Sa = reinterpret_cast<const unsigned*>(As_ + 2 * F8_TILE);
-    const unsigned* Sb = reinterpret_cast<const unsigned*>(As_ + 2 * F8_TILE + 512);
+    const unsigned char* As_ = smem + (kt % NST) * STAGE;
+    const unsigned char* Bs_ = As_ + A_TILE;
+    const unsigned* Sa = reinterpret_cast<const unsigned*>(As_ + A_TILE + B_TILE);
+    const unsigned* Sb = reinterpret_cast<const unsigned*>(As_ + A_TILE + B_TILE + BM * 4);
     i32x8 af[4], bfr[4];
     int sa[4], sb[4];
 #pragma unroll
@@ -226,18 +262,19 @@ __global__ __launch_bounds__(256) void gemm_mx_fp8_kernel(F8Args p) {
     }
     // next stage's DMA after this K-tile's fragment reads: its issue time overlaps their LDS
     // latency and the MFMAs (as in the bf16 LDS-DMA GEMM)
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    if (kt + NST - 1 < nk) F8_ISSUE(kt + NST - 1, (kt + NST - 1) % NST);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)  // C^T block: B rows as the MFMA A operand
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0, 0, 0, sb[j], 0,
-                                                                     sa[i]);
+        acc[i][j] = f8_mfma(bfr[j], af[i], acc[i][j], sb[j], sa[i]);
   }
 
   // epilogue: lane holds C[row 16 i + r16][cols 16 j + 4 g .. +3]; lane pairs (g, g^1) trade
-  // halves -> 8 consecutive columns per lane -> one 16-byte (bf16) / 2 x 16-byte (f32) store
+  // halves -> 8 consecutive columns per lane -> one 16-byte (bf16) / 2 x 16-byte (f32) store.
+  // A 32-column MX block of a row sits in the 4 lanes r16, r16 + 16, + 32, + 48 (g = 0..3).
   const bool relu = p.flags & 1, has_bias = p.flags & 2, bias_f32 = p.flags & 4, out_f32 = p.flags & 32;
+  const bool res_add = p.flags & 64, res_mask = p.flags & 128, qout = p.flags & 256;
   const bool even = (g & 1) == 0;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -267,12 +304,47 @@ __global__ __launch_bounds__(256) void gemm_mx_fp8_kernel(F8Args p) {
         }
       }
       const int row = m0 + wr * 64 + 16 * i + r16;
-      if (row >= p.M || col >= p.N) continue;  // N % 8 == 0 (launcher)
+      const bool ok = row < p.M && col < p.N;  // N % 8 == 0 (launcher)
+      if ((res_add || res_mask) && ok) {
+        const u32x4 rw = *reinterpret_cast<const u32x4*>(p.R + (long)row * p.ldr + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float r0 = __uint_as_float(rw[e] << 16), r1 = __uint_as_float(rw[e] & 0xffff0000u);
+          if (res_add) {  // bf16(bf16(y) + R): the unfused bf16 add
+            v[2 * e] = bf2f(f2bf(v[2 * e])) + r0;
+            v[2 * e + 1] = bf2f(f2bf(v[2 * e + 1])) + r1;
+          } else {
+            v[2 * e] = r0 > 0.f ? v[2 * e] : 0.f;
+            v[2 * e + 1] = r1 > 0.f ? v[2 * e + 1] : 0.f;
+          }
+        }
+      }
+      if (qout) {
+        // MX-fp8 copy of the bf16-rounded outputs: block amax over the 4 lanes of the block,
+        // then each lane stores its 8 e4m3 bytes and lane g = 0 the block's e8m0 scale
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = bf2f(f2bf(v[e]));
+          amax = fmaxf(amax, fabsf(v[e]));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        const int x = mx_exponent(amax);
+        const float inv = ldexpf(1.f, -x);
+        if (ok) {
+          const u32x2 qq = u32x2{pack4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
+                                 pack4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv)};
+          *reinterpret_cast<u32x2*>(p.QC + (long)row * p.N + col) = qq;
+          if (g == 0) p.SC[(long)row * (p.N / 32) + col / 32] = (unsigned char)(x + 127);
+        }
+      }
+      if (!ok) continue;
       if (out_f32) {
         float* C = reinterpret_cast<float*>(p.C) + (long)row * p.ldc + col;
         *reinterpret_cast<f32x4*>(C) = f32x4{v[0], v[1], v[2], v[3]};
         *reinterpret_cast<f32x4*>(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
-      } else {
+      } else if (p.C) {
         u32x4 pk;
 #pragma unroll
         for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
@@ -280,6 +352,18 @@ __global__ __launch_bounds__(256) void gemm_mx_fp8_kernel(F8Args p) {
       }
     }
   }
+}
+
+#undef F8_ISSUE
+template __global__ void gemm_mx_fp8_kernel<128, 2>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<128, 3>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<256, 2>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<256, 3>(F8Args);
+
+template <int BM, int NST>
+hipError_t launch_f8(const F8Args& a, int tiles, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_mx_fp8_kernel<BM, NST>), dim3(tiles), dim3(BM * 2), 0, s, a);
+  return hipGetLastError();
 }
 
 // one wave, one block-scaled MFMA on raw per-lane operands (layout validation in the tests)
@@ -319,16 +403,32 @@ LJS_API int ljs_quant_mx_cols(const void* in, int is_bf16, long ld, int K, int N
   return (int)hipGetLastError();
 }
 
-// C[M][N] (bf16, or f32 with flags & 32) = A . B^T of MX-fp8 operands; K % 128 == 0, N % 8 == 0
+// C[M][N] (bf16, or f32 with flags & 32) = A . B^T of MX-fp8 operands; K % 128 == 0, N % 8 == 0.
+// R (bf16 [M][N], row stride ldr) with flags 64 / 128: residual add / ReLU mask in the epilogue;
+// QC / SC with flags 256: also an MX-fp8 copy of the output (N % 32 == 0).  tile: 1282 / 1283 /
+// 2562 / 2563 = BM x 128 with 2 or 3 stages (0: automatic).
 LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const void* SB, void* C, const void* bias,
-                            int M, int N, int K, long ldc, int flags, hipStream_t stream) {
+                            int M, int N, int K, long ldc, int flags, const void* R, long ldr, void* QC, void* SC,
+                            int tile, hipStream_t stream) {
   if (K % F8_BK || N % 8 || ldc % 8 || (long)M * K >= (1L << 31) || (long)N * K >= (1L << 31))
     return (int)hipErrorInvalidValue;
+  if ((flags & (64 | 128)) && (!R || ldr % 8 || (((uintptr_t)R) & 15) || (flags & 32)))
+    return (int)hipErrorInvalidValue;
+  if ((flags & 256) && (!QC || !SC || N % 32)) return (int)hipErrorInvalidValue;
   F8Args a;
   a.A = (const unsigned char*)A; a.B = (const unsigned char*)B;
   a.SA = (const unsigned char*)SA; a.SB = (const unsigned char*)SB;
   a.C = C; a.bias = bias; a.ldc = ldc; a.M = M; a.N = N; a.K = K; a.flags = flags;
-  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  hipLaunchKernelGGL(gemm_mx_fp8_kernel, dim3(tiles), dim3(256), 0, stream, a);
-  return (int)hipGetLastError();
+  a.R = (const bf16_t*)R; a.ldr = ldr; a.QC = (unsigned char*)QC; a.SC = (unsigned char*)SC;
+  if (tile == 0) {
+    // 256-row tiles (8 waves, 3 stages) once they still give >= 2 blocks per CU (256 CUs)
+    const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128);
+    tile = t256 >= 512 ? 2563 : 1282;
+  }
+  const int bm = tile / 10 >= 256 ? 256 : 128;
+  const int tiles = ((M + bm - 1) / bm) * ((N + 127) / 128);
+  if (tile == 1283) return (int)launch_f8<128, 3>(a, tiles, stream);
+  if (tile == 2562) return (int)launch_f8<256, 2>(a, tiles, stream);
+  if (tile == 2563) return (int)launch_f8<256, 3>(a, tiles, stream);
+  return (int)launch_f8<128, 2>(a, tiles, stream);
 }

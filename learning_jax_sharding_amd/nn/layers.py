@@ -90,8 +90,10 @@ class FeedForward(Module):
 
     Logical axes ``Win: ('embed','hidden')``, ``Wout: ('hidden','embed')`` so the
     declared rule ``('hidden','model')`` (``case6_attention.py:186``) shards the
-    hidden dim Megatron-style.  ``fp8=True`` runs both GEMMs on the CDNA4 fp8
-    (e4m3) MFMA path with per-tensor scaling.
+    hidden dim Megatron-style.  ``fp8=True`` runs the GEMMs on CDNA4's MX-fp8 block-scaled MFMA
+    (e4m3 elements, e8m0 scales per 32 elements along K): with replicated weights the fused
+    block of :func:`ops.fp8.ff_block` (forward and backward-dX GEMMs in fp8), otherwise the two
+    forward GEMMs in fp8 with a bf16 backward.
     """
 
     hidden_dim: int
@@ -109,7 +111,12 @@ class FeedForward(Module):
                            (self.hidden_dim, d), torch.float32)
         dt = _dt.canonicalize(self.dtype)
         if self.fp8:
-            from ..ops.fp8 import fp8_dense
+            from ..ops.fp8 import ff_block, fp8_dense
+            if dt == torch.bfloat16 and w_in.tile.is_fully_replicated and w_out.tile.is_fully_replicated \
+                    and d % 128 == 0 and self.hidden_dim % 128 == 0:
+                # replicated weights (data-parallel / single device): the fused block, fp8
+                # forward and backward-dX GEMMs, quantized operands written by the producers
+                return ff_block(x, w_in, w_out, residual=residual)
             h = fp8_dense(x, w_in, relu=True, out_dtype=dt)
             h = with_logical_constraint(h, ("batch", "length", "hidden"))
             y = fp8_dense(h, w_out, relu=False, out_dtype=dt)

@@ -38,6 +38,7 @@ _SIGS = {
                           ctypes.c_void_p, ctypes.c_void_p],
     "ljs_gemm_mx_fp8": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int,
+                        ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                         ctypes.c_void_p],
 }
 _bound = False
@@ -139,12 +140,30 @@ def _weight_q(w: torch.Tensor):
     return q, s
 
 
-def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: torch.Tensor, bias: Optional[torch.Tensor] = None,
-            relu: bool = False) -> torch.Tensor:
+def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: Optional[torch.Tensor], bias: Optional[torch.Tensor] = None,
+            relu: bool = False, res: Optional[torch.Tensor] = None, res_mode: str = "add",
+            qout: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, tile: int = 0) -> Optional[torch.Tensor]:
+    """out[M][N] = qa . qb^T (MX-fp8 operands, f32 accumulation) (+bias)(relu); epilogue options:
+    ``res`` (bf16 [M][N]) added as a residual (``res_mode="add"``, bit-exact with the unfused bf16
+    add) or used as a ReLU mask (``"mask"``: keep where res > 0); ``qout = (q, s)`` also receives
+    the MX-fp8 quantization of the (bf16-rounded) output, blocks of 32 along N - the next GEMM's
+    operand without a quantization pass.  ``out`` may be None when only ``qout`` is wanted.
+    ``tile``: 1282 / 1283 / 2562 / 2563 (BM x 128, stages), 0 = automatic."""
+    od = out if out is not None else None
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
-        (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (32 if out.dtype == torch.float32 else 0)
-    rc = _lib().ljs_gemm_mx_fp8(hip._p(qa), hip._p(sa), hip._p(qb), hip._p(sb), hip._p(out), hip._p(bias), M, N, K,
-                                out.stride(0), flags, hip._stream(out))
+        (4 if (bias is not None and bias.dtype == torch.float32) else 0) | \
+        (32 if (od is not None and od.dtype == torch.float32) else 0)
+    ldr = 0
+    if res is not None:
+        assert res.dtype == torch.bfloat16 and res.stride(-1) == 1
+        flags |= 64 if res_mode == "add" else 128
+        ldr = res.stride(0) if res.dim() == 2 else N
+    q_o, s_o = qout if qout is not None else (None, None)
+    if qout is not None:
+        flags |= 256
+    rc = _lib().ljs_gemm_mx_fp8(hip._p(qa), hip._p(sa), hip._p(qb), hip._p(sb), hip._p(od), hip._p(bias), M, N, K,
+                                od.stride(0) if od is not None else N, flags, hip._p(res), ldr, hip._p(q_o),
+                                hip._p(s_o), tile, hip._stream(qa))
     hip._ck(rc, "gemm_mx_fp8")
     return out
 
@@ -226,3 +245,174 @@ def fp8_dense(x, w, bias=None, relu: bool = False, out_dtype=torch.bfloat16):
     partitioning (weight gathers, partial sums over a sharded contraction) is :func:`core.dense`'s."""
     from . import core
     return core.dense(x, [w], bias, compute_dtype=out_dtype, relu=relu, fp8=True)[0]
+
+
+# ----------------------------------------------------------------------------- fused FF block
+def _weight_q_rows(w: torch.Tensor):
+    """Cached MX quantization of ``w`` along its LAST dim (``quant_rows``), per weight version:
+    the B operand of a dX GEMM (``dX = dY W^T`` reads W's rows as [n][k])."""
+    key = ("rows", w.data_ptr(), tuple(w.shape), w.dtype, w.device)
+    ent = _WCACHE.get(key)
+    if ent is not None and ent[0] == w._version:
+        return ent[1], ent[2]
+    q, s = quant_rows(w.detach())
+    _WCACHE[key] = (w._version, q, s)
+    return q, s
+
+
+def _quant_grad_rows(dy2: torch.Tensor):
+    """MX-fp8 rows of a bf16 gradient; a broadcast row (stride 0, the cotangent of y.sum()) is
+    quantized once and its bytes repeated."""
+    if dy2.stride(0) == 0:
+        q1, s1 = quant_rows(dy2[:1].contiguous())
+        return q1.expand(dy2.shape[0], -1).contiguous(), s1.expand(dy2.shape[0], -1).contiguous()
+    return quant_rows(dy2)
+
+
+class _FFBlockFp8(torch.autograd.Function):
+    """``y = relu(x Win) Wout (+ res)`` with every FF GEMM that reads an activation on MX-fp8
+    block-scaled MFMA, forward AND backward dX:
+
+    * forward: x quantized per row; the up projection's epilogue writes the bf16 ReLU output
+      (kept for the backward) and its MX-fp8 copy (the down projection's operand: no
+      quantization pass); the down projection's epilogue adds the residual;
+    * backward: dY quantized per row; dA = dY Wout^T on fp8 with the ReLU mask (the saved a > 0)
+      and the MX-fp8 copy of dA written by its epilogue; dX = dA Win^T on fp8; the weight
+      gradients (reductions over tokens) stay bf16 split-K slabs, f32 accumulation.
+
+    Weights are quantized along K for the forward and along N for the dX GEMMs (cached per
+    weight version).  The host emulation :class:`_FFBlockFp8Ref` is the numerical oracle."""
+
+    @staticmethod
+    def forward(ctx, x, w_in, w_out, res):
+        from .linear import _dw_slabs  # noqa: F401  (backward)
+        lead = x.shape[:-1]
+        M = x.shape[-1]
+        F = w_in.shape[1]
+        x2 = _bf16(x.reshape(-1, M).contiguous())
+        T = x2.shape[0]
+        qx, sx = quant_rows(x2)
+        qwi, swi = _weight_q(w_in)                   # [F][M], blocks along M
+        a = torch.empty((T, F), dtype=torch.bfloat16, device=x.device)
+        qa = torch.empty((T, F), dtype=torch.uint8, device=x.device)
+        sa = torch.empty((T, F // BLOCK), dtype=torch.uint8, device=x.device)
+        gemm_mx(qx, sx, qwi, swi, T, F, M, a, relu=True, qout=(qa, sa))
+        qwo, swo = _weight_q(w_out)                  # [M][F], blocks along F
+        y = torch.empty((T, M), dtype=torch.bfloat16, device=x.device)
+        r2 = None
+        if res is not None:
+            r2 = _bf16(res.reshape(T, M).contiguous())
+        gemm_mx(qa, sa, qwo, swo, T, M, F, y, res=r2)
+        ctx.save_for_backward(x2, a, w_in, w_out)
+        ctx.meta = (lead, M, F, T, res is not None)
+        return y.view(tuple(lead) + (M,))
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .linear import _dw_slabs, _row_view
+        x2, a, w_in, w_out = ctx.saved_tensors
+        lead, M, F, T, has_res = ctx.meta
+        dev = x2.device
+        dy2 = dy.reshape(T, M)
+        if dy2.dtype != torch.bfloat16:
+            dy2 = dy2.to(torch.bfloat16)
+        qdy, sdy = _quant_grad_rows(dy2)
+        qwo_r, swo_r = _weight_q_rows(w_out)         # Wout [F][M] rows: blocks along M
+        dA = torch.empty((T, F), dtype=torch.bfloat16, device=dev)
+        qdA = torch.empty((T, F), dtype=torch.uint8, device=dev)
+        sdA = torch.empty((T, F // BLOCK), dtype=torch.uint8, device=dev)
+        gemm_mx(qdy, sdy, qwo_r, swo_r, T, F, M, dA, res=a, res_mode="mask", qout=(qdA, sdA))
+        dx = dwi = dwo = None
+        if ctx.needs_input_grad[0]:
+            qwi_r, swi_r = _weight_q_rows(w_in)      # Win [M][F] rows: blocks along F
+            dx = torch.empty((T, M), dtype=torch.bfloat16, device=dev)
+            gemm_mx(qdA, sdA, qwi_r, swi_r, T, M, F, dx)
+            dx = dx.view(tuple(lead) + (M,))
+        if ctx.needs_input_grad[2]:
+            t, ld = _row_view(dy2, T, M)
+            dwo = torch.empty((F, M), dtype=torch.float32, device=dev)
+            _dw_slabs(a, t, ld, T, F, M, dwo, M, 0)
+        if ctx.needs_input_grad[1]:
+            dwi = torch.empty((M, F), dtype=torch.float32, device=dev)
+            _dw_slabs(x2, dA, F, T, M, F, dwi, F, 0)
+        dres = dy if (has_res and ctx.needs_input_grad[3]) else None
+        return dx, dwi, dwo, dres
+
+
+class _FFBlockFp8Ref(torch.autograd.Function):
+    """Host emulation of :class:`_FFBlockFp8` (quantize -> dequantize -> f32 matmul, the same
+    roundings in the same places)."""
+
+    @staticmethod
+    def forward(ctx, x, w_in, w_out, res):
+        lead, M = x.shape[:-1], x.shape[-1]
+        x2 = x.reshape(-1, M).to(torch.bfloat16).float()
+        xd = dequantize_mx_ref(*quantize_mx_ref(x2))
+        wid = dequantize_mx_ref(*quantize_mx_ref(w_in.t().contiguous()))     # [F][M]
+        a = torch.relu(xd @ wid.t()).to(torch.bfloat16)
+        ad = dequantize_mx_ref(*quantize_mx_ref(a.float()))
+        wod = dequantize_mx_ref(*quantize_mx_ref(w_out.t().contiguous()))    # [M][F]
+        y = (ad @ wod.t()).to(torch.bfloat16)
+        if res is not None:
+            y = y + res.reshape(y.shape).to(torch.bfloat16)
+        ctx.save_for_backward(x2, a, w_in, w_out)
+        ctx.meta = (lead, M, res is not None)
+        return y.reshape(tuple(lead) + (M,))
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, a, w_in, w_out = ctx.saved_tensors
+        lead, M, has_res = ctx.meta
+        dy2 = dy.reshape(-1, M).to(torch.bfloat16).float()
+        dyd = dequantize_mx_ref(*quantize_mx_ref(dy2))
+        wod_r = dequantize_mx_ref(*quantize_mx_ref(w_out))                  # [F][M], blocks along M
+        dA = (dyd @ wod_r.t()).to(torch.bfloat16)
+        dA = torch.where(a > 0, dA, torch.zeros_like(dA))
+        dAd = dequantize_mx_ref(*quantize_mx_ref(dA.float()))
+        wid_r = dequantize_mx_ref(*quantize_mx_ref(w_in))                   # [M][F], blocks along F
+        dx = (dAd @ wid_r.t()).to(torch.bfloat16).reshape(tuple(lead) + (M,)) if ctx.needs_input_grad[0] else None
+        dwo = (a.float().t() @ dy2).to(w_out.dtype) if ctx.needs_input_grad[2] else None
+        dwi = (x2.t() @ dA.float()).to(w_in.dtype) if ctx.needs_input_grad[1] else None
+        dres = dy if (has_res and ctx.needs_input_grad[3]) else None
+        return dx, dwi, dwo, dres
+
+
+def ff_block_supported(x: torch.Tensor, w_in: torch.Tensor, w_out: torch.Tensor) -> bool:
+    M, F = w_in.shape
+    return (x.shape[-1] == M and tuple(w_out.shape) == (F, M) and M % 128 == 0 and F % 128 == 0
+            and M % 32 == 0 and F % 32 == 0)
+
+
+def ff_block_local(x: torch.Tensor, w_in: torch.Tensor, w_out: torch.Tensor,
+                   res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-shard fused MX-fp8 FF block (GPU kernels; exact emulation on host devices)."""
+    if not ff_block_supported(x, w_in, w_out):
+        raise ValueError(f"fp8 FF block needs M, F % 128 == 0: x {tuple(x.shape)} w_in {tuple(w_in.shape)}")
+    if x.is_cuda:
+        return _FFBlockFp8.apply(x, w_in, w_out, res)
+    return _FFBlockFp8Ref.apply(x, w_in, w_out, res)
+
+
+def ff_block(x, w_in, w_out, residual=None):
+    """Global-view fused fp8 FF block ``relu(x Win) Wout (+ residual)`` on sharded arrays: x keeps
+    its tiling (its feature dim gathered if split), the weights are used replicated (data / FSDP
+    meshes; a hidden dim split over a mesh axis takes the two-dense path in ``FeedForward``)."""
+    from ..sharding.tile import TileAssignment
+    from ..spmd.reshard import reshard_tile
+    from ..sharding.shardings import sharding_from_tile
+    from ..array import ShardedArray
+    from . import core
+    xt = x.tile
+    if xt.tile_shape[-1] > 1:
+        x = reshard_tile(x, xt.unshard([x.ndim - 1]), note="ff.x")
+        xt = x.tile
+    devs = xt.device_ids
+    wi = reshard_tile(w_in, TileAssignment.replicated(devs, 2), note="ff.w_in")
+    wo = reshard_tile(w_out, TileAssignment.replicated(devs, 2), note="ff.w_out")
+    r_loc = None
+    if residual is not None:
+        r_loc = reshard_tile(residual, xt, note="ff.residual").local
+    core._plan.record("ff_block", fp8=True, tiles=xt.tile_shape)
+    loc = {d: ff_block_local(x.local[d], wi.local[d], wo.local[d], r_loc[d] if r_loc is not None else None)
+           for d in x.local}
+    return ShardedArray(tuple(x.shape), torch.bfloat16, sharding_from_tile(xt, like=[x.sharding]), loc)

@@ -498,9 +498,10 @@ def test_fp8_quantization_matches_reference(hip):
     assert torch.equal(qc.cpu(), qr3.view(torch.uint8)) and torch.equal(sc.cpu().long(), (er3 + 127).long())
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (300, 136, 256), (1024, 2560, 640)])
+@pytest.mark.parametrize("tile", [1282, 1283, 2562, 2563])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (300, 136, 256), (1024, 2560, 640), (512, 640, 2560)])
 @pytest.mark.parametrize("bias,relu,out_f32", [(False, False, True), (True, True, False)])
-def test_fp8_gemm_matches_emulation(hip, M, N, K, bias, relu, out_f32):
+def test_fp8_gemm_matches_emulation(hip, M, N, K, bias, relu, out_f32, tile):
     from learning_jax_sharding_amd.ops import fp8 as F
     x = _rand(M, K, dtype=torch.float32, seed=42)
     w = _rand(K, N, dtype=torch.float32, seed=43) * 0.05
@@ -508,10 +509,37 @@ def test_fp8_gemm_matches_emulation(hip, M, N, K, bias, relu, out_f32):
     qa, sa = F.quant_rows(x)
     qb, sb = F.quant_cols(w)
     out = torch.empty((M, N), dtype=torch.float32 if out_f32 else torch.bfloat16, device=dev)
-    F.gemm_mx(qa, sa, qb, sb, M, N, K, out, b, relu)
+    F.gemm_mx(qa, sa, qb, sb, M, N, K, out, b, relu, tile=tile)
     ref = F.mx_linear_ref(x.cpu(), w.cpu(), None if b is None else b.cpu(), relu, out.dtype)
     tol = 1e-3 if out_f32 else 2e-2
     torch.testing.assert_close(out.float().cpu(), ref.float(), rtol=tol, atol=tol * 4)
+
+
+@pytest.mark.parametrize("tile", [1282, 2563])
+@pytest.mark.parametrize("mode", ["add", "mask", None])
+def test_fp8_gemm_epilogue_residual_mask_and_quantized_copy(hip, tile, mode):
+    """MX-fp8 GEMM epilogue: residual add / ReLU mask on a bf16 operand (bit-exact with the
+    unfused ops on the plain output) and the MX-fp8 copy of the output (== quant_rows of it)."""
+    from learning_jax_sharding_amd.ops import fp8 as F
+    M, N, K = 1024, 640, 512
+    qa, sa = F.quant_rows(_rand(M, K, dtype=torch.float32, seed=48))
+    qb, sb = F.quant_cols(_rand(K, N, dtype=torch.float32, seed=49) * 0.05)
+    plain = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    F.gemm_mx(qa, sa, qb, sb, M, N, K, plain, tile=tile)
+    R = _rand(M, N, seed=50)
+    if mode == "mask":
+        R = torch.relu(R)
+    out = torch.empty_like(plain)
+    q = torch.empty((M, N), dtype=torch.uint8, device=dev)
+    sc = torch.empty((M, N // 32), dtype=torch.uint8, device=dev)
+    F.gemm_mx(qa, sa, qb, sb, M, N, K, out, res=R if mode else None, res_mode=mode or "add", qout=(q, sc), tile=tile)
+    torch.cuda.synchronize()
+    # masked elements are +0 (as the bf16 GEMM's mask and relu_bwd write them)
+    ref = plain + R if mode == "add" else (torch.where(R > 0, plain, torch.zeros_like(plain)) if mode == "mask"
+                                           else plain)
+    assert torch.equal(out, ref)
+    q2, s2 = F.quant_rows(ref)
+    assert torch.equal(q, q2) and torch.equal(sc, s2)
 
 
 def test_fp8_linear_autograd(hip):
@@ -548,3 +576,41 @@ def test_native_runtime_device_info_and_single_member_comm(hip):
     nat.close()
     maps = open(f"/proc/{__import__('os').getpid()}/maps").read()
     assert "libljs_runtime.so" in maps
+
+
+@pytest.mark.parametrize("T,M,Fd,bcast", [(2048, 640, 2560, False), (1024, 256, 512, True)])
+def test_fp8_ff_block_matches_emulation(hip, T, M, Fd, bcast):
+    """Fused MX-fp8 FF block on the GPU (fp8 forward + fp8 dX GEMMs, epilogue-quantized
+    operands, fused residual / ReLU mask) == its host emulation, to f32 summation order."""
+    from learning_jax_sharding_amd.ops import fp8 as F
+    x = _rand(T, M, seed=60).requires_grad_()
+    wi = (_rand(M, Fd, dtype=torch.float32, seed=61) * 0.05).requires_grad_()
+    wo = (_rand(Fd, M, dtype=torch.float32, seed=62) * 0.03).requires_grad_()
+    res = _rand(T, M, seed=63).requires_grad_()
+    y = F.ff_block_local(x, wi, wo, res)
+    cot = torch.ones((), dtype=torch.bfloat16, device=dev).expand(T, M) if bcast else _rand(T, M, seed=64)
+    y.backward(cot)
+    xc, wic, woc, rc = (t.detach().cpu().requires_grad_() for t in (x, wi, wo, res))
+    yc = F.ff_block_local(xc, wic, woc, rc)
+    yc.backward(cot.cpu())
+    torch.testing.assert_close(y.float().cpu(), yc.float(), rtol=2e-2, atol=2e-2)
+    for got, want in ((x.grad, xc.grad), (wi.grad, wic.grad), (wo.grad, woc.grad), (res.grad, rc.grad)):
+        err = ((got.float().cpu() - want.float()).norm() / want.float().norm().clamp(min=1e-6)).item()
+        assert err < 2e-2, err
+
+
+def test_fp8_transformer_layer_trains(gpu_devices):
+    """TransformerLayer(fp8=True) takes the fused fp8 FF block and its train step runs."""
+    gpu_devices(1)
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd.models import TransformerLayer
+    from learning_jax_sharding_amd.spmd import plan as _plan
+    model = TransformerLayer(640, heads=8, dim_head=64, ff_dim=2560, fp8=True)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (2, 256, 640))
+    params = model.init(ljs.random.PRNGKey(1), x)["params"]
+    with _plan.record_plan() as rec:
+        val, g = ljs.value_and_grad(lambda p: model.apply({"params": p}, x).sum())(params)
+    torch.cuda.synchronize()
+    assert any(st.kind == "ff_block" for st in rec.steps)
+    leaves = ljs.tree_util.tree_leaves(ljs.nn.unbox(g))
+    assert all(torch.isfinite(l.to_torch()).all() for l in leaves)
