@@ -36,17 +36,9 @@ struct GemmArgs {
   float* psum;  // LDS-DMA kernels, bf16 out: per (item, wave) sums of the stored values, or null
   const void* res;  // R[b][row][col] at res + b * sR + row * ldr + col (ldr may be 0: one broadcast row)
   long ldr, sR;
-  // flags & 512 (f32 LDS-DMA kernels): the batch index is a K-chunk of ONE product; the last
-  // chunk to finish a tile sums every chunk's slab tile (fixed order) into fin, whose columns are
-  // stored as blocks of fin_cb columns fin_bs floats apart (+ the bf16 twin fin_bf16 if set);
-  // tickets: one zero-at-rest word per output tile
-  float* fin;
-  bf16_t* fin_bf16;
-  long fin_cb, fin_bs;
-  unsigned* tickets;
 };
 
-constexpr int kResAdd = 64, kResMask = 128, kResF32 = 256, kSplitCombine = 512;
+constexpr int kResAdd = 64, kResMask = 128, kResF32 = 256;
 
 // Epilogue operand R applied to 8 consecutive output values (after bias / ReLU, f32):
 //   residual add: out = bf16(bf16(v) + bf16(R))   (the unfused "y = dense(x); y + R" in bf16:
@@ -433,7 +425,6 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
   constexpr int S_EPI = TM * TN / 2;
   static_assert(L * (NST - 1) + S_EPI + 1 <= 63, "vmcnt immediate range");
   __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
-  __shared__ int s_last;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -658,7 +649,6 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
     } else {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]
       const bool vec = (p.ldc & 3) == 0 && (p.sC & 3) == 0 && ((((uintptr_t)p.C) & 15) == 0);
-      const bool combine = p.flags & kSplitCombine;  // host checks: vec, splitk == 1, sc1 stores
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + j * 16 + 4 * g;
@@ -681,7 +671,7 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
             v[e] = acc[ii][j][e] * p.alpha + bv[e];
             if (relu) v[e] = fmaxf(v[e], 0.f);
           }
-          acc[ii][j] = combine ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+          acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           if (row >= p.M || col >= p.N) continue;
           float* C = reinterpret_cast<float*>(p.C) + (long)w.b * p.sC + (long)row * p.ldc + col;
           if (p.splitk > 1) {
@@ -700,71 +690,6 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
               if (col + e < p.N) C[e] = accumulate ? C[e] + v[e] : v[e];
           }
         }
-      }
-      if (combine) {
-        // split-K combine without a second launch: this block's slab tile is out (sc1 stores),
-        // drained by every wave before one lane draws the tile's ticket; the block that draws
-        // the last one reads the other chunks' tiles (sc1 loads) and writes the sum
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-          unsigned* tk = p.tickets + (w.m0 * ntn + w.n0);
-          const unsigned t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_last = t == (unsigned)p.batch - 1;
-          if (s_last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        if (s_last) {
-          // chunk by chunk in a fixed order (deterministic sums); each chunk's TM x TN loads are
-          // issued back to back before any is used
-          f32x4 sum[TM][TN];
-#pragma unroll
-          for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) sum[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          for (int sp = 0; sp < p.batch; ++sp) {
-            if (sp == w.b) {
-#pragma unroll
-              for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) sum[ii][j] += acc[ii][j];
-              continue;
-            }
-            f32x4 ld[TM][TN];
-#pragma unroll
-            for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-              for (int j = 0; j < TN; ++j) {
-                const int col = n0 + j * 16 + 4 * g, row = m0 + ii * 16 + (lane & 15);
-                const bool ok = row < p.M && col < p.N;
-                const int off = ok ? (int)(((long)sp * p.sC + (long)row * p.ldc + col) * 4) : 0x7ffffff0;
-                ld[ii][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, off, 0, kSC1));
-              }
-#pragma unroll
-            for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-              for (int j = 0; j < TN; ++j) sum[ii][j] += ld[ii][j];
-          }
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int col = n0 + j * 16 + 4 * g;
-#pragma unroll
-            for (int ii = 0; ii < TM; ++ii) {
-              const int row = m0 + ii * 16 + (lane & 15);
-              if (row >= p.M || col >= p.N) continue;
-              const long blk = col / p.fin_cb, cc = col % p.fin_cb;
-              const long fo = blk * p.fin_bs + (long)row * p.fin_cb + cc;
-              *reinterpret_cast<f32x4*>(p.fin + fo) = sum[ii][j];
-              if (p.fin_bf16)
-                *reinterpret_cast<u32x2*>(p.fin_bf16 + fo) = u32x2{pack_bf16x2(sum[ii][j][0], sum[ii][j][1]),
-                                                                   pack_bf16x2(sum[ii][j][2], sum[ii][j][3])};
-            }
-          }
-        }
-#pragma unroll
-        for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
       // drain before the next item's counted waits; after the block's last item the wave just
       // ends (its stores complete on their own and the CU is free for the next block sooner)
@@ -887,8 +812,7 @@ hipError_t dispatch_layout(const GemmArgs& a, int a_kc, int b_kc, int out_f32, h
 LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
                           long lda, long ldb, long ldc, long sA, long sB, long sC, long sBias, int batch,
                           int a_kc, int b_kc, int out_f32, int flags, float alpha, int splitk, int tile,
-                          void* psum, int* psum_count, const void* res, long ldr, long sR, void* fin,
-                          void* fin_bf16, long fin_cb, long fin_bs, void* tickets, hipStream_t stream) {
+                          void* psum, int* psum_count, const void* res, long ldr, long sR, hipStream_t stream) {
   if (K % 8 || (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
   if (splitk > 1 && !out_f32) return (int)hipErrorInvalidValue;
   // the epilogue operand applies to bf16 outputs (its 16-byte loads need aligned 8-column chunks)
@@ -910,11 +834,6 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   a.res = res;
   a.ldr = ldr;
   a.sR = sR;
-  a.fin = (float*)fin;
-  a.fin_bf16 = (bf16_t*)fin_bf16;
-  a.fin_cb = fin_cb;
-  a.fin_bs = fin_bs;
-  a.tickets = (unsigned*)tickets;
 
   if (psum_count) *psum_count = 0;
   int nkt = (K + BK - 1) / BK;
@@ -945,14 +864,6 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if ((flags & (kResAdd | kResMask)) && tile > 1000 && !(a_kc && b_kc)) tile = 128;
   if ((flags & (kResAdd | kResMask)) && (tile == 643 || tile == 644)) tile = 64;
   if ((tile == 643 || tile == 644) && !(dma_ok && dma_store_ok)) tile = 64;
-  if (flags & kSplitCombine) {
-    // in-kernel combine: f32 slabs [batch][M][N] from an LDS-DMA tile, 16-byte rows, sc1 stores
-    const bool tile_ok = (tile == 1282 || tile == 1284 || tile == 643 || tile == 644) && dma_ok;
-    if (!out_f32 || !fin || !tickets || a.splitk > 1 || !tile_ok || ldc % 4 || sC % 4 || fin_cb % 4 ||
-        (((uintptr_t)C) & 15) || (((uintptr_t)fin) & 15) || (fin_bf16 && (((uintptr_t)fin_bf16) & 7)))
-      return (int)hipErrorInvalidValue;
-    a.flags |= 32;
-  }
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
   if (tile == 1602 && !(a_kc && b_kc && !out_f32 && a.splitk == 1)) tile = 1282;
   if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;

@@ -30,8 +30,7 @@ _LP = ctypes.POINTER(ctypes.c_long)
 _SIGS = {
     "ljs_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
                       c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
-                      ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p, c_void_p, c_long, c_long, c_void_p,
-                      c_void_p],
+                      ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p],
     "ljs_sum_partials": [c_void_p, c_int, c_void_p, c_int, c_void_p],
     "ljs_gemm_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long,
                      c_long, c_long, c_long, c_int, c_void_p],
@@ -168,9 +167,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
          bias: Optional[torch.Tensor] = None, sBias: int = 0, relu: bool = False, alpha: float = 1.0,
          accumulate: bool = False, splitk: int = 1, tile: Optional[int] = None, a_off: int = 0, b_off: int = 0,
          c_off: int = 0, zero_c: bool = False, psum: Optional[torch.Tensor] = None,
-         res: Optional[torch.Tensor] = None, res_ld: int = 0, res_mode: str = "add", sR: int = 0,
-         combine: Optional[torch.Tensor] = None, combine_bf16: Optional[torch.Tensor] = None, combine_cb: int = 0,
-         combine_bs: int = 0) -> int:
+         res: Optional[torch.Tensor] = None, res_ld: int = 0, res_mode: str = "add", sR: int = 0) -> int:
     """Raw launcher.  A/B bf16; C bf16 or f32 (split-K/accumulate need f32 C).
 
     ``lda``/``ldb`` may be 0 for an operand that repeats one row (a broadcast gradient).
@@ -182,10 +179,6 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     broadcast row; bf16 C only) is an epilogue operand: ``res_mode="add"`` adds it as a residual
     (``bf16(bf16(y) + bf16(res))``, bit-exact with the unfused add), ``"mask"`` keeps the outputs
     where ``res > 0`` (a ReLU backward fused into the dX GEMM).
-    ``combine`` (f32; with f32 C = slabs [batch][M][N] whose batch index is a K-chunk of one
-    product): the last chunk to finish each output tile sums all chunks' tiles into ``combine``
-    (columns in blocks of ``combine_cb``, ``combine_bs`` floats apart; ``combine_bf16`` also gets
-    the bf16 rounding) - a split-K combine inside the GEMM launch (LDS-DMA tiles only).
     """
     assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
     out_f32 = C.dtype == torch.float32
@@ -195,11 +188,6 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     if res is not None:
         assert not out_f32 and res.dtype in (torch.bfloat16, torch.float32), (C.dtype, res.dtype)
         flags |= (64 if res_mode == "add" else 128) | (256 if res.dtype == torch.float32 else 0)
-    tickets = None
-    if combine is not None:
-        assert out_f32 and combine.dtype == torch.float32 and combine_cb > 0
-        flags |= 512
-        tickets = _workspace(C.device, "gemm_tickets", 64 << 10)
     if tile is None:
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc)
     eA = A.element_size()
@@ -207,8 +195,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     rc = lib().ljs_gemm_bf16(ctypes.c_void_p(A.data_ptr() + a_off * eA), ctypes.c_void_p(B.data_ptr() + b_off * eA),
                              ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb,
                              ldc, sA, sB, sC, sBias, batch, int(a_kc), int(b_kc), int(out_f32), flags, alpha,
-                             splitk, tile, _p(psum), ctypes.byref(cnt), _p(res), res_ld, sR, _p(combine),
-                             _p(combine_bf16), combine_cb, combine_bs, _p(tickets), _stream(C))
+                             splitk, tile, _p(psum), ctypes.byref(cnt), _p(res), res_ld, sR, _stream(C))
     _ck(rc, "ljs_gemm_bf16")
     return cnt.value
 

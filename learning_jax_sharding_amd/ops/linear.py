@@ -78,9 +78,6 @@ def _splitk(M: int, N: int, K: int, batch: int, tile: int) -> int:
 
 
 _DW_SPLIT = int(os.environ.get("LJS_DW_SPLIT", "0"))
-# weight-gradient split-K combined by the last chunk of each tile inside the GEMM (S <= 4); opt-in:
-# measured slower in the B=8 step than the separate slab_reduce (0.1111 vs 0.1078 ms, PERF_NOTES)
-_COMBINE_IN_GEMM = os.environ.get("LJS_DW_COMBINE", "0") == "1"
 # large bf16 dense outputs also carry their fused per-tile sums (see hip._PSUM): y.sum() is free
 _FUSED_SUM = os.environ.get("LJS_FUSED_SUM", "1") == "1"  # tuning override of the K-chunk count
 
@@ -95,12 +92,6 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
         S = _DW_SPLIT
     kc = T // S
     slabs = torch.empty((S, K, Nt), dtype=torch.float32, device=xb.device)
-    tiles = -(-K // (64 if tile in (643, 644) else 128)) * -(-Nt // (64 if tile in (643, 644) else 128))
-    if _COMBINE_IN_GEMM and 1 < S <= 4 and tiles * 4 <= (64 << 10) // 4 and cb % 4 == 0:
-        # few chunks: the last chunk of each tile sums the slabs inside the GEMM launch
-        hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
-                 tile=tile, combine=out, combine_bf16=twin, combine_cb=cb, combine_bs=out_bs)
-        return
     hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
              tile=tile)
     hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)

@@ -132,31 +132,3 @@ def test_transformer_layer_fused_matches_unfused(gpu_devices, fp8):
     lf, lu = ljs.tree_util.tree_leaves(ljs.nn.unbox(gf)), ljs.tree_util.tree_leaves(ljs.nn.unbox(gu))
     for a, b in zip(lf, lu):
         torch.testing.assert_close(a.to_torch(), b.to_torch(), rtol=0, atol=0)
-
-
-@pytest.mark.parametrize("tile", [644, 643, 1282])
-@pytest.mark.parametrize("K,N,T,S,cb", [(512, 640, 2048, 4, 640), (640, 1536, 2048, 2, 512), (640, 512, 3072, 3, 512)])
-@pytest.mark.parametrize("twin", [False, True])
-def test_weight_grad_in_gemm_combine(hip, tile, K, N, T, S, cb, twin):
-    """Split-K weight gradient combined by the last K-chunk of each tile inside the GEMM launch
-    == the slab GEMM + separate slab_reduce (to f32 rounding of the summation order)."""
-    X, dY = _rand(T, K, seed=21), _rand(T, N, seed=22)
-    kc = T // S
-    nb = N // cb
-    ref = torch.empty(nb, K, cb, device=dev)
-    ref_tw = torch.empty(nb, K, cb, dtype=torch.bfloat16, device=dev)
-    slabs = torch.empty(S, K, N, device=dev)
-    hip.gemm(X, dY, slabs, K, N, kc, K, N, N, False, False, batch=S, sA=kc * K, sB=kc * N, sC=K * N, tile=tile)
-    hip.slab_reduce(slabs, ref, cb, K * cb, out_bf16=ref_tw)
-    for rep in range(2):  # twice: the tile tickets must re-arm
-        out = torch.full((nb, K, cb), float("nan"), device=dev)
-        tw = torch.full((nb, K, cb), float("nan"), dtype=torch.bfloat16, device=dev) if twin else None
-        slabs2 = torch.empty(S, K, N, device=dev)
-        hip.gemm(X, dY, slabs2, K, N, kc, K, N, N, False, False, batch=S, sA=kc * K, sB=kc * N, sC=K * N, tile=tile,
-                 combine=out, combine_bf16=tw, combine_cb=cb, combine_bs=K * cb)
-        torch.cuda.synchronize()
-        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
-        full = (X.float().t() @ dY.float()).reshape(K, nb, cb).permute(1, 0, 2)
-        torch.testing.assert_close(out, full, rtol=1e-3, atol=2e-2)
-        if twin:
-            torch.testing.assert_close(tw.float(), out, rtol=1e-2, atol=1e-2)
