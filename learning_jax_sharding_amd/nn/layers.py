@@ -110,13 +110,16 @@ class FeedForward(Module):
         w_out = self.param("w_out", with_logical_partitioning(init.lecun_normal(), ("hidden", "embed")),
                            (self.hidden_dim, d), torch.float32)
         dt = _dt.canonicalize(self.dtype)
+        replicated = w_in.tile.is_fully_replicated and w_out.tile.is_fully_replicated
+        if dt == torch.bfloat16 and replicated and (residual is None or residual is x) \
+                and (d % 128 == 0 and self.hidden_dim % 128 == 0 if self.fp8 else True):
+            # replicated weights (data-parallel / single device): the fused block - one autograd
+            # node, epilogue fusions across its GEMMs; fp8: forward and backward-dX GEMMs on
+            # MX-fp8 with the quantized operands written by their producers
+            from ..ops.fp8 import ff_block
+            return ff_block(x, w_in, w_out, residual=residual, fp8=self.fp8)
         if self.fp8:
-            from ..ops.fp8 import ff_block, fp8_dense
-            if dt == torch.bfloat16 and w_in.tile.is_fully_replicated and w_out.tile.is_fully_replicated \
-                    and d % 128 == 0 and self.hidden_dim % 128 == 0:
-                # replicated weights (data-parallel / single device): the fused block, fp8
-                # forward and backward-dX GEMMs, quantized operands written by the producers
-                return ff_block(x, w_in, w_out, residual=residual)
+            from ..ops.fp8 import fp8_dense
             h = fp8_dense(x, w_in, relu=True, out_dtype=dt)
             h = with_logical_constraint(h, ("batch", "length", "hidden"))
             y = fp8_dense(h, w_out, relu=False, out_dtype=dt)

@@ -393,15 +393,18 @@ def ff_block_local(x: torch.Tensor, w_in: torch.Tensor, w_out: torch.Tensor,
     return _FFBlockFp8Ref.apply(x, w_in, w_out, res)
 
 
-def ff_block(x, w_in, w_out, residual=None):
-    """Global-view fused fp8 FF block ``relu(x Win) Wout (+ residual)`` on sharded arrays: x keeps
-    its tiling (its feature dim gathered if split), the weights are used replicated (data / FSDP
-    meshes; a hidden dim split over a mesh axis takes the two-dense path in ``FeedForward``)."""
+def ff_block(x, w_in, w_out, residual=None, fp8: bool = True):
+    """Global-view fused FF block ``relu(x Win) Wout (+ residual)`` on sharded arrays: x keeps its
+    tiling (its feature dim gathered if split), the weights are used replicated (data / FSDP
+    meshes; a hidden dim split over a mesh axis takes the two-dense path in ``FeedForward``).
+    ``fp8``: the MX-fp8 block (:class:`_FFBlockFp8`); else bf16 (:class:`.linear._FFBlock`, where
+    a residual that is x itself is summed into the dX GEMM's epilogue)."""
     from ..sharding.tile import TileAssignment
     from ..spmd.reshard import reshard_tile
     from ..sharding.shardings import sharding_from_tile
     from ..array import ShardedArray
     from . import core
+    from . import linear as L
     xt = x.tile
     if xt.tile_shape[-1] > 1:
         x = reshard_tile(x, xt.unshard([x.ndim - 1]), note="ff.x")
@@ -409,10 +412,21 @@ def ff_block(x, w_in, w_out, residual=None):
     devs = xt.device_ids
     wi = reshard_tile(w_in, TileAssignment.replicated(devs, 2), note="ff.w_in")
     wo = reshard_tile(w_out, TileAssignment.replicated(devs, 2), note="ff.w_out")
+    self_res = residual is x
     r_loc = None
-    if residual is not None:
+    if residual is not None and not self_res:
         r_loc = reshard_tile(residual, xt, note="ff.residual").local
-    core._plan.record("ff_block", fp8=True, tiles=xt.tile_shape)
-    loc = {d: ff_block_local(x.local[d], wi.local[d], wo.local[d], r_loc[d] if r_loc is not None else None)
-           for d in x.local}
+    core._plan.record("ff_block", fp8=fp8, tiles=xt.tile_shape)
+    loc = {}
+    for d in x.local:
+        xl, wil, wol = x.local[d], wi.local[d], wo.local[d]
+        rl = xl if self_res else (r_loc[d] if r_loc is not None else None)
+        if fp8:
+            loc[d] = ff_block_local(xl, wil, wol, rl)
+        elif xl.is_cuda and L.ff_block_supported(xl, wil, wol) and (rl is None or self_res):
+            loc[d] = L.ff_block(xl, wil, wol, self_res)
+        else:  # host devices / other shapes: the unfused dense pair (same roundings)
+            from . import kernels as K
+            h = K.linear(xl, [wil], None, torch.bfloat16, relu=True)[0]
+            loc[d] = K.linear(h, [wol], None, torch.bfloat16, residual=rl)[0]
     return ShardedArray(tuple(x.shape), torch.bfloat16, sharding_from_tile(xt, like=[x.sharding]), loc)

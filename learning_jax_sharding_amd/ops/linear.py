@@ -340,3 +340,71 @@ def linear(x: torch.Tensor, ws: List[torch.Tensor], b: Optional[torch.Tensor], r
         ys = list(_Linear.apply(x, b, None, relu, out_dtype, *ws))
         return [ys[0] + residual.to(ys[0].dtype)] + ys[1:]
     return list(_Linear.apply(x, b, residual, relu, out_dtype, *ws))
+
+
+# ----------------------------------------------------------------------------- fused FF block
+class _FFBlock(torch.autograd.Function):
+    """``y = relu(x Win) Wout + x`` (the transformer layer's FF sub-block with its skip
+    connection; ``res`` False: without it) as ONE autograd node, so the gradient of x - the
+    skip path's dY plus the FF path's dX - is summed inside the dX GEMM's epilogue instead of
+    by a separate autograd accumulation kernel:
+
+    * forward: up projection with ReLU, down projection with the residual in its epilogue;
+    * backward: dA = dY Wout^T with the ReLU mask in the epilogue; dX = dA Win^T (+ dY, the
+      residual, in the epilogue, bit-exact with the separate bf16 add); weight gradients as
+      split-K slabs (+ bf16 wire twins under a bf16 data-parallel wire)."""
+
+    @staticmethod
+    def forward(ctx, x, w_in, w_out, res):
+        lead, M = x.shape[:-1], x.shape[-1]
+        F = w_in.shape[1]
+        x2 = _bf16(x.reshape(-1, M).contiguous())
+        T = x2.shape[0]
+        a = torch.empty((T, F), dtype=torch.bfloat16, device=x.device)
+        hip.gemm(x2, shadow.get(w_in, "T"), a, T, F, M, M, M, F, True, True, relu=True)
+        y = torch.empty((T, M), dtype=torch.bfloat16, device=x.device)
+        hip.gemm(a, shadow.get(w_out, "T"), y, T, M, F, F, F, M, True, True, res=x2 if res else None, res_ld=M)
+        ctx.save_for_backward(x2, a, w_in, w_out)
+        ctx.meta = (lead, M, F, T, bool(res), x.dtype)
+        return y.view(tuple(lead) + (M,))
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..parallel import data as _dp
+        x2, a, w_in, w_out = ctx.saved_tensors
+        lead, M, F, T, res, xdt = ctx.meta
+        dev = x2.device
+        t, ld = _row_view(dy, T, M)
+        wire = _dp.active_wire_dtype() == torch.bfloat16
+        dA = torch.empty((T, F), dtype=torch.bfloat16, device=dev)
+        hip.gemm(t, shadow.get(w_out, "N"), dA, T, F, M, ld, M, F, True, True, res=a, res_ld=F, res_mode="mask")
+        dx = dwi = dwo = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((T, M), dtype=torch.bfloat16, device=dev)
+            hip.gemm(dA, shadow.get(w_in, "N"), dx, T, M, F, F, F, M, True, True, res=t if res else None, res_ld=ld)
+            dx = dx.to(xdt).view(tuple(lead) + (M,))
+
+        def wgrad(xb, g, g_ld, K, N):
+            out = torch.empty((K, N), dtype=torch.float32, device=dev)
+            twin = torch.empty((K, N), dtype=torch.bfloat16, device=dev) if wire else None
+            _dw_slabs(xb, g, g_ld, T, K, N, out, N, 0, twin)
+            if twin is not None:
+                _dp.register_wire_twin(out, twin)
+            return out
+        if ctx.needs_input_grad[2]:
+            dwo = wgrad(a, t, ld, F, M)
+        if ctx.needs_input_grad[1]:
+            dwi = wgrad(x2, dA, F, M, F)
+        return dx, dwi, dwo, None
+
+
+def ff_block_supported(x: torch.Tensor, w_in: torch.Tensor, w_out: torch.Tensor) -> bool:
+    M, F = w_in.shape
+    T = x.numel() // max(1, x.shape[-1])
+    return (x.is_cuda and x.shape[-1] == M and tuple(w_out.shape) == (F, M) and M % 64 == 0 and F % 64 == 0
+            and T % 64 == 0 and w_in.dtype == torch.float32 and w_out.dtype == torch.float32)
+
+
+def ff_block(x: torch.Tensor, w_in: torch.Tensor, w_out: torch.Tensor, residual: bool) -> torch.Tensor:
+    """Local fused FF block (bf16 compute): ``relu(x Win) Wout (+ x if residual)``."""
+    return _FFBlock.apply(x, w_in, w_out, residual)

@@ -132,3 +132,27 @@ def test_transformer_layer_fused_matches_unfused(gpu_devices, fp8):
     lf, lu = ljs.tree_util.tree_leaves(ljs.nn.unbox(gf)), ljs.tree_util.tree_leaves(ljs.nn.unbox(gu))
     for a, b in zip(lf, lu):
         torch.testing.assert_close(a.to_torch(), b.to_torch(), rtol=0, atol=0)
+
+
+
+@pytest.mark.parametrize("bcast", [False, True])
+@pytest.mark.parametrize("res", [True, False])
+def test_ff_block_bf16_matches_unfused(hip, bcast, res):
+    """Fused bf16 FF block (one autograd node; skip-path gradient summed in the dX GEMM's
+    epilogue) == the unfused dense pair + add, bit for bit."""
+    from learning_jax_sharding_amd.ops import linear as L
+    T, M, Fd = 2048, 640, 2560
+    x = _rand(T, M, seed=70).requires_grad_()
+    wi = (_rand(M, Fd, dtype=torch.float32, seed=71) * 0.04).requires_grad_()
+    wo = (_rand(Fd, M, dtype=torch.float32, seed=72) * 0.02).requires_grad_()
+    cot = torch.ones((), dtype=torch.bfloat16, device=dev).expand(T, M) if bcast else _rand(T, M, seed=73)
+    y = L.ff_block(x, wi, wo, res)
+    y.backward(cot)
+    x2, wi2, wo2 = (t.detach().clone().requires_grad_() for t in (x, wi, wo))
+    (h,) = hip.linear(x2, [wi2], None, torch.bfloat16, True, torch.bfloat16)
+    (y2,) = hip.linear(h, [wo2], None, torch.bfloat16, False, torch.bfloat16, residual=x2 if res else None)
+    y2.backward(cot)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    for a, b in ((x.grad, x2.grad), (wi.grad, wi2.grad), (wo.grad, wo2.grad)):
+        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
