@@ -567,7 +567,9 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
       // chunks at once cost the second resident block its registers); rows / columns past
       // M / N read 0 through the buffer range check, and the compiler's counted vmcnt waits
       // for them at first use
-      u32x4 rv[TN / 2][RES == 2 ? 2 : 1];
+      // (two row blocks in registers: block ii + 1's loads are issued before block ii is
+      // processed, so only the first block's latency is exposed per item)
+      u32x4 rv[2][TN / 2][RES == 2 ? 2 : 1];
       __amdgpu_buffer_rsrc_t rr;
       if constexpr (RES != 0)
         rr = make_rsrc(p.res, (RES == 2 ? 4 : 2) * ((long)(p.batch - 1) * p.sR + (long)(p.M - 1) * p.ldr + p.N));
@@ -579,11 +581,13 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
             const int row = m0 + ii * 16 + (lane & 15);
             const bool ok = row < p.M && col < p.N;
             const int off = ok ? (int)(((long)w.b * p.sR + (long)row * p.ldr + col) * (RES == 2 ? 4 : 2)) : 0x7ffffff0;
-            rv[q][0] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
-            if constexpr (RES == 2) rv[q][RES == 2 ? 1 : 0] = __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? off + 16 : off, 0, 0);
+            rv[ii & 1][q][0] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+            if constexpr (RES == 2)
+              rv[ii & 1][q][RES == 2 ? 1 : 0] = __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? off + 16 : off, 0, 0);
           }
         }
       };
+      load_r(0);
       float bvs[TN / 2][8];
 #pragma unroll
       for (int q = 0; q < TN / 2; ++q) {
@@ -600,7 +604,7 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
       }
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) {
-        load_r(ii);
+        if (ii + 1 < TM) load_r(ii + 1);
 #pragma unroll
         for (int q = 0; q < TN / 2; ++q) {  // both halves of a row's 128 B back to back
           const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
@@ -624,7 +628,7 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
             v[e] += bv[e];
             if (relu) v[e] = fmaxf(v[e], 0.f);
           }
-          if constexpr (RES != 0) apply_res8(v, p.flags, rv[q][0], rv[q][0], rv[q][RES == 2 ? 1 : 0]);
+          if constexpr (RES != 0) apply_res8(v, p.flags, rv[ii & 1][q][0], rv[ii & 1][q][0], rv[ii & 1][q][RES == 2 ? 1 : 0]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
           const int row = m0 + ii * 16 + (lane & 15);
