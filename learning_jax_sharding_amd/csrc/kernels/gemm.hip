@@ -39,6 +39,13 @@ struct GemmArgs {
 };
 
 constexpr int kResAdd = 64, kResMask = 128, kResF32 = 256;
+// f32 output, m/n-contiguous operands, batch 1: split s writes its own slab C + s * sC (no
+// atomics; summed by slab_reduce) and the splits need not divide the K-tiles -- the last one
+// runs past K, where the buffer range check reads zeros
+constexpr int kSlabs = 512;
+// item order with the tile-row fastest (set by the launcher when there are fewer tile rows
+// than tile columns; see decode_item)
+constexpr int kMFast = 1024;
 
 // Epilogue operand R applied to 8 consecutive output values (after bias / ReLU, f32):
 //   residual add: out = bf16(bf16(v) + bf16(R))   (the unfused "y = dense(x); y + R" in bf16:
@@ -330,11 +337,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
 //  * The MFMA operands are swapped (C^T = B^T A^T per 16x16 block), so each lane ends with 4
 //    CONSECUTIVE columns of one output row: bf16 results leave as packed 8-byte stores and
 //    f32 as 16-byte stores straight from the accumulators (no LDS round trip).
-//  * Work items are ordered (split, batch, tile-row, tile-col) and dealt XCD-aware, so blocks
-//    sharing an XCD's L2 work on neighbouring tiles (shared operand panels).
+//  * Work items are ordered (split, batch, tiles; the dimension of fewer tiles fastest) and
+//    dealt XCD-aware, so blocks sharing an XCD's L2 work on neighbouring tiles (shared panels).
 // Edges: rows/cols past M/N read garbage that only reaches discarded outputs; the buffer
 // descriptor's range check turns every out-of-range read into 0 without faulting; K must be a
-// multiple of 64 and the split must divide the K-tiles (checked by the launcher).
+// multiple of 64 and the split must divide the K-tiles (checked by the launcher) except in
+// slab mode (kSlabs), whose last split reads zeros past K.
 
 // XOR applied to the 16-byte chunk index of k-row `krow` of an m/n-contiguous image (R rows)
 template <int R>
@@ -381,22 +389,33 @@ struct DmaTile {
 };
 
 struct WorkItem {
-  int b, m0, n0, kt0;
+  int b, m0, n0, kt0, split;
 };
 
-// item order (split, batch, tile-row, tile-col), tile-col fastest: with the XCD-aware deal,
-// an XCD's blocks share one K-range (split), so its L2 holds that range's operand panels
+// item order (split, batch, tile-row, tile-col) with the dimension of FEWER tiles fastest: with
+// the XCD-aware deal an XCD's blocks then share one K-range (split) and cover a compact block
+// of tiles -- all of the narrow operand's panels and a slice of the wide one's -- so its L2
+// holds both (the FF weight gradient dW_in [640 x 2560] read every dA panel on every XCD with
+// the tile-col-fastest order: 80 us vs 63 for the transposed dW_out)
 __device__ __forceinline__ WorkItem decode_item(const GemmArgs& p, int item, int ntm, int ntn) {
   WorkItem w;
-  const int tn_i = item % ntn;
-  int r = item / ntn;
-  const int tm_i = r % ntm;
-  r /= ntm;
+  int tm_i, tn_i, r;
+  if (p.flags & kMFast) {
+    tm_i = item % ntm;
+    r = item / ntm;
+    tn_i = r % ntn;
+    r /= ntn;
+  } else {
+    tn_i = item % ntn;
+    r = item / ntn;
+    tm_i = r % ntm;
+    r /= ntm;
+  }
   w.b = r % p.batch;
-  const int split = r / p.batch;
+  w.split = r / p.batch;
   w.m0 = tm_i;
   w.n0 = tn_i;
-  w.kt0 = split * p.kt_per_split;
+  w.kt0 = w.split * p.kt_per_split;
   return w;
 }
 
@@ -502,8 +521,9 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
   const bool st_sc1 = p.flags & 32;
   const bool psum_on = !OUT_F32 && p.psum != nullptr;
   float tsum = 0.f;
-  const __amdgpu_buffer_rsrc_t rc =
-      make_rsrc(p.C, (OUT_F32 ? 4 : 2) * ((long)(p.batch - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
+  const bool slabs = OUT_F32 && (p.flags & kSlabs);
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(
+      p.C, (OUT_F32 ? 4 : 2) * ((long)((slabs ? p.splitk : p.batch) - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
   bool after_epi = false;
 
   for (int it = 0, f = 0; it < my_items; ++it) {
@@ -653,6 +673,7 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
     } else {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]
       const bool vec = (p.ldc & 3) == 0 && (p.sC & 3) == 0 && ((((uintptr_t)p.C) & 15) == 0);
+      const long cb = (long)(slabs ? w.split : w.b) * p.sC;  // this item's output block
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + j * 16 + 4 * g;
@@ -677,14 +698,14 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
           }
           acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           if (row >= p.M || col >= p.N) continue;
-          float* C = reinterpret_cast<float*>(p.C) + (long)w.b * p.sC + (long)row * p.ldc + col;
-          if (p.splitk > 1) {
+          float* C = reinterpret_cast<float*>(p.C) + cb + (long)row * p.ldc + col;
+          if (p.splitk > 1 && !slabs) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
               if (col + e < p.N) atomicAdd(C + e, v[e]);
           } else if (vec && col + 4 <= p.N) {
             if (accumulate) v += *reinterpret_cast<const f32x4*>(C);
-            const int off = (int)(((long)w.b * p.sC + (long)row * p.ldc + col) * 4);
+            const int off = (int)((cb + (long)row * p.ldc + col) * 4);
             const u32x4 bits = __builtin_bit_cast(u32x4, v);
             if (st_sc1) __builtin_amdgcn_raw_buffer_store_b128(bits, rc, off, 0, kSC1);
             else __builtin_amdgcn_raw_buffer_store_b128(bits, rc, off, 0, 0);
@@ -762,6 +783,9 @@ hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   }
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   const int items = ntm * ntn * a.batch * a.splitk;
+  static const int order_env = getenv("LJS_GEMM_ORDER") ? atoi(getenv("LJS_GEMM_ORDER")) : 1;
+  GemmArgs a2 = a;
+  if (order_env && ntm < ntn) a2.flags |= kMFast;
   static const int bpc_env = getenv("LJS_DMA_BPC") ? atoi(getenv("LJS_DMA_BPC")) : 0;  // tuning override
   // blocks_per_cu 0 = one block per work item (measured best at the bench shapes: the
   // dispatcher balances), else a persistent grid of blocks_per_cu x CUs
@@ -776,7 +800,7 @@ hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   int grid = bpc > 0 ? g_cus * bpc : items;
   if (grid > items) grid = items;
   hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, NST, AK, BKc, OF, RES>), dim3(grid), dim3(WM * WN * 64), 0, s,
-                     a);
+                     a2);
   return hipGetLastError();
 }
 
@@ -858,9 +882,15 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   // 128x128, 4 waves, 2 stages, 2 blocks/CU.  They need K % 64 == 0, a split that divides the
   // K-tiles and operands addressable with 32-bit byte offsets.
   const int nkt64 = K / BK;
-  const bool dma_ok = K % BK == 0 && nkt64 % a.splitk == 0 &&
-                      (a_kc ? (long)M * lda : (long)K * lda) < (1L << 30) &&
-                      (b_kc ? (long)N * ldb : (long)K * ldb) < (1L << 30);
+  const bool slabs = flags & kSlabs;
+  if (slabs && (!out_f32 || a_kc || b_kc || batch != 1 || (flags & (8 | 16)) || K % BK ||
+                a.splitk != splitk || tile < 1000))
+    return (int)hipErrorInvalidValue;  // the caller's slab count must be the launched split count
+  const long k_ext = slabs ? (long)a.splitk * a.kt_per_split * BK : K;  // K-rows the splits address
+  const bool dma_ok = K % BK == 0 && (slabs || nkt64 % a.splitk == 0) &&
+                      (a_kc ? (long)M * lda : k_ext * lda) < (1L << 30) &&
+                      (b_kc ? (long)N * ldb : k_ext * ldb) < (1L << 30);
+  if (slabs && !dma_ok) return (int)hipErrorInvalidValue;
   const bool dma_store_ok = out_f32 || (N % 8 == 0 && ldc % 8 == 0 && (sC % 8 == 0 || batch == 1) &&
                                         (((uintptr_t)C) & 15) == 0);
   if (tile > 1000 && !(dma_ok && dma_store_ok)) tile = 128;

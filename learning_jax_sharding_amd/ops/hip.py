@@ -167,7 +167,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
          bias: Optional[torch.Tensor] = None, sBias: int = 0, relu: bool = False, alpha: float = 1.0,
          accumulate: bool = False, splitk: int = 1, tile: Optional[int] = None, a_off: int = 0, b_off: int = 0,
          c_off: int = 0, zero_c: bool = False, psum: Optional[torch.Tensor] = None,
-         res: Optional[torch.Tensor] = None, res_ld: int = 0, res_mode: str = "add", sR: int = 0) -> int:
+         res: Optional[torch.Tensor] = None, res_ld: int = 0, res_mode: str = "add", sR: int = 0,
+         slabs: bool = False) -> int:
     """Raw launcher.  A/B bf16; C bf16 or f32 (split-K/accumulate need f32 C).
 
     ``lda``/``ldb`` may be 0 for an operand that repeats one row (a broadcast gradient).
@@ -179,12 +180,15 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     broadcast row; bf16 C only) is an epilogue operand: ``res_mode="add"`` adds it as a residual
     (``bf16(bf16(y) + bf16(res))``, bit-exact with the unfused add), ``"mask"`` keeps the outputs
     where ``res > 0`` (a ReLU backward fused into the dX GEMM).
+    ``slabs`` (f32 C, m/n-contiguous operands, batch 1, an LDS-DMA tile): split s of the K range
+    writes its own slab ``C + s * sC``; ``splitk`` must be :func:`slab_count`-consistent (the
+    last split may run past K, where it reads zeros), so the split need not divide the K-tiles.
     """
     assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
     out_f32 = C.dtype == torch.float32
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
-        (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0)
+        (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0) | (512 if slabs else 0)
     if res is not None:
         assert not out_f32 and res.dtype in (torch.bfloat16, torch.float32), (C.dtype, res.dtype)
         flags |= (64 if res_mode == "add" else 128) | (256 if res.dtype == torch.float32 else 0)
@@ -263,18 +267,55 @@ def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f3
     return 128 if tiles128 >= 160 else 64
 
 
+_DW_SLAB_MODE = os.environ.get("LJS_DW_SLAB_MODE", "1") == "1"  # A/B switch: 0 = power-of-two batched slabs
+
+
+def slab_count(nkt: int, S: int) -> int:
+    """Splits actually launched for ``S`` requested over ``nkt`` K-tiles (ceil-sized splits)."""
+    kps = -(-nkt // max(1, S))
+    return -(-nkt // kps)
+
+
+def _cus() -> int:
+    try:
+        return torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    except Exception:
+        return 256
+
+
 def pick_dw_slabs(K: int, N: int, T: int):
-    """(tile, K-chunks) of a weight-gradient slab GEMM [K, N] = X^T dY over T tokens: 128x128 tiles
-    with ~512 work items at large T; at T <= 4096 the 64x64 tile with the largest power-of-two
-    split keeping <= 512 items and >= 512 tokens per chunk (dWo at 2048 tokens: 14.8 -> 11.5 us,
-    dW[q|k|v] 25.6 -> 19.1 us with the combine; scripts/gemm_small.py)."""
-    if T > 4096 or K % 64 or N % 64:
-        return 1282, pick_splitk_dma(K, N, T, 1)
+    """(tile, K-chunks, slab mode) of a weight-gradient slab GEMM [K, N] = X^T dY over T tokens.
+
+    T > 4096: 128x128 tiles (2 blocks per CU) in slab mode, the split count chosen by a cost
+    model -- rounds of resident blocks x K-tiles per split, plus the slab reduction's extra f32
+    traffic -- instead of a power of two dividing the K-tiles: the FF weight gradients (100
+    tiles) ran 400 items on 512 block slots (78 %), now 5 x 52 K-tiles = 500 items; dW_o (20
+    tiles) 16 x 16 -> 24 x 11.  At T <= 4096 the 64x64 tile with the largest power-of-two
+    batched split keeping <= 512 items and >= 512 tokens per chunk (dWo at 2048 tokens:
+    14.8 -> 11.5 us, dW[q|k|v] 25.6 -> 19.1 us; scripts/gemm_small.py)."""
+    if K % 64 or N % 64 or T % 64:
+        return 1282, pick_splitk_dma(K, N, T, 1), False
+    if T > 4096 and not _DW_SLAB_MODE:
+        return 1282, pick_splitk_dma(K, N, T, 1), False
+    if T > 4096:
+        nkt, tiles, slots = T // 64, -(-K // 128) * -(-N // 128), 2 * _cus()
+        best, best_cost = 1, None
+        for S in range(1, min(64, nkt) + 1):
+            if slab_count(nkt, S) != S:
+                continue
+            kps = -(-nkt // S)
+            # ~1.2 us per K-tile round of a full chip of 128x128 blocks, ~1 us per round of
+            # prologue/epilogue, and the reduction reads each f32 slab once (~5 TB/s)
+            rounds = -(-tiles * S // slots)
+            cost = rounds * (kps * 1.2 + 1.0) + S * K * N * 4 / 5e6
+            if best_cost is None or cost < best_cost - 1e-9:
+                best, best_cost = S, cost
+        return 1282, best, True
     tiles = (K // 64) * (N // 64)
     s = 1
     while tiles * s * 2 <= 512 and T % (64 * s * 2) == 0 and T // (s * 2) >= 512:
         s *= 2
-    return 644, s
+    return 644, s, False
 
 
 def pick_splitk_dma(M: int, N: int, K: int, batch: int) -> int:

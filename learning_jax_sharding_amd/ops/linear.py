@@ -87,13 +87,16 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
     """out (column blocks of width cb, out_bs apart) = xb^T @ dy for xb [T][K], dy [T][Nt] (row
     stride ld, 0 = broadcast row): S K-chunks of the token dim run as one batched LDS-DMA GEMM
     into f32 slabs [S][K][Nt], combined by one streaming reduction."""
-    tile, S = hip.pick_dw_slabs(K, Nt, T)
+    tile, S, slab_mode = hip.pick_dw_slabs(K, Nt, T)
     if _DW_SPLIT and T % (64 * _DW_SPLIT) == 0:
-        S = _DW_SPLIT
-    kc = T // S
+        S, slab_mode = _DW_SPLIT, False
     slabs = torch.empty((S, K, Nt), dtype=torch.float32, device=xb.device)
-    hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
-             tile=tile)
+    if slab_mode:  # one launch, split s of the token range into slab s (uneven last split)
+        hip.gemm(xb, dy, slabs, K, Nt, T, K, ld, Nt, False, False, sC=K * Nt, splitk=S, tile=tile, slabs=True)
+    else:
+        kc = T // S
+        hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
+                 tile=tile)
     hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
 
 

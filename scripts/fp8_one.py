@@ -1,0 +1,33 @@
+"""Run ONE MX-fp8 GEMM configuration repeatedly (rocprofv3 counter runs): T x N x K, tile.
+
+usage: python scripts/fp8_one.py N K TILE [ITERS] [qout]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from learning_jax_sharding_amd.ops import fp8 as F  # noqa: E402
+
+T = 16384
+
+
+def main():
+    N, K, tile = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    iters = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+    qo = len(sys.argv) > 5 and sys.argv[5] == "qout"
+    x = torch.randn(T, K, device="cuda").bfloat16()
+    w = torch.randn(N, K, device="cuda").bfloat16()
+    qa, sa = F.quant_rows(x)
+    qb, sb = F.quant_rows(w)
+    c = torch.empty(T, N, device="cuda").bfloat16()
+    q = torch.empty(T, N, dtype=torch.uint8, device="cuda")
+    s = torch.empty(T, N // 32, dtype=torch.uint8, device="cuda")
+    for _ in range(iters):
+        F.gemm_mx(qa, sa, qb, sb, T, N, K, c, qout=(q, s) if qo else None, tile=tile)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

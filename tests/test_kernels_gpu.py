@@ -430,6 +430,22 @@ def test_slab_reduce(hip, S, R, C, cb):
     torch.testing.assert_close(out, 2 * ref, rtol=1e-5, atol=2e-4)
 
 
+@pytest.mark.parametrize("T,K,N,S", [(16384, 640, 2560, 5), (16384, 512, 640, 24), (4160, 256, 384, 4),
+                                     (16384, 2560, 640, 5)])
+def test_gemm_slab_mode_uneven_splits(hip, T, K, N, S):
+    """Slab mode: split s of the token range writes slab s, the last split runs past T (zeros
+    from the range check) -- the slabs sum to X^T dY, and each slab is its own token range."""
+    assert hip.slab_count(T // 64, S) == S
+    x, dy = _rand(T, K, seed=70), _rand(T, N, seed=71)
+    slabs = torch.full((S, K, N), float("nan"), dtype=torch.float32, device=dev)
+    hip.gemm(x, dy, slabs, K, N, T, K, N, N, False, False, sC=K * N, splitk=S, tile=1282, slabs=True)
+    ref = x.float().t() @ dy.float()
+    torch.testing.assert_close(slabs.sum(0), ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
+    kc = -(-(T // 64) // S) * 64
+    last = x[kc * (S - 1):].float().t() @ dy[kc * (S - 1):].float()
+    torch.testing.assert_close(slabs[S - 1], last, rtol=2e-3, atol=2e-3 * last.abs().max().item())
+
+
 @pytest.mark.parametrize("T", [16384, 4096, 192])
 def test_linear_weight_grad_slabs(hip, T):
     """dW of the fused QKV dense (3 kernels, one [T][1536] cotangent) and of a single dense with a
