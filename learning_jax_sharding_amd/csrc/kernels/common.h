@@ -163,3 +163,25 @@ __device__ __forceinline__ float warp_sum64(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// ---- MX-fp8 (OCP e4m3 elements, e8m0 block scales over 32 elements)
+// shared e8m0 exponent of a block from its amax; returns the unbiased exponent X (2^X scale).
+// OCP's floor(log2 amax) - 8, plus one when amax / 2^X would exceed 448 (mantissa > 1.75), so
+// no element of the block saturates.
+__device__ __forceinline__ int mx_exponent(float amax) {
+  if (!(amax > 0.f)) return -127;
+  int e;
+  const float m = frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1): floor(log2 amax) = e - 1
+  int x = e - 1 - 8 + (m > 0.875f ? 1 : 0);
+  return x < -127 ? -127 : (x > 127 ? 127 : x);
+}
+
+__device__ __forceinline__ unsigned pack4_e4m3(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f);
+  d = fminf(fmaxf(d, -448.f), 448.f);
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);   // bytes 0,1
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, lo, true);   // bytes 2,3
+  return (unsigned)hi;
+}

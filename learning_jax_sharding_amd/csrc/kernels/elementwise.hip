@@ -489,6 +489,10 @@ __global__ void adam_kernel(const float* __restrict__ p, const G* __restrict__ g
 // removes every per-step f32->bf16 weight cast kernel from the training step.
 struct AdamTensor {
   long p, g, m, v, st, sn, R, C, g_bf16, tiles_c, vec;  // vec: 4-wide path allowed (C % 4, alignment)
+  // MX-fp8 shadows of the new weight (0 = none; R, C % 64 == 0, 64-row tiles, vec path):
+  // qn[R][C] + sn8[R][C/32] (blocks along rows, quant_mx_rows' layout: a dX GEMM's B operand)
+  // and qt[C][R] + st8[C][R/32] (blocks along columns, transposed: a forward GEMM's B operand)
+  long qn, sn8, qt, st8;
 };
 constexpr int kAdamMax = 32;
 // rows per Adam tile (x 64 columns): a template parameter (LJS_ADAM_ROWS = 16 / 32 / 64); smaller
@@ -568,8 +572,23 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
           *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(T.sn) + i) =
               u32x2{pack_bf16x2(pv[q][0], pv[q][1]), pack_bf16x2(pv[q][2], pv[q][3])};
       }
+      if (T.qn) {
+        // MX block = 32 columns of this row = the 8 lanes (tid & 15) / 8 of a 16-lane row group
+        float amax = fmaxf(fmaxf(fabsf(pv[q][0]), fabsf(pv[q][1])), fmaxf(fabsf(pv[q][2]), fabsf(pv[q][3])));
+        amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+        const int x = mx_exponent(amax);
+        const float inv = ldexpf(1.f, -x);
+        if (ok[q]) {
+          const long i = (long)(tr_i * kAdamRows + rl) * T.C + cbase;
+          *reinterpret_cast<unsigned*>(reinterpret_cast<unsigned char*>(T.qn) + i) =
+              pack4_e4m3(pv[q][0] * inv, pv[q][1] * inv, pv[q][2] * inv, pv[q][3] * inv);
+          if ((threadIdx.x & 7) == 0) reinterpret_cast<unsigned char*>(T.sn8)[i / 32] = (unsigned char)(x + 127);
+        }
+      }
     }
-    if (T.st) {
+    if (T.st || T.qt) {
       __syncthreads();
       // shadow_t[c][r]: thread -> 4 consecutive rows r4..r4+3 of output row c (bank-conflict
       // free: tr's row stride is 65 words)
@@ -580,12 +599,28 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
 #pragma unroll
       for (int q = 0; q < 64 / (256 / RL); ++q) {
         const int cl = cl0 + (256 / RL) * q, c = orow0 + cl;
-        bf16_t* dst = reinterpret_cast<bf16_t*>(T.st) + (long)c * T.R + ocol;
-        if (rows_vec) {
-          *reinterpret_cast<u32x2*>(dst) = u32x2{pack_bf16x2(tr[r4][cl], tr[r4 + 1][cl]),
-                                                 pack_bf16x2(tr[r4 + 2][cl], tr[r4 + 3][cl])};
-        } else {
-          for (int k = 0; k < 4 && ocol + k < T.R; ++k) dst[k] = f2bf(tr[r4 + k][cl]);
+        if (T.st) {
+          bf16_t* dst = reinterpret_cast<bf16_t*>(T.st) + (long)c * T.R + ocol;
+          if (rows_vec) {
+            *reinterpret_cast<u32x2*>(dst) = u32x2{pack_bf16x2(tr[r4][cl], tr[r4 + 1][cl]),
+                                                   pack_bf16x2(tr[r4 + 2][cl], tr[r4 + 3][cl])};
+          } else {
+            for (int k = 0; k < 4 && ocol + k < T.R; ++k) dst[k] = f2bf(tr[r4 + k][cl]);
+          }
+        }
+        if (T.qt) {
+          // MX block = 32 consecutive rows of column c = 8 lanes of RL (= 16 at 64-row tiles)
+          const float a0 = tr[r4][cl], a1 = tr[r4 + 1][cl], a2 = tr[r4 + 2][cl], a3 = tr[r4 + 3][cl];
+          float amax = fmaxf(fmaxf(fabsf(a0), fabsf(a1)), fmaxf(fabsf(a2), fabsf(a3)));
+          amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+          amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+          amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+          const int x = mx_exponent(amax);
+          const float inv = ldexpf(1.f, -x);
+          const long o = (long)c * T.R + ocol;
+          *reinterpret_cast<unsigned*>(reinterpret_cast<unsigned char*>(T.qt) + o) =
+              pack4_e4m3(a0 * inv, a1 * inv, a2 * inv, a3 * inv);
+          if ((threadIdx.x & 7) == 0) reinterpret_cast<unsigned char*>(T.st8)[o / 32] = (unsigned char)(x + 127);
         }
       }
     }
@@ -921,14 +956,20 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   const int kAdamRows = rows == 16 || rows == 32 ? rows : 64;
   int tiles = 0;
   for (int i = 0; i < n; ++i) {
-    const long* r = table + 10 * i;
+    const long* r = table + 14 * i;
     AdamTensor& t = b.t[i];
     t.p = r[0]; t.g = r[1]; t.m = r[2]; t.v = r[3]; t.st = r[4]; t.sn = r[5]; t.R = r[6]; t.C = r[7];
     t.g_bf16 = r[8];
+    t.qn = r[10]; t.sn8 = r[11]; t.qt = r[12]; t.st8 = r[13];
     t.tiles_c = (t.C + 63) / 64;
     auto al = [](long ptr, long a) { return ptr % a == 0; };
     t.vec = t.C % 4 == 0 && al(t.p, 16) && al(t.m, 16) && al(t.v, 16) && al(t.g, t.g_bf16 ? 8 : 16) &&
             al(t.sn, 8) && al(t.st, 8);
+    // MX shadows are written by the 4-wide path of full 64 x 64 tiles only: refuse anything else
+    // (a shadow left stale would silently feed old weights to the fp8 GEMMs)
+    if ((t.qn || t.qt) && (!t.vec || kAdamRows != 64 || t.R % 64 || t.C % 64 || !al(t.qn, 4) || !al(t.qt, 4) ||
+                           (t.qn && !t.sn8) || (t.qt && !t.st8)))
+      return (int)hipErrorInvalidValue;
     b.tile_start[i] = tiles;
     tiles += (int)(((t.R + kAdamRows - 1) / kAdamRows) * t.tiles_c);
   }

@@ -29,26 +29,7 @@ __device__ __forceinline__ float ldf(const void* p, long i, int is_bf16) {
   return is_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(p)[i]) : reinterpret_cast<const float*>(p)[i];
 }
 
-// shared e8m0 exponent of a block from its amax; returns the unbiased exponent X (2^X scale).
-// OCP's floor(log2 amax) - 8, plus one when amax / 2^X would exceed 448 (mantissa > 1.75), so
-// no element of the block saturates.
-__device__ __forceinline__ int mx_exponent(float amax) {
-  if (!(amax > 0.f)) return -127;
-  int e;
-  const float m = frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1): floor(log2 amax) = e - 1
-  int x = e - 1 - 8 + (m > 0.875f ? 1 : 0);
-  return x < -127 ? -127 : (x > 127 ? 127 : x);
-}
-
-__device__ __forceinline__ unsigned pack4_e4m3(float a, float b, float c, float d) {
-  a = fminf(fmaxf(a, -448.f), 448.f);
-  b = fminf(fmaxf(b, -448.f), 448.f);
-  c = fminf(fmaxf(c, -448.f), 448.f);
-  d = fminf(fmaxf(d, -448.f), 448.f);
-  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);   // bytes 0,1
-  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, lo, true);   // bytes 2,3
-  return (unsigned)hi;
-}
+// (mx_exponent / pack4_e4m3: common.h, shared with the optimizer's MX weight shadows)
 
 // one thread per 32-element block of a row
 __global__ void quant_mx_rows_kernel(const void* __restrict__ in, int is_bf16, long ld, int R, int K,
@@ -133,6 +114,7 @@ struct F8Args {
   long ldr;
   unsigned char* QC;    // MX-fp8 copy of the (bf16-rounded) output: QC[M][N] e4m3, SC[M][N/32] e8m0
   unsigned char* SC;
+  int lda, ldsa;        // A / SA row strides in bytes (K, K / 32; both 0: one broadcast row)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t f8_rsrc(const void* base, long bytes) {
@@ -178,9 +160,9 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   const int KB = p.K / 32;  // scale bytes per row
   const int nk = p.K / F8_BK;
 
-  const __amdgpu_buffer_rsrc_t ra = f8_rsrc(p.A, (long)p.M * p.K);
+  const __amdgpu_buffer_rsrc_t ra = f8_rsrc(p.A, (long)(p.M - 1) * p.lda + p.K);
   const __amdgpu_buffer_rsrc_t rb = f8_rsrc(p.B, (long)p.N * p.K);
-  const __amdgpu_buffer_rsrc_t rsa = f8_rsrc(p.SA, (long)p.M * KB);
+  const __amdgpu_buffer_rsrc_t rsa = f8_rsrc(p.SA, (long)(p.M - 1) * p.ldsa + KB);
   const __amdgpu_buffer_rsrc_t rsb = f8_rsrc(p.SB, (long)p.N * KB);
 
   int voa[PA], vob[PB];
@@ -188,7 +170,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   for (int i = 0; i < PA; ++i) {
     const int q = wave + NW * i;
     const int row = 8 * q + (lane >> 3), slot = lane & 7;
-    voa[i] = (m0 + row) * p.K + 16 * f8_swz(row, slot);
+    voa[i] = (m0 + row) * p.lda + 16 * f8_swz(row, slot);
   }
 #pragma unroll
   for (int i = 0; i < PB; ++i) {
@@ -202,7 +184,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   const int sw = wave < BM / 64 ? wave : (BM / 64 + ((wave - BM / 64) & 1));
   const bool s_is_a = sw < BM / 64;
   const int s_row = 64 * (s_is_a ? sw : sw - BM / 64) + lane;
-  const int vos = ((s_is_a ? m0 : n0) + s_row) * KB;
+  const int vos = s_is_a ? (m0 + s_row) * p.ldsa : (n0 + s_row) * KB;
   const __amdgpu_buffer_rsrc_t rs = s_is_a ? rsa : rsb;
   const int s_dst = s_is_a ? 64 * 4 * sw : BM * 4 + 64 * 4 * (sw - BM / 64);
 
@@ -276,6 +258,24 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   const bool relu = p.flags & 1, has_bias = p.flags & 2, bias_f32 = p.flags & 4, out_f32 = p.flags & 32;
   const bool res_add = p.flags & 64, res_mask = p.flags & 128, qout = p.flags & 256;
   const bool even = (g & 1) == 0;
+  // the epilogue operand's 8 chunks per lane are all requested before the first is used (one
+  // exposed latency per item instead of one per 16-row block); rows / columns outside the
+  // output read 0 through the buffer range check
+  u32x4 rv[2][4];
+  if (res_add || res_mask) {
+    const __amdgpu_buffer_rsrc_t rr = f8_rsrc(p.R, 2 * ((long)(p.M - 1) * p.ldr + p.N));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int col = n0 + wc * 64 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 64 + 16 * i + r16;
+        const bool ok = row < p.M && col < p.N;
+        rv[q][i] = __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? (int)(((long)row * p.ldr + col) * 2) : 0x7ffffff0,
+                                                         0, 0);
+      }
+    }
+  }
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int col = n0 + wc * 64 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
@@ -305,8 +305,8 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
       }
       const int row = m0 + wr * 64 + 16 * i + r16;
       const bool ok = row < p.M && col < p.N;  // N % 8 == 0 (launcher)
-      if ((res_add || res_mask) && ok) {
-        const u32x4 rw = *reinterpret_cast<const u32x4*>(p.R + (long)row * p.ldr + col);
+      if (res_add || res_mask) {
+        const u32x4 rw = rv[q][i];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float r0 = __uint_as_float(rw[e] << 16), r1 = __uint_as_float(rw[e] & 0xffff0000u);
@@ -383,6 +383,28 @@ LJS_API int ljs_debug_mfma_f8(const void* a, const void* b, const void* sa, cons
   return (int)hipGetLastError();
 }
 
+// a scalar cotangent g broadcast over a row of C: its bf16 row and that row's MX-fp8 rows (every
+// 32-block has amax |bf16(g)|) in one launch -- the broadcast dY of y.sum(), read by the GEMMs
+// as ONE row (ld 0 / a_bcast); C % 32 == 0
+__global__ void bcast_scalar_mx_kernel(const void* __restrict__ g, int g_bf16, int C, bf16_t* __restrict__ row,
+                                       unsigned char* __restrict__ q, unsigned char* __restrict__ s) {
+  const int c4 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (c4 >= C) return;
+  const float v = bf2f(f2bf(g_bf16 ? bf2f(*reinterpret_cast<const bf16_t*>(g)) : *reinterpret_cast<const float*>(g)));
+  *reinterpret_cast<u32x2*>(row + c4) = u32x2{pack_bf16x2(v, v), pack_bf16x2(v, v)};
+  const int x = mx_exponent(fabsf(v));
+  const float sv = v * ldexpf(1.f, -x);
+  *reinterpret_cast<unsigned*>(q + c4) = pack4_e4m3(sv, sv, sv, sv);
+  if ((c4 & 31) == 0) s[c4 / 32] = (unsigned char)(x + 127);
+}
+
+LJS_API int ljs_bcast_scalar_mx(const void* g, int g_bf16, int C, void* row, void* q, void* s, hipStream_t stream) {
+  if (C % 32) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bcast_scalar_mx_kernel, dim3((C / 4 + 255) / 256), dim3(256), 0, stream, g, g_bf16, C,
+                     (bf16_t*)row, (unsigned char*)q, (unsigned char*)s);
+  return (int)hipGetLastError();
+}
+
 // x[R][K] (row stride ld elements) -> q[R][K], s[R][K/32]; K % 32 == 0, 16-byte aligned rows
 LJS_API int ljs_quant_mx_rows(const void* in, int is_bf16, long ld, int R, int K, void* q, void* s,
                               hipStream_t stream) {
@@ -409,7 +431,7 @@ LJS_API int ljs_quant_mx_cols(const void* in, int is_bf16, long ld, int K, int N
 // 2562 / 2563 = BM x 128 with 2 or 3 stages (0: automatic).
 LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const void* SB, void* C, const void* bias,
                             int M, int N, int K, long ldc, int flags, const void* R, long ldr, void* QC, void* SC,
-                            int tile, hipStream_t stream) {
+                            int tile, int a_bcast, hipStream_t stream) {
   if (K % F8_BK || N % 8 || ldc % 8 || (long)M * K >= (1L << 31) || (long)N * K >= (1L << 31))
     return (int)hipErrorInvalidValue;
   if ((flags & (64 | 128)) && (!R || ldr % 8 || (((uintptr_t)R) & 15) || (flags & 32)))
@@ -420,6 +442,8 @@ LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const 
   a.SA = (const unsigned char*)SA; a.SB = (const unsigned char*)SB;
   a.C = C; a.bias = bias; a.ldc = ldc; a.M = M; a.N = N; a.K = K; a.flags = flags;
   a.R = (const bf16_t*)R; a.ldr = ldr; a.QC = (unsigned char*)QC; a.SC = (unsigned char*)SC;
+  a.lda = a_bcast ? 0 : K;  // a_bcast: A / SA hold ONE row, read for every output row
+  a.ldsa = a_bcast ? 0 : K / 32;
   if (tile == 0) {
     // 256-row tiles (8 waves, 3 stages) once they still give >= 2 blocks per CU (256 CUs)
     const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128);

@@ -79,7 +79,7 @@ __device__ __forceinline__ void apply_res8(float* v, int flags, const u32x4& rb,
 template <int R>
 __device__ __forceinline__ int swz_mn(int krow, int c8) {
   int f;
-  if constexpr (R == 128) f = ((krow & 3) | (((krow >> 3) & 1) << 2)) << 2;
+  if constexpr (R >= 128) f = ((krow & 3) | (((krow >> 3) & 1) << 2)) << 2;
   else f = ((((krow >> 1) & 1)) | (((krow >> 3) & 1) << 1)) << 2;
   return c8 ^ f;
 }
@@ -347,7 +347,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
 // XOR applied to the 16-byte chunk index of k-row `krow` of an m/n-contiguous image (R rows)
 template <int R>
 __device__ __forceinline__ int swz_mn16(int krow) {
-  if constexpr (R == 128) return ((krow & 3) | (((krow >> 3) & 1) << 2)) << 1;
+  // (rows of 128 or 256 bf16 start on the same bank; rows of 64 alternate halves)
+  if constexpr (R >= 128) return ((krow & 3) | (((krow >> 3) & 1) << 2)) << 1;
   else return ((((krow >> 1) & 1)) | (((krow >> 3) & 1) << 1)) << 1;
 }
 
@@ -423,10 +424,12 @@ constexpr int kSC1 = 16;  // buffer-instruction cache policy bit: sc1 (gfx940-fa
 
 // RES: epilogue operand R (bf16 output only; see apply_res8): 0 none, 1 bf16 R, 2 f32 R.  A
 // template parameter so kernels without it keep their register allocation.
-// (a RES variant is told to keep two 4-wave blocks per CU: its epilogue registers would otherwise
-// push VGPR + AGPR past 256 and halve the resident blocks)
+// (a 4-wave kernel whose LDS ring lets two blocks share a CU is told so: the pipelined main loop's
+// second fragment set and the epilogue registers would otherwise push VGPR + AGPR past 256 and
+// halve the resident blocks)
 template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0>
-__global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2) ? 2 : 1) void gemm_dma_kernel(
+__global__ __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
+gemm_dma_kernel(
     GemmArgs p) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
@@ -526,11 +529,11 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
       p.C, (OUT_F32 ? 4 : 2) * ((long)((slabs ? p.splitk : p.batch) - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
   bool after_epi = false;
 
-  for (int it = 0, f = 0; it < my_items; ++it) {
-  for (int kk = 0; kk < nk; ++kk, ++f) {
-    // step f landed (this wave's pieces); the younger steps (and, right after an epilogue,
-    // its S_EPI stores) may stay in flight
-    const bool tail = f + NST - 2 >= total;
+  // K-tile g landed in LDS for every wave, and every wave's fragment reads of tile g - 1
+  // completed (so its stage may be refilled): this wave's pieces of g (the younger tiles' pieces
+  // and, right after an epilogue, its S_EPI stores may stay in flight), then the barrier
+  auto wait_landed = [&](int g) {
+    const bool tail = g + NST - 2 >= total;
     if constexpr (NST >= 3) {
       if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else if (SWAP && after_epi && psum_on)
@@ -543,36 +546,73 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     after_epi = false;
-    // every wave's reads of the stage about to be refilled completed (lgkmcnt) before it
-    // arrives; every wave's pieces of step f are in LDS once all have arrived
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const bool more = f + NST - 1 < total;
-    const int nst = (f + NST - 1) % NST;
-    const bf16_t* As_ = smem + (f % NST) * STAGE;
+  };
+  // Software-pipelined by half a K-tile: the fragments of k-step 0 of tile g + 1 are read (and
+  // tile g + 1's barrier passed) while the k-step 1 MFMAs of tile g are still to issue, so the
+  // MFMA pipe never waits for a barrier plus an LDS round trip at a tile boundary (it did, once
+  // per K-tile per wave).  ka/kb: k-step 0 fragments, la/lb: k-step 1.
+  bf16x8 ka[TM], kb[TN], la[TM], lb[TN];
+  auto read_frags = [&](int g, int ks, bf16x8* af, bf16x8* bfr) {
+    const bf16_t* As_ = smem + (g % NST) * STAGE;
     const bf16_t* Bs_ = As_ + A_TILE;
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 af[TM], bfr[TN];
+    for (int ii = 0; ii < TM; ++ii) af[ii] = frag<BM, A_KC>(As_, wr * (BM / WM) + ii * 16, ks, lane);
 #pragma unroll
-      for (int ii = 0; ii < TM; ++ii) af[ii] = frag<BM, A_KC>(As_, wr * (BM / WM) + ii * 16, ks, lane);
+    for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, B_KC>(Bs_, wc * (BN / WN) + j * 16, ks, lane);
+  };
+  auto mfmas = [&](const bf16x8* af, const bf16x8* bfr) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, B_KC>(Bs_, wc * (BN / WN) + j * 16, ks, lane);
-      // the next stage's DMA pieces are issued AFTER this k-step's fragment reads, half per
-      // k-step: their issue time (60-185 cycles per piece) then overlaps the LDS latency and
-      // the MFMAs instead of delaying the first fragment read behind all L pieces
-      if (more) {
-        if (ks == 0) issue_half(nst, false);
-        if (ks == BK / 32 - 1) issue_half(nst, true);
+    for (int ii = 0; ii < TM; ++ii)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (SWAP) acc[ii][j] = mfma16x16x32(bfr[j], af[ii], acc[ii][j]);  // C^T block
+        else acc[ii][j] = mfma16x16x32(af[ii], bfr[j], acc[ii][j]);
       }
-#pragma unroll
-      for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if constexpr (SWAP) acc[ii][j] = mfma16x16x32(bfr[j], af[ii], acc[ii][j]);  // C^T block
-          else acc[ii][j] = mfma16x16x32(af[ii], bfr[j], acc[ii][j]);
-        }
+  };
+  static_assert(BK == 64, "two k-steps per K-tile");
+  // (wave tiles with more than 8 fragments per k-step -- 128x160's 32x160 -- keep the plain
+  // loop: two fragment sets would not fit beside their epilogue registers; so do the
+  // transposed-read weight-gradient kernels, 1-2 % slower pipelined while the k-contiguous
+  // forward / dX kernels gain 3-4 %: QKV 2561 45.3 -> 43.7 us, 1282 48.1 -> 46.1 us)
+  constexpr bool PIPE = TM + TN <= 8 && A_KC && B_KC;
+  if (PIPE && total > 0) {
+    wait_landed(0);
+    read_frags(0, 0, ka, kb);
+    if (NST - 1 < total) issue_next((NST - 1) % NST);
+  }
+
+  for (int it = 0, f = 0; it < my_items; ++it) {
+  for (int kk = 0; kk < nk; ++kk, ++f) {
+    if constexpr (!PIPE) {
+      // barrier for tile f, then per k-step: fragment reads, half of tile f + NST - 1's DMA
+      // pieces (their issue time overlaps the LDS latency), MFMAs
+      wait_landed(f);
+      const bool more = f + NST - 1 < total;
+      const int nst = (f + NST - 1) % NST;
+      read_frags(f, 0, ka, kb);
+      if (more) issue_half(nst, false);
+      mfmas(ka, kb);
+      read_frags(f, 1, la, lb);
+      if (more) issue_half(nst, true);
+      mfmas(la, lb);
+      continue;
     }
+    read_frags(f, 1, la, lb);
+    mfmas(ka, kb);
+    // inside an item: DMA of tile f + NST into the stage of tile f (free once barrier f + 1 is
+    // passed), issued in two halves around the k-step 1 MFMAs.  An item's last tile does this
+    // after its epilogue instead (below), so no fragments are live across the epilogue.
+    const bool inner = kk + 1 < nk;
+    const bool more = inner && f + NST < total;
+    if (inner) {
+      wait_landed(f + 1);
+      read_frags(f + 1, 0, ka, kb);
+      if (more) issue_half(f % NST, false);
+    }
+    mfmas(la, lb);
+    if (more) issue_half(f % NST, true);
   }
 
     // ------------------------------------------------------------ epilogue of this item
@@ -720,6 +760,13 @@ __global__ __launch_bounds__(WM * WN * 64, (RES != 0 && WM * WN == 4 && NST == 2
       // ends (its stores complete on their own and the CU is free for the next block sooner)
       if (it + 1 < my_items) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    // the next item's first tile (f): its barrier, k-step 0 fragments and the DMA of tile
+    // f + NST - 1 (the stage of tile f - 1, read by every wave before this barrier)
+    if (PIPE && f < total) {
+      wait_landed(f);
+      read_frags(f, 0, ka, kb);
+      if (f + NST - 1 < total) issue_next((f + NST - 1) % NST);
+    }
   }
 }
 
@@ -746,6 +793,10 @@ LJS_DMA_INST_64(4)
 #undef LJS_DMA_INST_64
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, false)
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, true)
+// weight gradients (m/n-contiguous operands, f32 slabs): 256-wide tiles, 8 waves, 3 stages, one
+// block per CU -- 48 KiB of operands per 64-deep K-tile for twice the MFMA work of 128x128
+LJS_DMA_INST(256, 128, 4, 2, 3, false, false, true)
+LJS_DMA_INST(128, 256, 2, 4, 3, false, false, true)
 // 128x160 with 4 waves stacked along M (32x160 each): N = 640 splits into 4 column tiles, so a
 // [16384, 640] output is exactly 512 items = one round of 2 blocks/CU (128x128: 640 items, 1.25)
 LJS_DMA_INST(128, 160, 4, 1, 2, true, true, false)
@@ -898,6 +949,7 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if ((flags & (kResAdd | kResMask)) && tile > 1000 && !(a_kc && b_kc)) tile = 128;
   if ((flags & (kResAdd | kResMask)) && (tile == 643 || tile == 644)) tile = 64;
   if ((tile == 643 || tile == 644) && !(dma_ok && dma_store_ok)) tile = 64;
+  if ((tile == 2563 || tile == 12856) && !(!a_kc && !b_kc && out_f32)) tile = 1282;
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
   if (tile == 1602 && !(a_kc && b_kc && !out_f32 && a.splitk == 1)) tile = 1282;
   if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;
@@ -908,7 +960,11 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     a.psum = (float*)psum;
     if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch * a.splitk * nw;
   }
-  if (tile == 1602) {
+  if (tile == 2563) {
+    e = launch_dma<256, 128, 4, 2, 3, false, false, true>(a, stream, 0);
+  } else if (tile == 12856) {
+    e = launch_dma<128, 256, 2, 4, 3, false, false, true>(a, stream, 0);
+  } else if (tile == 1602) {
     e = launch_dma_kk<128, 160, 4, 1, 2>(a, stream);
   } else if (tile == 2561) {
     if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);

@@ -23,6 +23,7 @@ from typing import Optional, Tuple
 import torch
 
 from . import hip
+from . import streams as _streams
 from .linear import _Linear, _bf16
 
 __all__ = ["quantize_mx_ref", "dequantize_mx_ref", "mx_linear_ref", "quant_rows", "quant_cols", "gemm_mx",
@@ -36,10 +37,12 @@ _SIGS = {
                           ctypes.c_void_p, ctypes.c_void_p],
     "ljs_quant_mx_cols": [ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                           ctypes.c_void_p, ctypes.c_void_p],
+    "ljs_bcast_scalar_mx": [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_void_p, ctypes.c_void_p],
     "ljs_gemm_mx_fp8": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int,
                         ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-                        ctypes.c_void_p],
+                        ctypes.c_int, ctypes.c_void_p],
 }
 _bound = False
 
@@ -100,26 +103,29 @@ def mx_linear_ref(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], r
 
 
 # ----------------------------------------------------------------------------- HIP path
-def quant_rows(x2: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """x[R][K] (f32/bf16, unit column stride) -> (q uint8 [R][K], s uint8 [R][K/32])."""
+def quant_rows(x2: torch.Tensor, out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+               ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """x[R][K] (f32/bf16, unit column stride) -> (q uint8 [R][K], s uint8 [R][K/32]) (``out``:
+    existing contiguous buffers to write)."""
     R, K = x2.shape
     if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
         x2 = x2.contiguous()
-    q = torch.empty((R, K), dtype=torch.uint8, device=x2.device)
-    s = torch.empty((R, K // BLOCK), dtype=torch.uint8, device=x2.device)
+    q, s = out if out is not None else (torch.empty((R, K), dtype=torch.uint8, device=x2.device),
+                                        torch.empty((R, K // BLOCK), dtype=torch.uint8, device=x2.device))
     rc = _lib().ljs_quant_mx_rows(hip._p(x2), int(x2.dtype == torch.bfloat16), x2.stride(0), R, K, hip._p(q),
                                   hip._p(s), hip._stream(x2))
     hip._ck(rc, "quant_mx_rows")
     return q, s
 
 
-def quant_cols(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def quant_cols(w: torch.Tensor, out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+               ) -> Tuple[torch.Tensor, torch.Tensor]:
     """w[K][N] -> (q uint8 [N][K], s uint8 [N][K/32]) (blocks along K, i.e. quantized W^T)."""
     K, N = w.shape
     if w.stride(1) != 1:
         w = w.contiguous()
-    q = torch.empty((N, K), dtype=torch.uint8, device=w.device)
-    s = torch.empty((N, K // BLOCK), dtype=torch.uint8, device=w.device)
+    q, s = out if out is not None else (torch.empty((N, K), dtype=torch.uint8, device=w.device),
+                                        torch.empty((N, K // BLOCK), dtype=torch.uint8, device=w.device))
     rc = _lib().ljs_quant_mx_cols(hip._p(w), int(w.dtype == torch.bfloat16), w.stride(0), K, N, hip._p(q), hip._p(s),
                                   hip._stream(w))
     hip._ck(rc, "quant_mx_cols")
@@ -130,7 +136,12 @@ _WCACHE = {}
 
 
 def _weight_q(w: torch.Tensor):
-    """Cached MX quantization of a weight, refreshed whenever the weight's version moves."""
+    """MX quantization of a weight along K (the forward GEMM's B operand): the optimizer-maintained
+    shadow when the weight qualifies (:func:`.shadow.get_mx`, rewritten by the fused Adam in the
+    pass that updates the weight: no per-step quantization kernel), else cached per version."""
+    from . import shadow
+    if shadow.mx_eligible(w):
+        return shadow.get_mx(w, "QT")
     key = (w.data_ptr(), tuple(w.shape), w.dtype, w.device)
     ent = _WCACHE.get(key)
     if ent is not None and ent[0] == w._version:
@@ -142,13 +153,15 @@ def _weight_q(w: torch.Tensor):
 
 def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: Optional[torch.Tensor], bias: Optional[torch.Tensor] = None,
             relu: bool = False, res: Optional[torch.Tensor] = None, res_mode: str = "add",
-            qout: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, tile: int = 0) -> Optional[torch.Tensor]:
+            qout: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, tile: int = 0,
+            a_bcast: bool = False) -> Optional[torch.Tensor]:
     """out[M][N] = qa . qb^T (MX-fp8 operands, f32 accumulation) (+bias)(relu); epilogue options:
     ``res`` (bf16 [M][N]) added as a residual (``res_mode="add"``, bit-exact with the unfused bf16
     add) or used as a ReLU mask (``"mask"``: keep where res > 0); ``qout = (q, s)`` also receives
     the MX-fp8 quantization of the (bf16-rounded) output, blocks of 32 along N - the next GEMM's
     operand without a quantization pass.  ``out`` may be None when only ``qout`` is wanted.
-    ``tile``: 1282 / 1283 / 2562 / 2563 (BM x 128, stages), 0 = automatic."""
+    ``tile``: 1282 / 1283 / 2562 / 2563 (BM x 128, stages), 0 = automatic.  ``a_bcast``: ``qa`` /
+    ``sa`` hold ONE row, used for all M rows (a broadcast gradient, never materialised)."""
     od = out if out is not None else None
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | \
@@ -163,7 +176,7 @@ def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: Optional[torch.Tensor],
         flags |= 256
     rc = _lib().ljs_gemm_mx_fp8(hip._p(qa), hip._p(sa), hip._p(qb), hip._p(sb), hip._p(od), hip._p(bias), M, N, K,
                                 od.stride(0) if od is not None else N, flags, hip._p(res), ldr, hip._p(q_o),
-                                hip._p(s_o), tile, hip._stream(qa))
+                                hip._p(s_o), tile, int(a_bcast), hip._stream(qa))
     hip._ck(rc, "gemm_mx_fp8")
     return out
 
@@ -250,7 +263,11 @@ def fp8_dense(x, w, bias=None, relu: bool = False, out_dtype=torch.bfloat16):
 # ----------------------------------------------------------------------------- fused FF block
 def _weight_q_rows(w: torch.Tensor):
     """Cached MX quantization of ``w`` along its LAST dim (``quant_rows``), per weight version:
-    the B operand of a dX GEMM (``dX = dY W^T`` reads W's rows as [n][k])."""
+    the B operand of a dX GEMM (``dX = dY W^T`` reads W's rows as [n][k]); an optimizer-maintained
+    shadow when the weight qualifies (see :func:`_weight_q`)."""
+    from . import shadow
+    if shadow.mx_eligible(w):
+        return shadow.get_mx(w, "QN")
     key = ("rows", w.data_ptr(), tuple(w.shape), w.dtype, w.device)
     ent = _WCACHE.get(key)
     if ent is not None and ent[0] == w._version:
@@ -261,12 +278,30 @@ def _weight_q_rows(w: torch.Tensor):
 
 
 def _quant_grad_rows(dy2: torch.Tensor):
-    """MX-fp8 rows of a bf16 gradient; a broadcast row (stride 0, the cotangent of y.sum()) is
-    quantized once and its bytes repeated."""
+    """(q, s, broadcast): MX-fp8 rows of a gradient.  A broadcast row (stride 0 over rows, the
+    cotangent of y.sum()) is quantized once and read by the GEMM for every row (``a_bcast``)."""
     if dy2.stride(0) == 0:
-        q1, s1 = quant_rows(dy2[:1].contiguous())
-        return q1.expand(dy2.shape[0], -1).contiguous(), s1.expand(dy2.shape[0], -1).contiguous()
-    return quant_rows(dy2)
+        row = dy2[:1]
+        q1, s1 = quant_rows(row if row.is_contiguous() else row.contiguous())
+        return q1, s1, True
+    q, s = quant_rows(dy2)
+    return q, s, False
+
+
+def _bcast_grad_mx(dy2: torch.Tensor):
+    """(bf16 row view [T][M] with stride 0, q [1][M], s [1][M/32]) of a broadcast SCALAR gradient
+    (the cotangent of y.sum()) from one launch, or None for any other gradient."""
+    T, M = dy2.shape
+    if not (dy2.is_cuda and dy2.numel() > 0 and dy2.stride(0) == 0 and dy2.stride(1) == 0 and M % 32 == 0
+            and dy2.dtype in (torch.float32, torch.bfloat16)):
+        return None
+    row = torch.empty((1, M), dtype=torch.bfloat16, device=dy2.device)
+    q = torch.empty((1, M), dtype=torch.uint8, device=dy2.device)
+    s = torch.empty((1, M // BLOCK), dtype=torch.uint8, device=dy2.device)
+    rc = _lib().ljs_bcast_scalar_mx(hip._p(dy2.as_strided((1,), (1,))), int(dy2.dtype == torch.bfloat16), M,
+                                    hip._p(row), hip._p(q), hip._p(s), hip._stream(row))
+    hip._ck(rc, "bcast_scalar_mx")
+    return row.expand(T, M), q, s
 
 
 class _FFBlockFp8(torch.autograd.Function):
@@ -276,9 +311,11 @@ class _FFBlockFp8(torch.autograd.Function):
     * forward: x quantized per row; the up projection's epilogue writes the bf16 ReLU output
       (kept for the backward) and its MX-fp8 copy (the down projection's operand: no
       quantization pass); the down projection's epilogue adds the residual;
-    * backward: dY quantized per row; dA = dY Wout^T on fp8 with the ReLU mask (the saved a > 0)
-      and the MX-fp8 copy of dA written by its epilogue; dX = dA Win^T on fp8; the weight
-      gradients (reductions over tokens) stay bf16 split-K slabs, f32 accumulation.
+    * backward: dY quantized per row (a broadcast dY once, read as one row); dA = dY Wout^T on
+      fp8 with the ReLU mask (the saved a > 0) and the MX-fp8 copy of dA written by its
+      epilogue; dX = dA Win^T on fp8, with the skip path's dY added in its epilogue when the
+      residual is x itself (no autograd accumulation kernel); the weight gradients
+      (reductions over tokens) stay bf16 split-K slabs, f32 accumulation.
 
     Weights are quantized along K for the forward and along N for the dX GEMMs (cached per
     weight version).  The host emulation :class:`_FFBlockFp8Ref` is the numerical oracle."""
@@ -304,39 +341,55 @@ class _FFBlockFp8(torch.autograd.Function):
             r2 = _bf16(res.reshape(T, M).contiguous())
         gemm_mx(qa, sa, qwo, swo, T, M, F, y, res=r2)
         ctx.save_for_backward(x2, a, w_in, w_out)
-        ctx.meta = (lead, M, F, T, res is not None)
+        ctx.meta = (lead, M, F, T, res is not None, res is x)
         return y.view(tuple(lead) + (M,))
 
     @staticmethod
     def backward(ctx, dy):
-        from .linear import _dw_slabs, _row_view
+        from .linear import _dw_slabs, _ff_bwd_order, _row_view
         x2, a, w_in, w_out = ctx.saved_tensors
-        lead, M, F, T, has_res = ctx.meta
+        lead, M, F, T, has_res, res_is_x = ctx.meta
         dev = x2.device
         dy2 = dy.reshape(T, M)
-        if dy2.dtype != torch.bfloat16:
-            dy2 = dy2.to(torch.bfloat16)
-        qdy, sdy = _quant_grad_rows(dy2)
+        bm = _bcast_grad_mx(dy2)
+        if bm is not None:                           # scalar broadcast: row + its MX row, one launch
+            t, qdy, sdy = bm
+            ld, bc = 0, True
+        else:
+            t, ld = _row_view(dy2, T, M)             # bf16 dY (one row, ld 0, when broadcast)
+            qdy, sdy, bc = _quant_grad_rows(t)
         qwo_r, swo_r = _weight_q_rows(w_out)         # Wout [F][M] rows: blocks along M
         dA = torch.empty((T, F), dtype=torch.bfloat16, device=dev)
         qdA = torch.empty((T, F), dtype=torch.uint8, device=dev)
         sdA = torch.empty((T, F // BLOCK), dtype=torch.uint8, device=dev)
-        gemm_mx(qdy, sdy, qwo_r, swo_r, T, F, M, dA, res=a, res_mode="mask", qout=(qdA, sdA))
-        dx = dwi = dwo = None
-        if ctx.needs_input_grad[0]:
-            qwi_r, swi_r = _weight_q_rows(w_in)      # Win [M][F] rows: blocks along F
-            dx = torch.empty((T, M), dtype=torch.bfloat16, device=dev)
-            gemm_mx(qdA, sdA, qwi_r, swi_r, T, M, F, dx)
-            dx = dx.view(tuple(lead) + (M,))
-        if ctx.needs_input_grad[2]:
-            t, ld = _row_view(dy2, T, M)
-            dwo = torch.empty((F, M), dtype=torch.float32, device=dev)
-            _dw_slabs(a, t, ld, T, F, M, dwo, M, 0)
-        if ctx.needs_input_grad[1]:
-            dwi = torch.empty((M, F), dtype=torch.float32, device=dev)
-            _dw_slabs(x2, dA, F, T, M, F, dwi, F, 0)
-        dres = dy if (has_res and ctx.needs_input_grad[3]) else None
-        return dx, dwi, dwo, dres
+        gemm_mx(qdy, sdy, qwo_r, swo_r, T, F, M, dA, res=a, res_mode="mask", qout=(qdA, sdA), a_bcast=bc)
+        out = {}
+        fold = has_res and res_is_x and ctx.needs_input_grad[0]
+
+        def run_dx():
+            if ctx.needs_input_grad[0]:
+                qwi_r, swi_r = _weight_q_rows(w_in)      # Win [M][F] rows: blocks along F
+                dx = torch.empty((T, M), dtype=torch.bfloat16, device=dev)
+                # the skip path's dY summed in the epilogue (bf16(bf16(dx) + dY), the unfused add)
+                gemm_mx(qdA, sdA, qwi_r, swi_r, T, M, F, dx, res=t if fold else None, res_mode="add")
+                out["dx"] = dx.view(tuple(lead) + (M,))
+
+        def run_wo():  # weight gradients on the side stream inside value_and_grad (ops/streams.py)
+            if ctx.needs_input_grad[2]:
+                with _streams.side(dev, [a, t]) as produced:
+                    out["wo"] = torch.empty((F, M), dtype=torch.float32, device=dev)
+                    _dw_slabs(a, t, ld, T, F, M, out["wo"], M, 0)
+                    produced.append(out["wo"])
+
+        def run_wi():
+            if ctx.needs_input_grad[1]:
+                with _streams.side(dev, [x2, dA]) as produced:
+                    out["wi"] = torch.empty((M, F), dtype=torch.float32, device=dev)
+                    _dw_slabs(x2, dA, F, T, M, F, out["wi"], F, 0)
+                    produced.append(out["wi"])
+        _ff_bwd_order(run_dx, run_wo, run_wi)
+        dres = dy if (has_res and ctx.needs_input_grad[3] and not fold) else None
+        return out.get("dx"), out.get("wi"), out.get("wo"), dres
 
 
 class _FFBlockFp8Ref(torch.autograd.Function):

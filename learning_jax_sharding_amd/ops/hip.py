@@ -20,7 +20,8 @@ __all__ = ["lib", "available", "gemm", "bmm_nt", "linear", "attention", "cast", 
            "adam", "rng_fill", "colsum", "supports_cast"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIBPATH = os.path.join(os.path.dirname(_HERE), "_lib", "libljs_kernels.so")
+# LJS_KERNELS_LIB: an alternative build of the library (A/B timing of kernel variants)
+_LIBPATH = os.environ.get("LJS_KERNELS_LIB") or os.path.join(os.path.dirname(_HERE), "_lib", "libljs_kernels.so")
 _LIB = None
 _LOCK = threading.Lock()
 
@@ -879,7 +880,7 @@ def adam(p, g, m, v, step, lr, b1, b2, eps, wd, inplace):
 def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step: bool = False) -> None:
     """In-place fused Adam over many params (one launch per 32): entries = [(p, g, m, v)].
 
-    Also rewrites each param's registered bf16 shadows (see :mod:`.shadow`).  With
+    Also rewrites each param's registered bf16 and MX-fp8 shadows (see :mod:`.shadow`).  With
     ``increment_step`` the bias corrections use ``step + 1`` and the last launch's last
     arriving block stores ``step + 1`` (int32 ``step`` updated in place, no extra kernel)."""
     from . import shadow
@@ -892,9 +893,11 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
         bufs = shadow.kinds_of(p) if p.dim() == 2 else {}
         st, sn = bufs.get("T"), bufs.get("N")
         R, C = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
+        ptr = lambda k: bufs[k].data_ptr() if k in bufs else 0  # noqa: E731
         rows.append(([p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
                       st.data_ptr() if st is not None else 0, sn.data_ptr() if sn is not None else 0,
-                      R, C, int(g.dtype == torch.bfloat16), 0], g))
+                      R, C, int(g.dtype == torch.bfloat16), 0,
+                      ptr("QN"), ptr("QNs"), ptr("QT"), ptr("QTs")], g))
     if increment_step:
         assert step.dtype == torch.int32 and step.is_contiguous()
     step_i = step if step.dtype == torch.int32 else step.to(torch.int32)

@@ -32,6 +32,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import hip
+from . import streams as _streams
 from . import shadow
 
 __all__ = ["linear"]
@@ -108,6 +109,11 @@ def _row_view(dy: torch.Tensor, M: int, N: int) -> Tuple[torch.Tensor, int]:
     M times, exactly as they would read a materialised matrix, without writing one.
     """
     d2 = dy.reshape(M, N)
+    if d2.is_cuda and d2.numel() > 0 and d2.stride(0) == 0 and d2.stride(1) == 0:
+        # one broadcast scalar (the cotangent of y.sum()): its bf16 row in one HIP launch (a
+        # torch .contiguous() of the stride-0 row ran as a 1-workgroup copy kernel, ~4.7 us)
+        row, _ = hip.bcast_scalar(d2.as_strided((1,), (1,)), N, M, False)
+        return row.unsqueeze(0).expand(M, N), 0
     if d2.stride(0) == 0:
         row = d2[0].contiguous()
         row = _bf16(row)
@@ -256,58 +262,14 @@ class _Linear(torch.autograd.Function):
             dx = dx.to(xdtype).view(tuple(lead) + (K,))
             if premask:
                 _register(_PREMASKED, dx, xb.data_ptr())
-        # ---- dW (MN-contiguous operands: X^T and dY read in place)
+        # ---- dW (MN-contiguous operands: X^T and dY read in place), on the side stream inside
+        # value_and_grad (ops/streams.py): it overlaps the layers' input-gradient chain
         want = [i for i in live if ctx.needs_input_grad[5 + i]]
-        if want:
-            t0, ld0 = mats[want[0]]
-            batched = (len(want) == nw and nw > 1 and ld0 > 0 and all(
-                mats[i][1] == ld0 and mats[i][0].data_ptr() == t0.data_ptr() + i * N * 2 for i in want))
-            dma = M % 64 == 0
-            if dma:
-                # split-K as a batch over K-chunks writing per-chunk f32 slabs, then one combine
-                # pass (no atomics, no memset): the column blocks of a fused [K][nw*N] product are
-                # the nw weight gradients
-                # under a data-parallel backward with a bf16 gradient wire, the combine also writes
-                # the bf16 twin the all-reduce sends (no separate cast kernel; parallel/data.py)
-                if joint is not None:
-                    t, ld = mats[0]
-                    dW = joint[:K * N].view(K, N)
-                    _dw_slabs(xb, t, ld, M, K, N, dW, N, 0,
-                              joint_bf16[:K * N].view(K, N) if joint_bf16 is not None else None)
-                    dws[0] = dW
-                elif batched:
-                    dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
-                    twin = torch.empty((nw, K, N), dtype=torch.bfloat16, device=dev) if wire else None
-                    _dw_slabs(xb, t0, ld0, M, K, nw * N, dW, N, K * N, twin)
-                    if twin is not None:
-                        _dp.register_wire_twin(dW, twin)
-                    for i in want:
-                        dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
-                else:
-                    for i in want:
-                        t, ld = mats[i]
-                        dW = torch.empty((K, N), dtype=torch.float32, device=dev)
-                        twin = torch.empty((K, N), dtype=torch.bfloat16, device=dev) if wire else None
-                        _dw_slabs(xb, t, ld, M, K, N, dW, N, 0, twin)
-                        if twin is not None:
-                            _dp.register_wire_twin(dW, twin)
-                        dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
-            else:
-                tile = 128 if (K >= 256 and N >= 256) else 64
-                if batched:
-                    dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
-                    sk = _splitk(K, N, M, nw, tile)
-                    hip.gemm(xb, t0, dW, K, N, M, K, ld0, N, False, False, batch=nw, sA=0, sB=N, sC=K * N,
-                             splitk=sk, tile=tile, zero_c=True)
-                    for i in want:
-                        dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
-                else:
-                    for i in want:
-                        t, ld = mats[i]
-                        dW = torch.empty((K, N), dtype=torch.float32, device=dev)
-                        sk = _splitk(K, N, M, 1, tile)
-                        hip.gemm(xb, t, dW, K, N, M, K, ld, N, False, False, splitk=sk, tile=tile, zero_c=True)
-                        dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
+        with _streams.side(dev, [xb, joint, joint_bf16] + [mats[i][0] for i in want]) as produced:
+            _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, dev)
+            produced.extend(d for d in dws if d is not None)
+            if joint is not None:
+                produced.append(joint)
         # ---- db
         if want_db and live:
             tot = None
@@ -324,6 +286,62 @@ class _Linear(torch.autograd.Function):
             if joint_bf16 is not None:
                 _dp.register_wire_twin(joint, joint_bf16)
         return (dx, db, dres, None, None, *dws)
+
+
+def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, dev):
+    """The weight gradients of :class:`_Linear` (``dws[i]`` for ``i`` in ``want``)."""
+    from ..parallel import data as _dp
+    if not want:
+        return
+    t0, ld0 = mats[want[0]]
+    batched = (len(want) == nw and nw > 1 and ld0 > 0 and all(
+        mats[i][1] == ld0 and mats[i][0].data_ptr() == t0.data_ptr() + i * N * 2 for i in want))
+    dma = M % 64 == 0
+    if dma:
+        # split-K as a batch over K-chunks writing per-chunk f32 slabs, then one combine
+        # pass (no atomics, no memset): the column blocks of a fused [K][nw*N] product are
+        # the nw weight gradients
+        # under a data-parallel backward with a bf16 gradient wire, the combine also writes
+        # the bf16 twin the all-reduce sends (no separate cast kernel; parallel/data.py)
+        if joint is not None:
+            t, ld = mats[0]
+            dW = joint[:K * N].view(K, N)
+            _dw_slabs(xb, t, ld, M, K, N, dW, N, 0,
+                      joint_bf16[:K * N].view(K, N) if joint_bf16 is not None else None)
+            dws[0] = dW
+        elif batched:
+            dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
+            twin = torch.empty((nw, K, N), dtype=torch.bfloat16, device=dev) if wire else None
+            _dw_slabs(xb, t0, ld0, M, K, nw * N, dW, N, K * N, twin)
+            if twin is not None:
+                _dp.register_wire_twin(dW, twin)
+            for i in want:
+                dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
+        else:
+            for i in want:
+                t, ld = mats[i]
+                dW = torch.empty((K, N), dtype=torch.float32, device=dev)
+                twin = torch.empty((K, N), dtype=torch.bfloat16, device=dev) if wire else None
+                _dw_slabs(xb, t, ld, M, K, N, dW, N, 0, twin)
+                if twin is not None:
+                    _dp.register_wire_twin(dW, twin)
+                dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
+    else:
+        tile = 128 if (K >= 256 and N >= 256) else 64
+        if batched:
+            dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
+            sk = _splitk(K, N, M, nw, tile)
+            hip.gemm(xb, t0, dW, K, N, M, K, ld0, N, False, False, batch=nw, sA=0, sB=N, sC=K * N,
+                     splitk=sk, tile=tile, zero_c=True)
+            for i in want:
+                dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
+        else:
+            for i in want:
+                t, ld = mats[i]
+                dW = torch.empty((K, N), dtype=torch.float32, device=dev)
+                sk = _splitk(K, N, M, 1, tile)
+                hip.gemm(xb, t, dW, K, N, M, K, ld, N, False, False, splitk=sk, tile=tile, zero_c=True)
+                dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
 
 
 def supported(x: torch.Tensor, ws: Sequence[torch.Tensor], b) -> bool:
@@ -381,24 +399,51 @@ class _FFBlock(torch.autograd.Function):
         wire = _dp.active_wire_dtype() == torch.bfloat16
         dA = torch.empty((T, F), dtype=torch.bfloat16, device=dev)
         hip.gemm(t, shadow.get(w_out, "N"), dA, T, F, M, ld, M, F, True, True, res=a, res_ld=F, res_mode="mask")
-        dx = dwi = dwo = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty((T, M), dtype=torch.bfloat16, device=dev)
-            hip.gemm(dA, shadow.get(w_in, "N"), dx, T, M, F, F, F, M, True, True, res=t if res else None, res_ld=ld)
-            dx = dx.to(xdt).view(tuple(lead) + (M,))
+        out = {}
+
+        def run_dx():
+            if ctx.needs_input_grad[0]:
+                dx = torch.empty((T, M), dtype=torch.bfloat16, device=dev)
+                hip.gemm(dA, shadow.get(w_in, "N"), dx, T, M, F, F, F, M, True, True, res=t if res else None,
+                         res_ld=ld)
+                out["dx"] = dx.to(xdt).view(tuple(lead) + (M,))
 
         def wgrad(xb, g, g_ld, K, N):
-            out = torch.empty((K, N), dtype=torch.float32, device=dev)
+            o = torch.empty((K, N), dtype=torch.float32, device=dev)
             twin = torch.empty((K, N), dtype=torch.bfloat16, device=dev) if wire else None
-            _dw_slabs(xb, g, g_ld, T, K, N, out, N, 0, twin)
+            _dw_slabs(xb, g, g_ld, T, K, N, o, N, 0, twin)
             if twin is not None:
-                _dp.register_wire_twin(out, twin)
-            return out
-        if ctx.needs_input_grad[2]:
-            dwo = wgrad(a, t, ld, F, M)
-        if ctx.needs_input_grad[1]:
-            dwi = wgrad(x2, dA, F, M, F)
-        return dx, dwi, dwo, None
+                _dp.register_wire_twin(o, twin)
+            return o
+
+        def run_wo():  # weight gradients on the side stream inside value_and_grad (ops/streams.py)
+            if ctx.needs_input_grad[2]:
+                with _streams.side(dev, [a, t]) as produced:
+                    out["wo"] = wgrad(a, t, ld, F, M)
+                    produced.append(out["wo"])
+
+        def run_wi():
+            if ctx.needs_input_grad[1]:
+                with _streams.side(dev, [x2, dA]) as produced:
+                    out["wi"] = wgrad(x2, dA, F, M, F)
+                    produced.append(out["wi"])
+        _ff_bwd_order(run_dx, run_wo, run_wi)
+        return out.get("dx"), out.get("wi"), out.get("wo"), None
+
+
+# order of the FF block's backward GEMMs after dA (dX, dW_out, dW_in): which operands are still
+# in the Infinity Cache when each runs.  dW_in right after dA (which it reads, 84 MB at the bench
+# shape) measured best: bf16 layer 0.700 -> 0.692 ms, fp8 0.746 -> 0.739 ms over dx,wo,wi
+# (A/B switch, e.g. LJS_FF_BWD_ORDER=dx,wo,wi)
+_FF_BWD_ORDER = [t for t in os.environ.get("LJS_FF_BWD_ORDER", "wi,dx,wo").split(",") if t]
+
+
+def _ff_bwd_order(run_dx, run_wo, run_wi):
+    fns = {"dx": run_dx, "wo": run_wo, "wi": run_wi}
+    for k in _FF_BWD_ORDER:
+        fns.pop(k)()
+    for fn in fns.values():
+        fn()
 
 
 def ff_block_supported(x: torch.Tensor, w_in: torch.Tensor, w_out: torch.Tensor) -> bool:

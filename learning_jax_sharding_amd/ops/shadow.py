@@ -20,7 +20,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-__all__ = ["get", "get_stacked", "entry", "adopt", "mark_fresh", "kinds_of"]
+__all__ = ["get", "get_stacked", "get_mx", "mx_eligible", "entry", "adopt", "mark_fresh", "kinds_of"]
 
 
 class _Entry:
@@ -91,6 +91,37 @@ def get(w: torch.Tensor, kind: str) -> torch.Tensor:
         e.bufs[kind] = _alloc(w, kind)
         e.versions[kind] = -1
     return _refresh(w, e, kind)
+
+
+def mx_eligible(w: torch.Tensor) -> bool:
+    """Weights whose MX-fp8 shadows the fused Adam can keep (64 x 64 tiles of its 4-wide path)."""
+    import os
+    return (w.is_cuda and w.dim() == 2 and w.dtype == torch.float32 and w.is_contiguous()
+            and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0
+            and os.environ.get("LJS_ADAM_ROWS", "64") == "64")
+
+
+def get_mx(w: torch.Tensor, kind: str):
+    """(q, s) MX-fp8 shadow of the f32 weight ``w`` [K][N]: ``"QT"`` = q [N][K] with scales
+    [N][K/32] (blocks along K: a forward GEMM's B operand, ``fp8.quant_cols``), ``"QN"`` = q [K][N]
+    with scales [K][N/32] (blocks along N: a dX GEMM's B operand, ``fp8.quant_rows``).  The fused
+    Adam rewrites them with the weight (``hip.adam_multi``); any other write re-quantizes."""
+    from . import fp8
+    e = entry(w)
+    K, N = w.shape
+    if kind not in e.bufs:
+        qs = (N, K) if kind == "QT" else (K, N)
+        e.bufs[kind] = torch.empty(qs, dtype=torch.uint8, device=w.device)
+        e.bufs[kind + "s"] = torch.empty((qs[0], qs[1] // 32), dtype=torch.uint8, device=w.device)
+        e.versions[kind] = -1
+    q, s = e.bufs[kind], e.bufs[kind + "s"]
+    if e.versions.get(kind) != w._version:
+        if kind == "QT":
+            fp8.quant_cols(w, out=(q, s))
+        else:
+            fp8.quant_rows(w, out=(q, s))
+        e.versions[kind] = e.versions[kind + "s"] = w._version
+    return q, s
 
 
 def get_stacked(ws: Sequence[torch.Tensor]) -> torch.Tensor:

@@ -415,7 +415,12 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
             if outs and inputs:
                 # under a segmented capture the backward must run on this thread: HIP ends a
                 # graph capture only on the thread that began it, and collectives cut captures
-                with torch.autograd.set_multithreading_enabled(_graphs.current() is None):
+                # weight gradients fork onto side streams (ops/streams.py) unless data-parallel
+                # hooks consume gradients as they are produced; joined before they are returned
+                from ..ops import streams as _streams
+                side = reducer is None and all(t.is_cuda for t in inputs)
+                with torch.autograd.set_multithreading_enabled(_graphs.current() is None), \
+                        _streams.wgrad_scope(side):
                     gs = torch.autograd.grad(outs, inputs, seeds, allow_unused=True)
             else:
                 gs = [None] * len(inputs)

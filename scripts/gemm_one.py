@@ -60,6 +60,21 @@ def build(case, tile, sk):
         dW = torch.empty(640, 1536, device=dev)
         return (lambda: hip.gemm(Xt, dYt, dW, 640, 1536, T, T, T, 1536, True, True, splitk=sk, tile=tile,
                                  zero_c=True), 2 * T * 640 * 1536)
+    if case.startswith("dwslab"):  # slab-mode weight gradient: dwslab:K:N (sk = slab count)
+        _, Kd, Nd = case.split(":")
+        Kd, Nd = int(Kd), int(Nd)
+        X, dY = torch.randn(T, Kd, device=dev).bfloat16(), torch.randn(T, Nd, device=dev).bfloat16()
+        dW = torch.empty(sk, Kd, Nd, device=dev)
+        return (lambda: hip.gemm(X, dY, dW, Kd, Nd, T, Kd, Nd, Nd, False, False, sC=Kd * Nd, splitk=sk, tile=tile,
+                                 slabs=True), 2 * T * Kd * Nd)
+    if case.startswith("dwkc"):  # diagnostic: dwkc:K:N with operands pre-transposed (ds_read_b128 path), S batch slabs
+        _, Kd, Nd = case.split(":")
+        Kd, Nd = int(Kd), int(Nd)
+        Xt, dYt = torch.randn(Kd, T, device=dev).bfloat16(), torch.randn(Nd, T, device=dev).bfloat16()
+        dW = torch.empty(sk, Kd, Nd, device=dev)
+        kc = T // sk
+        return (lambda: hip.gemm(Xt, dYt, dW, Kd, Nd, kc, T, T, Nd, True, True, batch=sk, sA=kc, sB=kc,
+                                 sC=Kd * Nd, tile=tile), 2 * T * Kd * Nd)
     raise SystemExit(f"unknown case {case}")
 
 

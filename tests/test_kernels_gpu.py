@@ -33,7 +33,7 @@ def _stored(mat, kc_rowmajor: bool):
 
 @pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (0, 0), (1, 0), (0, 1)])
 @pytest.mark.parametrize("out_f32", [0, 1])
-@pytest.mark.parametrize("tile", [64, 128, 2561, 1284, 1282, 12883, 12884, 1602, 643, 644])
+@pytest.mark.parametrize("tile", [64, 128, 2561, 1284, 1282, 12883, 12884, 1602, 643, 644, 2563, 12856])
 @pytest.mark.parametrize("M,N,K", [(256, 192, 320), (136, 72, 40), (512, 1536, 640), (304, 136, 128), (384, 640, 512)])
 def test_gemm_layouts(hip, a_kc, b_kc, out_f32, tile, M, N, K):
     A = _rand(M, K, seed=1)
@@ -296,6 +296,37 @@ def test_adam_multi_and_shadows(hip):
     torch.testing.assert_close(shadow.entry(ws[1], create=False).bufs["N"], ws[1].bfloat16())
 
 
+@pytest.mark.parametrize("with_bf16", [False, True])
+def test_adam_multi_mx_shadows(hip, with_bf16):
+    """The fused Adam rewrites a weight's MX-fp8 shadows (blocks along rows and, transposed,
+    along columns) bit-exactly equal to quantizing the updated weight, and marks them fresh."""
+    from learning_jax_sharding_amd.ops import fp8 as F, shadow
+    ws = [torch.randn(640, 2560, device=dev) * 0.05, torch.randn(2560, 640, device=dev) * 0.03]
+    gs = [torch.randn_like(w) for w in ws]
+    ms = [torch.zeros_like(w) for w in ws]
+    vs = [torch.zeros_like(w) for w in ws]
+    for w in ws:
+        assert shadow.mx_eligible(w)
+        shadow.get_mx(w, "QT")
+        shadow.get_mx(w, "QN")
+        if with_bf16:
+            shadow.get(w, "T")
+    step = torch.zeros((), dtype=torch.int32, device=dev)
+    for _ in range(2):
+        hip.adam_multi(list(zip(ws, gs, ms, vs)), step, 1e-3, 0.9, 0.999, 1e-8, 0.0, increment_step=True)
+    torch.cuda.synchronize()
+    for w in ws:
+        e = shadow.entry(w, create=False)
+        assert e.versions["QT"] == w._version and e.versions["QN"] == w._version
+        qt, st = F.quant_cols(w)
+        qn, sn = F.quant_rows(w)
+        assert torch.equal(e.bufs["QT"], qt) and torch.equal(e.bufs["QTs"], st)
+        assert torch.equal(e.bufs["QN"], qn) and torch.equal(e.bufs["QNs"], sn)
+        assert shadow.get_mx(w, "QT")[0].data_ptr() == e.bufs["QT"].data_ptr()  # no re-quantization
+        if with_bf16:
+            torch.testing.assert_close(e.bufs["T"], w.t().bfloat16())
+
+
 @pytest.mark.parametrize("R,C", [(640, 512), (200, 132), (96, 100), (70, 66), (33, 7)])
 @pytest.mark.parametrize("g_bf16", [False, True])
 def test_adam_multi_vector_and_edges(hip, R, C, g_bf16):
@@ -432,13 +463,14 @@ def test_slab_reduce(hip, S, R, C, cb):
 
 @pytest.mark.parametrize("T,K,N,S", [(16384, 640, 2560, 5), (16384, 512, 640, 24), (4160, 256, 384, 4),
                                      (16384, 2560, 640, 5)])
-def test_gemm_slab_mode_uneven_splits(hip, T, K, N, S):
+@pytest.mark.parametrize("tile", [1282, 2563, 12856])
+def test_gemm_slab_mode_uneven_splits(hip, T, K, N, S, tile):
     """Slab mode: split s of the token range writes slab s, the last split runs past T (zeros
     from the range check) -- the slabs sum to X^T dY, and each slab is its own token range."""
     assert hip.slab_count(T // 64, S) == S
     x, dy = _rand(T, K, seed=70), _rand(T, N, seed=71)
     slabs = torch.full((S, K, N), float("nan"), dtype=torch.float32, device=dev)
-    hip.gemm(x, dy, slabs, K, N, T, K, N, N, False, False, sC=K * N, splitk=S, tile=1282, slabs=True)
+    hip.gemm(x, dy, slabs, K, N, T, K, N, N, False, False, sC=K * N, splitk=S, tile=tile, slabs=True)
     ref = x.float().t() @ dy.float()
     torch.testing.assert_close(slabs.sum(0), ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
     kc = -(-(T // 64) // S) * 64
@@ -594,19 +626,22 @@ def test_native_runtime_device_info_and_single_member_comm(hip):
     assert "libljs_runtime.so" in maps
 
 
-@pytest.mark.parametrize("T,M,Fd,bcast", [(2048, 640, 2560, False), (1024, 256, 512, True)])
-def test_fp8_ff_block_matches_emulation(hip, T, M, Fd, bcast):
+@pytest.mark.parametrize("T,M,Fd,bcast,self_res", [(2048, 640, 2560, False, False), (1024, 256, 512, True, False),
+                                                   (2048, 640, 2560, False, True), (1024, 256, 512, True, True)])
+def test_fp8_ff_block_matches_emulation(hip, T, M, Fd, bcast, self_res):
     """Fused MX-fp8 FF block on the GPU (fp8 forward + fp8 dX GEMMs, epilogue-quantized
-    operands, fused residual / ReLU mask) == its host emulation, to f32 summation order."""
+    operands, fused residual / ReLU mask, broadcast dY read as one row, the skip gradient of a
+    residual that is x folded into dX's epilogue) == its host emulation, to f32 summation order."""
     from learning_jax_sharding_amd.ops import fp8 as F
     x = _rand(T, M, seed=60).requires_grad_()
     wi = (_rand(M, Fd, dtype=torch.float32, seed=61) * 0.05).requires_grad_()
     wo = (_rand(Fd, M, dtype=torch.float32, seed=62) * 0.03).requires_grad_()
-    res = _rand(T, M, seed=63).requires_grad_()
+    res = x if self_res else _rand(T, M, seed=63).requires_grad_()
     y = F.ff_block_local(x, wi, wo, res)
-    cot = torch.ones((), dtype=torch.bfloat16, device=dev).expand(T, M) if bcast else _rand(T, M, seed=64)
+    cot = torch.full((), 0.5, dtype=torch.bfloat16, device=dev).expand(T, M) if bcast else _rand(T, M, seed=64)
     y.backward(cot)
-    xc, wic, woc, rc = (t.detach().cpu().requires_grad_() for t in (x, wi, wo, res))
+    xc, wic, woc = (t.detach().cpu().requires_grad_() for t in (x, wi, wo))
+    rc = xc if self_res else res.detach().cpu().requires_grad_()
     yc = F.ff_block_local(xc, wic, woc, rc)
     yc.backward(cot.cpu())
     # an f32 summation-order difference can move a value across a bf16 / e4m3 rounding boundary
