@@ -261,6 +261,15 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   // the epilogue operand's 8 chunks per lane are all requested before the first is used (one
   // exposed latency per item instead of one per 16-row block); rows / columns outside the
   // output read 0 through the buffer range check
+  // bf16 outputs (and their MX copy) are staged through LDS (the idle ring) and leave as whole
+  // tile rows -- 256 B of bf16 / 128 B of e4m3 per row, 16 B per lane -- instead of 64 B / 32 B
+  // row pieces per 16-lane group and single scale bytes
+  const bool staged = !out_f32;
+  unsigned char* const Cs = smem;                 // [BM][256 B], 16 B chunks ^ (row & 15)
+  unsigned char* const Qs = smem + BM * 256;      // [BM][128 B], 16 B chunks ^ (row & 7)
+  unsigned char* const Ss = smem + BM * 384;      // [BM][4] scale bytes
+  static_assert(BM * 388 <= NST * STAGE, "staging fits the ring");
+  if (staged) __syncthreads();  // every wave's last fragment reads are done with the ring
   u32x4 rv[2][4];
   if (res_add || res_mask) {
     const __amdgpu_buffer_rsrc_t rr = f8_rsrc(p.R, 2 * ((long)(p.M - 1) * p.ldr + p.N));
@@ -332,12 +341,26 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
         amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
         const int x = mx_exponent(amax);
         const float inv = ldexpf(1.f, -x);
-        if (ok) {
-          const u32x2 qq = u32x2{pack4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
-                                 pack4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv)};
+        const u32x2 qq = u32x2{pack4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
+                               pack4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv)};
+        if (staged) {
+          const int lr = row - m0, lc = col - n0;
+          *reinterpret_cast<u32x2*>(Qs + lr * 128 + (((lc >> 4) ^ (lr & 7)) << 4) + (((lc >> 3) & 1) << 3)) = qq;
+          if (g == 0) Ss[lr * 4 + (lc >> 5)] = (unsigned char)(x + 127);
+        } else if (ok) {
           *reinterpret_cast<u32x2*>(p.QC + (long)row * p.N + col) = qq;
           if (g == 0) p.SC[(long)row * (p.N / 32) + col / 32] = (unsigned char)(x + 127);
         }
+      }
+      if (staged) {
+        if (p.C) {
+          u32x4 pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+          const int lr = row - m0, lc = col - n0;
+          *reinterpret_cast<u32x4*>(Cs + lr * 256 + (((lc >> 3) ^ (lr & 15)) << 4)) = pk;
+        }
+        continue;
       }
       if (!ok) continue;
       if (out_f32) {
@@ -349,6 +372,41 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
         *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(p.C) + (long)row * p.ldc + col) = pk;
+      }
+    }
+  }
+  if (!staged) return;
+  __syncthreads();
+  constexpr int NT = BM * 2;  // threads
+  if (p.C) {
+#pragma unroll
+    for (int r = 0; r < BM * 16 / NT; ++r) {
+      const int c = tid + NT * r, lr = c >> 4, ch = c & 15;
+      const int grow = m0 + lr, gcol = n0 + ch * 8;
+      const u32x4 val = *reinterpret_cast<const u32x4*>(Cs + lr * 256 + ((ch ^ (lr & 15)) << 4));
+      if (grow < p.M && gcol < p.N)
+        *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(p.C) + (long)grow * p.ldc + gcol) = val;
+    }
+  }
+  if (qout) {
+#pragma unroll
+    for (int r = 0; r < BM * 8 / NT; ++r) {
+      const int c = tid + NT * r, lr = c >> 3, ch = c & 7;
+      const int grow = m0 + lr, gcol = n0 + ch * 16;
+      const u32x4 val = *reinterpret_cast<const u32x4*>(Qs + lr * 128 + ((ch ^ (lr & 7)) << 4));
+      if (grow < p.M && gcol < p.N) *reinterpret_cast<u32x4*>(p.QC + (long)grow * p.N + gcol) = val;
+    }
+    if (tid < BM) {
+      const int grow = m0 + tid;
+      const int nsb = p.N / 32;  // scale bytes per row
+      if (grow < p.M) {
+        const unsigned val = *reinterpret_cast<const unsigned*>(Ss + tid * 4);
+        unsigned char* dst = p.SC + (long)grow * nsb + n0 / 32;
+        if (n0 + 128 <= p.N && (nsb & 3) == 0) {
+          *reinterpret_cast<unsigned*>(dst) = val;
+        } else {
+          for (int b = 0; b < 4 && n0 + 32 * b < p.N; ++b) dst[b] = (unsigned char)(val >> (8 * b));
+        }
       }
     }
   }

@@ -17,7 +17,7 @@ def main():
     N, K, tile = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     iters = int(sys.argv[4]) if len(sys.argv) > 4 else 20
     mode = sys.argv[5] if len(sys.argv) > 5 else ""
-    qo = mode in ("qout", "qmask")
+    qo = mode in ("qout", "qmask", "qonly")
     r = torch.randn(T, N, device="cuda").bfloat16() if mode in ("qmask", "res") else None
     x = torch.randn(T, K, device="cuda").bfloat16()
     w = torch.randn(N, K, device="cuda").bfloat16()
@@ -27,8 +27,8 @@ def main():
     q = torch.empty(T, N, dtype=torch.uint8, device="cuda")
     s = torch.empty(T, N // 32, dtype=torch.uint8, device="cuda")
     def run():
-        F.gemm_mx(qa, sa, qb, sb, T, N, K, c, qout=(q, s) if qo else None, tile=tile, res=r,
-                  res_mode="mask" if mode == "qmask" else "add", relu=mode == "qout")
+        F.gemm_mx(qa, sa, qb, sb, T, N, K, None if mode == "qonly" else c, qout=(q, s) if qo else None, tile=tile,
+                  res=r, res_mode="mask" if mode == "qmask" else "add", relu=mode in ("qout", "relu", "qonly"))
     for _ in range(3):
         run()
     torch.cuda.synchronize()

@@ -60,6 +60,11 @@ def build(case, tile, sk):
         dW = torch.empty(640, 1536, device=dev)
         return (lambda: hip.gemm(Xt, dYt, dW, 640, 1536, T, T, T, 1536, True, True, splitk=sk, tile=tile,
                                  zero_c=True), 2 * T * 640 * 1536)
+    if case == "ffup":  # FF up-projection [T][640] x [640][2560], ReLU epilogue (bf16 reference for fp8)
+        X, W = torch.randn(T, 640, device=dev).bfloat16(), torch.randn(2560, 640, device=dev).bfloat16()
+        C = torch.empty(T, 2560, device=dev).bfloat16()
+        return lambda: hip.gemm(X, W, C, T, 2560, 640, 640, 640, 2560, True, True, relu=True, tile=tile), \
+            2 * T * 2560 * 640
     if case.startswith("dwslab"):  # slab-mode weight gradient: dwslab:K:N (sk = slab count)
         _, Kd, Nd = case.split(":")
         Kd, Nd = int(Kd), int(Nd)
