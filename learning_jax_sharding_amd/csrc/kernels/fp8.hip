@@ -503,9 +503,10 @@ LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const 
   a.lda = a_bcast ? 0 : K;  // a_bcast: A / SA hold ONE row, read for every output row
   a.ldsa = a_bcast ? 0 : K / 32;
   if (tile == 0) {
-    // 256-row tiles (8 waves, 3 stages) once they still give >= 2 blocks per CU (256 CUs)
-    const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128);
-    tile = t256 >= 512 ? 2563 : 1282;
+    // 128x128, 2 stages, 2 blocks per CU: with the LDS-staged epilogue it beats the 256-row
+    // tiles at every FF shape (scripts/fp8_one.py: up-projection + MX copy 70.5 vs 76.0 us,
+    // dA with mask + MX copy 83.9 vs 89.5, down-projection 50.1 vs 54.4)
+    tile = 1282;
   }
   const int bm = tile / 10 >= 256 ? 256 : 128;
   const int tiles = ((M + bm - 1) / bm) * ((N + 127) / 128);

@@ -935,7 +935,7 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   const int nkt64 = K / BK;
   const bool slabs = flags & kSlabs;
   if (slabs && (!out_f32 || a_kc || b_kc || batch != 1 || (flags & (8 | 16)) || K % BK ||
-                a.splitk != splitk || tile < 1000))
+                a.splitk != splitk || !(tile > 1000 || tile == 643 || tile == 644)))
     return (int)hipErrorInvalidValue;  // the caller's slab count must be the launched split count
   const long k_ext = slabs ? (long)a.splitk * a.kt_per_split * BK : K;  // K-rows the splits address
   const bool dma_ok = K % BK == 0 && (slabs || nkt64 % a.splitk == 0) &&
