@@ -35,6 +35,12 @@ __all__ = ["get_comm", "reset_comm", "LocalComm", "DistComm", "Transfer"]
 Groups = Sequence[Tuple[int, ...]]
 
 
+
+def _hip():
+    """The HIP pack / unpack kernels (ops/hip.py; torch on host tensors)."""
+    from ..ops import hip
+    return hip
+
 class Transfer:
     """Copy ``src_slices`` of device ``src``'s tensor into ``dst_slices`` of device ``dst``'s output."""
 
@@ -106,14 +112,15 @@ class LocalComm:
                 else:
                     gathered = nat.all_gather([xs[d].contiguous() for d in g])
                 for d, buf in zip(g, gathered):
-                    x = xs[d]
-                    out[d] = buf.movedim(0, dim).reshape(x.shape[:dim] + (n * x.shape[dim],) +
-                                                         x.shape[dim + 1:]).contiguous()
+                    out[d] = _hip().from_rank_major(buf, dim)   # rank-major -> gathered layout
                 continue
             parts = [xs[d] for d in g]
             for d in g:
                 dev = xs[d].device
-                out[d] = torch.cat([p.to(dev) for p in parts], dim)
+                if all(p.device == dev for p in parts):
+                    out[d] = _hip().concat_parts(parts, dim)     # one HIP launch on a GPU
+                else:
+                    out[d] = torch.cat([p.to(dev) for p in parts], dim)
         return out
 
     def reduce_scatter(self, xs, groups, dim):
@@ -126,11 +133,7 @@ class LocalComm:
             nat = self._rccl(g, xs) if grp is None else None
             if grp is not None or nat is not None:
                 n = len(g)
-                ins = []
-                for d in g:
-                    x = xs[d]
-                    s = x.shape[dim] // n
-                    ins.append(x.reshape(x.shape[:dim] + (n, s) + x.shape[dim + 1:]).movedim(dim, 0).contiguous())
+                ins = [_hip().rank_major(xs[d], dim, n) for d in g]   # chunk r -> slot r
                 if grp is not None:
                     res = grp.reduce_scatter(dict(enumerate(ins)))
                     outs = [res[i] for i in range(n)]
@@ -196,14 +199,14 @@ class LocalComm:
             nat = self._rccl(g, xs) if n > 1 and grp is None else None
             if grp is not None or nat is not None:
                 # member i sends chunk perm[r] to member r; receives member-major
-                sends = [torch.stack([chunks[d][perm[r]] for r in range(n)]).contiguous() for d in g]
+                sends = [_hip().rank_major(xs[d], split_dim, n, perm) for d in g]
                 if grp is not None:
                     res = grp.all_to_all(dict(enumerate(sends)))
                     recvs = [res[i] for i in range(n)]
                 else:
                     recvs = nat.all_to_all(sends)
                 for d, recv in zip(g, recvs):
-                    out[d] = torch.cat(list(recv.unbind(0)), concat_dim).contiguous()
+                    out[d] = _hip().from_rank_major(recv, concat_dim)
                 continue
             for i, d in enumerate(g):
                 dev = xs[d].device
@@ -329,11 +332,8 @@ class DistComm:
             buf = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
             dist.all_gather_into_tensor(buf.view((n * x.shape[0],) + tuple(x.shape[1:])) if x.dim() else buf.view(n),
                                         x, group=pg)
-        if not self._member_order_ok(g):
-            order = [sorted(g).index(d) for d in g]
-            buf = buf[order]
-        out = buf.movedim(0, dim).reshape(x.shape[:dim] + (n * x.shape[dim],) + x.shape[dim + 1:])
-        return {self.me: out.contiguous()}
+        order = None if self._member_order_ok(g) else [sorted(g).index(d) for d in g]
+        return {self.me: _hip().from_rank_major(buf, dim, order)}
 
     def reduce_scatter(self, xs, groups, dim):
         g, pg = self._group_of(groups)
@@ -341,13 +341,8 @@ class DistComm:
         if pg is None:
             return {self.me: x.clone()}
         n = len(g)
-        s = x.shape[dim] // n
-        xt = x.reshape(x.shape[:dim] + (n, s) + x.shape[dim + 1:]).movedim(dim, 0)
-        if not self._member_order_ok(g):
-            # chunk k belongs to member g[k]; the collective hands chunk r to the r-th sorted rank
-            srt = sorted(g)
-            xt = xt[[g.index(d) for d in srt]]
-        xt = xt.contiguous()
+        # chunk k belongs to member g[k]; the collective hands chunk r to the r-th sorted rank
+        xt = _hip().rank_major(x, dim, n, None if self._member_order_ok(g) else [g.index(d) for d in sorted(g)])
         grp = self._p2p(g, pg, xt, chunked=True)
         if grp is not None:
             return {self.me: grp.reduce_scatter({grp.rank: xt})[grp.rank]}
@@ -386,10 +381,8 @@ class DistComm:
         gi = [tuple(gg) for gg in groups].index(tuple(g))
         perm = perms[gi] if perms is not None else list(range(n))
         srt = sorted(g)
-        s = x.shape[split_dim] // n
-        chunks = x.reshape(x.shape[:split_dim] + (n, s) + x.shape[split_dim + 1:]).movedim(split_dim, 0)
         # the chunk sent to group member at tile position i is chunk perm[i]; order sends by sorted rank
-        send = chunks[[perm[g.index(r)] for r in srt]].contiguous()
+        send = _hip().rank_major(x, split_dim, n, [perm[g.index(r)] for r in srt])
         grp = self._p2p(g, pg, send, chunked=True)
         nh = None if grp is not None else self._nat(groups, send)
         if grp is not None:
@@ -400,11 +393,7 @@ class DistComm:
             recv = torch.empty_like(send)
             dist.all_to_all_single(recv.view(n, -1), send.view(n, -1), group=pg)
         # recv[k] came from sorted rank srt[k]; concatenate in member (tile) order
-        recv = recv[[srt.index(d) for d in g]]
-        out = recv.movedim(0, concat_dim)
-        shp = list(recv.shape[1:])
-        shp[concat_dim] *= n
-        return {self.me: out.reshape(shp).contiguous()}
+        return {self.me: _hip().from_rank_major(recv, concat_dim, [srt.index(d) for d in g])}
 
     def exchange(self, xs, transfers, out_meta, accumulate=False):
         me = self.me

@@ -987,3 +987,78 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
                        (unsigned*)ticket, lr, b1, b2, eps, wd);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------ collective pack / unpack
+// The layout changes around a collective (comm/backend.py): a tensor [A][n x s][rest] viewed
+// as rows of `inner` bytes, moved to / from the rank-major buffer a collective sends and
+// receives, with an optional rank permutation (tile order vs sorted process ranks), or the
+// per-member parts of a loopback all-gather concatenated along the gather dim.
+//   mode 0 (pack)  : dst[b][a] = src0[a][perm[b]]       (A x B rows in, B x A rows out)
+//   mode 1 (unpack): dst[a][b] = src0[perm[b]][a]
+//   mode 2 (concat): dst[a][b] = src_b[a]                (B separate sources of A rows each)
+// One thread per 16 / 4 / 1-byte unit (the widest that divides `inner` and every address).
+namespace {
+constexpr int kPackMax = 64;
+struct PackArgs {
+  const unsigned char* src[kPackMax];
+  unsigned char* dst;
+  long A, B, inner;
+  int mode, unit;
+  int perm[kPackMax];
+};
+
+template <typename U>
+__global__ void pack_rows_kernel(PackArgs p) {
+  const long upr = p.inner / (long)sizeof(U);  // units per row
+  const long total = p.A * p.B * upr;
+  for (long u = (long)blockIdx.x * blockDim.x + threadIdx.x; u < total; u += (long)gridDim.x * blockDim.x) {
+    const long row = u / upr, off = u - row * upr;
+    const unsigned char* src;
+    long drow;
+    if (p.mode == 0) {          // out row (b, a)
+      const long b = row / p.A, a = row - b * p.A;
+      src = p.src[0] + (a * p.B + p.perm[b]) * p.inner;
+      drow = row;
+    } else {                    // out row (a, b)
+      const long a = row / p.B, b = row - a * p.B;
+      src = p.mode == 1 ? p.src[0] + ((long)p.perm[b] * p.A + a) * p.inner : p.src[b] + a * p.inner;
+      drow = row;
+    }
+    reinterpret_cast<U*>(p.dst + drow * p.inner)[off] = reinterpret_cast<const U*>(src)[off];
+  }
+}
+}  // namespace
+
+LJS_API int ljs_pack_rows(const void* const* srcs, int nsrc, void* dst, long A, long B, long inner, int mode,
+                          const int* perm, hipStream_t s) {
+  if (B < 1 || B > kPackMax || A < 0 || inner < 0 || nsrc < 1 || nsrc > kPackMax || (mode == 2 && nsrc != B) ||
+      mode < 0 || mode > 2)
+    return (int)hipErrorInvalidValue;
+  PackArgs p;
+  uintptr_t al = (uintptr_t)dst | (uintptr_t)inner;
+  for (int i = 0; i < nsrc; ++i) {
+    p.src[i] = (const unsigned char*)srcs[i];
+    al |= (uintptr_t)srcs[i];
+  }
+  for (int i = nsrc; i < kPackMax; ++i) p.src[i] = nullptr;
+  for (int b = 0; b < kPackMax; ++b) p.perm[b] = b < B ? (perm ? perm[b] : b) : 0;
+  for (int b = 0; b < B; ++b)
+    if (p.perm[b] < 0 || p.perm[b] >= B) return (int)hipErrorInvalidValue;
+  p.dst = (unsigned char*)dst;
+  p.A = A;
+  p.B = B;
+  p.inner = inner;
+  p.mode = mode;
+  const long bytes = A * B * inner;
+  if (bytes == 0) return 0;
+  const int unit = (al & 15) == 0 ? 16 : ((al & 3) == 0 ? 4 : 1);
+  p.unit = unit;
+  const long units = bytes / unit;
+  const int threads = 256;
+  long blocks = (units + threads - 1) / threads;
+  if (blocks > 8192) blocks = 8192;
+  if (unit == 16) hipLaunchKernelGGL(pack_rows_kernel<u32x4>, dim3((unsigned)blocks), dim3(threads), 0, s, p);
+  else if (unit == 4) hipLaunchKernelGGL(pack_rows_kernel<unsigned>, dim3((unsigned)blocks), dim3(threads), 0, s, p);
+  else hipLaunchKernelGGL(pack_rows_kernel<unsigned char>, dim3((unsigned)blocks), dim3(threads), 0, s, p);
+  return (int)hipGetLastError();
+}

@@ -29,6 +29,7 @@ c_void_p, c_int, c_long, c_float, c_uint = ctypes.c_void_p, ctypes.c_int, ctypes
 _LP = ctypes.POINTER(ctypes.c_long)
 
 _SIGS = {
+    "ljs_pack_rows": [c_void_p, c_int, c_void_p, c_long, c_long, c_long, c_int, c_void_p, c_void_p],
     "ljs_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
                       c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
                       ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p],
@@ -713,6 +714,69 @@ def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, ac
     rc = lib().ljs_slab_reduce(_p(slabs), S, R * C, R, C, _p(out), cb, out_bs, int(accumulate), _p(out_bf16),
                                _stream(out))
     _ck(rc, "slab_reduce")
+
+
+# ============================================================================ collective pack / unpack
+def _pack_launch(srcs, dst: torch.Tensor, A: int, B: int, inner: int, mode: int, perm) -> None:
+    arr = (c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
+    pa = (c_int * B)(*[int(p) for p in perm]) if perm is not None else None
+    rc = lib().ljs_pack_rows(arr, len(srcs), _p(dst), A, B, inner, mode, pa, _stream(dst))
+    _ck(rc, "pack_rows")
+
+
+def _pack_ok(*ts) -> bool:
+    return all(t.is_cuda for t in ts)
+
+
+def rank_major(x: torch.Tensor, dim: int, n: int, perm=None) -> torch.Tensor:
+    """[.., n*s (dim), ..] -> [n][.., s, ..] contiguous, chunk ``perm[k]`` first-axis slot k (the
+    send buffer of a reduce-scatter / all-to-all), one HIP launch on GPU tensors."""
+    shp = tuple(x.shape)
+    s = shp[dim] // n
+    out_shape = (n,) + shp[:dim] + (s,) + shp[dim + 1:]
+    if not _pack_ok(x) or n > 64:
+        v = x.reshape(shp[:dim] + (n, s) + shp[dim + 1:]).movedim(dim, 0)
+        return (v[list(perm)] if perm is not None else v).contiguous()
+    x = x.contiguous()
+    A = math.prod(shp[:dim])
+    inner = x.element_size() * s * math.prod(shp[dim + 1:])
+    out = torch.empty(out_shape, dtype=x.dtype, device=x.device)
+    _pack_launch([x], out, A, n, inner, 0, perm)
+    return out
+
+
+def from_rank_major(buf: torch.Tensor, dim: int, perm=None) -> torch.Tensor:
+    """[n][.., c (dim), ..] -> [.., n*c, ..]: slot ``perm[k]`` of ``buf`` becomes chunk k along
+    ``dim`` (the receive buffer of an all-gather / all-to-all back in the tensor's layout)."""
+    n = buf.shape[0]
+    cs = tuple(buf.shape[1:])
+    out_shape = cs[:dim] + (n * cs[dim],) + cs[dim + 1:]
+    if not _pack_ok(buf) or n > 64:
+        b = buf[list(perm)] if perm is not None else buf
+        return b.movedim(0, dim).reshape(out_shape).contiguous()
+    buf = buf.contiguous()
+    A = math.prod(cs[:dim])
+    inner = buf.element_size() * math.prod(cs[dim:])
+    out = torch.empty(out_shape, dtype=buf.dtype, device=buf.device)
+    _pack_launch([buf], out, A, n, inner, 1, perm)
+    return out
+
+
+def concat_parts(parts, dim: int) -> torch.Tensor:
+    """``torch.cat(parts, dim)`` of same-shape parts on one GPU in one HIP launch (a loopback
+    all-gather over virtual devices)."""
+    p0 = parts[0]
+    n = len(parts)
+    if not _pack_ok(*parts) or n > 64 or any(p.shape != p0.shape or p.dtype != p0.dtype or p.device != p0.device
+                                            for p in parts):
+        return torch.cat(parts, dim)
+    parts = [p.contiguous() for p in parts]
+    cs = tuple(p0.shape)
+    A = math.prod(cs[:dim])
+    inner = p0.element_size() * math.prod(cs[dim:])
+    out = torch.empty(cs[:dim] + (n * cs[dim],) + cs[dim + 1:], dtype=p0.dtype, device=p0.device)
+    _pack_launch(parts, out, A, n, inner, 2, None)
+    return out
 
 
 def bcast_scalar(g: torch.Tensor, C: int, R: int, want_db: bool, db_out: Optional[torch.Tensor] = None,

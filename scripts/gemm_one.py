@@ -12,7 +12,7 @@ from learning_jax_sharding_amd.ops import hip  # noqa: E402
 from scripts.gemm_tune import timeit  # noqa: E402
 
 dev = torch.device("cuda")
-T = 16384
+T = int(os.environ.get("T", "16384"))
 
 
 def build(case, tile, sk):

@@ -669,3 +669,23 @@ def test_fp8_transformer_layer_trains(gpu_devices):
     assert any(st.kind == "ff_block" for st in rec.steps)
     leaves = ljs.tree_util.tree_leaves(ljs.nn.unbox(g))
     assert all(torch.isfinite(l.to_torch()).all() for l in leaves)
+
+
+@pytest.mark.parametrize("shape,dim,n", [((8, 256, 640), 0, 4), ((8, 256, 640), 1, 2), ((4, 6, 10), 2, 5),
+                                         ((3, 7), 1, 7), ((16,), 0, 8), ((2, 8, 3), 1, 4)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.uint8])
+def test_collective_pack_unpack(hip, shape, dim, n, dtype):
+    """HIP pack / unpack around collectives == the torch movedim / index / cat formulation
+    (rank permutations, 16 / 4 / 1-byte units)."""
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x = (torch.randn(shape, generator=g) * 50).to(dtype).to(dev)
+    perm = list(range(n))[::-1] if n > 1 else [0]
+    s = shape[dim] // n
+    ref = x.reshape(shape[:dim] + (n, s) + shape[dim + 1:]).movedim(dim, 0)
+    assert torch.equal(hip.rank_major(x, dim, n), ref.contiguous())
+    assert torch.equal(hip.rank_major(x, dim, n, perm), ref[perm].contiguous())
+    buf = ref.contiguous()
+    assert torch.equal(hip.from_rank_major(buf, dim), x)
+    assert torch.equal(hip.from_rank_major(buf[perm].contiguous(), dim, perm), x)
+    parts = [t.contiguous() for t in x.chunk(n, dim)]
+    assert torch.equal(hip.concat_parts(parts, dim), torch.cat(parts, dim))
