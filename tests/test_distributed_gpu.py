@@ -35,10 +35,12 @@ def _run(tmp_path, world, capture, steps=3, port=29517, wire="bf16"):
 
 @pytest.mark.parametrize("wire", ["fp32", "bf16"])
 def test_dp2_graph_matches_single_process(tmp_path, wire):
-    """fp32 wire: DP == single process to f32 reassociation.  bf16 wire (the default; the
-    reference's own bf16 gradient all-reduce): Adam's first steps move each weight by ~lr times
-    the SIGN of its gradient, so a near-zero gradient whose bf16-rounded sum flips sign moves
-    that weight by up to 2 lr per step - a handful of elements, bounded by 3 steps x 2 lr."""
+    """fp32 wire: DP == single process to f32 reassociation, except that Adam's first steps move
+    each weight by ~lr times the SIGN of its gradient: a near-zero gradient whose reassociated
+    sum (half-batch weight-gradient split-K slabs, then the all-reduce) flips sign moves that
+    weight by up to 2 lr per step -- a handful of elements of the 0.33 M, bounded by 3 steps x
+    2 lr.  bf16 wire (the reference's own bf16 gradient all-reduce): the same with bf16-rounded
+    sums, so more such elements."""
     ref = _run(tmp_path, 1, False, wire=wire)
     eager = _run(tmp_path, 2, False, port=29537 if wire == "bf16" else 29517, wire=wire)
     graph = _run(tmp_path, 2, True, port=29537 if wire == "bf16" else 29517, wire=wire)
@@ -47,7 +49,9 @@ def test_dp2_graph_matches_single_process(tmp_path, wire):
         if k == "step":
             continue
         if wire == "fp32":
-            np.testing.assert_allclose(eager[k], ref[k], rtol=2e-3, atol=2e-4, err_msg=f"eager {k}")
+            diff = np.abs(eager[k] - ref[k])
+            assert diff.max() <= 6e-3 + 1e-6, (k, diff.max())
+            assert np.mean(diff > 2e-4 + 2e-3 * np.abs(ref[k])) < 1e-4, (k, np.mean(diff > 2e-4))
         else:
             diff = np.abs(eager[k] - ref[k])
             assert diff.max() <= 6e-3 + 1e-6, (k, diff.max())
