@@ -101,6 +101,46 @@ __global__ void quant_mx_cols_kernel(const void* __restrict__ in, int is_bf16, l
   s[(long)n * (K / 32) + kb] = (unsigned char)(x + 127);
 }
 
+// bf16 x[K][N] -> q[N][K], s[N][K/32] through an LDS tile of 128 (K) x 64 (N): rows are read
+// coalesced (128 B per row), and the 4 blocks of a column go to 4 consecutive lanes, so every
+// wave writes 16 rows of q as 128-byte runs (the one-thread-per-block kernel above wrote 32-byte
+// pieces of 64 different rows per wave-instruction: ~1 TB/s on a [16384][640] input)
+__global__ __launch_bounds__(256) void quant_mx_cols_tiled_kernel(const bf16_t* __restrict__ in, long ld, int K, int N,
+                                                                  unsigned char* __restrict__ q,
+                                                                  unsigned char* __restrict__ s) {
+  __shared__ __attribute__((aligned(16))) unsigned char tile[128 * 128];  // [k][n] bf16, 16 B chunk ^ (k >> 5)
+  const int tid = threadIdx.x;
+  const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 128;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = tid + 256 * j, r = c >> 3, ch = c & 7;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(in + (long)(k0 + r) * ld + n0 + ch * 8);
+    *reinterpret_cast<u32x4*>(tile + r * 128 + ((ch ^ ((r >> 5) & 3)) << 4)) = v;
+  }
+  __syncthreads();
+  const int n = tid >> 2, kb = tid & 3;
+  float v[32];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int r = kb * 32 + i;
+    const unsigned short h =
+        *reinterpret_cast<const unsigned short*>(tile + r * 128 + (((n >> 3) ^ kb) << 4) + ((n & 7) << 1));
+    v[i] = __uint_as_float((unsigned)h << 16);
+    amax = fmaxf(amax, fabsf(v[i]));
+  }
+  const int x = mx_exponent(amax);
+  const float inv = ldexpf(1.f, -x);
+  u32x4 o[2];
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    o[c >> 2][c & 3] = pack4_e4m3(v[4 * c] * inv, v[4 * c + 1] * inv, v[4 * c + 2] * inv, v[4 * c + 3] * inv);
+  u32x4* qo = reinterpret_cast<u32x4*>(q + (long)(n0 + n) * K + k0 + kb * 32);
+  qo[0] = o[0];
+  qo[1] = o[1];
+  s[(long)(n0 + n) * (K / 32) + k0 / 32 + kb] = (unsigned char)(x + 127);
+}
+
 // ---------------------------------------------------------------------------- GEMM
 struct F8Args {
   const unsigned char *A, *B, *SA, *SB;  // A[M][K], B[N][K] e4m3; SA[M][K/32], SB[N][K/32] e8m0
@@ -109,12 +149,19 @@ struct F8Args {
   long ldc;
   int M, N, K;
   int flags;  // 1 relu, 2 bias, 4 bias f32, 32 f32 output, 64 residual add, 128 ReLU mask (R > 0),
-              // 256 quantized output copy (QC / SC)
-  const bf16_t* R;      // epilogue operand [M][N] bf16, row stride ldr (ldr 0: one broadcast row)
+              // 256 quantized output copy (QC / SC), 512 transposed quantized copy (QT / ST),
+              // 1024 R is e4m3 bytes (mask mode: keep where the e4m3 value is > 0)
+  const bf16_t* R;      // epilogue operand [M][N] bf16 (or e4m3), row stride ldr elements (0: one row)
   long ldr;
   unsigned char* QC;    // MX-fp8 copy of the (bf16-rounded) output: QC[M][N] e4m3, SC[M][N/32] e8m0
   unsigned char* SC;
+  unsigned char* QT;    // TRANSPOSED MX-fp8 copy: QT[N][M] (row stride ldqt), blocks of 32 along M,
+  unsigned char* ST;    //   ST[N][M/32] -- the output as the K-major operand of a GEMM over M
+  long ldqt;
   int lda, ldsa;        // A / SA row strides in bytes (K, K / 32; both 0: one broadcast row)
+  int ldb, ldsb;        // B / SB row strides in bytes (K, K / 32; both 0: one broadcast row)
+  int kps, nsplit;      // split-K: K-tiles per split, splits (split s -> f32 slab C + s * sC)
+  long sC;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t f8_rsrc(const void* base, long bytes) {
@@ -154,16 +201,20 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
   const int ntn = (p.N + 127) / 128;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = ((p.M + BM - 1) / BM) * ntn;
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = item % ntiles, split = item / ntiles;
   const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * 128;
   if (m0 >= p.M) return;
   const int KB = p.K / 32;  // scale bytes per row
-  const int nk = p.K / F8_BK;
+  // this split's K-tiles [kt0, kt0 + nk)
+  const int kt0 = split * p.kps;
+  const int nk = min(p.K / F8_BK - kt0, p.kps);
 
   const __amdgpu_buffer_rsrc_t ra = f8_rsrc(p.A, (long)(p.M - 1) * p.lda + p.K);
-  const __amdgpu_buffer_rsrc_t rb = f8_rsrc(p.B, (long)p.N * p.K);
+  const __amdgpu_buffer_rsrc_t rb = f8_rsrc(p.B, (long)(p.N - 1) * p.ldb + p.K);
   const __amdgpu_buffer_rsrc_t rsa = f8_rsrc(p.SA, (long)(p.M - 1) * p.ldsa + KB);
-  const __amdgpu_buffer_rsrc_t rsb = f8_rsrc(p.SB, (long)p.N * KB);
+  const __amdgpu_buffer_rsrc_t rsb = f8_rsrc(p.SB, (long)(p.N - 1) * p.ldsb + KB);
 
   int voa[PA], vob[PB];
 #pragma unroll
@@ -176,7 +227,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   for (int i = 0; i < PB; ++i) {
     const int q = wave + NW * i;
     const int row = 8 * q + (lane >> 3), slot = lane & 7;
-    vob[i] = (n0 + row) * p.K + 16 * f8_swz(row, slot);
+    vob[i] = (n0 + row) * p.ldb + 16 * f8_swz(row, slot);
   }
   // scale words (4 B per lane = one row's 4 scale bytes of a K-tile, 64 rows per instruction):
   // the first BM / 64 waves load A's, the next two B's, any further waves repeat B's (same
@@ -184,7 +235,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   const int sw = wave < BM / 64 ? wave : (BM / 64 + ((wave - BM / 64) & 1));
   const bool s_is_a = sw < BM / 64;
   const int s_row = 64 * (s_is_a ? sw : sw - BM / 64) + lane;
-  const int vos = s_is_a ? (m0 + s_row) * p.ldsa : (n0 + s_row) * KB;
+  const int vos = s_is_a ? (m0 + s_row) * p.ldsa : (n0 + s_row) * p.ldsb;
   const __amdgpu_buffer_rsrc_t rs = s_is_a ? rsa : rsb;
   const int s_dst = s_is_a ? 64 * 4 * sw : BM * 4 + 64 * 4 * (sw - BM / 64);
 
@@ -194,10 +245,10 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   do {                                                                                             \
     unsigned char* base_ = smem + (ST) * STAGE;                                                    \
     _Pragma("unroll") for (int i_ = 0; i_ < PA; ++i_)                                              \
-        f8_dma(ra, base_ + (wave + NW * i_) * 1024, 16, voa[i_], (KT) * F8_BK);                    \
+        f8_dma(ra, base_ + (wave + NW * i_) * 1024, 16, voa[i_], (kt0 + (KT)) * F8_BK);            \
     _Pragma("unroll") for (int i_ = 0; i_ < PB; ++i_)                                              \
-        f8_dma(rb, base_ + A_TILE + (wave + NW * i_) * 1024, 16, vob[i_], (KT) * F8_BK);           \
-    f8_dma(rs, base_ + A_TILE + B_TILE + s_dst, 4, vos, (KT) * 4);                                 \
+        f8_dma(rb, base_ + A_TILE + (wave + NW * i_) * 1024, 16, vob[i_], (kt0 + (KT)) * F8_BK);   \
+    f8_dma(rs, base_ + A_TILE + B_TILE + s_dst, 4, vos, (kt0 + (KT)) * 4);                         \
   } while (0)
 
   f32x4 acc[4][4];
@@ -257,6 +308,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   // A 32-column MX block of a row sits in the 4 lanes r16, r16 + 16, + 32, + 48 (g = 0..3).
   const bool relu = p.flags & 1, has_bias = p.flags & 2, bias_f32 = p.flags & 4, out_f32 = p.flags & 32;
   const bool res_add = p.flags & 64, res_mask = p.flags & 128, qout = p.flags & 256;
+  const bool qtout = p.flags & 512, r_fp8 = p.flags & 1024;
   const bool even = (g & 1) == 0;
   // the epilogue operand's 8 chunks per lane are all requested before the first is used (one
   // exposed latency per item instead of one per 16-row block); rows / columns outside the
@@ -272,7 +324,8 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   if (staged) __syncthreads();  // every wave's last fragment reads are done with the ring
   u32x4 rv[2][4];
   if (res_add || res_mask) {
-    const __amdgpu_buffer_rsrc_t rr = f8_rsrc(p.R, 2 * ((long)(p.M - 1) * p.ldr + p.N));
+    const int esz = r_fp8 ? 1 : 2;
+    const __amdgpu_buffer_rsrc_t rr = f8_rsrc(p.R, esz * ((long)(p.M - 1) * p.ldr + p.N));
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int col = n0 + wc * 64 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
@@ -280,8 +333,13 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + wr * 64 + 16 * i + r16;
         const bool ok = row < p.M && col < p.N;
-        rv[q][i] = __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? (int)(((long)row * p.ldr + col) * 2) : 0x7ffffff0,
-                                                         0, 0);
+        const int off = ok ? (int)(((long)row * p.ldr + col) * esz) : 0x7ffffff0;
+        if (r_fp8) {  // 8 e4m3 bytes
+          const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
+          rv[q][i] = u32x4{b[0], b[1], 0u, 0u};
+        } else {
+          rv[q][i] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+        }
       }
     }
   }
@@ -314,7 +372,15 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
       }
       const int row = m0 + wr * 64 + 16 * i + r16;
       const bool ok = row < p.M && col < p.N;  // N % 8 == 0 (launcher)
-      if (res_add || res_mask) {
+      if (res_mask && r_fp8) {
+        // the mask of a ReLU whose output is kept only as e4m3: keep where that value is > 0
+        // (sign clear, not zero)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const unsigned byte = (rv[q][i][e >> 2] >> (8 * (e & 3))) & 0xffu;
+          v[e] = (byte & 0x80u) == 0u && byte != 0u ? v[e] : 0.f;
+        }
+      } else if (res_add || res_mask) {
         const u32x4 rw = rv[q][i];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -353,7 +419,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
         }
       }
       if (staged) {
-        if (p.C) {
+        if (p.C || qtout) {  // (the transposed MX copy is formed from this bf16 image)
           u32x4 pk;
 #pragma unroll
           for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
@@ -364,7 +430,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
       }
       if (!ok) continue;
       if (out_f32) {
-        float* C = reinterpret_cast<float*>(p.C) + (long)row * p.ldc + col;
+        float* C = reinterpret_cast<float*>(p.C) + split * p.sC + (long)row * p.ldc + col;
         *reinterpret_cast<f32x4*>(C) = f32x4{v[0], v[1], v[2], v[3]};
         *reinterpret_cast<f32x4*>(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
       } else if (p.C) {
@@ -406,6 +472,51 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
           *reinterpret_cast<unsigned*>(dst) = val;
         } else {
           for (int b = 0; b < 4 && n0 + 32 * b < p.N; ++b) dst[b] = (unsigned char)(val >> (8 * b));
+        }
+      }
+    }
+  }
+  if (qtout) {
+    // transposed MX copy from the bf16 image: work item (column pair c, c + 1; 32-row block tb),
+    // one 4-byte LDS read per row for both columns; the row blocks of a pair sit in consecutive
+    // lanes, so each store instruction writes 16 rows of QT as 128-byte runs
+    constexpr int NB = BM / 32;
+#pragma unroll
+    for (int r = 0; r < 64 * NB / NT; ++r) {
+      const int w = tid + NT * r, c = 2 * (w / NB), tb = w % NB;
+      float v0[32], v1[32];
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        const int lr = tb * 32 + k;
+        const unsigned h2 =
+            *reinterpret_cast<const unsigned*>(Cs + lr * 256 + (((c >> 3) ^ (lr & 15)) << 4) + ((c & 7) << 1));
+        v0[k] = __uint_as_float(h2 << 16);
+        v1[k] = __uint_as_float(h2 & 0xffff0000u);
+        a0 = fmaxf(a0, fabsf(v0[k]));
+        a1 = fmaxf(a1, fabsf(v1[k]));
+      }
+      const int x0 = mx_exponent(a0), x1 = mx_exponent(a1);
+      const float i0 = ldexpf(1.f, -x0), i1 = ldexpf(1.f, -x1);
+      u32x4 o0[2], o1[2];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o0[k >> 2][k & 3] = pack4_e4m3(v0[4 * k] * i0, v0[4 * k + 1] * i0, v0[4 * k + 2] * i0, v0[4 * k + 3] * i0);
+        o1[k >> 2][k & 3] = pack4_e4m3(v1[4 * k] * i1, v1[4 * k + 1] * i1, v1[4 * k + 2] * i1, v1[4 * k + 3] * i1);
+      }
+      const int gcol = n0 + c, grow = m0 + tb * 32;
+      if (grow < p.M) {  // M % 32 == 0 (launcher): blocks are whole; N % 8: pairs are whole
+        if (gcol < p.N) {
+          u32x4* dst = reinterpret_cast<u32x4*>(p.QT + (long)gcol * p.ldqt + grow);
+          dst[0] = o0[0];
+          dst[1] = o0[1];
+          p.ST[(long)gcol * (p.ldqt / 32) + grow / 32] = (unsigned char)(x0 + 127);
+        }
+        if (gcol + 1 < p.N) {
+          u32x4* dst = reinterpret_cast<u32x4*>(p.QT + (long)(gcol + 1) * p.ldqt + grow);
+          dst[0] = o1[0];
+          dst[1] = o1[1];
+          p.ST[(long)(gcol + 1) * (p.ldqt / 32) + grow / 32] = (unsigned char)(x1 + 127);
         }
       }
     }
@@ -477,6 +588,11 @@ LJS_API int ljs_quant_mx_rows(const void* in, int is_bf16, long ld, int R, int K
 LJS_API int ljs_quant_mx_cols(const void* in, int is_bf16, long ld, int K, int N, void* q, void* s,
                               hipStream_t stream) {
   if (K % 32) return (int)hipErrorInvalidValue;
+  if (is_bf16 && K % 128 == 0 && N % 64 == 0 && ld % 8 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)q & 15) == 0) {
+    hipLaunchKernelGGL(quant_mx_cols_tiled_kernel, dim3(N / 64, K / 128), dim3(256), 0, stream, (const bf16_t*)in, ld,
+                       K, N, (unsigned char*)q, (unsigned char*)s);
+    return (int)hipGetLastError();
+  }
   dim3 grid((N + 63) / 64, K / 32);
   hipLaunchKernelGGL(quant_mx_cols_kernel, grid, dim3(64), 0, stream, in, is_bf16, ld, K, N, (unsigned char*)q,
                      (unsigned char*)s);
@@ -485,16 +601,29 @@ LJS_API int ljs_quant_mx_cols(const void* in, int is_bf16, long ld, int K, int N
 
 // C[M][N] (bf16, or f32 with flags & 32) = A . B^T of MX-fp8 operands; K % 128 == 0, N % 8 == 0.
 // R (bf16 [M][N], row stride ldr) with flags 64 / 128: residual add / ReLU mask in the epilogue;
-// QC / SC with flags 256: also an MX-fp8 copy of the output (N % 32 == 0).  tile: 1282 / 1283 /
-// 2562 / 2563 = BM x 128 with 2 or 3 stages (0: automatic).
+// QC / SC with flags 256: also an MX-fp8 copy of the output (N % 32 == 0); QT / ST with flags 512:
+// its TRANSPOSED MX copy QT[N][M] (row stride ldqt = M, blocks along M; M % 32 == 0, bf16-path
+// outputs only); flags 1024: R is e4m3 [M][N] (ReLU mask of an fp8-only activation).
+// a_bcast / b_bcast: A / B (and scales) hold one row, read for every row.  nsplit > 1: split-K,
+// split s writing the f32 slab C + s * sC (summed by the caller).  tile: 1282 / 1283 / 2562 /
+// 2563 = BM x 128 with 2 or 3 stages (0: automatic).
 LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const void* SB, void* C, const void* bias,
                             int M, int N, int K, long ldc, int flags, const void* R, long ldr, void* QC, void* SC,
-                            int tile, int a_bcast, hipStream_t stream) {
+                            int tile, int a_bcast, int b_bcast, void* QT, void* ST, long ldqt, int nsplit, long sC,
+                            hipStream_t stream) {
   if (K % F8_BK || N % 8 || ldc % 8 || (long)M * K >= (1L << 31) || (long)N * K >= (1L << 31))
     return (int)hipErrorInvalidValue;
   if ((flags & (64 | 128)) && (!R || ldr % 8 || (((uintptr_t)R) & 15) || (flags & 32)))
     return (int)hipErrorInvalidValue;
+  if ((flags & 1024) && !(flags & 128)) return (int)hipErrorInvalidValue;
   if ((flags & 256) && (!QC || !SC || N % 32)) return (int)hipErrorInvalidValue;
+  if ((flags & 512) && (!QT || !ST || M % 32 || ldqt < M || ldqt % 32 || (flags & 32) || ((uintptr_t)QT & 15)))
+    return (int)hipErrorInvalidValue;
+  if (nsplit < 1) nsplit = 1;
+  const int nkt = K / F8_BK;
+  const int kps = (nkt + nsplit - 1) / nsplit;
+  if (nsplit > 1 && (!(flags & 32) || (flags & (64 | 128 | 256 | 512 | 2)) || (nkt + kps - 1) / kps != nsplit))
+    return (int)hipErrorInvalidValue;  // split-K: plain f32 slabs, and the caller's slab count exact
   F8Args a;
   a.A = (const unsigned char*)A; a.B = (const unsigned char*)B;
   a.SA = (const unsigned char*)SA; a.SB = (const unsigned char*)SB;
@@ -502,6 +631,10 @@ LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const 
   a.R = (const bf16_t*)R; a.ldr = ldr; a.QC = (unsigned char*)QC; a.SC = (unsigned char*)SC;
   a.lda = a_bcast ? 0 : K;  // a_bcast: A / SA hold ONE row, read for every output row
   a.ldsa = a_bcast ? 0 : K / 32;
+  a.ldb = b_bcast ? 0 : K;
+  a.ldsb = b_bcast ? 0 : K / 32;
+  a.QT = (unsigned char*)QT; a.ST = (unsigned char*)ST; a.ldqt = ldqt;
+  a.kps = kps; a.nsplit = nsplit; a.sC = sC;
   if (tile == 0) {
     // 128x128, 2 stages, 2 blocks per CU: with the LDS-staged epilogue it beats the 256-row
     // tiles at every FF shape (scripts/fp8_one.py: up-projection + MX copy 70.5 vs 76.0 us,
@@ -509,7 +642,7 @@ LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const 
     tile = 1282;
   }
   const int bm = tile / 10 >= 256 ? 256 : 128;
-  const int tiles = ((M + bm - 1) / bm) * ((N + 127) / 128);
+  const int tiles = ((M + bm - 1) / bm) * ((N + 127) / 128) * nsplit;
   if (tile == 1283) return (int)launch_f8<128, 3>(a, tiles, stream);
   if (tile == 2562) return (int)launch_f8<256, 2>(a, tiles, stream);
   if (tile == 2563) return (int)launch_f8<256, 3>(a, tiles, stream);

@@ -111,11 +111,14 @@ class FeedForward(Module):
                            (self.hidden_dim, d), torch.float32)
         dt = _dt.canonicalize(self.dtype)
         replicated = w_in.tile.is_fully_replicated and w_out.tile.is_fully_replicated
+        loc = next(iter(x.local.values())) if x.local else None
+        tokens_ok = loc is not None and (loc.numel() // max(1, d)) % 128 == 0
         if dt == torch.bfloat16 and replicated and (residual is None or residual is x) \
-                and (d % 128 == 0 and self.hidden_dim % 128 == 0 if self.fp8 else True):
+                and (d % 128 == 0 and self.hidden_dim % 128 == 0 and tokens_ok if self.fp8 else True):
             # replicated weights (data-parallel / single device): the fused block - one autograd
-            # node, epilogue fusions across its GEMMs; fp8: forward and backward-dX GEMMs on
-            # MX-fp8 with the quantized operands written by their producers
+            # node, epilogue fusions across its GEMMs; fp8: every FF GEMM (forward, dX and the
+            # weight gradients) on MX-fp8, the hidden activation stored only as MX-fp8, the
+            # quantized operands written by their producers' epilogues
             from ..ops.fp8 import ff_block
             return ff_block(x, w_in, w_out, residual=residual, fp8=self.fp8)
         if self.fp8:

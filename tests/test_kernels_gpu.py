@@ -544,6 +544,13 @@ def test_fp8_quantization_matches_reference(hip):
     qc, sc = F.quant_cols(w)
     qr3, er3 = F.quantize_mx_ref(w.t().contiguous().cpu())
     assert torch.equal(qc.cpu(), qr3.view(torch.uint8)) and torch.equal(sc.cpu().long(), (er3 + 127).long())
+    # the LDS-tiled bf16 path (K % 128, N % 64), incl. a row-strided view
+    xb = (_rand(1024, 704, dtype=torch.float32, seed=42) * 2).bfloat16()
+    xb[64:96, 5] = 0
+    for src in (xb[:, :640], xb[:, 64:]):
+        qt, st = F.quant_cols(src)
+        qr4, er4 = F.quantize_mx_ref(src.t().contiguous().cpu())
+        assert torch.equal(qt.cpu(), qr4.view(torch.uint8)) and torch.equal(st.cpu().long(), (er4 + 127).long())
 
 
 @pytest.mark.parametrize("tile", [1282, 1283, 2562, 2563])
@@ -689,3 +696,48 @@ def test_collective_pack_unpack(hip, shape, dim, n, dtype):
     assert torch.equal(hip.from_rank_major(buf[perm].contiguous(), dim, perm), x)
     parts = [t.contiguous() for t in x.chunk(n, dim)]
     assert torch.equal(hip.concat_parts(parts, dim), torch.cat(parts, dim))
+
+
+def test_fp8_gemm_transposed_copy_splitk_bcast_and_fp8_mask(hip):
+    """MX GEMM options of the fp8 FF block: the transposed MX copy == quant_cols of the bf16
+    output (bit-exact), split-K slabs sum to the unsplit f32 result, a broadcast B row == the
+    materialised rows, and a ReLU mask read from e4m3 bytes == the mask of their bf16 values."""
+    from learning_jax_sharding_amd.ops import fp8 as F
+    T, N, K = 1024, 640, 512
+    x, w = _rand(T, K, seed=80), _rand(N, K, seed=81)
+    qa, sa = F.quant_rows(x)
+    qb, sb = F.quant_rows(w)
+    c = torch.empty(T, N, dtype=torch.bfloat16, device=dev)
+    F.gemm_mx(qa, sa, qb, sb, T, N, K, c, relu=True)
+    qt = torch.empty(N, T, dtype=torch.uint8, device=dev)
+    st = torch.empty(N, T // 32, dtype=torch.uint8, device=dev)
+    q = torch.empty(T, N, dtype=torch.uint8, device=dev)
+    s = torch.empty(T, N // 32, dtype=torch.uint8, device=dev)
+    F.gemm_mx(qa, sa, qb, sb, T, N, K, None, relu=True, qout=(q, s), qtout=(qt, st))
+    qt_ref, st_ref = F.quant_cols(c)
+    assert torch.equal(qt, qt_ref) and torch.equal(st, st_ref)
+    q_ref, s_ref = F.quant_rows(c)
+    assert torch.equal(q, q_ref) and torch.equal(s, s_ref)
+    # split-K (uneven last split: 4 K-tiles over 3 splits)
+    full = torch.empty(T, N, device=dev)
+    F.gemm_mx(qa, sa, qb, sb, T, N, K, full)
+    assert hip.slab_count(K // 128, 3) == 2   # 4 K-tiles: 3 requested -> 2 x 2
+    slabs = torch.empty(2, T, N, device=dev)
+    F.gemm_mx(qa, sa, qb, sb, T, N, K, slabs, nsplit=2)
+    torch.testing.assert_close(slabs.sum(0), full, rtol=1e-5, atol=1e-4)
+    # broadcast B row
+    wb = _rand(1, K, seed=82)
+    qbr, sbr = F.quant_rows(wb)
+    o1 = torch.empty(T, N, device=dev)
+    o2 = torch.empty(T, N, device=dev)
+    F.gemm_mx(qa, sa, qbr, sbr, T, N, K, o1, b_bcast=True)
+    F.gemm_mx(qa, sa, qbr.expand(N, K).contiguous(), sbr.expand(N, K // 32).contiguous(), T, N, K, o2)
+    assert torch.equal(o1, o2)
+    # ReLU mask from e4m3 bytes (q of the ReLU output) == mask from their dequantized bf16 values
+    vals = q.view(torch.float8_e4m3fn).float().reshape(T, N // 32, 32)
+    dq = (vals * torch.ldexp(torch.ones_like(vals[..., :1]), s.int()[..., None] - 127)).reshape(T, N).bfloat16()
+    m1 = torch.empty(T, N, dtype=torch.bfloat16, device=dev)
+    m2 = torch.empty(T, N, dtype=torch.bfloat16, device=dev)
+    F.gemm_mx(qa, sa, qb, sb, T, N, K, m1, res=q, res_mode="mask")
+    F.gemm_mx(qa, sa, qb, sb, T, N, K, m2, res=dq, res_mode="mask")
+    assert torch.equal(m1, m2)
