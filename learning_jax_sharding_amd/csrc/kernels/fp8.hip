@@ -105,9 +105,13 @@ __global__ void quant_mx_cols_kernel(const void* __restrict__ in, int is_bf16, l
 // coalesced (128 B per row), and the 4 blocks of a column go to 4 consecutive lanes, so every
 // wave writes 16 rows of q as 128-byte runs (the one-thread-per-block kernel above wrote 32-byte
 // pieces of 64 different rows per wave-instruction: ~1 TB/s on a [16384][640] input)
+// (qr / sr non-null: the same pass also writes the row-blocked quantization qr[K][N], sr[K][N/32]
+// -- one read of x for both MX operands it feeds)
 __global__ __launch_bounds__(256) void quant_mx_cols_tiled_kernel(const bf16_t* __restrict__ in, long ld, int K, int N,
                                                                   unsigned char* __restrict__ q,
-                                                                  unsigned char* __restrict__ s) {
+                                                                  unsigned char* __restrict__ s,
+                                                                  unsigned char* __restrict__ qr,
+                                                                  unsigned char* __restrict__ sr) {
   __shared__ __attribute__((aligned(16))) unsigned char tile[128 * 128];  // [k][n] bf16, 16 B chunk ^ (k >> 5)
   const int tid = threadIdx.x;
   const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 128;
@@ -139,6 +143,74 @@ __global__ __launch_bounds__(256) void quant_mx_cols_tiled_kernel(const bf16_t* 
   qo[0] = o[0];
   qo[1] = o[1];
   s[(long)(n0 + n) * (K / 32) + k0 / 32 + kb] = (unsigned char)(x + 127);
+  if (qr) {
+    // row blocks: thread (tile row r, 32-column half hb) -- 4 x 16 B LDS chunks
+    const int r = tid >> 1, hb = tid & 1;
+    float w[32];
+    float am = 0.f;
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const int ch = hb * 4 + c4;
+      const u32x4 raw = *reinterpret_cast<const u32x4*>(tile + r * 128 + ((ch ^ ((r >> 5) & 3)) << 4));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w[8 * c4 + 2 * e] = __uint_as_float(raw[e] << 16);
+        w[8 * c4 + 2 * e + 1] = __uint_as_float(raw[e] & 0xffff0000u);
+        am = fmaxf(am, fmaxf(fabsf(w[8 * c4 + 2 * e]), fabsf(w[8 * c4 + 2 * e + 1])));
+      }
+    }
+    const int xr = mx_exponent(am);
+    const float ir = ldexpf(1.f, -xr);
+    u32x4 orr[2];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      orr[c >> 2][c & 3] = pack4_e4m3(w[4 * c] * ir, w[4 * c + 1] * ir, w[4 * c + 2] * ir, w[4 * c + 3] * ir);
+    u32x4* qd = reinterpret_cast<u32x4*>(qr + (long)(k0 + r) * N + n0 + hb * 32);
+    qd[0] = orr[0];
+    qd[1] = orr[1];
+    sr[(long)(k0 + r) * (N / 32) + n0 / 32 + hb] = (unsigned char)(xr + 127);
+  }
+}
+
+// bf16 x[K][N] -> BOTH its row-blocked (qr [K][N]) and transposed column-blocked (q [N][K]) MX
+// quantizations in one pass; K % 128, N % 64
+LJS_API int ljs_quant_mx_both(const void* in, long ld, int K, int N, void* q, void* s, void* qr, void* sr,
+                              hipStream_t stream) {
+  if (K % 128 || N % 64 || ld % 8 || ((uintptr_t)in & 15) || ((uintptr_t)q & 15) || ((uintptr_t)qr & 15))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(quant_mx_cols_tiled_kernel, dim3(N / 64, K / 128), dim3(256), 0, stream, (const bf16_t*)in, ld, K,
+                     N, (unsigned char*)q, (unsigned char*)s, (unsigned char*)qr, (unsigned char*)sr);
+  return (int)hipGetLastError();
+}
+
+// one scalar cotangent broadcast as TWO rows (lengths C1, C2): bf16 row 1 and the MX bytes of
+// both (the dY rows of y.sum() that the FF block's dA GEMM and dW_out GEMM read), one launch
+__global__ void bcast_scalar_mx2_kernel(const void* __restrict__ g, int g_bf16, int C1, bf16_t* __restrict__ row,
+                                        unsigned char* __restrict__ q1, unsigned char* __restrict__ s1, int C2,
+                                        unsigned char* __restrict__ q2, unsigned char* __restrict__ s2) {
+  const int c4 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  const float v = bf2f(f2bf(g_bf16 ? bf2f(*reinterpret_cast<const bf16_t*>(g)) : *reinterpret_cast<const float*>(g)));
+  const int x = mx_exponent(fabsf(v));
+  const float sv = v * ldexpf(1.f, -x);
+  const unsigned qq = pack4_e4m3(sv, sv, sv, sv);
+  if (c4 < C1) {
+    *reinterpret_cast<u32x2*>(row + c4) = u32x2{pack_bf16x2(v, v), pack_bf16x2(v, v)};
+    *reinterpret_cast<unsigned*>(q1 + c4) = qq;
+    if ((c4 & 31) == 0) s1[c4 / 32] = (unsigned char)(x + 127);
+  }
+  if (c4 < C2) {
+    *reinterpret_cast<unsigned*>(q2 + c4) = qq;
+    if ((c4 & 31) == 0) s2[c4 / 32] = (unsigned char)(x + 127);
+  }
+}
+
+LJS_API int ljs_bcast_scalar_mx2(const void* g, int g_bf16, int C1, void* row, void* q1, void* s1, int C2, void* q2,
+                                 void* s2, hipStream_t stream) {
+  if (C1 % 32 || C2 % 32) return (int)hipErrorInvalidValue;
+  const int c = C1 > C2 ? C1 : C2;
+  hipLaunchKernelGGL(bcast_scalar_mx2_kernel, dim3((c / 4 + 255) / 256), dim3(256), 0, stream, g, g_bf16, C1,
+                     (bf16_t*)row, (unsigned char*)q1, (unsigned char*)s1, C2, (unsigned char*)q2, (unsigned char*)s2);
+  return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------- GEMM
@@ -590,7 +662,7 @@ LJS_API int ljs_quant_mx_cols(const void* in, int is_bf16, long ld, int K, int N
   if (K % 32) return (int)hipErrorInvalidValue;
   if (is_bf16 && K % 128 == 0 && N % 64 == 0 && ld % 8 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)q & 15) == 0) {
     hipLaunchKernelGGL(quant_mx_cols_tiled_kernel, dim3(N / 64, K / 128), dim3(256), 0, stream, (const bf16_t*)in, ld,
-                       K, N, (unsigned char*)q, (unsigned char*)s);
+                       K, N, (unsigned char*)q, (unsigned char*)s, nullptr, nullptr);
     return (int)hipGetLastError();
   }
   dim3 grid((N + 63) / 64, K / 32);

@@ -37,6 +37,10 @@ _SIGS = {
                           ctypes.c_void_p, ctypes.c_void_p],
     "ljs_quant_mx_cols": [ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                           ctypes.c_void_p, ctypes.c_void_p],
+    "ljs_quant_mx_both": [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+    "ljs_bcast_scalar_mx2": [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
     "ljs_bcast_scalar_mx": [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                             ctypes.c_void_p, ctypes.c_void_p],
     "ljs_gemm_mx_fp8": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -323,6 +327,24 @@ def _t_quant(t2: torch.Tensor):
     return quant_cols(t2)
 
 
+def _quant_both(x2: torch.Tensor):
+    """((q [T][M], s): row-blocked, (qT [M][T], sT): token-blocked transposed) MX quantizations of
+    a bf16 [T][M] in one pass over it (or two passes when the shape does not tile)."""
+    T, M = x2.shape
+    if x2.is_cuda and x2.dtype == torch.bfloat16 and T % 128 == 0 and M % 64 == 0 and x2.stride(1) == 1 \
+            and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0:
+        dev = x2.device
+        q = torch.empty((T, M), dtype=torch.uint8, device=dev)
+        s = torch.empty((T, M // BLOCK), dtype=torch.uint8, device=dev)
+        qT = torch.empty((M, T), dtype=torch.uint8, device=dev)
+        sT = torch.empty((M, T // BLOCK), dtype=torch.uint8, device=dev)
+        rc = _lib().ljs_quant_mx_both(hip._p(x2), x2.stride(0), T, M, hip._p(qT), hip._p(sT), hip._p(q), hip._p(s),
+                                      hip._stream(x2))
+        hip._ck(rc, "quant_mx_both")
+        return (q, s), (qT, sT)
+    return quant_rows(x2), _t_quant(x2)
+
+
 def _pick_split(tiles: int, nkt: int) -> int:
     """Split-K count for an MX weight-gradient GEMM: the most splits keeping the work items within
     two 128x128 blocks per CU (2 x 256), each split at least 8 K-tiles, ceil-consistent."""
@@ -377,8 +399,9 @@ class _FFBlockFp8(torch.autograd.Function):
         x2 = _bf16(x.reshape(-1, M).contiguous())
         T = x2.shape[0]
         dev = x.device
-        qx, sx = quant_rows(x2)                     # [T][M], blocks along M
-        qxT, sxT = _t_quant(x2)                     # [M][T], blocks along T (dW_in)
+        # [T][M] blocked along M (the up projection's operand) and [M][T] blocked along T
+        # (dW_in's), from one pass over x
+        (qx, sx), (qxT, sxT) = _quant_both(x2)
         qwi, swi = _weight_q(w_in)                  # [F][M], blocks along M
         qa = torch.empty((T, F), dtype=torch.uint8, device=dev)
         sa = torch.empty((T, F // BLOCK), dtype=torch.uint8, device=dev)
@@ -402,9 +425,9 @@ class _FFBlockFp8(torch.autograd.Function):
         lead, M, F, T, has_res, res_is_x = ctx.meta
         dev = qa.device
         dy2 = dy.reshape(T, M)
-        bm = _bcast_grad_mx(dy2)
-        if bm is not None:                          # scalar broadcast: row + its MX row, one launch
-            t, qdy, sdy = bm
+        bm = _bcast_grad_mx2(dy2, T) if ctx.needs_input_grad[2] else _bcast_grad_mx(dy2)
+        if bm is not None:                          # scalar broadcast: its rows + MX rows, one launch
+            t, qdy, sdy = bm[:3]
             ld, bc = 0, True
         else:
             t, ld = _row_view(dy2, T, M)            # bf16 dY (one row, ld 0, when broadcast)
@@ -427,7 +450,7 @@ class _FFBlockFp8(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             # dY blocked along tokens: one constant row for a broadcast scalar, else a column pass
             if bm is not None:
-                qdyT, sdyT = _bcast_row_mx(dy2, T)
+                qdyT, sdyT = bm[3], bm[4]
                 dwo = _mx_wgrad(qaT, saT, qdyT, sdyT, F, M, T, b_bcast=True)
             else:
                 qdyT, sdyT = _t_quant(t)
@@ -437,6 +460,25 @@ class _FFBlockFp8(torch.autograd.Function):
             out["wi"] = _mx_wgrad(qxT, sxT, qdAT, sdAT, M, F, T)
         dres = dy if (has_res and ctx.needs_input_grad[3] and not fold) else None
         return out.get("dx"), out.get("wi"), out.get("wo"), dres
+
+
+def _bcast_grad_mx2(dy2: torch.Tensor, n: int):
+    """:func:`_bcast_grad_mx` plus the MX row of length ``n`` (the token-blocked dY^T row), one
+    launch; None unless ``dy2`` is a broadcast scalar."""
+    T, M = dy2.shape
+    if not (dy2.is_cuda and dy2.numel() > 0 and dy2.stride(0) == 0 and dy2.stride(1) == 0 and M % 32 == 0
+            and n % 32 == 0 and dy2.dtype in (torch.float32, torch.bfloat16)):
+        return None
+    dev = dy2.device
+    row = torch.empty((1, M), dtype=torch.bfloat16, device=dev)
+    q1 = torch.empty((1, M), dtype=torch.uint8, device=dev)
+    s1 = torch.empty((1, M // BLOCK), dtype=torch.uint8, device=dev)
+    q2 = torch.empty((1, n), dtype=torch.uint8, device=dev)
+    s2 = torch.empty((1, n // BLOCK), dtype=torch.uint8, device=dev)
+    rc = _lib().ljs_bcast_scalar_mx2(hip._p(dy2.as_strided((1,), (1,))), int(dy2.dtype == torch.bfloat16), M,
+                                     hip._p(row), hip._p(q1), hip._p(s1), n, hip._p(q2), hip._p(s2), hip._stream(row))
+    hip._ck(rc, "bcast_scalar_mx2")
+    return row.expand(T, M), q1, s1, q2, s2
 
 
 def _bcast_row_mx(dy2: torch.Tensor, n: int):

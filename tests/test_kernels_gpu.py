@@ -551,6 +551,10 @@ def test_fp8_quantization_matches_reference(hip):
         qt, st = F.quant_cols(src)
         qr4, er4 = F.quantize_mx_ref(src.t().contiguous().cpu())
         assert torch.equal(qt.cpu(), qr4.view(torch.uint8)) and torch.equal(st.cpu().long(), (er4 + 127).long())
+        # one pass, both layouts
+        (q1, s1), (q2, s2) = F._quant_both(src)
+        qr5, sr5 = F.quant_rows(src)
+        assert torch.equal(q1, qr5) and torch.equal(s1, sr5) and torch.equal(q2, qt) and torch.equal(s2, st)
 
 
 @pytest.mark.parametrize("tile", [1282, 1283, 2562, 2563])
