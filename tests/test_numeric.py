@@ -321,27 +321,29 @@ def test_column_row_parallel_and_fsdp_prefetch(host_devices):
 def test_fp8_ff_block_emulation_matches_reference_recipe(host_devices):
     """The host emulation of the fused MX-fp8 FF block: forward == the two-dense MX-fp8 forward
     (same quantization points), gradients close to an f32 autograd oracle of relu(x Win) Wout
-    (fp8 operands: loose tolerance), residual gradient passed through."""
+    (fp8 operands everywhere, weight gradients included: loose tolerance), residual gradient
+    passed through."""
     host_devices(1)
     from learning_jax_sharding_amd.ops import fp8 as F
     g = torch.Generator().manual_seed(0)
-    x = torch.randn(64, 256, generator=g).to(torch.bfloat16).requires_grad_()
+    x = torch.randn(128, 256, generator=g).to(torch.bfloat16).requires_grad_()
     wi = (torch.randn(256, 512, generator=g) * 0.05).requires_grad_()
     wo = (torch.randn(512, 256, generator=g) * 0.05).requires_grad_()
-    res = torch.randn(64, 256, generator=g).to(torch.bfloat16).requires_grad_()
+    res = torch.randn(128, 256, generator=g).to(torch.bfloat16).requires_grad_()
     y = F.ff_block_local(x, wi, wo, res)
     a = F.mx_linear_ref(x, wi, None, True, torch.bfloat16)
     y2 = F.mx_linear_ref(a, wo, None, False, torch.bfloat16) + res
     assert torch.equal(y, y2)
-    cot = torch.randn(64, 256, generator=g).to(torch.bfloat16)
+    cot = torch.randn(128, 256, generator=g).to(torch.bfloat16)
     (y.float() * cot.float()).sum().backward()
     # vs the straight-through backward of the same fp8 forward (f32 math, the forward's ReLU
-    # mask): the fp8 dX GEMMs' quantization of dY / dA and the weights is the only difference
+    # mask): the fp8 quantization of the backward GEMMs' operands (dY, dA, the weights, and the
+    # token-blocked activations of the weight gradients) is the only difference (~5 %)
     a = F.mx_linear_ref(x.detach(), wi.detach(), None, True, torch.bfloat16).float()
     dA = (cot.float() @ wo.detach().t()) * (a > 0)
     want = {"x": dA @ wi.detach().t(), "wi": x.detach().float().t() @ dA, "wo": a.t() @ cot.float()}
     got = {"x": x.grad.float(), "wi": wi.grad, "wo": wo.grad}
-    for k, tol in (("x", 0.08), ("wi", 0.06), ("wo", 1e-6)):
+    for k, tol in (("x", 0.08), ("wi", 0.08), ("wo", 0.06)):
         err = ((got[k] - want[k]).norm() / want[k].norm()).item()
         assert err < tol, (k, err)
     # and a loose sanity bound against the f32 oracle (mask flips of the fp8 forward included)
