@@ -16,6 +16,7 @@
 // the row reads and the transposed reads are bank-conflict free, XCD-aware tile order.
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace {
 
@@ -36,6 +37,8 @@ struct GemmArgs {
   float* psum;  // LDS-DMA kernels, bf16 out: per (item, wave) sums of the stored values, or null
   const void* res;  // R[b][row][col] at res + b * sR + row * ldr + col (ldr may be 0: one broadcast row)
   long ldr, sR;
+  bf16_t* acopy;    // f32-A kernels: the bf16 rounding of A ([M][K], dense), written by the items of
+                    // batch 0 / tile column 0 (the operand the backward's weight gradient reads)
 };
 
 constexpr int kResAdd = 64, kResMask = 128, kResF32 = 256;
@@ -389,6 +392,46 @@ struct DmaTile {
   }
 };
 
+// An f32, k-contiguous operand tile (R rows x BK f32 = 256-byte rows): 1 KiB DMA pieces of 4 rows;
+// 16-byte chunk c of row r lands at chunk c ^ (r & 15) (conflict-free 2 x ds_read_b128 fragment
+// reads: the 16 rows of a lane group hit 16 different chunk positions)
+template <int R, int NW>
+struct DmaTileF32 {
+  static constexpr int PIECES = R * BK * 4 / 1024;
+  static constexpr int PER_WAVE = PIECES / NW;
+  static_assert(PIECES % NW == 0, "pieces must split evenly over the waves");
+  int voff[PER_WAVE];
+
+  __device__ __forceinline__ void init(long ld, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int q = wave + NW * i;
+      const int row = 4 * q + (lane >> 4), slot = lane & 15;
+      voff[i] = (int)(((long)row * ld + 4 * (slot ^ (row & 15))) * 4);
+    }
+  }
+
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, bf16_t* lds, int soff, int wave) const {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_PTR(void))(lds + (wave + NW * i) * 512), 16, voff[i], soff,
+                                               0, 0);
+  }
+};
+
+// bf16 MFMA operand (8 consecutive k of row rb + lane & 15, k-step ks) from an f32 image, rounded
+// to nearest-even exactly like cast_f32_bf16
+__device__ __forceinline__ bf16x8 frag_f32(const bf16_t* lds, int rb, int ks, int lane) {
+  const int row = rb + (lane & 15);
+  const int kc = ks * 4 + (lane >> 4);
+  const unsigned char* base = reinterpret_cast<const unsigned char*>(lds) + row * 256;
+  const f32x4 lo = *reinterpret_cast<const f32x4*>(base + (((2 * kc) ^ (row & 15)) << 4));
+  const f32x4 hi = *reinterpret_cast<const f32x4*>(base + (((2 * kc + 1) ^ (row & 15)) << 4));
+  const u32x4 u = u32x4{pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
+                        pack_bf16x2(hi[2], hi[3])};
+  return __builtin_bit_cast(bf16x8, u);
+}
+
 struct WorkItem {
   int b, m0, n0, kt0, split;
 };
@@ -427,14 +470,19 @@ constexpr int kSC1 = 16;  // buffer-instruction cache policy bit: sc1 (gfx940-fa
 // (a 4-wave kernel whose LDS ring lets two blocks share a CU is told so: the pipelined main loop's
 // second fragment set and the epilogue registers would otherwise push VGPR + AGPR past 256 and
 // halve the resident blocks)
-template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0>
-__global__ __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
+// AF32: A is f32 (k-contiguous), rounded to bf16 at the fragment read -- the activation cast
+// fused into the GEMM; the items of batch 0 / tile column 0 also write A's bf16 rounding
+// (p.acopy) for the backward.
+template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0, bool AF32 = false>
+__global__ __launch_bounds__(WM * WN * 64,
+                            (WM * WN == 4 && NST * ((AF32 ? 2 : 1) * BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
 gemm_dma_kernel(
     GemmArgs p) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-  constexpr int A_TILE = BM * BK, B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
-  using TA = DmaTile<BM, A_KC, NW>;
+  static_assert(!AF32 || A_KC, "f32 A is k-contiguous");
+  constexpr int A_TILE = BM * BK * (AF32 ? 2 : 1), B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
+  using TA = typename std::conditional<AF32, DmaTileF32<BM, NW>, DmaTile<BM, A_KC, NW>>::type;
   using TB = DmaTile<BN, B_KC, NW>;
   constexpr int L = TA::PER_WAVE + TB::PER_WAVE;  // DMA instructions per wave per K-tile
   // Operands swapped (C^T = B^T A^T per 16x16 block): each lane ends with 4 CONSECUTIVE
@@ -459,9 +507,10 @@ gemm_dma_kernel(
   const int nk = p.kt_per_split;               // K-tiles per item (the split divides them)
   const int total = my_items * nk;
 
-  const long a_bytes = 2 * (A_KC ? (long)(p.M - 1) * p.lda + p.K : (long)(p.K - 1) * p.lda + p.M);
+  constexpr int AES = AF32 ? 4 : 2;  // A element bytes
+  const long a_bytes = AES * (A_KC ? (long)(p.M - 1) * p.lda + p.K : (long)(p.K - 1) * p.lda + p.M);
   const long b_bytes = 2 * (B_KC ? (long)(p.N - 1) * p.ldb + p.K : (long)(p.K - 1) * p.ldb + p.N);
-  const long a_kt = A_KC ? (long)BK * 2 : (long)BK * p.lda * 2;  // bytes per K-tile step
+  const long a_kt = A_KC ? (long)BK * AES : (long)BK * p.lda * 2;  // bytes per K-tile step
   const long b_kt = B_KC ? (long)BK * 2 : (long)BK * p.ldb * 2;
 
   TA ta;
@@ -477,10 +526,10 @@ gemm_dma_kernel(
   const int a_step = (int)a_kt, b_step = (int)b_kt;
   auto load_item = [&](int k) {
     const WorkItem w = decode_item(p, slot + G * k, ntm, ntn);
-    ra = make_rsrc(p.A + (long)w.b * p.sA, a_bytes);
+    ra = make_rsrc(reinterpret_cast<const unsigned char*>(p.A) + (long)w.b * p.sA * AES, a_bytes);
     rb = make_rsrc(p.B + (long)w.b * p.sB, b_bytes);
     a_off = __builtin_amdgcn_readfirstlane(
-        (int)((A_KC ? (long)w.m0 * BM * p.lda : (long)w.m0 * BM) * 2 + w.kt0 * a_kt));
+        (int)((A_KC ? (long)w.m0 * BM * p.lda : (long)w.m0 * BM) * AES + w.kt0 * a_kt));
     b_off = __builtin_amdgcn_readfirstlane(
         (int)((B_KC ? (long)w.n0 * BN * p.ldb : (long)w.n0 * BN) * 2 + w.kt0 * b_kt));
   };
@@ -558,7 +607,10 @@ gemm_dma_kernel(
     const bf16_t* As_ = smem + (g % NST) * STAGE;
     const bf16_t* Bs_ = As_ + A_TILE;
 #pragma unroll
-    for (int ii = 0; ii < TM; ++ii) af[ii] = frag<BM, A_KC>(As_, wr * (BM / WM) + ii * 16, ks, lane);
+    for (int ii = 0; ii < TM; ++ii) {
+      if constexpr (AF32) af[ii] = frag_f32(As_, wr * (BM / WM) + ii * 16, ks, lane);
+      else af[ii] = frag<BM, A_KC>(As_, wr * (BM / WM) + ii * 16, ks, lane);
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, B_KC>(Bs_, wc * (BN / WN) + j * 16, ks, lane);
   };
@@ -619,6 +671,25 @@ gemm_dma_kernel(
     const WorkItem w = decode_item(p, slot + G * it, ntm, ntn);
     const int m0 = w.m0 * BM + wr * (BM / WM), n0 = w.n0 * BN + wc * (BN / WN);
     const int g = lane >> 4;
+    if constexpr (AF32) {
+      if (p.acopy && w.b == 0 && w.n0 == 0) {
+        // this row block's bf16 A for the backward (re-read from L2 where the DMA just streamed
+        // it); drained before the epilogue so the counted waits below stay exact
+        const float* A32 = reinterpret_cast<const float*>(p.A);
+        const int kc8 = p.K / 8;
+        for (int c = tid; c < BM * kc8; c += WM * WN * 64) {
+          const int row = c / kc8, k = (c - row * kc8) * 8, grow = w.m0 * BM + row;
+          if (grow < p.M) {
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(A32 + (long)grow * p.lda + k);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(A32 + (long)grow * p.lda + k + 4);
+            *reinterpret_cast<u32x4*>(p.acopy + (long)grow * p.K + k) =
+                u32x4{pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
+                      pack_bf16x2(hi[2], hi[3])};
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
     if constexpr (!OUT_F32) {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]; lanes g, g^1 trade halves so
       // even g owns cols 16 j0 + 4 g .. +7 and odd g owns 16 j1 + 4 (g - 1) .. +7
@@ -819,12 +890,14 @@ LJS_DMA_INST_RES(128, 128, 2, 2, 4)
 LJS_DMA_INST_RES(128, 128, 2, 4, 3)
 LJS_DMA_INST_RES(128, 128, 2, 4, 4)
 #undef LJS_DMA_INST_RES
+// f32-A (cast-on-load) forward GEMMs: 128x128, 8 waves, 3 stages (144 KiB with the f32 A image)
+template __global__ void gemm_dma_kernel<128, 128, 2, 4, 3, true, true, false, 0, true>(GemmArgs);
 #undef LJS_DMA_INST_LAYOUTS
 #undef LJS_DMA_INST
 
 int g_cus = 0;
 
-template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF, int RES = 0>
+template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF, int RES = 0, bool AF32 = false>
 hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   if (!g_cus) {
     int dev = 0;
@@ -845,13 +918,13 @@ hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   // walks `rounds` items with the next item's first K-tiles in flight during the current
   // item's epilogue (measured at T = 16384: QKV projection 43.8 -> 39.9 us on 128x128 x 2/CU).
   // Otherwise one block per item, which lets the dispatcher balance a ragged last round.
-  constexpr int kLdsBytes = NST * (BM + BN) * BK * 2;
+  constexpr int kLdsBytes = NST * ((AF32 ? 2 : 1) * BM + BN) * BK * 2;
   constexpr int kNatural = (WM * WN == 4 && kLdsBytes <= 80 * 1024) ? 2 : 1;  // resident blocks / CU
   if (bpc == 0 && bpc_env == 0 && items > g_cus * kNatural && items % (g_cus * kNatural) == 0) bpc = kNatural;
   int grid = bpc > 0 ? g_cus * bpc : items;
   if (grid > items) grid = items;
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, NST, AK, BKc, OF, RES>), dim3(grid), dim3(WM * WN * 64), 0, s,
-                     a2);
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, NST, AK, BKc, OF, RES, AF32>), dim3(grid), dim3(WM * WN * 64), 0,
+                     s, a2);
   return hipGetLastError();
 }
 
@@ -888,10 +961,13 @@ hipError_t dispatch_layout(const GemmArgs& a, int a_kc, int b_kc, int out_f32, h
 // Returns 0 on success.  Preconditions checked here (the Python wrapper checks them too):
 // K % 8 == 0; for an m/n-contiguous operand its M (or N) % 8 == 0; 16-byte aligned bases
 // and leading dimensions that are multiples of 8 elements.
+constexpr int kAF32 = 2048;  // A is f32 (k-contiguous): rounded to bf16 in the GEMM (acopy: its bf16 copy)
+
 LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
                           long lda, long ldb, long ldc, long sA, long sB, long sC, long sBias, int batch,
                           int a_kc, int b_kc, int out_f32, int flags, float alpha, int splitk, int tile,
-                          void* psum, int* psum_count, const void* res, long ldr, long sR, hipStream_t stream) {
+                          void* psum, int* psum_count, const void* res, long ldr, long sR, void* acopy,
+                          hipStream_t stream) {
   if (K % 8 || (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
   if (splitk > 1 && !out_f32) return (int)hipErrorInvalidValue;
   // the epilogue operand applies to bf16 outputs (its 16-byte loads need aligned 8-column chunks)
@@ -913,6 +989,19 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   a.res = res;
   a.ldr = ldr;
   a.sR = sR;
+  a.acopy = (bf16_t*)acopy;
+  if (flags & kAF32) {
+    // f32 A: the 8-wave 128x128 LDS-DMA kernel only (bf16 output, k-contiguous operands, no
+    // split, no epilogue operand / fused sum); every condition is the caller's to meet
+    if (!a_kc || !b_kc || out_f32 || splitk > 1 || (flags & (kResAdd | kResMask | 8 | 16)) || psum || K % 64 ||
+        lda % 4 || N % 8 || ldc % 8 || (((uintptr_t)A) & 15) || (acopy && (sA != 0 && batch > 1)) ||
+        (long)M * lda * 4 >= (1L << 31) || (long)N * ldb >= (1L << 30))
+      return (int)hipErrorInvalidValue;
+    a.kt_per_split = K / 64;
+    a.splitk = 1;
+    a.flags = flags & ~kAF32;
+    return (int)launch_dma<128, 128, 2, 4, 3, true, true, false, 0, true>(a, stream, 0);
+  }
 
   if (psum_count) *psum_count = 0;
   int nkt = (K + BK - 1) / BK;

@@ -32,7 +32,7 @@ _SIGS = {
     "ljs_pack_rows": [c_void_p, c_int, c_void_p, c_long, c_long, c_long, c_int, c_void_p, c_void_p],
     "ljs_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
                       c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
-                      ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p],
+                      ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p, c_void_p],
     "ljs_sum_partials": [c_void_p, c_int, c_void_p, c_int, c_void_p],
     "ljs_gemm_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long,
                      c_long, c_long, c_long, c_int, c_void_p],
@@ -170,7 +170,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
          accumulate: bool = False, splitk: int = 1, tile: Optional[int] = None, a_off: int = 0, b_off: int = 0,
          c_off: int = 0, zero_c: bool = False, psum: Optional[torch.Tensor] = None,
          res: Optional[torch.Tensor] = None, res_ld: int = 0, res_mode: str = "add", sR: int = 0,
-         slabs: bool = False) -> int:
+         slabs: bool = False, acopy: Optional[torch.Tensor] = None) -> int:
     """Raw launcher.  A/B bf16; C bf16 or f32 (split-K/accumulate need f32 C).
 
     ``lda``/``ldb`` may be 0 for an operand that repeats one row (a broadcast gradient).
@@ -182,15 +182,19 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     broadcast row; bf16 C only) is an epilogue operand: ``res_mode="add"`` adds it as a residual
     (``bf16(bf16(y) + bf16(res))``, bit-exact with the unfused add), ``"mask"`` keeps the outputs
     where ``res > 0`` (a ReLU backward fused into the dX GEMM).
+    ``A`` may be f32 (k-contiguous, bf16 output, no split / epilogue operand / fused sum): the
+    GEMM rounds it to bf16 as it reads it (the activation cast fused in) and, with ``acopy`` (bf16
+    [M][K]), also writes that rounding for the backward.
     ``slabs`` (f32 C, m/n-contiguous operands, batch 1, an LDS-DMA tile): split s of the K range
     writes its own slab ``C + s * sC``; ``splitk`` must be :func:`slab_count`-consistent (the
     last split may run past K, where it reads zeros), so the split need not divide the K-tiles.
     """
-    assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
+    assert A.dtype in (torch.bfloat16, torch.float32) and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
     out_f32 = C.dtype == torch.float32
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
-        (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0) | (512 if slabs else 0)
+        (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0) | (512 if slabs else 0) | \
+        (2048 if A.dtype == torch.float32 else 0)
     if res is not None:
         assert not out_f32 and res.dtype in (torch.bfloat16, torch.float32), (C.dtype, res.dtype)
         flags |= (64 if res_mode == "add" else 128) | (256 if res.dtype == torch.float32 else 0)
@@ -201,7 +205,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     rc = lib().ljs_gemm_bf16(ctypes.c_void_p(A.data_ptr() + a_off * eA), ctypes.c_void_p(B.data_ptr() + b_off * eA),
                              ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb,
                              ldc, sA, sB, sC, sBias, batch, int(a_kc), int(b_kc), int(out_f32), flags, alpha,
-                             splitk, tile, _p(psum), ctypes.byref(cnt), _p(res), res_ld, sR, _stream(C))
+                             splitk, tile, _p(psum), ctypes.byref(cnt), _p(res), res_ld, sR, _p(acopy), _stream(C))
     _ck(rc, "ljs_gemm_bf16")
     return cnt.value
 
@@ -260,6 +264,10 @@ def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f3
     if K % 64 == 0 and tiles128 >= 96 and (out_f32 or (N % 8 == 0 and ldc % 8 == 0)):
         if _TILE_2561 and a_kc and b_kc and not out_f32 and M >= 4096 and N * batch >= 1024 and N % 128 == 0:
             return 2561
+        if a_kc and b_kc and not out_f32 and tiles128 < 256 and splitk <= 1:
+            # under one round of 128x128 blocks (the 2048-token QKV projection: 192 tiles): the
+            # 8-wave, 3-stage tile (qkv3 10.3 -> 9.5 us; scripts/gemm_small.py)
+            return 12883
         return 1282
     if K % 64 == 0 and a_kc and b_kc and (out_f32 or (N % 8 == 0 and ldc % 8 == 0)):
         # few 128x128 tiles (the 2048-token reference shape): the 64x64 LDS-DMA tile, 4 stages

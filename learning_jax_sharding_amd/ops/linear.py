@@ -140,9 +140,15 @@ class _Linear(torch.autograd.Function):
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
         M = x2.shape[0]
-        xb = _bf16(x2 if x2.is_contiguous() else x2.contiguous())
         nw = len(ws)
         N = ws[0].shape[1]
+        # f32 activations (the reference's f32 input under a bf16 Dense): the GEMM rounds them as
+        # it reads them and writes the bf16 copy the backward needs -- no separate cast pass
+        cast_on_load = (_CAST_ON_LOAD and x2.is_cuda and x2.dtype == torch.float32 and x2.is_contiguous()
+                        and res is None and b is None and not relu and K % 64 == 0 and N % 8 == 0
+                        and out_dtype == torch.bfloat16 and x2.data_ptr() % 16 == 0
+                        and M * nw * N >= (1 << 20))
+        xb = None if cast_on_load else _bf16(x2 if x2.is_contiguous() else x2.contiguous())
         if nw == 1:
             wt = shadow.get(ws[0], "T")
             sB = 0
@@ -169,8 +175,15 @@ class _Linear(torch.autograd.Function):
             r_ld = r2.stride(0)
             if nw != 1 or od != torch.bfloat16 or N % 8:
                 r2 = None
-        cnt = hip.gemm(xb, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=sB, sC=N,
-                       bias=bias, sBias=0, relu=relu, psum=partials, res=r2, res_ld=r_ld)
+        if cast_on_load and partials is None:
+            xb = torch.empty((M, K), dtype=torch.bfloat16, device=x.device)
+            cnt = hip.gemm(x2, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=sB, sC=N,
+                           acopy=xb)
+        else:
+            if cast_on_load:  # (a fused output sum wanted: the cast pass, then the plain GEMM)
+                xb = _bf16(x2)
+            cnt = hip.gemm(xb, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=sB, sC=N,
+                           bias=bias, sBias=0, relu=relu, psum=partials, res=r2, res_ld=r_ld)
         ys = [out[:, i * N:(i + 1) * N].view(tuple(lead) + (N,)) for i in range(nw)]
         if res is not None and r2 is None:
             ys = [ys[0] + res.to(ys[0].dtype)]
@@ -430,6 +443,13 @@ class _FFBlock(torch.autograd.Function):
         _ff_bwd_order(run_dx, run_wo, run_wi)
         return out.get("dx"), out.get("wi"), out.get("wo"), None
 
+
+# f32 activations rounded inside the consuming GEMM (opt-in, LJS_CAST_ON_LOAD=1): measured slower
+# than the separate cast pass + bf16 GEMM at both bench shapes (QKV at 16384 tokens: cast + 2561
+# tile 52.7 us vs 59.6 us for the f32-A kernel alone, 75.6 with the bf16 copy the backward needs;
+# at 2048 tokens 19.4 vs 18.5 us; scripts/col_one.py) -- the f32 A image doubles the operand bytes
+# and LDS reads of the K-loop, which costs more than the cast pass it saves
+_CAST_ON_LOAD = os.environ.get("LJS_CAST_ON_LOAD", "0") == "1"
 
 # order of the FF block's backward GEMMs after dA (dX, dW_out, dW_in): which operands are still
 # in the Infinity Cache when each runs.  dW_in right after dA (which it reads, 84 MB at the bench

@@ -46,15 +46,20 @@ def main():
     C1 = torch.empty(T, 1536, device=dev).bfloat16()
     C2 = torch.empty(T, 640, device=dev).bfloat16()
     C3 = torch.empty(T, 512, device=dev).bfloat16()
+    W3 = Wqkv.view(3, 512, 640)
     fw = {
         "qkv": (lambda t: hip.gemm(X, Wqkv, C1, T, 1536, 640, 640, 640, 1536, True, True, tile=t), 2 * T * 1536 * 640),
+        "qkv3": (lambda t: hip.gemm(X, W3, C1, T, 512, 640, 640, 640, 1536, True, True, batch=3, sB=512 * 640, sC=512,
+                                    tile=t), 2 * T * 1536 * 640),
         "out": (lambda t: hip.gemm(H, Wo_t, C2, T, 640, 512, 512, 512, 640, True, True, tile=t), 2 * T * 640 * 512),
         "dh": (lambda t: hip.gemm(dY, Wo, C3, T, 512, 640, 640, 640, 512, True, True, tile=t), 2 * T * 640 * 512),
     }
     for name, (mk, fl) in fw.items():
-        for t in (64, 128, 643, 644, 1282, 1284):
+        for t in (64, 128, 643, 644, 1282, 1284, 12883, 12884, 2561, 1602):
             us = graph_time(lambda: mk(t))
             print(f"{name} tile={t}: {us:.2f} us {fl / us / 1e6:.0f} TF", flush=True)
+    if os.environ.get("FWD_ONLY") == "1":
+        return
     # weight gradients: S K-chunks into f32 slabs (+ the combine), tile choices
     for name, A, B, K_, N_ in (("dwo", H, dY, 512, 640), ("dwqkv", X, dQKV, 640, 1536)):
         out = torch.empty(K_, N_, device=dev)

@@ -745,3 +745,35 @@ def test_fp8_gemm_transposed_copy_splitk_bcast_and_fp8_mask(hip):
     F.gemm_mx(qa, sa, qb, sb, T, N, K, m1, res=q, res_mode="mask")
     F.gemm_mx(qa, sa, qb, sb, T, N, K, m2, res=dq, res_mode="mask")
     assert torch.equal(m1, m2)
+
+
+@pytest.mark.parametrize("M,N,K,batch", [(2048, 512, 640, 3), (300, 136, 128, 1), (16384, 512, 640, 3)])
+def test_gemm_f32_a_cast_on_load(hip, M, N, K, batch):
+    """The f32-A LDS-DMA GEMM (activation cast fused into the fragment reads) == cast pass + bf16
+    GEMM bit for bit, and its bf16 copy of A == the cast pass's output."""
+    x = _rand(M, K, dtype=torch.float32, seed=90)
+    w = _rand(batch, N, K, seed=91)
+    ref_x = x.bfloat16()
+    ref = torch.empty(M, batch * N, dtype=torch.bfloat16, device=dev)
+    hip.gemm(ref_x, w, ref, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N)
+    out = torch.full((M, batch * N), float("nan"), dtype=torch.bfloat16, device=dev)
+    xb = torch.full((M, K), float("nan"), dtype=torch.bfloat16, device=dev)
+    hip.gemm(x, w, out, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N, acopy=xb)
+    assert torch.equal(out, ref)
+    assert torch.equal(xb, ref_x)
+
+
+def test_linear_f32_input_cast_on_load(hip, monkeypatch):
+    """hip.linear on an f32 activation: the cast-on-load GEMM path gives the same outputs and
+    weight gradients as the separate-cast path."""
+    from learning_jax_sharding_amd.ops import linear as L
+    x = _rand(4096, 640, dtype=torch.float32, seed=92)
+    ws = [(_rand(640, 512, dtype=torch.float32, seed=93 + i) * 0.05).requires_grad_() for i in range(3)]
+    res = {}
+    for flag in (False, True):
+        monkeypatch.setattr(L, "_CAST_ON_LOAD", flag)
+        ys = hip.linear(x, ws, None, torch.bfloat16, False, torch.bfloat16)
+        gs = torch.autograd.grad(ys, ws, [torch.ones_like(y) for y in ys])
+        res[flag] = [y.clone() for y in ys] + [g.clone() for g in gs]
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
