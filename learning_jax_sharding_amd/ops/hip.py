@@ -278,6 +278,9 @@ def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f3
 
 
 _DW_SLAB_MODE = os.environ.get("LJS_DW_SLAB_MODE", "1") == "1"  # A/B switch: 0 = power-of-two batched slabs
+# weight-grad tile at <= 4096 tokens: 12884 (8-wave 128x128, 4 stages, uneven slab splits) measured
+# 0.1033-0.1053 ms vs 0.1071-0.1076 for 644 (64x64, power-of-two batched slabs) at B=8
+_DW_SMALL_TILE = int(os.environ.get("LJS_DW_SMALL_TILE", "12884"))
 
 
 def slab_count(nkt: int, S: int) -> int:
@@ -300,9 +303,9 @@ def pick_dw_slabs(K: int, N: int, T: int):
     model -- rounds of resident blocks x K-tiles per split, plus the slab reduction's extra f32
     traffic -- instead of a power of two dividing the K-tiles: the FF weight gradients (100
     tiles) ran 400 items on 512 block slots (78 %), now 5 x 52 K-tiles = 500 items; dW_o (20
-    tiles) 16 x 16 -> 24 x 11.  At T <= 4096 the 64x64 tile with the largest power-of-two
-    batched split keeping <= 512 items and >= 512 tokens per chunk (dWo at 2048 tokens:
-    14.8 -> 11.5 us, dW[q|k|v] 25.6 -> 19.1 us; scripts/gemm_small.py)."""
+    tiles) 16 x 16 -> 24 x 11.  At T <= 4096 the 8-wave 128x128 tile (one block per CU) in slab
+    mode; ``LJS_DW_SMALL_TILE=644``: the 64x64 tile with the largest power-of-two batched split
+    keeping <= 512 items and >= 512 tokens per chunk (the round-2 default before)."""
     if K % 64 or N % 64 or T % 64:
         return 1282, pick_splitk_dma(K, N, T, 1), False
     if T > 4096 and not _DW_SLAB_MODE:
@@ -321,6 +324,17 @@ def pick_dw_slabs(K: int, N: int, T: int):
             if best_cost is None or cost < best_cost - 1e-9:
                 best, best_cost = S, cost
         return 1282, best, True
+    if _DW_SMALL_TILE == 12884:
+        # (A/B: 8-wave 128x128, 4 stages, one block per CU, uneven slab splits)
+        nkt, tiles = T // 64, -(-K // 128) * -(-N // 128)
+        best, best_cost = 1, None
+        for S in range(1, min(32, nkt) + 1):
+            if slab_count(nkt, S) != S:
+                continue
+            cost = -(-tiles * S // _cus()) * (-(-nkt // S) * 1.2 + 1.0) + S * K * N * 4 / 5e6
+            if best_cost is None or cost < best_cost - 1e-9:
+                best, best_cost = S, cost
+        return 12884, best, True
     tiles = (K // 64) * (N // 64)
     s = 1
     while tiles * s * 2 <= 512 and T % (64 * s * 2) == 0 and T // (s * 2) >= 512:
