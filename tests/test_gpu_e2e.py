@@ -107,6 +107,43 @@ def test_jit_graph_train_step_matches_eager(gpu_devices):
         np.testing.assert_allclose(np.asarray(b), np.asarray(a), rtol=1e-4, atol=1e-5)
 
 
+def test_jit_graph_multi_step_capture_matches_single_steps(gpu_devices):
+    """bench.py --graph-steps: G complete train steps captured into one hipGraph give the same
+    state as G replays of the one-step graph (same kernels, same order: bit-exact)."""
+    gpu_devices(1)
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd import optim
+    from learning_jax_sharding_amd.models import MultiHeadAttention
+    from learning_jax_sharding_amd.training import TrainState
+    model = MultiHeadAttention(640, heads=8, dim_head=64)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (4, 256, 640))
+
+    def make():
+        params = model.init(ljs.random.PRNGKey(1), x)["params"]
+        return TrainState.create(apply_fn=model.apply, params=params, tx=optim.adam(1e-3))
+
+    def step(state, x):
+        g = ljs.grad(lambda p: model.apply({"params": p}, x).sum())(state.params)
+        return state.apply_gradients(grads=g)
+
+    def steps3(state, x):
+        for _ in range(3):
+            state = step(state, x)
+        return state
+
+    one = ljs.jit(step, donate_argnums=0, capture=True)
+    three = ljs.jit(steps3, donate_argnums=0, capture=True)
+    s1, s3 = make(), make()
+    for _ in range(3):  # 9 steps each: the first calls capture, later ones replay
+        for _ in range(3):
+            s1 = one(s1, x)
+        s3 = three(s3, x)
+    torch.cuda.synchronize()
+    assert int(np.asarray(s1.step)) == 9 and int(np.asarray(s3.step)) == 9
+    for a, b in zip(ljs.tree_util.tree_leaves(s1), ljs.tree_util.tree_leaves(s3)):
+        np.testing.assert_array_equal(np.asarray(b), np.asarray(a))
+
+
 def _run_layer(mesh_shape, fp8, B=2, S=128, M=640, ff=2560):
     import learning_jax_sharding_amd as ljs
     import learning_jax_sharding_amd.numpy as jnp
