@@ -708,7 +708,7 @@ __device__ __forceinline__ float dot_bf16x8(const u32x4& x, const u32x4& y) {
 template <bool MASK>
 __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, const bf16_t* Ot,
                                            const float* lse_s, const float* dl_s, bf16_t* dSt,
-                                           const bf16_t* Ks, const bf16_t* Vs, f32x4 (&dk)[2][4],
+                                           const bf16x8 (&kr)[2][2], const bf16x8 (&vr)[2][2], f32x4 (&dk)[2][4],
                                            f32x4 (&dv)[2][4], int q0, int key0, int lane) {
   const int g = lane >> 4;
   // two 32-query halves: P / dS of a half feed the dK/dV MFMAs right away (register pressure)
@@ -727,10 +727,10 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-        s = mfma16x16x32(q0f, frag_rows(Ks, key0 + 16 * j, 0, lane), s);
-        s = mfma16x16x32(q1f, frag_rows(Ks, key0 + 16 * j, 1, lane), s);
-        dp = mfma16x16x32(o0f, frag_rows(Vs, key0 + 16 * j, 0, lane), dp);
-        dp = mfma16x16x32(o1f, frag_rows(Vs, key0 + 16 * j, 1, lane), dp);
+        s = mfma16x16x32(q0f, kr[j][0], s);
+        s = mfma16x16x32(q1f, kr[j][1], s);
+        dp = mfma16x16x32(o0f, vr[j][0], dp);
+        dp = mfma16x16x32(o1f, vr[j][1], dp);
         float pv[4], dsv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -848,6 +848,16 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       dk[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
       dv[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  // this wave's 32 keys as MFMA B operands stay in registers for the whole query sweep (they
+  // were re-read from LDS per 16-query tile: a third of the kernel's LDS traffic)
+  bf16x8 kr[2][2], vr[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kr[j][ks] = frag_rows(Ks, key0 + 16 * j, ks, lane);
+      vr[j][ks] = frag_rows(Vs, key0 + 16 * j, ks, lane);
+    }
   const int qt = wave & 3, dt0 = 2 * (wave >> 2);
   // static priority for the second-dispatched half (MI355X_MICROARCH "Two waves per SIMD" item
   // 4): waves 4-7 lose VALU arbitration to their SIMD partners on every segment otherwise
@@ -861,8 +871,8 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
     const bf16_t* Ot = QO + (2 + cur) * BLK * D;
     if (active) {
       const bool need_mask = q0 + BLK > a.Sq || key0 + 32 > a.Sk || (a.causal && key0 + 31 > q0 + a.q_offset);
-      if (need_mask) fused_tile<true>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, Ks, Vs, dk, dv, q0, key0, lane);
-      else fused_tile<false>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, Ks, Vs, dk, dv, q0, key0, lane);
+      if (need_mask) fused_tile<true>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, kr, vr, dk, dv, q0, key0, lane);
+      else fused_tile<false>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, kr, vr, dk, dv, q0, key0, lane);
     }
     // this wave's DMA pieces of the next block landed; after the barrier everyone's have, so the
     // next block's delta is formed inside the dQ phase (two barriers per query block, not three)

@@ -318,7 +318,17 @@ __global__ void colsum_bcast_kernel(const void* __restrict__ in, int is_bf16, in
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slabs, int S, long slab_stride,
                                                           int R, int C, float* __restrict__ out, int cb,
                                                           long out_bs, int accumulate,
-                                                          bf16_t* __restrict__ out_bf16) {
+                                                          bf16_t* __restrict__ out_bf16, float* __restrict__ tail,
+                                                          bf16_t* __restrict__ tail_bf16, int tail_n,
+                                                          float tail_val) {
+  // constant tail (the bias gradient R * bf16(g) of a loss-sum cotangent, stored right after
+  // dW in the joint gradient buffer): written here instead of by a launch of its own
+  if (blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < tail_n; i += blockDim.x) {
+      tail[i] = tail_val;
+      if (tail_bf16) tail_bf16[i] = f2bf(tail_val);
+    }
+  }
   const long n4 = (long)R * C / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const long e = 4 * i;
@@ -819,7 +829,9 @@ LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void*
 // out (column blocks of width cb, out_bs floats apart) = sum of S f32 [R][C] slabs (slab_stride
 // floats apart).  Requires C % 4 == 0, cb % 4 == 0, C % cb == 0 and 16-byte aligned buffers.
 LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, int C, void* out, int cb, long out_bs,
-                            int accumulate, void* out_bf16, hipStream_t s) {
+                            int accumulate, void* out_bf16, void* tail, void* tail_bf16, int tail_n, float tail_val,
+                            hipStream_t s) {
+  if (tail_n < 0 || (tail_n > 0 && !tail)) return (int)hipErrorInvalidValue;
   if (C % 4 || cb % 4 || C % cb || slab_stride % 4 || out_bs % 4 || S < 1 || (((uintptr_t)slabs) & 15) ||
       (((uintptr_t)out) & 15))
     return (int)hipErrorInvalidValue;
@@ -829,7 +841,8 @@ LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, i
   if (grid < 1) grid = 1;
   if (out_bf16 && (((uintptr_t)out_bf16) & 7)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, s, (const float*)slabs, S, slab_stride, R, C,
-                     (float*)out, cb, out_bs, accumulate, (bf16_t*)out_bf16);
+                     (float*)out, cb, out_bs, accumulate, (bf16_t*)out_bf16, (float*)tail, (bf16_t*)tail_bf16,
+                     tail_n, tail_val);
   return (int)hipGetLastError();
 }
 

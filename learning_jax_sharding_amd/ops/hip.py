@@ -50,7 +50,8 @@ _SIGS = {
     "ljs_relu_bwd_colsum": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_relu_bwd": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p, c_void_p],
     "ljs_bcast_scalar": [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
-    "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p],
+    "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p,
+                        c_void_p, c_int, c_float, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ljs_adam_f32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
@@ -552,8 +553,46 @@ def _sum_all_raw(t: torch.Tensor, out_dtype: torch.dtype = torch.float32) -> tor
 _SEEDS_BF16 = {}
 
 
-def register_seed_bf16(seed: torch.Tensor, seed_bf16: torch.Tensor) -> None:
+def register_seed_bf16(seed: torch.Tensor, seed_bf16: torch.Tensor, value: Optional[float] = None) -> None:
     _SEEDS_BF16[seed.data_ptr()] = (seed, seed_bf16)
+    if value is not None:
+        bv = float(torch.tensor(value, dtype=torch.float32).to(torch.bfloat16).float())
+        _SEED_CONST[seed.data_ptr()] = (seed, bv)
+        _SEED_CONST[seed_bf16.data_ptr()] = (seed_bf16, bv)
+
+
+def register_seed_const(seed: torch.Tensor, value: float) -> None:
+    """A cached 1-element bf16 seed holding bf16(value) (spmd.api._seed)."""
+    assert seed.dtype == torch.bfloat16 and seed.numel() == 1
+    _SEED_CONST[seed.data_ptr()] = (seed, float(torch.tensor(value, dtype=torch.float32).to(torch.bfloat16).float()))
+
+
+# constant seeds -> bf16(value) known on the host: a dense layer fed by one (the cotangent of a
+# loss sum) takes its broadcast dY row from a cached constant and writes its bias gradient
+# R * bf16(g) inside the weight-gradient combine -- no launch of its own (bcast_scalar)
+_SEED_CONST = {}
+_CONST_ROWS = {}
+
+
+def seed_constant(g: torch.Tensor) -> Optional[float]:
+    """bf16(value) of ``g`` when it is (a 1-element view of) a registered constant seed."""
+    ent = _SEED_CONST.get(g.data_ptr())
+    if ent is not None and ent[0].data_ptr() == g.data_ptr() and ent[0].dtype == g.dtype and ent[0].numel() == 1:
+        return ent[1]
+    return None
+
+
+def const_row_bf16(value: float, n: int, device) -> Optional[torch.Tensor]:
+    """A cached bf16 [n] row filled with ``value`` (None while a graph capture is running and
+    the row does not exist yet: it is never allocated from a capture's private pool)."""
+    key = (value, n, str(device))
+    row = _CONST_ROWS.get(key)
+    if row is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        row = torch.full((n,), value, dtype=torch.bfloat16, device=device)
+        _CONST_ROWS[key] = row
+    return row
 
 
 def _seed_bf16(g: torch.Tensor) -> torch.Tensor:
@@ -726,15 +765,23 @@ class _MatmulF32(torch.autograd.Function):
 
 
 def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, accumulate: bool = False,
-                out_bf16: Optional[torch.Tensor] = None) -> None:
+                out_bf16: Optional[torch.Tensor] = None, tail: Optional[torch.Tensor] = None,
+                tail_bf16: Optional[torch.Tensor] = None, tail_val: float = 0.0) -> None:
     """out = sum over the leading dim of f32 ``slabs`` [S][R][C], written as C/cb column blocks of
     width ``cb`` stored ``out_bs`` floats apart (the split-K combine of the weight-grad GEMMs).
-    ``out_bf16`` (same layout as ``out``) also receives the sums rounded to bf16."""
+    ``out_bf16`` (same layout as ``out``) also receives the sums rounded to bf16.  ``tail`` (f32,
+    and ``tail_bf16``) is filled with the constant ``tail_val`` by the same launch."""
     S, R, C = slabs.shape
     assert slabs.dtype == torch.float32 and out.dtype == torch.float32 and slabs.is_contiguous()
     assert out_bf16 is None or (out_bf16.dtype == torch.bfloat16 and out_bf16.numel() == out.numel())
+    tn = 0
+    if tail is not None:
+        assert tail.dtype == torch.float32 and tail.is_contiguous() and tail.device == out.device
+        assert tail_bf16 is None or (tail_bf16.dtype == torch.bfloat16 and tail_bf16.numel() == tail.numel()
+                                     and tail_bf16.is_contiguous())
+        tn = tail.numel()
     rc = lib().ljs_slab_reduce(_p(slabs), S, R * C, R, C, _p(out), cb, out_bs, int(accumulate), _p(out_bf16),
-                               _stream(out))
+                               _p(tail), _p(tail_bf16 if tn else None), tn, float(tail_val), _stream(out))
     _ck(rc, "slab_reduce")
 
 

@@ -29,6 +29,7 @@ from __future__ import annotations
 import os
 from typing import List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from . import hip
@@ -84,10 +85,11 @@ _FUSED_SUM = os.environ.get("LJS_FUSED_SUM", "1") == "1"  # tuning override of t
 
 
 def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: int, out: torch.Tensor, cb: int,
-              out_bs: int, twin: Optional[torch.Tensor] = None) -> None:
+              out_bs: int, twin: Optional[torch.Tensor] = None, tail=None) -> None:
     """out (column blocks of width cb, out_bs apart) = xb^T @ dy for xb [T][K], dy [T][Nt] (row
     stride ld, 0 = broadcast row): S K-chunks of the token dim run as one batched LDS-DMA GEMM
-    into f32 slabs [S][K][Nt], combined by one streaming reduction."""
+    into f32 slabs [S][K][Nt], combined by one streaming reduction (which also fills ``tail`` =
+    (f32 tensor, bf16 twin or None, constant))."""
     tile, S, slab_mode = hip.pick_dw_slabs(K, Nt, T)
     if _DW_SPLIT and T % (64 * _DW_SPLIT) == 0:
         S, slab_mode = _DW_SPLIT, False
@@ -98,7 +100,10 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
         kc = T // S
         hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
                  tile=tile)
-    hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
+    if tail is not None:
+        hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin, tail=tail[0], tail_bf16=tail[1], tail_val=tail[2])
+    else:
+        hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
 
 
 def _row_view(dy: torch.Tensor, M: int, N: int) -> Tuple[torch.Tensor, int]:
@@ -110,9 +115,14 @@ def _row_view(dy: torch.Tensor, M: int, N: int) -> Tuple[torch.Tensor, int]:
     """
     d2 = dy.reshape(M, N)
     if d2.is_cuda and d2.numel() > 0 and d2.stride(0) == 0 and d2.stride(1) == 0:
-        # one broadcast scalar (the cotangent of y.sum()): its bf16 row in one HIP launch (a
-        # torch .contiguous() of the stride-0 row ran as a 1-workgroup copy kernel, ~4.7 us)
-        row, _ = hip.bcast_scalar(d2.as_strided((1,), (1,)), N, M, False)
+        # one broadcast scalar (the cotangent of y.sum()): a cached constant row when it is a
+        # constant seed, else its bf16 row in one HIP launch (a torch .contiguous() of the
+        # stride-0 row ran as a 1-workgroup copy kernel, ~4.7 us)
+        g1 = d2.as_strided((1,), (1,))
+        cval = hip.seed_constant(g1)
+        row = hip.const_row_bf16(cval, N, d2.device) if cval is not None else None
+        if row is None:
+            row, _ = hip.bcast_scalar(g1, N, M, False)
         return row.unsqueeze(0).expand(M, N), 0
     if d2.stride(0) == 0:
         row = d2[0].contiguous()
@@ -221,7 +231,7 @@ class _Linear(torch.autograd.Function):
         # them as one producer group -- no concatenation, no cast kernel (parallel/data.py)
         from ..parallel import data as _dp
         wire = _dp.active_wire_dtype() == torch.bfloat16
-        joint = joint_bf16 = None
+        joint = joint_bf16 = tail = None
         if (nw == 1 and want_db and ctx.needs_input_grad[5] and dys[0] is not None and M % 64 == 0 and not relu
                 and b.dtype == torch.float32 and ws[0].dtype == torch.float32 and dys[0].is_cuda
                 and dys[0].numel() > 0 and all(st == 0 for st in dys[0].stride())):
@@ -251,7 +261,18 @@ class _Linear(torch.autograd.Function):
                 dy = (dy * (ys[i] > 0)).reshape(M, N)
             elif dy.is_cuda and dy.numel() > 0 and all(st == 0 for st in dy.stride()):
                 # one scalar broadcast (the cotangent of y.sum()): its bf16 row and the bias
-                # gradient come out of one kernel; the GEMMs read the row with ld = 0
+                # gradient come out of one kernel; the GEMMs read the row with ld = 0.  A constant
+                # seed's row is a cached constant and its bias gradient M * bf16(g) is written by
+                # the weight-gradient combine into the joint buffer: no launch at all
+                g1 = dy.as_strided((1,), (1,))
+                cval = hip.seed_constant(g1) if joint is not None else None
+                row = hip.const_row_bf16(cval, N, dev) if cval is not None else None
+                if row is not None:
+                    db_bcast[i] = joint[K * N:]
+                    tail = (joint[K * N:], joint_bf16[K * N:] if joint_bf16 is not None else None,
+                            float(np.float32(cval) * np.float32(M)))
+                    mats.append((row.unsqueeze(0).expand(M, N), 0))
+                    continue
                 row, db_bcast[i] = hip.bcast_scalar(
                     dy.as_strided((1,), (1,)), N, M, want_db,
                     db_out=joint[K * N:] if joint is not None else None,
@@ -279,7 +300,7 @@ class _Linear(torch.autograd.Function):
         # value_and_grad (ops/streams.py): it overlaps the layers' input-gradient chain
         want = [i for i in live if ctx.needs_input_grad[5 + i]]
         with _streams.side(dev, [xb, joint, joint_bf16] + [mats[i][0] for i in want]) as produced:
-            _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, dev)
+            _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, dev, tail)
             produced.extend(d for d in dws if d is not None)
             if joint is not None:
                 produced.append(joint)
@@ -301,7 +322,7 @@ class _Linear(torch.autograd.Function):
         return (dx, db, dres, None, None, *dws)
 
 
-def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, dev):
+def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, dev, tail=None):
     """The weight gradients of :class:`_Linear` (``dws[i]`` for ``i`` in ``want``)."""
     from ..parallel import data as _dp
     if not want:
@@ -320,7 +341,7 @@ def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, 
             t, ld = mats[0]
             dW = joint[:K * N].view(K, N)
             _dw_slabs(xb, t, ld, M, K, N, dW, N, 0,
-                      joint_bf16[:K * N].view(K, N) if joint_bf16 is not None else None)
+                      joint_bf16[:K * N].view(K, N) if joint_bf16 is not None else None, tail)
             dws[0] = dW
         elif batched:
             dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)

@@ -350,7 +350,10 @@ def _seed(t: torch.Tensor, value: float) -> torch.Tensor:
         if t.is_cuda and t.dtype == torch.float32 and s.numel() == 1:
             # its bf16 rounding, for a bf16 sum's backward fed by this f32 seed (no cast kernel)
             from ..ops import hip as _hip
-            _hip.register_seed_bf16(s, s.to(torch.bfloat16))
+            _hip.register_seed_bf16(s, s.to(torch.bfloat16), value)
+        elif t.is_cuda and t.dtype == torch.bfloat16 and s.numel() == 1:
+            from ..ops import hip as _hip
+            _hip.register_seed_const(s, value)
     return s
 
 
