@@ -503,7 +503,34 @@ struct AdamTensor {
   // qn[R][C] + sn8[R][C/32] (blocks along rows, quant_mx_rows' layout: a dX GEMM's B operand)
   // and qt[C][R] + st8[C][R/32] (blocks along columns, transposed: a forward GEMM's B operand)
   long qn, sn8, qt, st8;
+  // gradient source: gS = 0 a plain [R][C] tensor (row stride g_ld = C); gS > 0 the gS f32
+  // split-K slabs of a weight-gradient GEMM, g_ss floats apart, row stride g_ld (the gradient is
+  // their sum, added in slab_reduce's order: bit-identical, and no combine launch); gS = -1 a
+  // constant gradient whose f32 bits are g_ld (the bias gradient of a loss-sum cotangent)
+  long gS, g_ld, g_ss;
 };
+
+// the slab sum of slab_reduce_kernel, in its order (bit-identical results)
+__device__ __forceinline__ f32x4 slab_sum4(const float* __restrict__ g, long gS, long ss, long i) {
+  f32x4 acc = *reinterpret_cast<const f32x4*>(g + i);
+  long s = 1;
+  for (; s + 3 < gS; s += 4) {
+    f32x4 v0 = *reinterpret_cast<const f32x4*>(g + s * ss + i);
+    f32x4 v1 = *reinterpret_cast<const f32x4*>(g + (s + 1) * ss + i);
+    f32x4 v2 = *reinterpret_cast<const f32x4*>(g + (s + 2) * ss + i);
+    f32x4 v3 = *reinterpret_cast<const f32x4*>(g + (s + 3) * ss + i);
+    acc += (v0 + v1) + (v2 + v3);
+  }
+  for (; s < gS; ++s) acc += *reinterpret_cast<const f32x4*>(g + s * ss + i);
+  return acc;
+}
+__device__ __forceinline__ float slab_sum1(const float* __restrict__ g, long gS, long ss, long i) {
+  float acc = g[i];
+  long s = 1;
+  for (; s + 3 < gS; s += 4) acc += (g[s * ss + i] + g[(s + 1) * ss + i]) + (g[(s + 2) * ss + i] + g[(s + 3) * ss + i]);
+  for (; s < gS; ++s) acc += g[s * ss + i];
+  return acc;
+}
 constexpr int kAdamMax = 32;
 // rows per Adam tile (x 64 columns): a template parameter (LJS_ADAM_ROWS = 16 / 32 / 64); smaller
 // tiles give more, shorter workgroups (a ragged last round of 64-row tiles idles most CUs)
@@ -548,12 +575,18 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
       const int row = tr_i * kAdamRows + r0 + 16 * q;
       ok[q] = row < T.R;
       const long i = ok[q] ? (long)row * T.C + cbase : cbase;
-      if (T.g_bf16) {
-        const u32x2 raw = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(T.g) + i);
+      const long gi = ok[q] ? (long)row * T.g_ld + cbase : cbase;
+      if (T.gS > 0) {
+        gv[q] = slab_sum4(reinterpret_cast<const float*>(T.g), T.gS, T.g_ss, gi);
+      } else if (T.gS < 0) {
+        const float c = __int_as_float((int)T.g_ld);
+        gv[q] = f32x4{c, c, c, c};
+      } else if (T.g_bf16) {
+        const u32x2 raw = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(T.g) + gi);
         gv[q] = f32x4{__uint_as_float(raw[0] << 16), __uint_as_float(raw[0] & 0xffff0000u),
                       __uint_as_float(raw[1] << 16), __uint_as_float(raw[1] & 0xffff0000u)};
       } else {
-        gv[q] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(T.g) + i);
+        gv[q] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(T.g) + gi);
       }
       mv[q] = *reinterpret_cast<const f32x4*>(Mm + i);
       vv[q] = *reinterpret_cast<const f32x4*>(Vv + i);
@@ -647,7 +680,11 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
     float newp = 0.f;
     if (row < T.R && col < T.C) {
       const long i = (long)row * T.C + col;
-      float g = T.g_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(T.g)[i]) : reinterpret_cast<const float*>(T.g)[i];
+      const long gi = (long)row * T.g_ld + col;
+      float g = T.gS > 0   ? slab_sum1(reinterpret_cast<const float*>(T.g), T.gS, T.g_ss, gi)
+                : T.gS < 0 ? __int_as_float((int)T.g_ld)
+                : T.g_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(T.g)[gi])
+                           : reinterpret_cast<const float*>(T.g)[gi];
       float m = b1 * Mm[i] + (1.f - b1) * g;
       float v = b2 * Vv[i] + (1.f - b2) * g * g;
       float p = P[i];
@@ -960,7 +997,8 @@ LJS_API int ljs_rng_fill(void* out, int is_bf16, int ndim, const long* start, co
   return (int)hipGetLastError();
 }
 
-// table: n x 10 int64 {p, g, m, v, shadow_t, shadow_n, R, C, g_bf16, unused}; up to 32 per call
+// table: n x 16 int64 {p, g, m, v, shadow_t, shadow_n, R, C, g_bf16, gS, qn, sn8, qt, st8, g_ld, g_ss}
+// (see AdamTensor); up to 32 per call
 LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset, void* ticket, float lr, float b1,
                            float b2, float eps, float wd, hipStream_t s) {
   if (n < 1 || n > kAdamMax) return (int)hipErrorInvalidValue;
@@ -969,15 +1007,18 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   const int kAdamRows = rows == 16 || rows == 32 ? rows : 64;
   int tiles = 0;
   for (int i = 0; i < n; ++i) {
-    const long* r = table + 14 * i;
+    const long* r = table + 16 * i;
     AdamTensor& t = b.t[i];
     t.p = r[0]; t.g = r[1]; t.m = r[2]; t.v = r[3]; t.st = r[4]; t.sn = r[5]; t.R = r[6]; t.C = r[7];
     t.g_bf16 = r[8];
     t.qn = r[10]; t.sn8 = r[11]; t.qt = r[12]; t.st8 = r[13];
+    t.gS = r[9]; t.g_ld = r[14]; t.g_ss = r[15];
+    if (t.gS == 0) t.g_ld = t.C;
+    if (t.gS > 0 && (t.g_bf16 || t.g_ld < t.C || t.g_ss < 1)) return (int)hipErrorInvalidValue;
     t.tiles_c = (t.C + 63) / 64;
     auto al = [](long ptr, long a) { return ptr % a == 0; };
-    t.vec = t.C % 4 == 0 && al(t.p, 16) && al(t.m, 16) && al(t.v, 16) && al(t.g, t.g_bf16 ? 8 : 16) &&
-            al(t.sn, 8) && al(t.st, 8);
+    t.vec = t.C % 4 == 0 && al(t.p, 16) && al(t.m, 16) && al(t.v, 16) && al(t.sn, 8) && al(t.st, 8) &&
+            (t.gS < 0 || (al(t.g, t.g_bf16 ? 8 : 16) && t.g_ld % 4 == 0 && (t.gS == 0 || t.g_ss % 4 == 0)));
     // MX shadows are written by the 4-wide path of full 64 x 64 tiles only: refuse anything else
     // (a shadow left stale would silently feed old weights to the fp8 GEMMs)
     if ((t.qn || t.qt) && (!t.vec || kAdamRows != 64 || t.R % 64 || t.C % 64 || !al(t.qn, 4) || !al(t.qt, 4) ||

@@ -1010,6 +1010,24 @@ def adam(p, g, m, v, step, lr, b1, b2, eps, wd, inplace):
     return po.view(p.shape), mo.view(m.shape), vo.view(v.shape)
 
 
+class SlabGrad:
+    """A weight gradient not yet combined: element (r, c) is the sum over s < S of
+    ``slabs.view(-1)[offset + s * slab_stride + r * ld + c]`` (the split-K slabs of its GEMM)."""
+    __slots__ = ("slabs", "S", "offset", "ld", "slab_stride", "shape")
+
+    def __init__(self, slabs, S, offset, ld, slab_stride, shape):
+        self.slabs, self.S, self.offset, self.ld, self.slab_stride = slabs, S, offset, ld, slab_stride
+        self.shape = tuple(shape)
+
+
+class ConstGrad:
+    """A gradient whose every element is ``value`` (f32)."""
+    __slots__ = ("value", "shape")
+
+    def __init__(self, value, shape):
+        self.value, self.shape = float(value), tuple(shape)
+
+
 def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step: bool = False) -> None:
     """In-place fused Adam over many params (one launch per 32): entries = [(p, g, m, v)].
 
@@ -1021,16 +1039,26 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
     rows = []
     for p, g, m, v in entries:
         assert p.is_contiguous() and m.is_contiguous() and v.is_contiguous() and p.dtype == torch.float32
-        if g.dtype not in (torch.float32, torch.bfloat16) or not g.is_contiguous():
-            g = g.float().contiguous() if g.dtype not in (torch.float32, torch.bfloat16) else g.contiguous()
+        R, C = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
+        if isinstance(g, SlabGrad):
+            # the weight gradient is still its split-K slabs: the kernel sums them (no combine)
+            assert g.shape == tuple(p.shape) and g.slabs.dtype == torch.float32 and g.slabs.is_contiguous()
+            gsrc = (g.slabs.data_ptr() + 4 * g.offset, 0, g.S, g.ld, g.slab_stride)
+        elif isinstance(g, ConstGrad):
+            assert g.shape == tuple(p.shape)
+            bits = int(np.asarray(g.value, dtype=np.float32).view(np.int32))
+            gsrc = (0, 0, -1, bits, 0)
+        else:
+            if g.dtype not in (torch.float32, torch.bfloat16) or not g.is_contiguous():
+                g = g.float().contiguous() if g.dtype not in (torch.float32, torch.bfloat16) else g.contiguous()
+            gsrc = (g.data_ptr(), int(g.dtype == torch.bfloat16), 0, C, 0)
         bufs = shadow.kinds_of(p) if p.dim() == 2 else {}
         st, sn = bufs.get("T"), bufs.get("N")
-        R, C = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
         ptr = lambda k: bufs[k].data_ptr() if k in bufs else 0  # noqa: E731
-        rows.append(([p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
+        rows.append(([p.data_ptr(), gsrc[0], m.data_ptr(), v.data_ptr(),
                       st.data_ptr() if st is not None else 0, sn.data_ptr() if sn is not None else 0,
-                      R, C, int(g.dtype == torch.bfloat16), 0,
-                      ptr("QN"), ptr("QNs"), ptr("QT"), ptr("QTs")], g))
+                      R, C, gsrc[1], gsrc[2],
+                      ptr("QN"), ptr("QNs"), ptr("QT"), ptr("QTs"), gsrc[3], gsrc[4]], g))
     if increment_step:
         assert step.dtype == torch.int32 and step.is_contiguous()
     step_i = step if step.dtype == torch.int32 else step.to(torch.int32)

@@ -84,12 +84,93 @@ _DW_SPLIT = int(os.environ.get("LJS_DW_SPLIT", "0"))
 _FUSED_SUM = os.environ.get("LJS_FUSED_SUM", "1") == "1"  # tuning override of the K-chunk count
 
 
+# Deferred weight-gradient combines.  Inside value_and_grad on one device (no gradient
+# all-reduce), a weight whose ONLY consumer is one _Linear (its AccumulateGrad node has a single
+# incoming edge, from that _Linear's backward) gets its dW returned uncombined: the tensor autograd
+# hands back is registered here with its split-K slabs, and value_and_grad wraps it in a LazyLocal
+# whose ``slabs`` the fused Adam sums as it reads them (hip.SlabGrad) -- no slab_reduce launch.
+# Anything else that reads the gradient forces the combine first.  Key: (data_ptr, shape).
+_DEFER = None     # None, or {"safe": set of keys, "pending": {data_ptr: (descriptor, materialize)}}
+_DEFER_ON = os.environ.get("LJS_DEFER_WGRAD", "1") == "1"
+
+
+def _key(t: torch.Tensor):
+    return (t.data_ptr(), tuple(t.shape))
+
+
+def defer_safe_leaves(outs) -> set:
+    """Keys of leaf tensors reached from ``outs`` by exactly one autograd edge, and that edge from
+    a _Linear backward (so autograd passes that Function's gradient through untouched)."""
+    counts, prod, seen = {}, {}, set()
+    stack = [t.grad_fn for t in outs if t.grad_fn is not None]
+    while stack:
+        fn = stack.pop()
+        if id(fn) in seen:
+            continue
+        seen.add(id(fn))
+        for nxt, _ in fn.next_functions:
+            if nxt is None:
+                continue
+            var = getattr(nxt, "variable", None)
+            if var is not None:
+                k = _key(var)
+                counts[k] = counts.get(k, 0) + 1
+                prod[k] = fn
+            elif id(nxt) not in seen:
+                stack.append(nxt)
+    return {k for k, c in counts.items() if c == 1 and type(prod[k]).__name__ == "_LinearBackward"}
+
+
+class defer_wgrads:
+    """Context manager around one autograd.grad call (spmd.api.value_and_grad)."""
+
+    def __init__(self, outs, enabled: bool):
+        self.state = None
+        if enabled and _DEFER_ON and not _streams.enabled():
+            self.state = {"safe": defer_safe_leaves(outs), "pending": {}}
+
+    def __enter__(self):
+        global _DEFER
+        self.prev, _DEFER = _DEFER, self.state
+        return self
+
+    def __exit__(self, *exc):
+        global _DEFER
+        _DEFER = self.prev
+        return False
+
+    def take(self, g: torch.Tensor):
+        """(descriptor, materialize) if ``g`` is a returned gradient still uncombined, else None."""
+        if self.state is None or g is None:
+            return None
+        ent = self.state["pending"].pop(g.data_ptr(), None)
+        if ent is None:
+            return None
+        if tuple(ent[0].shape) != tuple(g.shape) or g.dtype != torch.float32 or not g.is_contiguous():
+            ent[1]()
+            return None
+        return ent
+
+    def flush(self):
+        """Combine whatever was deferred but not handed back (nothing, when the safety walk holds)."""
+        if self.state is not None:
+            for _, mat in list(self.state["pending"].values()):
+                mat()
+            self.state["pending"].clear()
+
+
+def _defer_ok(*ts) -> bool:
+    d = _DEFER
+    return d is not None and all(t is not None and t.dtype == torch.float32 and _key(t) in d["safe"] for t in ts)
+
+
 def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: int, out: torch.Tensor, cb: int,
-              out_bs: int, twin: Optional[torch.Tensor] = None, tail=None) -> None:
+              out_bs: int, twin: Optional[torch.Tensor] = None, tail=None, defer=None) -> None:
     """out (column blocks of width cb, out_bs apart) = xb^T @ dy for xb [T][K], dy [T][Nt] (row
     stride ld, 0 = broadcast row): S K-chunks of the token dim run as one batched LDS-DMA GEMM
     into f32 slabs [S][K][Nt], combined by one streaming reduction (which also fills ``tail`` =
-    (f32 tensor, bf16 twin or None, constant))."""
+    (f32 tensor, bf16 twin or None, constant)).  ``defer(slabs, S, materialize)``: the
+    reduction is not launched; ``materialize()`` runs it (once) if the sums are ever read."""
     tile, S, slab_mode = hip.pick_dw_slabs(K, Nt, T)
     if _DW_SPLIT and T % (64 * _DW_SPLIT) == 0:
         S, slab_mode = _DW_SPLIT, False
@@ -100,10 +181,21 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
         kc = T // S
         hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
                  tile=tile)
-    if tail is not None:
-        hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin, tail=tail[0], tail_bf16=tail[1], tail_val=tail[2])
+    done = []
+
+    def materialize():
+        if done:
+            return
+        done.append(True)
+        if tail is not None:
+            hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin, tail=tail[0], tail_bf16=tail[1],
+                            tail_val=tail[2])
+        else:
+            hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
+    if defer is not None:
+        defer(slabs, S, materialize)
     else:
-        hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
+        materialize()
 
 
 def _row_view(dy: torch.Tensor, M: int, N: int) -> Tuple[torch.Tensor, int]:
@@ -219,6 +311,7 @@ class _Linear(torch.autograd.Function):
         dres = dys[0] if (ctx.has_res and ctx.needs_input_grad[2]) else None
         saved = ctx.saved_tensors
         xb, b = saved[0], saved[1]
+        ctx.bias_leaf = b
         ws = saved[2:2 + nw]
         ys = saved[2 + nw:] if relu else None
         dev = xb.device
@@ -322,6 +415,10 @@ class _Linear(torch.autograd.Function):
         return (dx, db, dres, None, None, *dws)
 
 
+def twin_free(joint_bf16, wire) -> bool:
+    return joint_bf16 is None and not wire
+
+
 def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, dev, tail=None):
     """The weight gradients of :class:`_Linear` (``dws[i]`` for ``i`` in ``want``)."""
     from ..parallel import data as _dp
@@ -337,16 +434,28 @@ def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, 
         # the nw weight gradients
         # under a data-parallel backward with a bf16 gradient wire, the combine also writes
         # the bf16 twin the all-reduce sends (no separate cast kernel; parallel/data.py)
+        pend = _DEFER["pending"] if _DEFER is not None and twin_free(joint_bf16, wire) else None
         if joint is not None:
             t, ld = mats[0]
             dW = joint[:K * N].view(K, N)
+            defer = None
+            if pend is not None and _defer_ok(ws[0], *([ctx.bias_leaf] if tail is not None else [])):
+                def defer(slabs, S, mat, dW=dW):
+                    pend[dW.data_ptr()] = (hip.SlabGrad(slabs, S, 0, N, K * N, (K, N)), mat)
+                    if tail is not None:
+                        pend[tail[0].data_ptr()] = (hip.ConstGrad(tail[2], (N,)), mat)
             _dw_slabs(xb, t, ld, M, K, N, dW, N, 0,
-                      joint_bf16[:K * N].view(K, N) if joint_bf16 is not None else None, tail)
+                      joint_bf16[:K * N].view(K, N) if joint_bf16 is not None else None, tail, defer)
             dws[0] = dW
         elif batched:
             dW = torch.empty((nw, K, N), dtype=torch.float32, device=dev)
             twin = torch.empty((nw, K, N), dtype=torch.bfloat16, device=dev) if wire else None
-            _dw_slabs(xb, t0, ld0, M, K, nw * N, dW, N, K * N, twin)
+            defer = None
+            if pend is not None and twin is None and _defer_ok(*[ws[i] for i in want]):
+                def defer(slabs, S, mat, dW=dW):
+                    for i in want:
+                        pend[dW[i].data_ptr()] = (hip.SlabGrad(slabs, S, i * N, nw * N, K * nw * N, (K, N)), mat)
+            _dw_slabs(xb, t0, ld0, M, K, nw * N, dW, N, K * N, twin, defer=defer)
             if twin is not None:
                 _dp.register_wire_twin(dW, twin)
             for i in want:
@@ -356,7 +465,11 @@ def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, 
                 t, ld = mats[i]
                 dW = torch.empty((K, N), dtype=torch.float32, device=dev)
                 twin = torch.empty((K, N), dtype=torch.bfloat16, device=dev) if wire else None
-                _dw_slabs(xb, t, ld, M, K, N, dW, N, 0, twin)
+                defer = None
+                if pend is not None and twin is None and _defer_ok(ws[i]):
+                    def defer(slabs, S, mat, dW=dW):
+                        pend[dW.data_ptr()] = (hip.SlabGrad(slabs, S, 0, N, K * N, (K, N)), mat)
+                _dw_slabs(xb, t, ld, M, K, N, dW, N, 0, twin, defer=defer)
                 if twin is not None:
                     _dp.register_wire_twin(dW, twin)
                 dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)

@@ -178,6 +178,9 @@ def _grad_local(g: ShardedArray, d: int) -> torch.Tensor:
     """Gradient shard for the fused kernel: a data-parallel gradient still in its bf16 wire
     buffer is read there (the kernel converts on load) instead of being cast back to f32."""
     loc = g.local
+    slabs = getattr(loc, "slabs", None)
+    if slabs is not None and getattr(loc, "pending", False) and d in slabs:
+        return slabs[d]  # hip.SlabGrad / hip.ConstGrad: summed (or broadcast) inside the kernel
     raw = getattr(loc, "raw", None)
     if raw is not None and getattr(loc, "pending", False) and d in raw:
         return raw[d]

@@ -321,6 +321,11 @@ def reduce_replica_grads(pairs: List[Tuple[ShardedArray, Dict[int, torch.Tensor]
     return out  # type: ignore
 
 
+def _multi_process() -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
 def _spans_gpus() -> bool:
     """Single-controller run over several physical GPUs: one HIP graph captures one device's
     stream only, so such a step runs eagerly (its collectives are grouped RCCL calls across the
@@ -421,23 +426,36 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
                 # weight gradients fork onto side streams (ops/streams.py) unless data-parallel
                 # hooks consume gradients as they are produced; joined before they are returned
                 from ..ops import streams as _streams
+                from ..ops import linear as _lin
                 side = reducer is None and all(t.is_cuda for t in inputs)
+                # one device, no gradient all-reduce: weight-gradient combines may be left to the
+                # fused Adam (ops/linear.defer_wgrads)
+                one_dev = side and all(len(l.local) == 1 for l in all_leaves) and len(
+                    {d for l in all_leaves for d in l.local}) == 1 and not _multi_process()
+                dfr = _lin.defer_wgrads(outs, one_dev)
                 with torch.autograd.set_multithreading_enabled(_graphs.current() is None), \
-                        _streams.wgrad_scope(side):
+                        _streams.wgrad_scope(side), dfr:
                     gs = torch.autograd.grad(outs, inputs, seeds, allow_unused=True)
             else:
                 gs = [None] * len(inputs)
+                dfr = None
         finally:
             for h in hooks:
                 h.remove()
         gmap = {id(t): g for t, g in zip(inputs, gs)}
         pairs = []
-        for l in all_leaves:
+        deferred = {}
+        for i, l in enumerate(all_leaves):
             loc = {}
             for d, t in l.local.items():
                 g = gmap.get(id(t))
                 loc[d] = torch.zeros_like(t) if g is None else g
+                ent = dfr.take(g) if (dfr is not None and g is not None) else None
+                if ent is not None:
+                    deferred[i] = (d, g, ent)
             pairs.append((l, loc))
+        if dfr is not None:
+            dfr.flush()
         if reducer is not None:
             red = reducer.finish({i: loc for i, (_, loc) in enumerate(pairs)})
             reduced = [red[i] for i in range(len(pairs))]
@@ -453,7 +471,16 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
                     i = next(it)
                     p = all_leaves[i]
                     r = reduced[i]
-                    if isinstance(r, LazyLocal) and r.pending:
+                    dfe = deferred.get(i)
+                    if dfe is not None and not isinstance(r, LazyLocal) and len(r) == 1 \
+                            and r.get(dfe[0]) is dfe[1]:
+                        # an uncombined weight gradient: the fused Adam sums its slabs (.slabs);
+                        # any other read combines it first
+                        d0, g0, (desc, mat) = dfe
+                        loc = LazyLocal(lambda d0=d0, g0=g0, mat=mat: (mat(), {d0: g0.detach()})[1])
+                        loc.slabs = {d0: desc}
+                        loc.materialize = mat
+                    elif isinstance(r, LazyLocal) and r.pending:
                         # keep a reduced-in-wire-dtype gradient lazy (the optimizer reads .raw)
                         loc = LazyLocal(lambda r=r: {d: t.detach() for d, t in r.items()})
                         loc.raw = {d: t.detach() for d, t in r.raw.items()}

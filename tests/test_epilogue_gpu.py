@@ -1,5 +1,6 @@
 """GEMM epilogue operand R (residual add / ReLU mask) and its users: bit-exact against the
 unfused kernels, and the fused transformer layer / FF block against their unfused forms."""
+import numpy as np
 import pytest
 import torch
 
@@ -194,3 +195,63 @@ def test_side_stream_weight_grads_bit_exact(gpu_devices, monkeypatch, model_kind
     assert forks, "no weight gradient took the side stream"
     for a, b in zip(res["0"], res["1"]):
         assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+
+
+@pytest.mark.parametrize("model_kind", ["attention", "layer"])
+def test_deferred_wgrad_combine_bit_exact(gpu_devices, monkeypatch, model_kind):
+    """Weight gradients handed to the fused Adam as their split-K slabs (ops/linear.defer_wgrads:
+    no slab_reduce launch) train bit-identically to the combined path, eagerly and under a
+    captured/replayed jit step; a gradient read directly is combined on demand (same bits)."""
+    gpu_devices(1)
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd import optim
+    from learning_jax_sharding_amd.models import MultiHeadAttention, TransformerLayer
+    from learning_jax_sharding_amd.ops import linear
+    from learning_jax_sharding_amd.training import TrainState
+    if model_kind == "attention":
+        model = MultiHeadAttention(640, 8, 64)
+    else:
+        model = TransformerLayer(640, heads=8, dim_head=64, ff_dim=2560)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (8, 256, 640))
+
+    def make():
+        params = model.init(ljs.random.PRNGKey(1), x)["params"]
+        return TrainState.create(apply_fn=model.apply, params=params, tx=optim.adam(1e-3))
+
+    def step(state, x):
+        g = ljs.grad(lambda p: model.apply({"params": p}, x).sum())(state.params)
+        return state.apply_gradients(grads=g)
+
+    deferred = []
+    orig = linear._dw_slabs
+
+    def counting(*a, **k):
+        if k.get("defer") is not None or (len(a) > 11 and a[11] is not None):
+            deferred.append(1)
+        return orig(*a, **k)
+    monkeypatch.setattr(linear, "_dw_slabs", counting)
+    res = {}
+    for flag in (False, True):
+        monkeypatch.setattr(linear, "_DEFER_ON", flag)
+        n0 = len(deferred)
+        _, g = ljs.value_and_grad(lambda p: model.apply({"params": p}, x).sum())(make().params)
+        se = make()
+        for _ in range(2):
+            se = step(se, x)
+        sj = make()
+        jstep = ljs.jit(step, donate_argnums=0, capture=True)
+        for _ in range(3):
+            sj = jstep(sj, x)
+        torch.cuda.synchronize()
+        if flag:
+            assert len(deferred) > n0, "no weight gradient was deferred"
+        else:
+            assert len(deferred) == n0
+        res[flag] = [l.to_torch().clone() for l in ljs.tree_util.tree_leaves(ljs.nn.unbox(g))] + \
+            [np.asarray(l).copy() for l in ljs.tree_util.tree_leaves(se)] + \
+            [np.asarray(l).copy() for l in ljs.tree_util.tree_leaves(sj)]
+    for a, b in zip(res[False], res[True]):
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+        else:
+            np.testing.assert_array_equal(a, b)
