@@ -431,6 +431,17 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 }
 
 // ============================================================================ backward
+// sum over 8 bf16 pairs of x[i] * y[i] in f32
+__device__ __forceinline__ float dot_bf16x8(const u32x4& x, const u32x4& y) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    s = fmaf(__uint_as_float(x[k] << 16), __uint_as_float(y[k] << 16), s);
+    s = fmaf(__uint_as_float(x[k] & 0xffff0000u), __uint_as_float(y[k] & 0xffff0000u), s);
+  }
+  return s;
+}
+
 // per-lane row constants of one 64-query block: lse/delta for queries q0 + 16t + 4g + r
 struct RowConst {
   f32x4 lse[4], dl[4];
@@ -495,12 +506,13 @@ __device__ __forceinline__ void dkv_tile(const AttnArgs& a, const bf16_t* Qt, co
   }
 }
 
-// dK, dV for one 64-key block (each wave: 16 keys), sweeping all query blocks
-__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
+// dK, dV for one 64-key block (each wave: 16 keys), sweeping all query blocks.  INLINE_DELTA:
+// delta = rowsum(dO o O) of each query block is formed here from the staged dO chunks and an O
+// prefetch (into dls[2][64]), instead of read from the dQ kernel's output -- so the dQ and dK/dV
+// work can run as ONE launch (attn_bwd_pair_kernel) with no ordering between them.
+template <bool INLINE_DELTA>
+__device__ __forceinline__ void dkv_body(const AttnArgs& a, int kblk, int h, int b, bf16_t* smem, float* dls) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const Tile3 tl = tile3((a.Sk + BLK - 1) / BLK, a.H);
-  const int kblk = tl.x, h = tl.h, b = tl.b;
   const int key0 = kblk * BLK + wave * 16;
   const int key = key0 + (lane & 15);
   const bool kok = key < a.Sk;
@@ -510,6 +522,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   bf16x8 vf[2] = {load_row_frag(vp, kok, 0, lane), load_row_frag(vp, kok, 1, lane)};
   const bf16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
   const bf16_t* ob = a.dout + b * a.do_sb + h * a.do_sh;
+  const bf16_t* oo = a.o + b * a.o_sb + h * a.o_sh;
   const float* lse = a.lse + ((long)b * a.H + h) * a.Sq;
   const float* delta = a.delta + ((long)b * a.H + h) * a.Sq;
   const bool vec = (a.Sq % 4) == 0;
@@ -524,12 +537,30 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     dk[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  TileRegs tq, tdo;
+  TileRegs tq, tdo, to;
   RowConst rc;
+  // delta of the query block whose dO / O chunks are in tdo / to -> dls[buf]
+  auto delta_to_lds = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float s = dot_bf16x8(to.v[i], tdo.v[i]);
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 4, 64);
+      const int c = tid + 256 * i;
+      if ((c & 7) == 0) dls[buf * BLK + (c >> 3)] = s;
+    }
+  };
   if (nqt > 0) {
     tq.load(qb, a.q_ss, qstart, a.Sq, tid);
     tdo.load(ob, a.do_ss, qstart, a.Sq, tid);
-    rc.load(lse, delta, qstart, a.Sq, g, vec);
+    if constexpr (INLINE_DELTA) {
+      to.load(oo, a.o_ss, qstart, a.Sq, tid);
+      rc.load(lse, lse, qstart, a.Sq, g, vec);
+      delta_to_lds(0);
+    } else {
+      rc.load(lse, delta, qstart, a.Sq, g, vec);
+    }
     tq.store(smem, tid);
     tdo.store(smem + 2 * BLK * D, tid);
   }
@@ -541,6 +572,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     if (more) {
       tq.load(qb, a.q_ss, q0 + BLK, a.Sq, tid);
       tdo.load(ob, a.do_ss, q0 + BLK, a.Sq, tid);
+      if constexpr (INLINE_DELTA) to.load(oo, a.o_ss, q0 + BLK, a.Sq, tid);
+    }
+    if constexpr (INLINE_DELTA) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) rc.dl[t] = *reinterpret_cast<const f32x4*>(dls + cur * BLK + 16 * t + 4 * g);
     }
     const bf16_t* Qt = smem + cur * BLK * D;
     const bf16_t* Ot = smem + (2 + cur) * BLK * D;
@@ -549,7 +585,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     if (need_mask) dkv_tile<true>(a, Qt, Ot, rc, kf, vf, dk, dv, q0, key, lane);
     else dkv_tile<false>(a, Qt, Ot, rc, kf, vf, dk, dv, q0, key, lane);
     if (more) {
-      rc.load(lse, delta, q0 + BLK, a.Sq, g, vec);
+      if constexpr (INLINE_DELTA) {
+        rc.load(lse, lse, q0 + BLK, a.Sq, g, vec);
+        delta_to_lds(cur ^ 1);
+      } else {
+        rc.load(lse, delta, q0 + BLK, a.Sq, g, vec);
+      }
       tq.store(smem + (cur ^ 1) * BLK * D, tid);
       tdo.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
     }
@@ -559,6 +600,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     store_row_T(a.out + b * a.out_sb + (long)key * a.out_ss + h * a.out_sh, dk, a.scale, lane);
     store_row_T(a.out2 + b * a.out2_sb + (long)key * a.out2_ss + h * a.out2_sh, dv, 1.f, lane);
   }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
+  const Tile3 tl = tile3((a.Sk + BLK - 1) / BLK, a.H);
+  dkv_body<false>(a, tl.x, tl.h, tl.b, smem, nullptr);
 }
 
 template <bool MASK>
@@ -599,11 +646,8 @@ __device__ __forceinline__ void dq_tile(const AttnArgs& a, const bf16_t* Kt, con
 }
 
 // dQ for one 64-query block (each wave: 16 queries), sweeping key blocks
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
+__device__ __forceinline__ void dq_body(const AttnArgs& a, int qb, int h, int b, bf16_t* smem, bool write_delta) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const Tile3 tl = tile3((a.Sq + BLK - 1) / BLK, a.H);
-  const int qb = tl.x, h = tl.h, b = tl.b;
   const int qrow0 = qb * BLK + wave * 16;
   const int qrow = qrow0 + (lane & 15);
   const bool qok = qrow < a.Sq;
@@ -630,7 +674,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     }
     s = row4_sum(s);
     dl_q = s;
-    if (qok && (lane >> 4) == 0) const_cast<float*>(a.delta)[((long)b * a.H + h) * a.Sq + qrow] = s;
+    if (write_delta && qok && (lane >> 4) == 0) const_cast<float*>(a.delta)[((long)b * a.H + h) * a.Sq + qrow] = s;
   }
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
@@ -672,6 +716,30 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   if (qok) store_row_T(a.out + b * a.out_sb + (long)qrow * a.out_ss + h * a.out_sh, dq, a.scale, lane);
 }
 
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
+  const Tile3 tl = tile3((a.Sq + BLK - 1) / BLK, a.H);
+  dq_body(a, tl.x, tl.h, tl.b, smem, true);
+}
+
+// dQ blocks and dK/dV blocks of the split backward in ONE launch (the dK/dV blocks form delta
+// themselves): at the reference shape (B = 8) the two kernels ran back to back as two half-full
+// grids of 256 four-wave blocks; here all 512 blocks are resident at once.  Block ids are dealt
+// XCD-major (tile3's mapping) over [dQ items | dK/dV items].
+__global__ __launch_bounds__(256) void attn_bwd_pair_kernel(AttnArgs dq, AttnArgs dkv) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
+  __shared__ __attribute__((aligned(16))) float dls[2 * BLK];
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int nq = (dq.Sq + BLK - 1) / BLK, nk = (dkv.Sk + BLK - 1) / BLK;
+  const int ndq = nq * dq.H * (gridDim.x / (nq + nk) / dq.H);
+  if (t < ndq) {
+    dq_body(dq, t % nq, (t / nq) % dq.H, t / (nq * dq.H), smem, false);
+  } else {
+    const int u = t - ndq;
+    dkv_body<true>(dkv, u % nk, (u / nk) % dkv.H, u / (nk * dkv.H), smem, dls);
+  }
+}
+
 // ---------------------------------------------------------------- fused short-key backward
 // Sk <= 256: ONE workgroup (8 waves) per (batch, head) keeps K and V in LDS (each wave
 // owns 32 keys for dK / dV), then sweeps the query blocks once.  S and dP are computed
@@ -693,16 +761,6 @@ struct TileRegs1 {
     *reinterpret_cast<u32x4*>(lds + img16(tid >> 3, tid & 7)) = v;
   }
 };
-
-__device__ __forceinline__ float dot_bf16x8(const u32x4& x, const u32x4& y) {
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    s = fmaf(__uint_as_float(x[k] << 16), __uint_as_float(y[k] << 16), s);
-    s = fmaf(__uint_as_float(x[k] & 0xffff0000u), __uint_as_float(y[k] & 0xffff0000u), s);
-  }
-  return s;
-}
 
 // S/P/dP/dS for this wave's 32 keys x 64 queries; dK^T, dV^T accumulate; dS^T -> LDS
 template <bool MASK>
@@ -914,6 +972,17 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
 
 }  // namespace
 
+// split backward as one launch (attn_bwd_pair_kernel): LJS_ATTN_BWD_PAIR=0 for two launches
+static int g_bwd_pair = -1;  // -1 = read LJS_ATTN_BWD_PAIR at the next call
+LJS_API void ljs_attn_set_bwd_pair(int v) { g_bwd_pair = v; }
+static int attn_pair() {
+  if (g_bwd_pair < 0) {
+    const char* e = getenv("LJS_ATTN_BWD_PAIR");
+    g_bwd_pair = e ? atoi(e) : 1;
+  }
+  return g_bwd_pair;
+}
+
 static int attn_prio() {
   static int v = -1;
   if (v < 0) {
@@ -1031,13 +1100,19 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
     hipLaunchKernelGGL(attn_bwd_fused_kernel, dim3(H, B), dim3(FT), 0, stream, f);
     return (int)hipGetLastError();
   }
-  // dQ first: it also computes delta, which the dK/dV kernel consumes (stream order)
   AttnArgs c = a;
   c.out = (bf16_t*)dq; c.out_sb = dqs[0]; c.out_ss = dqs[1]; c.out_sh = dqs[2];
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Sq + BLK - 1) / BLK * H * B), dim3(256), 0, stream, c);
   AttnArgs b = a;
   b.out = (bf16_t*)dk; b.out_sb = dks[0]; b.out_ss = dks[1]; b.out_sh = dks[2];
   b.out2 = (bf16_t*)dv; b.out2_sb = dvs[0]; b.out2_ss = dvs[1]; b.out2_sh = dvs[2];
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((Sk + BLK - 1) / BLK * H * B), dim3(256), 0, stream, b);
+  const long nq = (Sq + BLK - 1) / BLK, nk = (Sk + BLK - 1) / BLK;
+  if (attn_pair() && (nq + nk) * H * B < (1L << 30)) {
+    // one launch: dQ blocks and dK/dV blocks (which form delta themselves) side by side
+    hipLaunchKernelGGL(attn_bwd_pair_kernel, dim3((unsigned)((nq + nk) * H * B)), dim3(256), 0, stream, c, b);
+    return (int)hipGetLastError();
+  }
+  // dQ first: it also computes delta, which the dK/dV kernel consumes (stream order)
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nq * H * B), dim3(256), 0, stream, c);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3(nk * H * B), dim3(256), 0, stream, b);
   return (int)hipGetLastError();
 }

@@ -99,6 +99,15 @@ def set_attention_bwd_fused(enabled: Optional[bool]):
     fn(2 if enabled is None else (1 if enabled else 0))
 
 
+def set_attention_bwd_pair(enabled: Optional[bool]):
+    """Split attention backward as ONE launch of dQ and dK/dV blocks (True, the default via
+    None) or as two launches ordered by the dQ kernel's delta output (False)."""
+    fn = lib().ljs_attn_set_bwd_pair
+    fn.argtypes = [c_int]
+    fn.restype = None
+    fn(1 if enabled is None or enabled else 0)
+
+
 def set_attention_fwd_nsub(nsub: int):
     """Forward query sub-tiles per wave (1 or 2; 0 = default)."""
     fn = lib().ljs_attn_set_fwd_nsub

@@ -191,6 +191,30 @@ def test_attention_bwd_block_fused_matches_split(hip, attn_fwd_nsub, Sq, Sk, cau
         torch.testing.assert_close(a.float(), b_.float(), rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("B,Sq,Sk,H,causal,q_offset", [(8, 256, 256, 8, False, 0), (2, 192, 128, 3, False, 0),
+                                                     (2, 130, 256, 3, True, 64), (1, 64, 100, 2, True, 0)])
+def test_attention_bwd_pair_matches_two_launches(hip, B, Sq, Sk, H, causal, q_offset):
+    """The split backward as one launch (dQ and dK/dV blocks side by side, the dK/dV blocks
+    forming delta = rowsum(dO o O) themselves) == the dQ kernel then the dK/dV kernel: dQ
+    bit-exact (same code), dK/dV up to delta's f32 summation order."""
+    D = 64
+    q, do = _rand(B, Sq, H, D, seed=1), _rand(B, Sq, H, D, seed=2)
+    k, v = _rand(B, Sk, H, D, seed=3), _rand(B, Sk, H, D, seed=4)
+    o, lse = hip.attn_fwd_lse(q, k, v, D ** -0.5, causal, q_offset)
+    hip.set_attention_bwd_fused(False)
+    outs = {}
+    try:
+        for pair in (True, False):
+            hip.set_attention_bwd_pair(pair)
+            outs[pair] = hip.attn_bwd_block(q, k, v, o, do, lse, D ** -0.5, causal, q_offset)
+    finally:
+        hip.set_attention_bwd_pair(None)
+        hip.set_attention_bwd_fused(None)
+    assert torch.equal(outs[True][0], outs[False][0])
+    for a, b_ in zip(outs[True][1:], outs[False][1:]):
+        torch.testing.assert_close(a.float(), b_.float(), rtol=1e-2, atol=1e-2)
+
+
 def test_attention_online_softmax_rescale(hip):
     """Force a running-max jump at a late key tile (exercises the rescale branch)."""
     B, S, H, D = 1, 256, 1, 64
