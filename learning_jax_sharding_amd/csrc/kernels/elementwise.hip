@@ -511,19 +511,6 @@ struct AdamTensor {
 };
 
 // the slab sum of slab_reduce_kernel, in its order (bit-identical results)
-__device__ __forceinline__ f32x4 slab_sum4(const float* __restrict__ g, long gS, long ss, long i) {
-  f32x4 acc = *reinterpret_cast<const f32x4*>(g + i);
-  long s = 1;
-  for (; s + 3 < gS; s += 4) {
-    f32x4 v0 = *reinterpret_cast<const f32x4*>(g + s * ss + i);
-    f32x4 v1 = *reinterpret_cast<const f32x4*>(g + (s + 1) * ss + i);
-    f32x4 v2 = *reinterpret_cast<const f32x4*>(g + (s + 2) * ss + i);
-    f32x4 v3 = *reinterpret_cast<const f32x4*>(g + (s + 3) * ss + i);
-    acc += (v0 + v1) + (v2 + v3);
-  }
-  for (; s < gS; ++s) acc += *reinterpret_cast<const f32x4*>(g + s * ss + i);
-  return acc;
-}
 __device__ __forceinline__ float slab_sum1(const float* __restrict__ g, long gS, long ss, long i) {
   float acc = g[i];
   long s = 1;
@@ -570,14 +557,42 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
     constexpr int NQ = kAdamRows / 16;
     f32x4 gv[NQ], mv[NQ], vv[NQ], pv[NQ];
     bool ok[NQ];
+    long gix[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int row = tr_i * kAdamRows + r0 + 16 * q;
       ok[q] = row < T.R;
+      gix[q] = ok[q] ? (long)row * T.g_ld + cbase : cbase;
       const long i = ok[q] ? (long)row * T.C + cbase : cbase;
-      const long gi = ok[q] ? (long)row * T.g_ld + cbase : cbase;
+      mv[q] = *reinterpret_cast<const f32x4*>(Mm + i);
+      vv[q] = *reinterpret_cast<const f32x4*>(Vv + i);
+      pv[q] = *reinterpret_cast<const f32x4*>(P + i);
+    }
+    if (T.gS > 0) {
+      // the slab sum of slab_reduce_kernel (same order, bit-identical) with the loads of all NQ
+      // rows of a 4-slab group in flight together
+      const float* G = reinterpret_cast<const float*>(T.g);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) gv[q] = *reinterpret_cast<const f32x4*>(G + gix[q]);
+      long s = 1;
+      for (; s + 3 < T.gS; s += 4) {
+        f32x4 v[NQ][4];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[q][j] = *reinterpret_cast<const f32x4*>(G + (s + j) * T.g_ss + gix[q]);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) gv[q] += (v[q][0] + v[q][1]) + (v[q][2] + v[q][3]);
+      }
+      for (; s < T.gS; ++s) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) gv[q] += *reinterpret_cast<const f32x4*>(G + s * T.g_ss + gix[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const long gi = gix[q];
       if (T.gS > 0) {
-        gv[q] = slab_sum4(reinterpret_cast<const float*>(T.g), T.gS, T.g_ss, gi);
       } else if (T.gS < 0) {
         const float c = __int_as_float((int)T.g_ld);
         gv[q] = f32x4{c, c, c, c};
@@ -588,9 +603,6 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
       } else {
         gv[q] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(T.g) + gi);
       }
-      mv[q] = *reinterpret_cast<const f32x4*>(Mm + i);
-      vv[q] = *reinterpret_cast<const f32x4*>(Vv + i);
-      pv[q] = *reinterpret_cast<const f32x4*>(P + i);
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {

@@ -357,9 +357,11 @@ def _pick_split(tiles: int, nkt: int) -> int:
     return best
 
 
-def _mx_wgrad(qa, sa, qb, sb, M: int, N: int, K: int, b_bcast: bool = False) -> torch.Tensor:
+def _mx_wgrad(qa, sa, qb, sb, M: int, N: int, K: int, b_bcast: bool = False, w=None) -> torch.Tensor:
     """f32 [M][N] = A B^T over K (both operands MX-fp8, K-major, blocks along K), split-K into f32
-    slabs summed by one streaming reduction."""
+    slabs summed by one streaming reduction -- or, for the gradient of weight ``w`` inside a
+    deferring value_and_grad, left to the fused Adam (ops/linear.defer_slabs)."""
+    from .linear import defer_slabs
     S = _pick_split(-(-M // 128) * -(-N // 128), K // 128)
     out = torch.empty((M, N), dtype=torch.float32, device=qa.device)
     if S == 1:
@@ -367,7 +369,11 @@ def _mx_wgrad(qa, sa, qb, sb, M: int, N: int, K: int, b_bcast: bool = False) -> 
         return out
     slabs = torch.empty((S, M, N), dtype=torch.float32, device=qa.device)
     gemm_mx(qa, sa, qb, sb, M, N, K, slabs, b_bcast=b_bcast, nsplit=S)
-    hip.slab_reduce(slabs, out, N, 0)
+    defer = defer_slabs(w, out, N) if w is not None else None
+    if defer is not None:
+        defer(slabs, S, lambda done=[]: done or (hip.slab_reduce(slabs, out, N, 0), done.append(1)))
+    else:
+        hip.slab_reduce(slabs, out, N, 0)
     return out
 
 
@@ -451,13 +457,13 @@ class _FFBlockFp8(torch.autograd.Function):
             # dY blocked along tokens: one constant row for a broadcast scalar, else a column pass
             if bm is not None:
                 qdyT, sdyT = bm[3], bm[4]
-                dwo = _mx_wgrad(qaT, saT, qdyT, sdyT, F, M, T, b_bcast=True)
+                dwo = _mx_wgrad(qaT, saT, qdyT, sdyT, F, M, T, b_bcast=True, w=w_out)
             else:
                 qdyT, sdyT = _t_quant(t)
-                dwo = _mx_wgrad(qaT, saT, qdyT, sdyT, F, M, T)
+                dwo = _mx_wgrad(qaT, saT, qdyT, sdyT, F, M, T, w=w_out)
             out["wo"] = dwo
         if ctx.needs_input_grad[1]:
-            out["wi"] = _mx_wgrad(qxT, sxT, qdAT, sdAT, M, F, T)
+            out["wi"] = _mx_wgrad(qxT, sxT, qdAT, sdAT, M, F, T, w=w_in)
         dres = dy if (has_res and ctx.needs_input_grad[3] and not fold) else None
         return out.get("dx"), out.get("wi"), out.get("wo"), dres
 

@@ -118,7 +118,25 @@ def defer_safe_leaves(outs) -> set:
                 prod[k] = fn
             elif id(nxt) not in seen:
                 stack.append(nxt)
-    return {k for k, c in counts.items() if c == 1 and type(prod[k]).__name__ == "_LinearBackward"}
+    return {k for k, c in counts.items() if c == 1 and type(prod[k]).__name__ in _DEFER_NODES}
+
+
+# autograd nodes whose weight gradients may stay uncombined (they call _defer_ok per weight)
+_DEFER_NODES = ("_LinearBackward", "_FFBlockBackward", "_FFBlockFp8Backward")
+
+
+def defer_slabs(w: torch.Tensor, out: torch.Tensor, ld: int, offset: int = 0):
+    """The ``defer`` callback of a weight-gradient GEMM writing ``out`` (= w's gradient, shape
+    w.shape, element (r, c) at slab offset + r * ld + c), or None when w's gradient must be
+    combined now (not inside a deferring value_and_grad, or w has another consumer)."""
+    d = _DEFER
+    if d is None or not _defer_ok(w) or tuple(out.shape) != tuple(w.shape) or out.dtype != torch.float32:
+        return None
+    pend = d["pending"]
+
+    def defer(slabs, S, mat):
+        pend[out.data_ptr()] = (hip.SlabGrad(slabs, S, offset, ld, slabs[0].numel(), tuple(out.shape)), mat)
+    return defer
 
 
 class defer_wgrads:
@@ -555,10 +573,10 @@ class _FFBlock(torch.autograd.Function):
                          res_ld=ld)
                 out["dx"] = dx.to(xdt).view(tuple(lead) + (M,))
 
-        def wgrad(xb, g, g_ld, K, N):
+        def wgrad(xb, g, g_ld, K, N, w):
             o = torch.empty((K, N), dtype=torch.float32, device=dev)
             twin = torch.empty((K, N), dtype=torch.bfloat16, device=dev) if wire else None
-            _dw_slabs(xb, g, g_ld, T, K, N, o, N, 0, twin)
+            _dw_slabs(xb, g, g_ld, T, K, N, o, N, 0, twin, defer=defer_slabs(w, o, N) if twin is None else None)
             if twin is not None:
                 _dp.register_wire_twin(o, twin)
             return o
@@ -566,13 +584,13 @@ class _FFBlock(torch.autograd.Function):
         def run_wo():  # weight gradients on the side stream inside value_and_grad (ops/streams.py)
             if ctx.needs_input_grad[2]:
                 with _streams.side(dev, [a, t]) as produced:
-                    out["wo"] = wgrad(a, t, ld, F, M)
+                    out["wo"] = wgrad(a, t, ld, F, M, w_out)
                     produced.append(out["wo"])
 
         def run_wi():
             if ctx.needs_input_grad[1]:
                 with _streams.side(dev, [x2, dA]) as produced:
-                    out["wi"] = wgrad(x2, dA, F, M, F)
+                    out["wi"] = wgrad(x2, dA, F, M, F, w_in)
                     produced.append(out["wi"])
         _ff_bwd_order(run_dx, run_wo, run_wi)
         return out.get("dx"), out.get("wi"), out.get("wo"), None

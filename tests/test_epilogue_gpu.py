@@ -197,7 +197,7 @@ def test_side_stream_weight_grads_bit_exact(gpu_devices, monkeypatch, model_kind
         assert torch.equal(a, b), (a.float() - b.float()).abs().max()
 
 
-@pytest.mark.parametrize("model_kind", ["attention", "layer"])
+@pytest.mark.parametrize("model_kind", ["attention", "layer", "layer_fp8"])
 def test_deferred_wgrad_combine_bit_exact(gpu_devices, monkeypatch, model_kind):
     """Weight gradients handed to the fused Adam as their split-K slabs (ops/linear.defer_wgrads:
     no slab_reduce launch) train bit-identically to the combined path, eagerly and under a
@@ -211,7 +211,7 @@ def test_deferred_wgrad_combine_bit_exact(gpu_devices, monkeypatch, model_kind):
     if model_kind == "attention":
         model = MultiHeadAttention(640, 8, 64)
     else:
-        model = TransformerLayer(640, heads=8, dim_head=64, ff_dim=2560)
+        model = TransformerLayer(640, heads=8, dim_head=64, ff_dim=2560, fp8=model_kind == "layer_fp8")
     x = ljs.random.normal(ljs.random.PRNGKey(0), (8, 256, 640))
 
     def make():
@@ -223,13 +223,22 @@ def test_deferred_wgrad_combine_bit_exact(gpu_devices, monkeypatch, model_kind):
         return state.apply_gradients(grads=g)
 
     deferred = []
-    orig = linear._dw_slabs
+    orig = linear.defer_slabs
 
     def counting(*a, **k):
-        if k.get("defer") is not None or (len(a) > 11 and a[11] is not None):
+        r = orig(*a, **k)
+        if r is not None:
             deferred.append(1)
-        return orig(*a, **k)
-    monkeypatch.setattr(linear, "_dw_slabs", counting)
+        return r
+    monkeypatch.setattr(linear, "defer_slabs", counting)
+    orig_ok = linear._defer_ok
+
+    def counting_ok(*a):
+        r = orig_ok(*a)
+        if r:
+            deferred.append(1)
+        return r
+    monkeypatch.setattr(linear, "_defer_ok", counting_ok)
     res = {}
     for flag in (False, True):
         monkeypatch.setattr(linear, "_DEFER_ON", flag)
