@@ -25,6 +25,8 @@
 // so Q/K/V can be column slices of the fused QKV GEMM output.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int D = 64;      // head dim
@@ -104,6 +106,19 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16_t* lds, int base0, int base
   int c8 = (db >> 2) + p;
   s16x4 lo = lds_read_tr16(lds + img8(base0 + q, c8));
   s16x4 hi = lds_read_tr16(lds + img8(base1 + q, c8));
+  return join_bf16x8(lo, hi);
+}
+
+// frag_tr with the row base split off: rows R0 + (4g + q) and R0 + 16 + (4g + q) for R0 a multiple
+// of 8 (the swizzle depends on (row >> 1) & 3 only, which R0 does not change), so the lane part
+// `off` = tr_off(db, lane) is computed once per kernel and R0 becomes an immediate LDS offset.
+__device__ __forceinline__ int tr_off(int db, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  return img8(4 * g + (i >> 2), (db >> 2) + (i & 3));
+}
+__device__ __forceinline__ bf16x8 frag_tr_o(const bf16_t* lds, int R0, int off) {
+  s16x4 lo = lds_read_tr16(lds + R0 * D + off);
+  s16x4 hi = lds_read_tr16(lds + (R0 + 16) * D + off);
   return join_bf16x8(lo, hi);
 }
 
@@ -767,7 +782,7 @@ template <bool MASK>
 __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, const bf16_t* Ot,
                                            const float* lse_s, const float* dl_s, bf16_t* dSt,
                                            const bf16x8 (&kr)[2][2], const bf16x8 (&vr)[2][2], f32x4 (&dk)[2][4],
-                                           f32x4 (&dv)[2][4], int q0, int key0, int lane) {
+                                           f32x4 (&dv)[2][4], int q0, int key0, int lane, const int (&offtr)[4]) {
   const int g = lane >> 4;
   // two 32-query halves: P / dS of a half feed the dK/dV MFMAs right away (register pressure)
 #pragma unroll
@@ -817,8 +832,8 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
     }
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      bf16x8 oa = frag_tr(Ot, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
-      bf16x8 qa = frag_tr(Qt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+      bf16x8 oa = frag_tr_o(Ot, 32 * s2, offtr[dt]);
+      bf16x8 qa = frag_tr_o(Qt, 32 * s2, offtr[dt]);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         dv[j][dt] = mfma16x16x32(oa, pb[j], dv[j][dt]);
@@ -917,49 +932,73 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       vr[j][ks] = frag_rows(Vs, key0 + 16 * j, ks, lane);
     }
   const int qt = wave & 3, dt0 = 2 * (wave >> 2);
+  int offtr[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) offtr[dt] = tr_off(16 * dt, lane);
+  const int off_q = tr_off(16 * qt, lane);
+  const int off_k[2] = {tr_off(16 * dt0, lane), tr_off(16 * (dt0 + 1), lane)};
   // static priority for the second-dispatched half (MI355X_MICROARCH "Two waves per SIMD" item
   // 4): waves 4-7 lose VALU arbitration to their SIMD partners on every segment otherwise
   if (a.prio_hi_half && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  for (int it = 0; it < nqt; ++it) {
-    const int cur = it & 1;
-    const int q0 = it * BLK;
-    const bool more = it + 1 < nqt;
-    if (more) issue(q0 + BLK, cur ^ 1);
-    const bf16_t* Qt = QO + cur * BLK * D;
-    const bf16_t* Ot = QO + (2 + cur) * BLK * D;
-    if (active) {
-      const bool need_mask = q0 + BLK > a.Sq || key0 + 32 > a.Sk || (a.causal && key0 + 31 > q0 + a.q_offset);
-      if (need_mask) fused_tile<true>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, kr, vr, dk, dv, q0, key0, lane);
-      else fused_tile<false>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, kr, vr, dk, dv, q0, key0, lane);
-    }
-    // this wave's DMA pieces of the next block landed; after the barrier everyone's have, so the
-    // next block's delta is formed inside the dQ phase (two barriers per query block, not three)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (more) finish(cur ^ 1);
-    // dQ^T (d tiles dt0, dt0+1) x queries 16qt..16qt+15 = K^T dS^T over all keys
-    f32x4 dq[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    for (int s2 = 0; s2 < nk32; ++s2) {
-      bf16x8 sb = frag_tr(dSt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * qt, lane);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        bf16x8 ka = frag_tr(Ks, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * (dt0 + i), lane);
-        dq[i] = mfma16x16x32(ka, sb, dq[i]);
+  // the query sweep as two instances: waves that never need a mask (the common case: Sq % 64 == 0,
+  // all 32 keys valid, not causal) run one whose tiles are all unmasked -- with both tile variants
+  // in one loop the compiler allocated dK / dV differently in each and copied all 64 accumulator
+  // registers at their join on every query block.  Same trip count and barriers in both.
+  const bool wave_mask = (a.Sq % BLK) != 0 || key0 + 32 > a.Sk || a.causal;
+  auto sweep = [&](auto wm) {
+    constexpr bool WM = decltype(wm)::value;
+    for (int it = 0; it < nqt; ++it) {
+      const int cur = it & 1;
+      const int q0 = it * BLK;
+      const bool more = it + 1 < nqt;
+      if (more) issue(q0 + BLK, cur ^ 1);
+      const bf16_t* Qt = QO + cur * BLK * D;
+      const bf16_t* Ot = QO + (2 + cur) * BLK * D;
+      if (active) {
+        if constexpr (WM) {
+          const bool need_mask = q0 + BLK > a.Sq || key0 + 32 > a.Sk || (a.causal && key0 + 31 > q0 + a.q_offset);
+          if (need_mask) fused_tile<true>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, kr, vr, dk, dv, q0, key0, lane, offtr);
+          else fused_tile<false>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, kr, vr, dk, dv, q0, key0, lane, offtr);
+        } else {
+          fused_tile<false>(a, Qt, Ot, rowc[cur][0], rowc[cur][1], dSt, kr, vr, dk, dv, q0, key0, lane, offtr);
+        }
       }
-    }
-    const int qrow = q0 + 16 * qt + (lane & 15);
-    if (qrow < a.Sq) {
-      bf16_t* rowp = a.out3 + b * a.out3_sb + (long)qrow * a.out3_ss + h * a.out3_sh;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        u32x2 w;
-        w[0] = pack_bf16x2(dq[i][0] * a.scale, dq[i][1] * a.scale);
-        w[1] = pack_bf16x2(dq[i][2] * a.scale, dq[i][3] * a.scale);
-        *reinterpret_cast<u32x2*>(rowp + 16 * (dt0 + i) + 4 * g) = w;
+      // this wave's DMA pieces of the next block landed; after the barrier everyone's have, so the
+      // next block's delta is formed inside the dQ phase (two barriers per query block, not three)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (more) finish(cur ^ 1);
+      // dQ^T (d tiles dt0, dt0+1) x queries 16qt..16qt+15 = K^T dS^T over all keys
+      f32x4 dq[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      // unrolled over the at most FK / 32 key slices: every LDS address is a lane offset plus an
+      // immediate (the rolled loop recomputed the swizzled addresses, 12 VALU per slice)
+  #pragma unroll
+      for (int s2 = 0; s2 < FK / 32; ++s2) {
+        if (s2 < nk32) {
+          bf16x8 sb = frag_tr_o(dSt, 32 * s2, off_q);
+  #pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            bf16x8 ka = frag_tr_o(Ks, 32 * s2, off_k[i]);
+            dq[i] = mfma16x16x32(ka, sb, dq[i]);
+          }
+        }
       }
+      const int qrow = q0 + 16 * qt + (lane & 15);
+      if (qrow < a.Sq) {
+        bf16_t* rowp = a.out3 + b * a.out3_sb + (long)qrow * a.out3_ss + h * a.out3_sh;
+  #pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          u32x2 w;
+          w[0] = pack_bf16x2(dq[i][0] * a.scale, dq[i][1] * a.scale);
+          w[1] = pack_bf16x2(dq[i][2] * a.scale, dq[i][3] * a.scale);
+          *reinterpret_cast<u32x2*>(rowp + 16 * (dt0 + i) + 4 * g) = w;
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
-  }
+  };
+  if (wave_mask) sweep(std::true_type{});
+  else sweep(std::false_type{});
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     int key = key0 + 16 * j + (lane & 15);
