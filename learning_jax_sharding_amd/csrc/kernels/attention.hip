@@ -186,19 +186,29 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
   float m_use = m_new;
   if constexpr (MASK) m_use = m_new == -INFINITY ? 0.f : m_new;  // row fully masked so far: p = 0
   const float alpha = fast_exp2(st.m - m_use);
-  float psum = 0.f;
+  // exponent arguments, the row sum and the O rescale as packed f32 pairs (v_pk_fma / v_pk_add /
+  // v_pk_mul: half the VALU issues; the row sum as a pairwise tree instead of a 16-long chain)
+  const f32x2 sc2 = {a.scale_log2, a.scale_log2}, mm2 = {m_use, m_use};
+  f32x2 ps2 = {0.f, 0.f};
 #pragma unroll
   for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float pv = fast_exp2(fmaf(s[jt][r], a.scale_log2, -m_use));
-      s[jt][r] = pv;
-      psum += pv;
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 x = f32x2{s[jt][2 * h], s[jt][2 * h + 1]} * sc2 - mm2;
+      const f32x2 pv = {fast_exp2(x[0]), fast_exp2(x[1])};
+      s[jt][2 * h] = pv[0];
+      s[jt][2 * h + 1] = pv[1];
+      ps2 += pv;
     }
+  const float psum = ps2[0] + ps2[1];
   st.l = st.l * alpha + psum;
   st.m = m_new;
+  const f32x2 al2 = {alpha, alpha};
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) st.o[dt] *= alpha;
+  for (int dt = 0; dt < 4; ++dt) {
+    const f32x2 lo = f32x2{st.o[dt][0], st.o[dt][1]} * al2, hi = f32x2{st.o[dt][2], st.o[dt][3]} * al2;
+    st.o[dt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+  }
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
     bf16x8 pb = frag_acc(s[2 * s2], s[2 * s2 + 1]);
@@ -256,12 +266,19 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int qrow0 = qb * QB + 16 * wave;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int kbase = kt * BLK;
-    if (a.causal && kbase > qrow0 + 15 + a.q_offset) break;
-    const bool need_mask = kbase + BLK > a.Sk || (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
-    if (need_mask) fwd_tile<true>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kbase, qrow, lane);
-    else fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kbase, qrow, lane);
+  if ((a.Sk % BLK) == 0 && !a.causal) {
+    // no tile needs a mask: one tile instance (with both in the loop the compiler copied the O
+    // accumulators at their join on every key tile)
+    for (int kt = 0; kt < nkt; ++kt)
+      fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kt * BLK, qrow, lane);
+  } else {
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int kbase = kt * BLK;
+      if (a.causal && kbase > qrow0 + 15 + a.q_offset) break;
+      const bool need_mask = kbase + BLK > a.Sk || (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
+      if (need_mask) fwd_tile<true>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kbase, qrow, lane);
+      else fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kbase, qrow, lane);
+    }
   }
   float lt = row4_sum(st.l);
   if (qok) {
@@ -794,26 +811,41 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
     for (int tt = 0; tt < 2; ++tt) {
       const int t = 2 * s2 + tt;
       const f32x4 lse = *reinterpret_cast<const f32x4*>(lse_s + 16 * t + 4 * g);
-      const f32x4 dl = *reinterpret_cast<const f32x4*>(dl_s + 16 * t + 4 * g);
+      const f32x4 ndl = *reinterpret_cast<const f32x4*>(dl_s + 16 * t + 4 * g);  // -delta
       const bf16x8 q0f = frag_rows(Qt, 16 * t, 0, lane), q1f = frag_rows(Qt, 16 * t, 1, lane);
       const bf16x8 o0f = frag_rows(Ot, 16 * t, 0, lane), o1f = frag_rows(Ot, 16 * t, 1, lane);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+        // dP - delta straight out of the MFMA chain: its accumulator starts at -delta (a row
+        // constant in the accumulator layout) -- no subtraction per element
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = ndl;
         s = mfma16x16x32(q0f, kr[j][0], s);
         s = mfma16x16x32(q1f, kr[j][1], s);
         dp = mfma16x16x32(o0f, vr[j][0], dp);
         dp = mfma16x16x32(o1f, vr[j][1], dp);
         float pv[4], dsv[4];
+        // exponent arguments and dS as packed f32 pairs (v_pk_fma_f32 / v_pk_mul_f32: half the
+        // VALU issues of the scalar forms; the kernel is VALU-bound at head_dim 64)
+        const f32x2 sc2 = {a.scale_log2, a.scale_log2};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pv[r] = fast_exp2(fmaf(s[r], a.scale_log2, -lse[r]));
-          if constexpr (MASK) {
+        for (int h = 0; h < 2; ++h) {
+          const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - f32x2{lse[2 * h], lse[2 * h + 1]};
+          pv[2 * h] = fast_exp2(x[0]);
+          pv[2 * h + 1] = fast_exp2(x[1]);
+        }
+        if constexpr (MASK) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
             int q = q0 + 16 * t + 4 * g + r, key = key0 + 16 * j + (lane & 15);
             bool ok = q < a.Sq && key < a.Sk && !(a.causal && key > q + a.q_offset);
             pv[r] = ok ? pv[r] : 0.f;
           }
-          dsv[r] = pv[r] * (dp[r] - dl[r]);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x2 d = f32x2{pv[2 * h], pv[2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+          dsv[2 * h] = d[0];
+          dsv[2 * h + 1] = d[1];
         }
         pbu[j][2 * tt] = pack_bf16x2(pv[0], pv[1]);
         pbu[j][2 * tt + 1] = pack_bf16x2(pv[2], pv[3]);
@@ -905,7 +937,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
-    if (c16 == 0) rowc[buf][1][row] = s;
+    if (c16 == 0) rowc[buf][1][row] = -s;  // stored negated: it seeds the dP accumulators
   };
   if (nqt > 0) issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -291,6 +291,9 @@ _DW_SLAB_MODE = os.environ.get("LJS_DW_SLAB_MODE", "1") == "1"  # A/B switch: 0 
 # weight-grad tile at <= 4096 tokens: 12884 (8-wave 128x128, 4 stages, uneven slab splits) measured
 # 0.1033-0.1053 ms vs 0.1071-0.1076 for 644 (64x64, power-of-two batched slabs) at B=8
 _DW_SMALL_TILE = int(os.environ.get("LJS_DW_SMALL_TILE", "12884"))
+# weight of the slab traffic (written by the GEMM, summed by the combine or the fused Adam) in
+# the split-count cost model (tuning knob)
+_DW_TRAFFIC_W = float(os.environ.get("LJS_DW_TRAFFIC_W", "1"))
 
 
 def slab_count(nkt: int, S: int) -> int:
@@ -330,7 +333,7 @@ def pick_dw_slabs(K: int, N: int, T: int):
             # ~1.2 us per K-tile round of a full chip of 128x128 blocks, ~1 us per round of
             # prologue/epilogue, and the reduction reads each f32 slab once (~5 TB/s)
             rounds = -(-tiles * S // slots)
-            cost = rounds * (kps * 1.2 + 1.0) + S * K * N * 4 / 5e6
+            cost = rounds * (kps * 1.2 + 1.0) + _DW_TRAFFIC_W * S * K * N * 4 / 5e6
             if best_cost is None or cost < best_cost - 1e-9:
                 best, best_cost = S, cost
         return 1282, best, True
@@ -341,7 +344,7 @@ def pick_dw_slabs(K: int, N: int, T: int):
         for S in range(1, min(32, nkt) + 1):
             if slab_count(nkt, S) != S:
                 continue
-            cost = -(-tiles * S // _cus()) * (-(-nkt // S) * 1.2 + 1.0) + S * K * N * 4 / 5e6
+            cost = -(-tiles * S // _cus()) * (-(-nkt // S) * 1.2 + 1.0) + _DW_TRAFFIC_W * S * K * N * 4 / 5e6
             if best_cost is None or cost < best_cost - 1e-9:
                 best, best_cost = S, cost
         return 12884, best, True
