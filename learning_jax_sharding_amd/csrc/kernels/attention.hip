@@ -40,7 +40,7 @@ struct AttnArgs {
   bf16_t* out2;                    // bwd dkv: dV
   bf16_t* out3;                    // bwd fused: dQ (out = dK, out2 = dV)
   float* lse;                      // [B][H][Sq], log2 domain of scaled scores
-  const float* delta;              // [B][H][Sq]
+  const float* delta;              // [B][H][Sq], NEGATED: -rowsum(dO o O) (it seeds dP accumulators)
   long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh;
   long do_sb, do_ss, do_sh, out_sb, out_ss, out_sh, out2_sb, out2_ss, out2_sh, out3_sb, out3_ss, out3_sh;
   int Sq, Sk, H;
@@ -503,24 +503,35 @@ __device__ __forceinline__ void dkv_tile(const AttnArgs& a, const bf16_t* Qt, co
   const int g = lane >> 4;
   // S = Q K^T (rows = queries 16t + 4g + r, col = this lane's key); P; dP = dO V^T; dS
   f32x4 p[4], ds[4];
+  const f32x2 sc2 = {a.scale_log2, a.scale_log2};
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+    // rc.dl holds -delta: dP - delta comes straight out of the MFMA chain it seeds
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = rc.dl[t];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       s = mfma16x16x32(frag_rows(Qt, 16 * t, ks, lane), kf[ks], s);
       dp = mfma16x16x32(frag_rows(Ot, 16 * t, ks, lane), vf[ks], dp);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float pv = fast_exp2(fmaf(s[r], a.scale_log2, -rc.lse[t][r]));
-      if constexpr (MASK) {
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - f32x2{rc.lse[t][2 * h], rc.lse[t][2 * h + 1]};
+      p[t][2 * h] = fast_exp2(x[0]);
+      p[t][2 * h + 1] = fast_exp2(x[1]);
+    }
+    if constexpr (MASK) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
         int q = q0 + 16 * t + 4 * g + r;
         bool ok = q < a.Sq && key < a.Sk && !(a.causal && key > q + a.q_offset);
-        pv = ok ? pv : 0.f;
+        p[t][r] = ok ? p[t][r] : 0.f;
       }
-      p[t][r] = pv;
-      ds[t][r] = pv * (dp[r] - rc.dl[t][r]);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 d = f32x2{p[t][2 * h], p[t][2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+      ds[t][2 * h] = d[0];
+      ds[t][2 * h + 1] = d[1];
     }
   }
   // dV^T += dO^T P ; dK^T += Q^T dS   (k = queries)
@@ -562,6 +573,9 @@ __device__ __forceinline__ void dkv_body(const AttnArgs& a, int kblk, int h, int
   int qstart = 0;
   if (a.causal) qstart = max(0, (kblk * BLK - a.q_offset) / BLK * BLK);
   const int nqt = (a.Sq - qstart + BLK - 1) / BLK;
+  // no tile of this wave needs a mask (the usual case): the sweep below runs as an instance
+  // without the masked tile variant (no accumulator copies at a join of the two)
+  const bool wave_mask = (a.Sq % BLK) != 0 || key0 + 16 > a.Sk || a.causal;
 
   f32x4 dk[4], dv[4];
 #pragma unroll
@@ -580,7 +594,7 @@ __device__ __forceinline__ void dkv_body(const AttnArgs& a, int kblk, int h, int
       s += __shfl_xor(s, 2, 64);
       s += __shfl_xor(s, 4, 64);
       const int c = tid + 256 * i;
-      if ((c & 7) == 0) dls[buf * BLK + (c >> 3)] = s;
+      if ((c & 7) == 0) dls[buf * BLK + (c >> 3)] = -s;  // negated, as the dQ kernel's delta
     }
   };
   if (nqt > 0) {
@@ -597,37 +611,45 @@ __device__ __forceinline__ void dkv_body(const AttnArgs& a, int kblk, int h, int
     tdo.store(smem + 2 * BLK * D, tid);
   }
   __syncthreads();
-  for (int it = 0; it < nqt; ++it) {
-    const int cur = it & 1;
-    const int q0 = qstart + it * BLK;
-    const bool more = it + 1 < nqt;
-    if (more) {
-      tq.load(qb, a.q_ss, q0 + BLK, a.Sq, tid);
-      tdo.load(ob, a.do_ss, q0 + BLK, a.Sq, tid);
-      if constexpr (INLINE_DELTA) to.load(oo, a.o_ss, q0 + BLK, a.Sq, tid);
-    }
-    if constexpr (INLINE_DELTA) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) rc.dl[t] = *reinterpret_cast<const f32x4*>(dls + cur * BLK + 16 * t + 4 * g);
-    }
-    const bf16_t* Qt = smem + cur * BLK * D;
-    const bf16_t* Ot = smem + (2 + cur) * BLK * D;
-    const bool need_mask = q0 + BLK > a.Sq || key0 + 16 > a.Sk ||
-                           (a.causal && key0 + 15 > q0 + a.q_offset);
-    if (need_mask) dkv_tile<true>(a, Qt, Ot, rc, kf, vf, dk, dv, q0, key, lane);
-    else dkv_tile<false>(a, Qt, Ot, rc, kf, vf, dk, dv, q0, key, lane);
-    if (more) {
-      if constexpr (INLINE_DELTA) {
-        rc.load(lse, lse, q0 + BLK, a.Sq, g, vec);
-        delta_to_lds(cur ^ 1);
-      } else {
-        rc.load(lse, delta, q0 + BLK, a.Sq, g, vec);
+  auto sweep = [&](auto wm) {
+    constexpr bool WM = decltype(wm)::value;
+    for (int it = 0; it < nqt; ++it) {
+      const int cur = it & 1;
+      const int q0 = qstart + it * BLK;
+      const bool more = it + 1 < nqt;
+      if (more) {
+        tq.load(qb, a.q_ss, q0 + BLK, a.Sq, tid);
+        tdo.load(ob, a.do_ss, q0 + BLK, a.Sq, tid);
+        if constexpr (INLINE_DELTA) to.load(oo, a.o_ss, q0 + BLK, a.Sq, tid);
       }
-      tq.store(smem + (cur ^ 1) * BLK * D, tid);
-      tdo.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
+      if constexpr (INLINE_DELTA) {
+  #pragma unroll
+        for (int t = 0; t < 4; ++t) rc.dl[t] = *reinterpret_cast<const f32x4*>(dls + cur * BLK + 16 * t + 4 * g);
+      }
+      const bf16_t* Qt = smem + cur * BLK * D;
+      const bf16_t* Ot = smem + (2 + cur) * BLK * D;
+      if constexpr (WM) {
+        const bool need_mask = q0 + BLK > a.Sq || key0 + 16 > a.Sk || (a.causal && key0 + 15 > q0 + a.q_offset);
+        if (need_mask) dkv_tile<true>(a, Qt, Ot, rc, kf, vf, dk, dv, q0, key, lane);
+        else dkv_tile<false>(a, Qt, Ot, rc, kf, vf, dk, dv, q0, key, lane);
+      } else {
+        dkv_tile<false>(a, Qt, Ot, rc, kf, vf, dk, dv, q0, key, lane);
+      }
+      if (more) {
+        if constexpr (INLINE_DELTA) {
+          rc.load(lse, lse, q0 + BLK, a.Sq, g, vec);
+          delta_to_lds(cur ^ 1);
+        } else {
+          rc.load(lse, delta, q0 + BLK, a.Sq, g, vec);
+        }
+        tq.store(smem + (cur ^ 1) * BLK * D, tid);
+        tdo.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
+      }
+      __syncthreads();
     }
-    __syncthreads();
-  }
+  };
+  if (wave_mask) sweep(std::true_type{});
+  else sweep(std::false_type{});
   if (kok) {
     store_row_T(a.out + b * a.out_sb + (long)key * a.out_ss + h * a.out_sh, dk, a.scale, lane);
     store_row_T(a.out2 + b * a.out2_sb + (long)key * a.out2_ss + h * a.out2_sh, dv, 1.f, lane);
@@ -646,23 +668,36 @@ __device__ __forceinline__ void dq_tile(const AttnArgs& a, const bf16_t* Kt, con
                                         int qrow, int lane) {
   const int g = lane >> 4;
   f32x4 ds[4];
+  const f32x2 sc2 = {a.scale_log2, a.scale_log2}, ls2 = {lse_q, lse_q};
 #pragma unroll
   for (int jt = 0; jt < 4; ++jt) {
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+    // dl_q is -delta: it seeds the dP accumulators (dP - delta out of the MFMA chain)
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{dl_q, dl_q, dl_q, dl_q};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       s = mfma16x16x32(frag_rows(Kt, 16 * jt, ks, lane), qf[ks], s);
       dp = mfma16x16x32(frag_rows(Vt, 16 * jt, ks, lane), df[ks], dp);
     }
+    float pv[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float pv = fast_exp2(fmaf(s[r], a.scale_log2, -lse_q));
-      if constexpr (MASK) {
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - ls2;
+      pv[2 * h] = fast_exp2(x[0]);
+      pv[2 * h + 1] = fast_exp2(x[1]);
+    }
+    if constexpr (MASK) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
         int key = kbase + 16 * jt + 4 * g + r;
         bool ok = qrow < a.Sq && key < a.Sk && !(a.causal && key > qrow + a.q_offset);
-        pv = ok ? pv : 0.f;
+        pv[r] = ok ? pv[r] : 0.f;
       }
-      ds[jt][r] = pv * (dp[r] - dl_q);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 d = f32x2{pv[2 * h], pv[2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+      ds[jt][2 * h] = d[0];
+      ds[jt][2 * h + 1] = d[1];
     }
   }
   // dQ^T += K^T dS^T   (k = keys)
@@ -705,8 +740,8 @@ __device__ __forceinline__ void dq_body(const AttnArgs& a, int qb, int h, int b,
       }
     }
     s = row4_sum(s);
-    dl_q = s;
-    if (write_delta && qok && (lane >> 4) == 0) const_cast<float*>(a.delta)[((long)b * a.H + h) * a.Sq + qrow] = s;
+    dl_q = -s;  // delta is kept negated (it seeds the dP accumulators)
+    if (write_delta && qok && (lane >> 4) == 0) const_cast<float*>(a.delta)[((long)b * a.H + h) * a.Sq + qrow] = -s;
   }
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
@@ -717,6 +752,7 @@ __device__ __forceinline__ void dq_body(const AttnArgs& a, int qb, int h, int b,
   f32x4 dq[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool wave_mask = (a.Sk % BLK) != 0 || qrow0 + 16 > a.Sq || a.causal;
   TileRegs tk, tv;
   if (nkt > 0) {
     tk.load(kb, a.k_ss, 0, a.Sk, tid);
@@ -725,26 +761,35 @@ __device__ __forceinline__ void dq_body(const AttnArgs& a, int qb, int h, int b,
     tv.store(smem + 2 * BLK * D, tid);
   }
   __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nkt;
-    if (more) {
-      tk.load(kb, a.k_ss, (kt + 1) * BLK, a.Sk, tid);
-      tv.load(vb, a.v_ss, (kt + 1) * BLK, a.Sk, tid);
+  auto sweep = [&](auto wm) {
+    constexpr bool WM = decltype(wm)::value;
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nkt;
+      if (more) {
+        tk.load(kb, a.k_ss, (kt + 1) * BLK, a.Sk, tid);
+        tv.load(vb, a.v_ss, (kt + 1) * BLK, a.Sk, tid);
+      }
+      const bf16_t* Kt = smem + cur * BLK * D;
+      const bf16_t* Vt = smem + (2 + cur) * BLK * D;
+      const int kbase = kt * BLK;
+      if constexpr (WM) {
+        const bool need_mask = kbase + BLK > a.Sk || qrow0 + 16 > a.Sq ||
+                               (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
+        if (need_mask) dq_tile<true>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow, lane);
+        else dq_tile<false>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow, lane);
+      } else {
+        dq_tile<false>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow, lane);
+      }
+      if (more) {
+        tk.store(smem + (cur ^ 1) * BLK * D, tid);
+        tv.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
+      }
+      __syncthreads();
     }
-    const bf16_t* Kt = smem + cur * BLK * D;
-    const bf16_t* Vt = smem + (2 + cur) * BLK * D;
-    const int kbase = kt * BLK;
-    const bool need_mask = kbase + BLK > a.Sk || qrow0 + 16 > a.Sq ||
-                           (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
-    if (need_mask) dq_tile<true>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow, lane);
-    else dq_tile<false>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow, lane);
-    if (more) {
-      tk.store(smem + (cur ^ 1) * BLK * D, tid);
-      tv.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
-    }
-    __syncthreads();
-  }
+  };
+  if (wave_mask) sweep(std::true_type{});
+  else sweep(std::false_type{});
   if (qok) store_row_T(a.out + b * a.out_sb + (long)qrow * a.out_ss + h * a.out_sh, dq, a.scale, lane);
 }
 
