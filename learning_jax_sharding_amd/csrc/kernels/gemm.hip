@@ -672,13 +672,17 @@ gemm_dma_kernel(
     const int m0 = w.m0 * BM + wr * (BM / WM), n0 = w.n0 * BN + wc * (BN / WN);
     const int g = lane >> 4;
     if constexpr (AF32) {
-      if (p.acopy && w.b == 0 && w.n0 == 0) {
-        // this row block's bf16 A for the backward (re-read from L2 where the DMA just streamed
-        // it); drained before the epilogue so the counted waits below stay exact
+      // this row block's bf16 A for the backward (re-read from L2 where the DMA just streamed
+      // it), shared out by K-tile over the row block's batch x column items (item j copies
+      // K-tiles j, j + J, ...), so no item carries the whole row block's copy and the round's
+      // blocks finish together; drained before the epilogue so the counted waits below stay exact
+      const int J = p.batch * ntn, j = w.b * ntn + w.n0, nkt_all = p.K / BK;
+      if (p.acopy && j < nkt_all) {
         const float* A32 = reinterpret_cast<const float*>(p.A);
-        const int kc8 = p.K / 8;
-        for (int c = tid; c < BM * kc8; c += WM * WN * 64) {
-          const int row = c / kc8, k = (c - row * kc8) * 8, grow = w.m0 * BM + row;
+        const int my_kt = (nkt_all - j + J - 1) / J;
+        for (int c = tid; c < BM * 8 * my_kt; c += WM * WN * 64) {
+          const int t = c / (BM * 8), r8 = c - t * (BM * 8), row = r8 >> 3;
+          const int k = (j + t * J) * BK + (r8 & 7) * 8, grow = w.m0 * BM + row;
           if (grow < p.M) {
             const f32x4 lo = *reinterpret_cast<const f32x4*>(A32 + (long)grow * p.lda + k);
             const f32x4 hi = *reinterpret_cast<const f32x4*>(A32 + (long)grow * p.lda + k + 4);

@@ -600,7 +600,9 @@ class _FFBlock(torch.autograd.Function):
 # than the separate cast pass + bf16 GEMM at both bench shapes (QKV at 16384 tokens: cast + 2561
 # tile 52.7 us vs 59.6 us for the f32-A kernel alone, 75.6 with the bf16 copy the backward needs;
 # at 2048 tokens 19.4 vs 18.5 us; scripts/col_one.py) -- the f32 A image doubles the operand bytes
-# and LDS reads of the K-loop, which costs more than the cast pass it saves
+# and LDS reads of the K-loop, which costs more than the cast pass it saves.  Re-measured inside the
+# step with the bf16 copy shared out over the items: B=8 even (0.0898-0.0904 vs 0.0896-0.0899 ms),
+# B=16 and B=64 slower (profiles/PERF_NOTES.md)
 _CAST_ON_LOAD = os.environ.get("LJS_CAST_ON_LOAD", "0") == "1"
 
 # order of the FF block's backward GEMMs after dA (dX, dW_out, dW_in): which operands are still

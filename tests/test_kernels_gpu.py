@@ -771,7 +771,8 @@ def test_fp8_gemm_transposed_copy_splitk_bcast_and_fp8_mask(hip):
     assert torch.equal(m1, m2)
 
 
-@pytest.mark.parametrize("M,N,K,batch", [(2048, 512, 640, 3), (300, 136, 128, 1), (16384, 512, 640, 3)])
+@pytest.mark.parametrize("M,N,K,batch", [(2048, 512, 640, 3), (300, 136, 128, 1), (16384, 512, 640, 3),
+                                         (520, 256, 1024, 1), (384, 128, 640, 1)])
 def test_gemm_f32_a_cast_on_load(hip, M, N, K, batch):
     """The f32-A LDS-DMA GEMM (activation cast fused into the fragment reads) == cast pass + bf16
     GEMM bit for bit, and its bf16 copy of A == the cast pass's output."""
