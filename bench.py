@@ -62,7 +62,7 @@ def parse():
                    help="attention: the case6 block (headline); layer: attention + FF transformer layer")
     p.add_argument("--ff-dim", type=int, default=2560)
     p.add_argument("--layers", type=int, default=4, help="fsdp: number of dim x dim Dense layers")
-    p.add_argument("--graph-steps", type=int, default=2,
+    p.add_argument("--graph-steps", type=int, default=8,
                    help="training steps per captured HIP graph (the timed K steps replay K / G graphs of G "
                         "complete steps each: one graph launch per G steps; K %% G steps run one by one). "
                         "Every step still runs all its kernels - forward, backward, gradient all-reduce, "
