@@ -294,6 +294,9 @@ _DW_SMALL_TILE = int(os.environ.get("LJS_DW_SMALL_TILE", "12884"))
 # weight of the slab traffic (written by the GEMM, summed by the combine or the fused Adam) in
 # the split-count cost model (tuning knob)
 _DW_TRAFFIC_W = float(os.environ.get("LJS_DW_TRAFFIC_W", "1"))
+# weight-grad tile above 4096 tokens: 1282 (cost-model split count) or, as an A/B switch, 644 /
+# 12884 with one round of slabs
+_DW_BIG_TILE = int(os.environ.get("LJS_DW_BIG_TILE", "1282"))
 
 
 def slab_count(nkt: int, S: int) -> int:
@@ -323,6 +326,17 @@ def pick_dw_slabs(K: int, N: int, T: int):
         return 1282, pick_splitk_dma(K, N, T, 1), False
     if T > 4096 and not _DW_SLAB_MODE:
         return 1282, pick_splitk_dma(K, N, T, 1), False
+    if T > 4096 and _DW_BIG_TILE in (644, 12884):
+        # (A/B: fewer, longer slabs -- 64x64 tiles at 2 blocks/CU or 8-wave 128x128 at 1 block/CU,
+        # split count filling one round of resident blocks)
+        nkt = T // 64
+        bm = 64 if _DW_BIG_TILE == 644 else 128
+        tiles = -(-K // bm) * -(-N // bm)
+        slots = (2 if _DW_BIG_TILE == 644 else 1) * _cus()
+        S = max(1, min(nkt, slots // max(1, tiles)))
+        while S > 1 and slab_count(nkt, S) != S:
+            S -= 1
+        return _DW_BIG_TILE, S, True
     if T > 4096:
         nkt, tiles, slots = T // 64, -(-K // 128) * -(-N // 128), 2 * _cus()
         best, best_cost = 1, None
