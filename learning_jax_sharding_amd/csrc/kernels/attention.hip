@@ -47,6 +47,7 @@ struct AttnArgs {
   float scale, scale_log2;
   int causal, q_offset;
   int prio_hi_half;  // 8-wave kernels: s_setprio 1 for waves 4-7 (LJS_ATTN_PRIO)
+  int flags32;       // attn_bwd_pair32_kernel's dQ blocks: 128 queries (dq32_body), else 64
 };
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -656,6 +657,197 @@ __device__ __forceinline__ void dkv_body(const AttnArgs& a, int kblk, int h, int
   }
 }
 
+// Long-key variant: each wave owns 32 keys (two 16-key halves j), so every Q / dO fragment read
+// from LDS feeds twice the MFMAs of dkv_tile (the 16-key tile re-read the 64-query operands once
+// per 16 keys: at S = 4096 the split backward was bound by those LDS reads).  P and dS of a
+// 32-query half are packed to bf16 as they are formed (register pressure), as in fused_tile.
+template <bool MASK>
+__device__ __forceinline__ void dkv32_tile(const AttnArgs& a, const bf16_t* Qt, const bf16_t* Ot, const float* lse_s,
+                                           const float* dl_s, const bf16x8 (&kr)[2][2], const bf16x8 (&vr)[2][2], f32x4 (&dk)[2][4],
+                                           f32x4 (&dv)[2][4], int q0, int key0, int lane) {
+  const int g = lane >> 4;
+  const f32x2 sc2 = {a.scale_log2, a.scale_log2};
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    u32x4 pbu[2], sbu[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 2 * s2 + tt;
+      const f32x4 lse = *reinterpret_cast<const f32x4*>(lse_s + 16 * t + 4 * g);
+      const f32x4 ndl = *reinterpret_cast<const f32x4*>(dl_s + 16 * t + 4 * g);  // -delta
+      const bf16x8 q0f = frag_rows(Qt, 16 * t, 0, lane), q1f = frag_rows(Qt, 16 * t, 1, lane);
+      const bf16x8 o0f = frag_rows(Ot, 16 * t, 0, lane), o1f = frag_rows(Ot, 16 * t, 1, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = ndl;
+        s = mfma16x16x32(q0f, kr[j][0], s);
+        s = mfma16x16x32(q1f, kr[j][1], s);
+        dp = mfma16x16x32(o0f, vr[j][0], dp);
+        dp = mfma16x16x32(o1f, vr[j][1], dp);
+        float pv[4], dsv[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - f32x2{lse[2 * h], lse[2 * h + 1]};
+          pv[2 * h] = fast_exp2(x[0]);
+          pv[2 * h + 1] = fast_exp2(x[1]);
+        }
+        if constexpr (MASK) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = q0 + 16 * t + 4 * g + r, key = key0 + 16 * j + (lane & 15);
+            const bool ok = q < a.Sq && key < a.Sk && !(a.causal && key > q + a.q_offset);
+            pv[r] = ok ? pv[r] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x2 d = f32x2{pv[2 * h], pv[2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+          dsv[2 * h] = d[0];
+          dsv[2 * h + 1] = d[1];
+        }
+        pbu[j][2 * tt] = pack_bf16x2(pv[0], pv[1]);
+        pbu[j][2 * tt + 1] = pack_bf16x2(pv[2], pv[3]);
+        sbu[j][2 * tt] = pack_bf16x2(dsv[0], dsv[1]);
+        sbu[j][2 * tt + 1] = pack_bf16x2(dsv[2], dsv[3]);
+      }
+    }
+    bf16x8 pb[2], sb[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      pb[j] = __builtin_bit_cast(bf16x8, pbu[j]);
+      sb[j] = __builtin_bit_cast(bf16x8, sbu[j]);
+    }
+    // dV^T += dO^T P ; dK^T += Q^T dS   (k = the 32 queries of this half)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 oa = frag_tr(Ot, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+      const bf16x8 qa = frag_tr(Qt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        dv[j][dt] = mfma16x16x32(oa, pb[j], dv[j][dt]);
+        dk[j][dt] = mfma16x16x32(qa, sb[j], dk[j][dt]);
+      }
+    }
+  }
+}
+
+// dK, dV for one 128-key block (4 waves x 32 keys), sweeping all query blocks.  The next query
+// block's Q / dO / O and lse arrive by LDS-DMA (no staging registers: with them the 32-key tile
+// ran out of VGPRs); delta = rowsum(dO o O) is formed from LDS once they land.
+// LDS: QO = [Q0 | Q1 | dO0 | dO1] (64 x D each), Os (64 x D), rowc[2][2][64] = [buf][lse, -delta]
+__device__ __forceinline__ void dkv32_body(const AttnArgs& a, int kblk, int h, int b, bf16_t* QO, bf16_t* Os,
+                                           float* rowc) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int key0 = kblk * (4 * 32) + wave * 32;
+  bf16x8 kr[2][2], vr[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = key0 + 16 * j + (lane & 15);
+    const bool kok = key < a.Sk;
+    const bf16_t* kp = a.k + b * a.k_sb + (long)key * a.k_ss + h * a.k_sh;
+    const bf16_t* vp = a.v + b * a.v_sb + (long)key * a.v_ss + h * a.v_sh;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kr[j][ks] = load_row_frag(kp, kok, ks, lane);
+      vr[j][ks] = load_row_frag(vp, kok, ks, lane);
+    }
+  }
+  const bf16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
+  const bf16_t* dob = a.dout + b * a.do_sb + h * a.do_sh;
+  const bf16_t* ob = a.o + b * a.o_sb + h * a.o_sh;
+  const float* lse = a.lse + ((long)b * a.H + h) * a.Sq;
+  const u32x4 rq = rsrc_u4(qb, 2 * ((long)(a.Sq - 1) * a.q_ss + D));
+  const u32x4 rdo = rsrc_u4(dob, 2 * ((long)(a.Sq - 1) * a.do_ss + D));
+  const u32x4 ro = rsrc_u4(ob, 2 * ((long)(a.Sq - 1) * a.o_ss + D));
+  const u32x4 rl = rsrc_u4(lse, 4L * a.Sq);
+  // pieces p = wave, wave + 4 of a 64-row tile: rows 8p .. 8p + 7, img16 swizzle on the source
+  auto issue = [&](int q0, int buf) {
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int pc = wave + 4 * pp, drow = 8 * pc + (lane >> 3);
+      const int dchunk = ((lane & 7) ^ (((drow >> 1) & 3) << 1)) * 8;
+      const int r = q0 + drow;
+      const bool ok = r < a.Sq;
+      dma_lds_x4(rq, ok ? (int)(((long)r * a.q_ss + dchunk) * 2) : 0x7ffffff0, QO + buf * BLK * D + pc * 512);
+      dma_lds_x4(rdo, ok ? (int)(((long)r * a.do_ss + dchunk) * 2) : 0x7ffffff0,
+                 QO + (2 + buf) * BLK * D + pc * 512);
+      dma_lds_x4(ro, ok ? (int)(((long)r * a.o_ss + dchunk) * 2) : 0x7ffffff0, Os + pc * 512);
+    }
+    if (wave == 0) dma_lds_x1(rl, q0 + lane < a.Sq ? (q0 + lane) * 4 : 0x7ffffff0, rowc + buf * 2 * BLK);
+  };
+  // after the DMA of `buf` landed for every wave: -delta of its 64 queries (4 threads per row)
+  auto finish = [&](int buf) {
+    const int row = tid >> 2, c = tid & 3;
+    float sacc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c16 = 2 * c + k;
+      const u32x4 o = *reinterpret_cast<const u32x4*>(Os + img16(row, c16));
+      const u32x4 d = *reinterpret_cast<const u32x4*>(QO + (2 + buf) * BLK * D + img16(row, c16));
+      sacc += dot_bf16x8(o, d);
+    }
+    sacc += __shfl_xor(sacc, 1, 64);
+    sacc += __shfl_xor(sacc, 2, 64);
+    if (c == 0) rowc[buf * 2 * BLK + BLK + row] = -sacc;
+  };
+  int qstart = 0;
+  if (a.causal) qstart = max(0, (kblk * 128 - a.q_offset) / BLK * BLK);
+  const int nqt = (a.Sq - qstart + BLK - 1) / BLK;  // every wave joins every barrier
+  const bool wave_mask = (a.Sq % BLK) != 0 || key0 + 32 > a.Sk || a.causal;
+  const bool active = key0 < a.Sk;
+
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dk[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  if (nqt > 0) issue(qstart, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nqt > 0) finish(0);
+  __syncthreads();
+  auto sweep = [&](auto wm) {
+    constexpr bool WM = decltype(wm)::value;
+    for (int it = 0; it < nqt; ++it) {
+      const int cur = it & 1;
+      const int q0 = qstart + it * BLK;
+      const bool more = it + 1 < nqt;
+      if (more) issue(q0 + BLK, cur ^ 1);
+      const float* lse_s = rowc + cur * 2 * BLK;
+      const bf16_t* Qt = QO + cur * BLK * D;
+      const bf16_t* Ot = QO + (2 + cur) * BLK * D;
+      if (active) {
+        if constexpr (WM) {
+          const bool need_mask = q0 + BLK > a.Sq || key0 + 32 > a.Sk || (a.causal && key0 + 31 > q0 + a.q_offset);
+          if (need_mask) dkv32_tile<true>(a, Qt, Ot, lse_s, lse_s + BLK, kr, vr, dk, dv, q0, key0, lane);
+          else dkv32_tile<false>(a, Qt, Ot, lse_s, lse_s + BLK, kr, vr, dk, dv, q0, key0, lane);
+        } else {
+          dkv32_tile<false>(a, Qt, Ot, lse_s, lse_s + BLK, kr, vr, dk, dv, q0, key0, lane);
+        }
+      }
+      // the next block's pieces landed (this wave's, then everyone's after the barrier), and
+      // every wave is done with block `cur` (its buffers are the next DMA's destination)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (more) finish(cur ^ 1);
+      __syncthreads();
+    }
+  };
+  if (wave_mask) sweep(std::true_type{});
+  else sweep(std::false_type{});
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = key0 + 16 * j + (lane & 15);
+    if (key < a.Sk) {
+      store_row_T(a.out + b * a.out_sb + (long)key * a.out_ss + h * a.out_sh, dk[j], a.scale, lane);
+      store_row_T(a.out2 + b * a.out2_sb + (long)key * a.out2_ss + h * a.out2_sh, dv[j], 1.f, lane);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * BLK * D];
   const Tile3 tl = tile3((a.Sk + BLK - 1) / BLK, a.H);
@@ -799,6 +991,154 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   dq_body(a, tl.x, tl.h, tl.b, smem, true);
 }
 
+// Long-key dQ variant: each wave owns 32 queries (two 16-query halves i), so every K / V
+// fragment read from LDS feeds twice the MFMAs of dq_tile.
+template <bool MASK>
+__device__ __forceinline__ void dq32_tile(const AttnArgs& a, const bf16_t* Kt, const bf16_t* Vt,
+                                          const bf16x8 (&qf)[2][2], const bf16x8 (&df)[2][2], const float (&lse_q)[2],
+                                          const float (&dl_q)[2], f32x4 (&dq)[2][4], int kbase, int qrow0, int lane) {
+  const int g = lane >> 4;
+  const f32x2 sc2 = {a.scale_log2, a.scale_log2};
+  u32x4 sbu[2][2];  // [i][s2]: dS of keys 32 s2 .. + 31 packed to bf16 (frag_acc layout)
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    const bf16x8 kf0 = frag_rows(Kt, 16 * jt, 0, lane), kf1 = frag_rows(Kt, 16 * jt, 1, lane);
+    const bf16x8 vf0 = frag_rows(Vt, 16 * jt, 0, lane), vf1 = frag_rows(Vt, 16 * jt, 1, lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{dl_q[i], dl_q[i], dl_q[i], dl_q[i]};
+      s = mfma16x16x32(kf0, qf[i][0], s);
+      s = mfma16x16x32(kf1, qf[i][1], s);
+      dp = mfma16x16x32(vf0, df[i][0], dp);
+      dp = mfma16x16x32(vf1, df[i][1], dp);
+      const f32x2 ls2 = {lse_q[i], lse_q[i]};
+      float pv[4], dsv[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - ls2;
+        pv[2 * h] = fast_exp2(x[0]);
+        pv[2 * h + 1] = fast_exp2(x[1]);
+      }
+      if constexpr (MASK) {
+        const int qrow = qrow0 + 16 * i + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kbase + 16 * jt + 4 * g + r;
+          const bool ok = qrow < a.Sq && key < a.Sk && !(a.causal && key > qrow + a.q_offset);
+          pv[r] = ok ? pv[r] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x2 d = f32x2{pv[2 * h], pv[2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+        dsv[2 * h] = d[0];
+        dsv[2 * h + 1] = d[1];
+      }
+      sbu[i][jt >> 1][2 * (jt & 1)] = pack_bf16x2(dsv[0], dsv[1]);
+      sbu[i][jt >> 1][2 * (jt & 1) + 1] = pack_bf16x2(dsv[2], dsv[3]);
+    }
+  }
+  // dQ^T += K^T dS^T   (k = keys)
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 ka = frag_tr(Kt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) dq[i][dt] = mfma16x16x32(ka, __builtin_bit_cast(bf16x8, sbu[i][s2]), dq[i][dt]);
+    }
+  }
+}
+
+// dQ for one 128-query block (4 waves x 32 queries), sweeping key blocks
+__device__ __forceinline__ void dq32_body(const AttnArgs& a, int qb, int h, int b, bf16_t* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qrow0 = qb * 128 + wave * 32;
+  bf16x8 qf[2][2], df[2][2];
+  float lse_q[2], dl_q[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int qrow = qrow0 + 16 * i + (lane & 15);
+    const bool qok = qrow < a.Sq;
+    const bf16_t* qp = a.q + b * a.q_sb + (long)qrow * a.q_ss + h * a.q_sh;
+    const bf16_t* dop = a.dout + b * a.do_sb + (long)qrow * a.do_ss + h * a.do_sh;
+    const bf16_t* op = a.o + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
+    qf[i][0] = load_row_frag(qp, qok, 0, lane);
+    qf[i][1] = load_row_frag(qp, qok, 1, lane);
+    df[i][0] = load_row_frag(dop, qok, 0, lane);
+    df[i][1] = load_row_frag(dop, qok, 1, lane);
+    lse_q[i] = qok ? a.lse[((long)b * a.H + h) * a.Sq + qrow] : INFINITY;
+    float sacc = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const u32x4 x = __builtin_bit_cast(u32x4, load_row_frag(op, qok, ks, lane));
+      const u32x4 y = __builtin_bit_cast(u32x4, df[i][ks]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sacc = fmaf(__uint_as_float(x[k] << 16), __uint_as_float(y[k] << 16), sacc);
+        sacc = fmaf(__uint_as_float(x[k] & 0xffff0000u), __uint_as_float(y[k] & 0xffff0000u), sacc);
+      }
+    }
+    dl_q[i] = -row4_sum(sacc);  // delta, kept negated (it seeds the dP accumulators)
+  }
+  const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
+  const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
+  int kend = a.Sk;
+  if (a.causal) kend = min(a.Sk, a.q_offset + (qb + 1) * 128);
+  const int nkt = (kend + BLK - 1) / BLK;
+  f32x4 dq[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dq[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool wave_mask = (a.Sk % BLK) != 0 || qrow0 + 32 > a.Sq || a.causal;
+  const bool active = qrow0 < a.Sq;
+  TileRegs tk, tv;
+  if (nkt > 0) {
+    tk.load(kb, a.k_ss, 0, a.Sk, tid);
+    tv.load(vb, a.v_ss, 0, a.Sk, tid);
+    tk.store(smem, tid);
+    tv.store(smem + 2 * BLK * D, tid);
+  }
+  __syncthreads();
+  auto sweep = [&](auto wm) {
+    constexpr bool WM = decltype(wm)::value;
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nkt;
+      if (more) {
+        tk.load(kb, a.k_ss, (kt + 1) * BLK, a.Sk, tid);
+        tv.load(vb, a.v_ss, (kt + 1) * BLK, a.Sk, tid);
+      }
+      const bf16_t* Kt = smem + cur * BLK * D;
+      const bf16_t* Vt = smem + (2 + cur) * BLK * D;
+      const int kbase = kt * BLK;
+      if (active) {
+        if constexpr (WM) {
+          const bool need_mask = kbase + BLK > a.Sk || qrow0 + 32 > a.Sq ||
+                                 (a.causal && kbase + BLK - 1 > qrow0 + a.q_offset);
+          if (need_mask) dq32_tile<true>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow0, lane);
+          else dq32_tile<false>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow0, lane);
+        } else {
+          dq32_tile<false>(a, Kt, Vt, qf, df, lse_q, dl_q, dq, kbase, qrow0, lane);
+        }
+      }
+      if (more) {
+        tk.store(smem + (cur ^ 1) * BLK * D, tid);
+        tv.store(smem + (2 + (cur ^ 1)) * BLK * D, tid);
+      }
+      __syncthreads();
+    }
+  };
+  if (wave_mask) sweep(std::true_type{});
+  else sweep(std::false_type{});
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int qrow = qrow0 + 16 * i + (lane & 15);
+    if (qrow < a.Sq) store_row_T(a.out + b * a.out_sb + (long)qrow * a.out_ss + h * a.out_sh, dq[i], a.scale, lane);
+  }
+}
+
 // dQ blocks and dK/dV blocks of the split backward in ONE launch (the dK/dV blocks form delta
 // themselves): at the reference shape (B = 8) the two kernels ran back to back as two half-full
 // grids of 256 four-wave blocks; here all 512 blocks are resident at once.  Block ids are dealt
@@ -814,6 +1154,25 @@ __global__ __launch_bounds__(256) void attn_bwd_pair_kernel(AttnArgs dq, AttnArg
   } else {
     const int u = t - ndq;
     dkv_body<true>(dkv, u % nk, (u / nk) % dkv.H, u / (nk * dkv.H), smem, dls);
+  }
+}
+
+// the same with 128-key dK/dV blocks (dkv32_body): long key ranges, where the 64-key blocks'
+// LDS reads of the staged query tiles bound the backward
+__global__ __launch_bounds__(256, 2) void attn_bwd_pair32_kernel(AttnArgs dq, AttnArgs dkv) {
+  __shared__ __attribute__((aligned(16))) bf16_t QO[4 * BLK * D];  // dQ blocks: their K/V ring
+  __shared__ __attribute__((aligned(16))) bf16_t Os[BLK * D];
+  __shared__ __attribute__((aligned(16))) float rowc[2 * 2 * BLK];
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int qbs = dq.flags32 ? 128 : BLK;  // dQ block: 128 queries (dq32_body) or 64 (dq_body)
+  const int nq = (dq.Sq + qbs - 1) / qbs, nk = (dkv.Sk + 127) / 128;
+  const int ndq = nq * dq.H * (gridDim.x / (nq + nk) / dq.H);
+  if (t < ndq) {
+    if (dq.flags32) dq32_body(dq, t % nq, (t / nq) % dq.H, t / (nq * dq.H), QO);
+    else dq_body(dq, t % nq, (t / nq) % dq.H, t / (nq * dq.H), QO, false);
+  } else {
+    const int u = t - ndq;
+    dkv32_body(dkv, u % nk, (u / nk) % dkv.H, u / (nk * dkv.H), QO, Os, rowc);
   }
 }
 
@@ -1099,6 +1458,29 @@ static int attn_pair() {
   return g_bwd_pair;
 }
 
+// 128-key dK/dV blocks in the split backward: LJS_ATTN_DKV32 = 1 always, 0 never, default: keys
+// above the fused kernel's range (FK)
+static int g_dkv32 = -2;  // -2 = read LJS_ATTN_DKV32 at the next call
+LJS_API void ljs_attn_set_dkv32(int v) { g_dkv32 = v; }
+static bool attn_dkv32(int Sk) {
+  if (g_dkv32 == -2) {
+    const char* e = getenv("LJS_ATTN_DKV32");
+    g_dkv32 = e ? atoi(e) : -1;
+  }
+  return g_dkv32 == 1 || (g_dkv32 == -1 && Sk > 256);
+}
+
+// 128-query dQ blocks beside the 128-key dK/dV blocks (LJS_ATTN_DQ32=0: 64-query dQ blocks)
+static int g_dq32 = -2;
+LJS_API void ljs_attn_set_dq32(int v) { g_dq32 = v; }
+static int attn_dq32() {
+  if (g_dq32 == -2) {
+    const char* e = getenv("LJS_ATTN_DQ32");
+    g_dq32 = e ? atoi(e) : 1;
+  }
+  return g_dq32 != 0;
+}
+
 static int attn_prio() {
   static int v = -1;
   if (v < 0) {
@@ -1222,6 +1604,13 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
   b.out = (bf16_t*)dk; b.out_sb = dks[0]; b.out_ss = dks[1]; b.out_sh = dks[2];
   b.out2 = (bf16_t*)dv; b.out2_sb = dvs[0]; b.out2_ss = dvs[1]; b.out2_sh = dvs[2];
   const long nq = (Sq + BLK - 1) / BLK, nk = (Sk + BLK - 1) / BLK;
+  if (attn_dkv32(Sk) && (nq + (Sk + 127) / 128) * H * B < (1L << 30)) {
+    const long nk128 = (Sk + 127) / 128;
+    c.flags32 = attn_dq32();
+    const long nqb = c.flags32 ? (Sq + 127) / 128 : nq;
+    hipLaunchKernelGGL(attn_bwd_pair32_kernel, dim3((unsigned)((nqb + nk128) * H * B)), dim3(256), 0, stream, c, b);
+    return (int)hipGetLastError();
+  }
   if (attn_pair() && (nq + nk) * H * B < (1L << 30)) {
     // one launch: dQ blocks and dK/dV blocks (which form delta themselves) side by side
     hipLaunchKernelGGL(attn_bwd_pair_kernel, dim3((unsigned)((nq + nk) * H * B)), dim3(256), 0, stream, c, b);

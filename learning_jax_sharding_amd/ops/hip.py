@@ -99,6 +99,23 @@ def set_attention_bwd_fused(enabled: Optional[bool]):
     fn(2 if enabled is None else (1 if enabled else 0))
 
 
+def set_attention_dkv32(enabled: Optional[bool]):
+    """Split attention backward with 128-key dK/dV blocks (4 waves x 32 keys): True always,
+    False never (64-key blocks), None the default (keys beyond the fused kernel's 256)."""
+    fn = lib().ljs_attn_set_dkv32
+    fn.argtypes = [c_int]
+    fn.restype = None
+    fn(-1 if enabled is None else (1 if enabled else 0))
+
+
+def set_attention_dq32(enabled: Optional[bool]):
+    """With 128-key dK/dV blocks: 128-query dQ blocks (True / None, the default) or 64 (False)."""
+    fn = lib().ljs_attn_set_dq32
+    fn.argtypes = [c_int]
+    fn.restype = None
+    fn(1 if enabled is None or enabled else 0)
+
+
 def set_attention_bwd_pair(enabled: Optional[bool]):
     """Split attention backward as ONE launch of dQ and dK/dV blocks (True, the default via
     None) or as two launches ordered by the dQ kernel's delta output (False)."""

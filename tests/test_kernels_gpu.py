@@ -215,6 +215,41 @@ def test_attention_bwd_pair_matches_two_launches(hip, B, Sq, Sk, H, causal, q_of
         torch.testing.assert_close(a.float(), b_.float(), rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("B,Sq,Sk,H,causal,q_offset", [(1, 1024, 1024, 2, False, 0), (2, 320, 320, 3, True, 0),
+                                                     (1, 200, 700, 2, True, 500), (2, 192, 130, 2, False, 0),
+                                                     (1, 64, 100, 2, True, 0)])
+@pytest.mark.parametrize("dq32", [True, False])
+def test_attention_bwd_dkv32_matches_dkv16(hip, B, Sq, Sk, H, causal, q_offset, dq32):
+    """Split backward with 128-key dK/dV blocks (32 keys per wave, LDS-DMA query tiles) and 64- or
+    128-query dQ blocks (32 queries per wave) == the 64-key / 64-query blocks: dQ bit-exact (same
+    per-query sums in the same order), dK/dV up to delta's f32 summation order; and against
+    autograd of the f32 reference."""
+    D = 64
+    scale = D ** -0.5
+    q, do = _rand(B, Sq, H, D, seed=11), _rand(B, Sq, H, D, seed=12)
+    k, v = _rand(B, Sk, H, D, seed=13), _rand(B, Sk, H, D, seed=14)
+    o, lse = hip.attn_fwd_lse(q, k, v, scale, causal, q_offset)
+    hip.set_attention_bwd_fused(False)
+    hip.set_attention_dq32(dq32)
+    outs = {}
+    try:
+        for d32 in (True, False):
+            hip.set_attention_dkv32(d32)
+            outs[d32] = hip.attn_bwd_block(q, k, v, o, do, lse, scale, causal, q_offset)
+    finally:
+        hip.set_attention_dkv32(None)
+        hip.set_attention_dq32(None)
+        hip.set_attention_bwd_fused(None)
+    assert torch.equal(outs[True][0], outs[False][0])
+    for a, b_ in zip(outs[True][1:], outs[False][1:]):
+        torch.testing.assert_close(a.float(), b_.float(), rtol=1e-2, atol=1e-2)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    (_attn_ref(qr, kr, vr, scale, causal, q_offset).float() * do.float()).sum().backward()
+    for a, b_, name in zip(outs[True], (qr.grad, kr.grad, vr.grad), ("dq", "dk", "dv")):
+        err = (a.float() - b_).abs().max().item()
+        assert err <= 3e-2 * max(1.0, b_.abs().max().item()), (name, err)
+
+
 def test_attention_online_softmax_rescale(hip):
     """Force a running-max jump at a late key tile (exercises the rescale branch)."""
     B, S, H, D = 1, 256, 1, 64
