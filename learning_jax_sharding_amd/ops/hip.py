@@ -100,8 +100,8 @@ def set_attention_bwd_fused(enabled: Optional[bool]):
 
 
 def set_attention_dkv32(enabled: Optional[bool]):
-    """Split attention backward with 128-key dK/dV blocks (4 waves x 32 keys): True always,
-    False never (64-key blocks), None the default (keys beyond the fused kernel's 256)."""
+    """Split attention backward with 128-key dK/dV blocks (4 waves x 32 keys): True / None (the
+    default) or False (64-key blocks)."""
     fn = lib().ljs_attn_set_dkv32
     fn.argtypes = [c_int]
     fn.restype = None

@@ -202,6 +202,7 @@ def test_attention_bwd_pair_matches_two_launches(hip, B, Sq, Sk, H, causal, q_of
     k, v = _rand(B, Sk, H, D, seed=3), _rand(B, Sk, H, D, seed=4)
     o, lse = hip.attn_fwd_lse(q, k, v, D ** -0.5, causal, q_offset)
     hip.set_attention_bwd_fused(False)
+    hip.set_attention_dkv32(False)  # the 64-row blocks (128-row ones: test_attention_bwd_dkv32_*)
     outs = {}
     try:
         for pair in (True, False):
@@ -209,6 +210,7 @@ def test_attention_bwd_pair_matches_two_launches(hip, B, Sq, Sk, H, causal, q_of
             outs[pair] = hip.attn_bwd_block(q, k, v, o, do, lse, D ** -0.5, causal, q_offset)
     finally:
         hip.set_attention_bwd_pair(None)
+        hip.set_attention_dkv32(None)
         hip.set_attention_bwd_fused(None)
     assert torch.equal(outs[True][0], outs[False][0])
     for a, b_ in zip(outs[True][1:], outs[False][1:]):
