@@ -202,11 +202,14 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
       ps2 += pv;
     }
   const float psum = ps2[0] + ps2[1];
+  // no lane's running max moved (the usual case after the first key tiles): alpha is exactly 1
+  // (or the row is still all-masked with O = 0), so the O rescale is skipped wave-uniformly
+  const bool rescale = !__all(m_new == st.m);
   st.l = st.l * alpha + psum;
   st.m = m_new;
   const f32x2 al2 = {alpha, alpha};
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
+  for (int dt = 0; dt < 4 && rescale; ++dt) {
     const f32x2 lo = f32x2{st.o[dt][0], st.o[dt][1]} * al2, hi = f32x2{st.o[dt][2], st.o[dt][3]} * al2;
     st.o[dt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
   }
