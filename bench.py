@@ -68,6 +68,12 @@ def parse():
                         "Every step still runs all its kernels - forward, backward, gradient all-reduce, "
                         "Adam - on the previous step's state; only the host launch is amortised")
     p.add_argument("--fp8", action="store_true", help="layer / ff: MX-fp8 FF GEMMs (CDNA4 block-scaled MFMA)")
+    p.add_argument("--loss", default="sum", choices=["sum", "mse"],
+                   help="sum: y.sum() as in case6_attention.py:211 (constant cotangent); mse: mean((y - target)^2) "
+                        "against a synthetic target (a general, data-dependent cotangent)")
+    p.add_argument("--comm-timeout", type=float, default=None,
+                   help="seconds a phase may run before the watchdog aborts the communicators and exits "
+                        "(default LJS_COMM_TIMEOUT_S or 300)")
     return p.parse_args()
 
 
@@ -78,20 +84,75 @@ def _free_port() -> int:
         return sk.getsockname()[1]
 
 
+def _visible_gpu_count() -> int:
+    """GPUs this job may use, counted WITHOUT initialising HIP in the launcher process: the KFD
+    topology's GPU nodes (``gpu_id`` != 0), narrowed by ROCR/HIP/CUDA_VISIBLE_DEVICES.  Each rank
+    re-checks its own device with torch before any GPU work (``_assert_rank_device``)."""
+    import glob
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+        try:
+            with open(f) as fh:
+                n += int(fh.read().strip() or "0") != 0
+        except (OSError, ValueError):
+            pass
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""])) if v.strip() else 0
+    return n
+
+
 def _launch_ranks(n: int) -> int:
-    """Run this benchmark as n rank processes (one per GPU) and return their exit status.
-    Called before anything initialises the GPU (device_count() does not, on ROCm torch)."""
+    """Run this benchmark as n rank processes (one per GPU) and return their exit status.  This
+    process never touches the GPU (no torch import): it counts devices from sysfs, starts
+    ``torch.distributed.run`` as a CHILD (no exec) and forwards SIGTERM / SIGINT to it."""
+    import signal
     import subprocess
-    import torch
     platform = os.environ.get("LJS_PLATFORM", "").lower()
     if platform != "cpu" and not os.environ.get("LJS_DIST_BACKEND"):
-        have = torch.cuda.device_count()
+        have = _visible_gpu_count()
         if have < n:
-            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}", file=sys.stderr)
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have} (KFD topology)", file=sys.stderr)
             return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd)
+    child = subprocess.Popen(cmd)
+
+    def fwd(sig, _frame):
+        try:
+            child.send_signal(sig)
+        except OSError:
+            pass
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, fwd)
+    return child.wait()
+
+
+HEAD_DIMS_GPU = (64,)  # head dims the HIP attention kernels implement (ops/hip.py attention)
+
+
+def check_args(args, on_gpu: bool) -> None:
+    """Reject configurations the GPU path does not implement BEFORE any GPU work."""
+    if on_gpu and args.model in ("attention", "layer") and args.dim_head not in HEAD_DIMS_GPU:
+        raise SystemExit(f"bench.py: --dim-head {args.dim_head} is not supported by the HIP attention kernels "
+                         f"(supported: {', '.join(map(str, HEAD_DIMS_GPU))})")
+    if args.model == "fsdp" and args.mesh not in ("dp",) and not args.mesh.endswith("x1"):
+        raise SystemExit("bench.py: --model fsdp shards weights over 'data' only; use --mesh dp or Nx1")
+    if args.loss == "mse" and args.mode != "train":
+        raise SystemExit("bench.py: --loss applies to --mode train")
+
+
+def _assert_rank_device(world: int) -> None:
+    """A GPU rank checks that its LOCAL_RANK names a visible device before using it."""
+    import torch
+    if os.environ.get("LJS_PLATFORM", "gpu").lower() == "cpu" or os.environ.get("LJS_DIST_BACKEND"):
+        return
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    have = torch.cuda.device_count()
+    if lr >= have:
+        raise SystemExit(f"bench.py: rank {os.environ.get('RANK')} has LOCAL_RANK {lr} but only {have} GPUs are "
+                         f"visible (world {world})")
 
 
 def main():
@@ -106,9 +167,12 @@ def main():
     if world > 1:
         os.environ.setdefault("LJS_PLATFORM", "gpu")
         os.environ.pop("LJS_NUM_DEVICES", None)
+        _assert_rank_device(world)
     else:
         os.environ.setdefault("LJS_NUM_DEVICES", "1")
     import torch
+    on_gpu = os.environ.get("LJS_PLATFORM", "").lower() != "cpu" and torch.cuda.is_available()
+    check_args(args, on_gpu)
     import learning_jax_sharding_amd as ljs
     from learning_jax_sharding_amd import nn, optim
     from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
@@ -124,8 +188,6 @@ def main():
         import torch.distributed as _dist
         assert _dist.is_initialized() and _dist.get_world_size() == world, "process group not initialised"
         assert n == world and ljs.local_device_count() == 1, (n, world)
-    if args.model == "fsdp" and args.mesh not in ("dp",) and not args.mesh.endswith("x1"):
-        raise SystemExit("bench.py: --model fsdp shards weights over 'data' only; use --mesh dp or Nx1")
     if args.mesh == "dp":
         mshape = (n, 1)
     elif args.mesh == "2d":
@@ -160,9 +222,17 @@ def main():
         state_sharding = nn.logical_to_mesh_sharding(nn.get_partition_spec(abstract), mesh, rules)
     state = ljs.jit(init_fn, out_shardings=state_sharding)(ljs.random.PRNGKey(1), x)
 
+    target = None
+    if args.loss == "mse":
+        # a synthetic regression target shaped (and sharded) like the block's output
+        target = ljs.random.normal(ljs.random.PRNGKey(2), (B, S, M), sharding=x_sharding)
+
     def train_step(state, x):
         def loss_fn(params):
-            return model.apply({"params": params}, x).sum()
+            y = model.apply({"params": params}, x)
+            if target is not None:
+                return ljs.ops.core.mse_loss(y, target)
+            return y.sum()
         grads = ljs.grad(loss_fn)(state.params)
         return state.apply_gradients(grads=grads)
 
@@ -213,18 +283,31 @@ def main():
         if cuda:
             torch.cuda.synchronize()
 
+    # failure detection: a daemon thread polls every RCCL communicator's async error and each
+    # phase's deadline; on an error or a hang it aborts the communicators, prints the phase and
+    # the partitions, and exits non-zero (comm/watchdog.py) instead of hanging in a synchronize
+    from learning_jax_sharding_amd.comm.backend import get_comm
+    wd = get_comm().watchdog(args.comm_timeout) if dist_on else None
+
+    def phase(name):
+        if wd is not None:
+            wd.phase(name)
+
     with mesh, nn.axis_rules(rules):
+        phase("capture + warmup")
         if multi is not None:
             # both graphs captured before the timed region, whatever W is
             run(2 * G)
             run(2)
         run(max(1, args.warmup))
         barrier_sync()
+        phase("timed steps")
         t0 = time.perf_counter()
         run(args.steps)
         th = time.perf_counter()  # host side done enqueuing (diagnostic: host- vs device-bound)
         barrier_sync()
         t1 = time.perf_counter()
+        phase("report")
     elapsed = t1 - t0
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if cuda else "cpu")
@@ -251,7 +334,6 @@ def main():
     n_gpus = world if world > 1 else (1 if cuda else 0)
     comm = "none"
     if dist_on:
-        from learning_jax_sharding_amd.comm.backend import get_comm
         c = get_comm()
         comm = dist.get_backend() + ("+native-rccl" if getattr(c, "_native", None) is not None else "")
     if rank == 0:
@@ -272,7 +354,8 @@ def main():
         rec = {
             "metric": METRIC if args.model == "attention" else f"step-time ms + TFLOPS/GPU, {args.model} train step",
             "value": round(tflops_total, 3),
-            "unit": "TFLOPS summed over all GPUs (matmul FLOPs of fwd+bwd); per GPU: tflops_per_gpu",
+            "unit": "TFLOPS, whole job (matmul FLOPs of fwd+bwd summed over the n_gpus GPUs; the per-GPU rate "
+                    "the metric names is tflops_per_gpu = value / n_gpus)",
             "n_gpus": n_gpus if cuda else n,
             "n_devices": n,
             "steps": args.steps,
@@ -289,11 +372,15 @@ def main():
             "config": {"model": model_desc,
                        "global_batch": B, "seq_len": S, "parallelism": par, "mode": args.mode,
                        "hip_graph": capture, "graph_segments": segs, "steps_per_graph": G, "mesh": list(mshape),
-                       "comm": comm, "grad_wire": os.environ.get("LJS_GRAD_COMM_DTYPE", "fp32")},
+                       "comm": comm, "grad_wire": os.environ.get("LJS_GRAD_COMM_DTYPE", "fp32"),
+                       "loss": "y.sum()" if args.loss == "sum" else "mean((y - target)^2)"},
         }
         print(json.dumps(rec), flush=True)
     if dist_on:
         dist.barrier()
+        if wd is not None:
+            wd.stop()
+        get_comm().close()          # ncclCommDestroy of the native communicators
         dist.destroy_process_group()
 
 

@@ -213,6 +213,15 @@ class LocalComm:
                 out[d] = torch.cat([chunks[s][perm[i]].to(dev) for s in g], concat_dim).contiguous()
         return out
 
+    def watchdog(self, timeout_s: Optional[float] = None):
+        from .watchdog import CommWatchdog
+        return CommWatchdog(self, timeout_s).start()
+
+    def close(self) -> None:
+        if self._native is not None:
+            self._native.close()
+            self._native = None
+
     def exchange(self, xs, transfers: Sequence[Transfer], out_meta: Dict[int, Tuple[tuple, torch.dtype, torch.device]],
                  accumulate: bool = False):
         out = {}
@@ -394,6 +403,17 @@ class DistComm:
             dist.all_to_all_single(recv.view(n, -1), send.view(n, -1), group=pg)
         # recv[k] came from sorted rank srt[k]; concatenate in member (tile) order
         return {self.me: _hip().from_rank_major(recv, concat_dim, [srt.index(d) for d in g])}
+
+    def watchdog(self, timeout_s: Optional[float] = None):
+        """A started :class:`~.watchdog.CommWatchdog` over this rank's communicators."""
+        from .watchdog import CommWatchdog
+        return CommWatchdog(self, timeout_s).start()
+
+    def close(self) -> None:
+        """Destroy the native RCCL communicators (the torch process groups are torch's)."""
+        if self._native is not None:
+            self._native.close()
+            self._native = None
 
     def exchange(self, xs, transfers, out_meta, accumulate=False):
         me = self.me

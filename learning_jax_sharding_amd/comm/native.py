@@ -207,10 +207,18 @@ class NativeRccl:
         self._check(rc, "all_to_all")
         return outs
 
+    def describe(self):
+        return [f"GPU group {list(g)}" for g in self._comms]
+
+    def abort(self) -> None:
+        for h in self._comms.values():
+            runtime().ljs_comm_abort(h)
+
     def close(self):
         for h in self._comms.values():
             runtime().ljs_comm_destroy(h)
         self._comms.clear()
+        self._world = None
 
 
 # ============================================================================ one process per GPU
@@ -245,6 +253,7 @@ class RankRccl:
         self.rank, self.world, self.device = rank, world, device
         self._world_h = self._init_world()
         self._parts: Dict[Tuple[Tuple[int, ...], ...], Optional[int]] = {}
+        self._log: Dict[int, Dict[str, Tuple[int, int]]] = {}
 
     def _init_world(self) -> int:
         import torch.distributed as dist
@@ -295,29 +304,79 @@ class RankRccl:
         return (_VP * 1)(torch.cuda.current_stream(t.device).cuda_stream)
 
     def all_reduce_(self, h: int, x: torch.Tensor) -> torch.Tensor:
+        self._note(h, "all_reduce", x.numel() * x.element_size())
         NativeRccl._check(runtime().ljs_comm_all_reduce(h, self._one(x), self._one(x), x.numel(), _DT[x.dtype], 0,
                                                         self._stream(x)), "all_reduce")
         return x
 
     def all_gather(self, h: int, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """out: [n * x.numel()] elements, rank-major."""
+        self._note(h, "all_gather", x.numel() * x.element_size())
         NativeRccl._check(runtime().ljs_comm_all_gather(h, self._one(x), self._one(out), x.numel(), _DT[x.dtype],
                                                         self._stream(x)), "all_gather")
         return out
 
     def reduce_scatter(self, h: int, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """x: n chunks of out.numel() elements (chunk r to rank r)."""
+        self._note(h, "reduce_scatter", x.numel() * x.element_size())
         NativeRccl._check(runtime().ljs_comm_reduce_scatter(h, self._one(x), self._one(out), out.numel(),
                                                             _DT[x.dtype], 0, self._stream(x)), "reduce_scatter")
         return out
 
     def all_to_all(self, h: int, send: torch.Tensor, recv: torch.Tensor, n: int) -> torch.Tensor:
+        self._note(h, "all_to_all", send.numel() * send.element_size())
         NativeRccl._check(runtime().ljs_comm_all_to_all(h, self._one(send), self._one(recv), send.numel() // n,
                                                         _DT[send.dtype], self._stream(send)), "all_to_all")
         return recv
 
+    def _handles(self):
+        hs = [self._world_h] if self._world_h else []
+        for v in self._parts.values():
+            if v and v not in hs:
+                hs.append(v)
+        return hs
+
+    def _name(self, h) -> str:
+        if h == self._world_h:
+            return f"world ({self.world} ranks)"
+        for groups, v in self._parts.items():
+            if v == h:
+                mine = next((g for g in groups if self.rank in g), ())
+                return f"partition {list(map(list, groups))} (this rank's group {list(mine)})"
+        return f"communicator {h:#x}"
+
     def check(self) -> None:
-        for h in [self._world_h] + [v for v in self._parts.values() if v]:
+        """Failure detection: raise on the first asynchronous RCCL error of any of
+        this rank's communicators (ncclCommGetAsyncError)."""
+        for h in self._handles():
             rc = runtime().ljs_comm_async_error(h)
             if rc:
-                raise RuntimeError(f"RCCL communicator failed: {runtime().ljs_comm_error_string(rc).decode()}")
+                raise RuntimeError(f"{self._name(h)}: {runtime().ljs_comm_error_string(rc).decode()}")
+
+    def describe(self):
+        """One line per communicator: its partition and the collectives issued on it (kinds,
+        counts, bytes per call) - what a hang diagnosis prints (comm/watchdog.py)."""
+        out = []
+        for h in self._handles():
+            ops = self._log.get(h, {})
+            ops_s = ", ".join(f"{k} x{n} ({b / 1e6:.3g} MB/call)" for k, (n, b) in sorted(ops.items())) or "idle"
+            out.append(f"{self._name(h)}: {ops_s}")
+        return out
+
+    def abort(self) -> None:
+        """ncclCommAbort on every communicator (RCCL kernels waiting on a peer return)."""
+        for h in self._handles():
+            runtime().ljs_comm_abort(h)
+
+    def close(self) -> None:
+        """Destroy the partition communicators, then the world one (ncclCommDestroy)."""
+        for h in self._handles()[::-1]:
+            runtime().ljs_comm_destroy(h)
+        self._parts.clear()
+        self._world_h = None
+        self._log.clear()
+
+    def _note(self, h, kind: str, nbytes: int) -> None:
+        ops = self._log.setdefault(h, {})
+        n, b = ops.get(kind, (0, 0))
+        ops[kind] = (n + 1, max(b, nbytes))

@@ -1,0 +1,119 @@
+"""Failure detection for one-process-per-GPU jobs (``ncclCommGetAsyncError`` and a
+timeout on collectives).
+
+The reference's collectives are XLA's in-process CPU ones and never fail
+(``case6_attention.py:212-214`` relies on the implicit gradient all-reduce).  Over RCCL a lost
+or wedged peer leaves every other rank blocked inside a collective - and, with the training
+step captured into a HIP graph, blocked in ``torch.cuda.synchronize()`` with no Python running.
+:class:`CommWatchdog` is a daemon thread that watches the job while the main thread blocks:
+
+* every ``poll_s`` it asks each native RCCL communicator for its asynchronous error
+  (``RankRccl.check``, i.e. ``ncclCommGetAsyncError``);
+* the main thread names what it is doing with :meth:`phase` (``"warmup"``, ``"timed steps"``,
+  ...); a phase that runs longer than ``timeout_s`` is a hang.
+
+On an error or a hang the watchdog aborts every communicator (``ncclCommAbort`` makes RCCL
+kernels spinning on a dead peer return), prints the phase, each communicator's partition and
+the collectives issued on it, and ends the process with exit code :data:`EXIT_CODE` - so a
+launcher (torchrun) sees a failed rank within the deadline instead of a job that hangs until
+someone kills it.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
+from typing import Callable, Optional
+
+__all__ = ["CommWatchdog", "EXIT_CODE", "default_timeout"]
+
+EXIT_CODE = 75
+
+
+def default_timeout() -> float:
+    """``LJS_COMM_TIMEOUT_S`` (default 300 s: the first capture of a step compiles nothing, but
+    the first RCCL call of a fresh node can take tens of seconds to set up its rings)."""
+    return float(os.environ.get("LJS_COMM_TIMEOUT_S", "300"))
+
+
+class CommWatchdog:
+    def __init__(self, comm=None, timeout_s: Optional[float] = None, poll_s: float = 0.1,
+                 exit_fn: Optional[Callable[[int], None]] = None, grace_s: float = 2.0):
+        """``comm``: the collective backend (``comm.backend.DistComm``) whose native communicators
+        are polled; None polls nothing and enforces only the phase deadline."""
+        self.comm = comm
+        self.timeout_s = default_timeout() if timeout_s is None else float(timeout_s)
+        self.poll_s = float(poll_s)
+        self.grace_s = float(grace_s)
+        self._exit = exit_fn or os._exit
+        self._phase = "startup"
+        self._t0 = time.monotonic()
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self.failed: Optional[str] = None
+
+    # ------------------------------------------------------------------ main-thread API
+    def start(self) -> "CommWatchdog":
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._run, name="ljs-comm-watchdog", daemon=True)
+            self._thread.start()
+        return self
+
+    def phase(self, name: str) -> None:
+        """Enter a new phase: its deadline starts now."""
+        self._phase, self._t0 = name, time.monotonic()
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thread is not None and self._thread is not threading.current_thread():
+            self._thread.join(timeout=5 * self.poll_s + 1.0)
+        self._thread = None
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+        return False
+
+    # ------------------------------------------------------------------ watcher thread
+    def _native(self):
+        return getattr(self.comm, "_native", None) if self.comm is not None else None
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.poll_s):
+            reason = None
+            nat = self._native()
+            if nat is not None:
+                try:
+                    nat.check()
+                except Exception as e:  # an asynchronous RCCL error on some communicator
+                    reason = f"asynchronous RCCL error: {e}"
+            if reason is None and time.monotonic() - self._t0 > self.timeout_s:
+                reason = f"phase exceeded its {self.timeout_s:g} s deadline (hang: a peer rank lost or wedged)"
+            if reason is not None:
+                self._fail(reason)
+                return
+
+    def _fail(self, reason: str) -> None:
+        self.failed = reason
+        rank = os.environ.get("RANK", "?")
+        lines = [f"[ljs watchdog] rank {rank}: {reason}",
+                 f"[ljs watchdog] phase: {self._phase!r}, {time.monotonic() - self._t0:.1f} s in"]
+        nat = self._native()
+        if nat is not None:
+            for desc in nat.describe():
+                lines.append(f"[ljs watchdog]   {desc}")
+            try:
+                nat.abort()
+                lines.append("[ljs watchdog] every RCCL communicator aborted (ncclCommAbort)")
+            except Exception as e:  # pragma: no cover - abort itself failing
+                lines.append(f"[ljs watchdog] abort failed: {e}")
+        else:
+            lines.append("[ljs watchdog] no native RCCL communicators (torch process groups only)")
+        print("\n".join(lines), file=sys.stderr, flush=True)
+        # give a main thread released by the abort a moment to unwind, then end the process:
+        # it may still be blocked in a device synchronize that never returns
+        time.sleep(self.grace_s)
+        self._exit(EXIT_CODE)

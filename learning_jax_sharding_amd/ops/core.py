@@ -36,7 +36,7 @@ from . import kernels as K
 __all__ = [
     "binary", "unary", "convert", "reshape", "transpose", "reduce_sum", "reduce_mean", "reduce_max",
     "getitem", "dot_general", "dot", "matmul", "einsum", "softmax", "dot_product_attention", "dense",
-    "with_sharding_constraint", "asarray_like", "broadcast_to", "where", "concatenate",
+    "with_sharding_constraint", "asarray_like", "broadcast_to", "where", "concatenate", "mse_loss",
 ]
 
 
@@ -387,6 +387,34 @@ def reduce_mean(x: ShardedArray, axis=None, keepdims=False) -> ShardedArray:
     n = int(np.prod([x.shape[a] for a in axes])) if axes else 1
     s = reduce_sum(x, axes, keepdims)
     return binary("div", s, float(n))
+
+
+def mse_loss(y: ShardedArray, target: ShardedArray) -> ShardedArray:
+    """``mean((y - target)^2)`` over every element, an f32 scalar (a target-based training loss
+    with a general, data-dependent cotangent - unlike ``y.sum()`` of ``case6_attention.py:211``).
+
+    Per shard one fused kernel computes the partial sum and, under ``grad``, dY in the same pass
+    (``ops.hip._MSELoss``).  Partial sums of a sharded ``y`` are all-reduced lazily (only if the
+    value is read); ``grad`` seeds them directly, as for :func:`reduce_sum`."""
+    if tuple(target.shape) != tuple(y.shape):
+        raise ValueError(f"mse_loss: target shape {target.shape} != prediction shape {y.shape}")
+    t = reshard_tile(target, y.tile, note="mse.target") if target.tile != y.tile else target
+    scale = 1.0 / max(1, y.size)
+    loc = {d: K.mse_loss(y.local[d], t.local[d], scale) for d in y.local}
+    sharded = [a for a in range(y.ndim) if y.tile.tile_shape[a] > 1]
+    groups = y.tile.groups_along(sharded) if sharded else None
+    _plan.record("mse_loss", shards=len(groups[0]) if groups else 1)
+    tile = y.tile.project([])
+    sh = sharding_from_tile(tile, like=[y.sharding])
+    if groups is None:
+        return ShardedArray((), torch.float32, sh, loc)
+    pre = loc
+
+    def thunk(pre=pre, groups=groups):
+        return C.all_reduce(pre, groups, note="reduce")
+    res = ShardedArray((), torch.float32, sh, LazyLocal(thunk) if _LAZY_SCALAR_SUMS else thunk())
+    res._sum_partials = (pre, len(groups[0]))
+    return res
 
 
 def reduce_max(x: ShardedArray, axis=None, keepdims=False) -> ShardedArray:

@@ -57,6 +57,7 @@ _SIGS = {
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
     "ljs_adam_multi": [_LP, c_int, c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float,
                        c_void_p],
+    "ljs_mse_loss": [c_void_p, c_void_p, c_int, c_long, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_rng_fill": [c_void_p, c_int, c_int, _LP, _LP, _LP, c_uint, c_uint, c_int, c_float, c_float, c_float,
                      c_float, c_void_p],
 }
@@ -677,6 +678,43 @@ def sum_all(t: torch.Tensor, acc_dtype: torch.dtype) -> torch.Tensor:
     if t.dtype not in (torch.float32, torch.bfloat16):
         return t.sum(dtype=acc_dtype)
     return _SumAll.apply(t, acc_dtype)
+
+
+class _MSELoss(torch.autograd.Function):
+    """scale * sum((y - t)^2) of one shard (bf16 y, f32 / bf16 t).  When y needs a gradient the
+    SAME kernel pass writes dY = bf16(2 * scale * (y - t)) (csrc/kernels/loss.hip): the loss's
+    backward is then free for the constant seed grad() feeds it, a scalar multiply otherwise."""
+
+    @staticmethod
+    def forward(ctx, y, t, scale):
+        want_dy = ctx.needs_input_grad[0]
+        y, t = y.contiguous(), t.contiguous()
+        out = torch.empty((), dtype=torch.float32, device=y.device)
+        dy = torch.empty_like(y) if want_dy else None
+        ws = _workspace(y.device, "mse", (1024 + 33) * 4)
+        rc = lib().ljs_mse_loss(_p(y), _p(t), int(t.dtype == torch.bfloat16), y.numel(), float(scale), _p(dy),
+                                _p(out), _p(ws), _stream(y))
+        _ck(rc, "mse_loss")
+        ctx.save_for_backward(dy)
+        ctx.t_dtype = t.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        dy, = ctx.saved_tensors
+        if dy is None:
+            return None, None, None
+        gy = dy if seed_constant(g) == 1.0 else (dy.float() * g.float()).to(dy.dtype)
+        gt = (-gy).to(ctx.t_dtype) if ctx.needs_input_grad[1] else None
+        return gy, gt, None
+
+
+def mse_loss(y: torch.Tensor, t: torch.Tensor, scale: float) -> torch.Tensor:
+    ok = (y.dtype == torch.bfloat16 and t.dtype in (torch.float32, torch.bfloat16) and y.shape == t.shape
+          and y.data_ptr() % 16 == 0 and t.data_ptr() % 16 == 0)
+    if not ok:
+        return ((y.float() - t.float()) ** 2).sum() * scale
+    return _MSELoss.apply(y, t, scale)
 
 
 def colsum(t2d: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:

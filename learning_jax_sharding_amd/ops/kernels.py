@@ -49,6 +49,13 @@ def reduce_sum(t: torch.Tensor, axes: Sequence[int], keepdim: bool, acc_dtype: t
     return t.sum(dim=tuple(axes), keepdim=keepdim, dtype=acc_dtype)
 
 
+def mse_loss(y: torch.Tensor, t: torch.Tensor, scale: float) -> torch.Tensor:
+    """``scale * sum((y - t)^2)`` of one shard in f32 (fused HIP pass with its gradient on GPU)."""
+    if use_hip(y):
+        return _hip().mse_loss(y, t, scale)
+    return ((y.float() - t.float()) ** 2).sum() * scale
+
+
 # ----------------------------------------------------------------------------- matmuls
 def _to_bmk(a: torch.Tensor, batch, free, contract):
     perm = list(batch) + list(free) + list(contract)

@@ -66,6 +66,13 @@ def _is_relu_out(t: torch.Tensor) -> bool:
     return _lookup(_RELU_OUT, t) is not None
 
 
+def _relu_node(x: torch.Tensor) -> bool:
+    """Whether ``x`` is an output of a ReLU :class:`_Linear` in the autograd graph (its grad_fn
+    is that Function's backward node, whose ctx carries ``meta`` with relu=True)."""
+    meta = getattr(x.grad_fn, "meta", None) if x.grad_fn is not None else None
+    return bool(meta is not None and len(meta) > 5 and meta[5])
+
+
 def _premasked_by(dy: torch.Tensor, y: torch.Tensor) -> bool:
     ent = _lookup(_PREMASKED, dy)
     return ent is not None and ent[2] == y.data_ptr() and dy.is_contiguous()
@@ -315,8 +322,10 @@ class _Linear(torch.autograd.Function):
         if relu and od == torch.bfloat16:
             for y in ys:
                 _register(_RELU_OUT, y)
-        # this dense's input is a ReLU output: its dX GEMM can apply that ReLU's backward mask
-        ctx.premask = bool(xb.dtype == torch.bfloat16 and K % 8 == 0 and _is_relu_out(xb))
+        # this dense's input is a ReLU output: its dX GEMM can apply that ReLU's backward mask.
+        # Keyed on autograd identity as well as storage: x must come straight out of a ReLU
+        # dense's backward node (a .detach()ed copy shares the storage but not the graph edge)
+        ctx.premask = bool(xb.dtype == torch.bfloat16 and K % 8 == 0 and _is_relu_out(xb) and _relu_node(x))
         ctx.has_res = res is not None
         ctx.save_for_backward(xb, b, *ws, *(ys if relu else []))
         ctx.meta = (lead, K, M, N, nw, relu, x.dtype, b is not None)

@@ -172,7 +172,9 @@ def initialize_distributed(backend: Optional[str] = None) -> None:
         # tests, which RCCL does not allow)
         backend = os.environ.get("LJS_DIST_BACKEND") or ("nccl" if platform == "gpu" else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    kwargs = {}
+    import datetime
+    # torch's own collectives (barriers, gloo fallbacks) give up after the job's comm timeout too
+    kwargs = {"timeout": datetime.timedelta(seconds=float(os.environ.get("LJS_COMM_TIMEOUT_S", "300")))}
     if platform == "gpu":
         torch.cuda.set_device(_local_gpu())
         if backend == "nccl":

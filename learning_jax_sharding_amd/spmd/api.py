@@ -83,6 +83,14 @@ class _Captured:
         self.aliased = aliased      # per leaf: the caller's own buffers (read-only in the graph)
 
 
+def _force_lazy(tree):
+    """Materialise every pending :class:`LazyLocal` among ``tree``'s arrays (returns ``tree``)."""
+    for l in T.tree_leaves(tree, is_leaf=_leaf_is_array):
+        if isinstance(l, ShardedArray) and isinstance(l.local, LazyLocal) and l.local.pending:
+            l.local._force()
+    return tree
+
+
 class Jitted:
     def __init__(self, fun: Callable, in_shardings=None, out_shardings=None, static_argnums=(),
                  donate_argnums=(), capture: Optional[bool] = None, warmup_calls: int = 1):
@@ -221,7 +229,9 @@ class Jitted:
         # one HIP graph per stretch between cross-process collectives (spmd/graphs.py)
         from .graphs import SegmentedGraph
         g = SegmentedGraph()
-        out, _ = g.capture(lambda: self._run(tuple(full), {}))
+        # lazy outputs (an unread loss, uncombined weight gradients) are forced INSIDE the
+        # capture: a thunk run after it would be eager, cached, and stale on every later replay
+        out = g.capture(lambda: _force_lazy(self._run(tuple(full), {})[0]))
         cap = _Captured(g, in_leaves, out, aliased)
         self._graphs[sig] = cap
         return self._replay(cap, args, sig)
@@ -480,7 +490,12 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
                         loc = LazyLocal(lambda d0=d0, g0=g0, mat=mat: (mat(), {d0: g0.detach()})[1])
                         loc.slabs = {d0: desc}
                         loc.materialize = mat
-                    elif isinstance(r, LazyLocal) and r.pending:
+                        return ShardedArray(p.shape, p.dtype, p.sharding, loc)
+                    if dfe is not None:
+                        # taken out of the deferral but not handed over as slabs: combine it now
+                        # (flush() no longer sees it)
+                        dfe[2][1]()
+                    if isinstance(r, LazyLocal) and r.pending:
                         # keep a reduced-in-wire-dtype gradient lazy (the optimizer reads .raw)
                         loc = LazyLocal(lambda r=r: {d: t.detach() for d, t in r.items()})
                         loc.raw = {d: t.detach() for d, t in r.raw.items()}

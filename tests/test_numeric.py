@@ -352,3 +352,29 @@ def test_fp8_ff_block_emulation_matches_reference_recipe(host_devices):
     for gt, w in ((x.grad.float(), xr.grad), (wi.grad, wir.grad), (wo.grad, wor.grad)):
         assert ((gt - w).norm() / w.norm()).item() < 0.25
     assert torch.equal(res.grad, cot)
+
+
+@pytest.mark.parametrize("n,spec", [(1, P()), (2, P("x")), (4, P("x", "y"))])
+def test_mse_loss_value_and_grad(host_devices, n, spec):
+    """ops.core.mse_loss: value and gradient equal torch's mean((y - t)^2) for every sharding
+    (the partial sums are all-reduced for the value, seeded directly for the gradient)."""
+    host_devices(n)
+    from learning_jax_sharding_amd.ops.core import mse_loss
+    mesh = Mesh(create_device_mesh((2, 2) if n == 4 else (n, 1)), ("x", "y"))
+    rng = np.random.default_rng(3)
+    Y = rng.standard_normal((4, 8, 16)).astype(np.float32)
+    Tg = rng.standard_normal((4, 8, 16)).astype(np.float32)
+    W = rng.standard_normal((16, 16)).astype(np.float32)
+    y = ljs.device_put(Y, NamedSharding(mesh, spec))
+    t = ljs.device_put(Tg, NamedSharding(mesh, spec))
+    w = ljs.device_put(W, NamedSharding(mesh, P()))
+
+    def f(w):
+        return mse_loss(ljs.numpy.einsum("bsk,kn->bsn", y, w), t)
+
+    val, g = ljs.value_and_grad(f)(w)
+    wt = torch.tensor(W, requires_grad=True)
+    ref = ((torch.einsum("bsk,kn->bsn", torch.tensor(Y), wt) - torch.tensor(Tg)) ** 2).mean()
+    ref.backward()
+    np.testing.assert_allclose(float(np.asarray(val)), float(ref), rtol=1e-5)
+    np.testing.assert_allclose(np.asarray(g), wt.grad.numpy(), rtol=1e-4, atol=1e-5)
