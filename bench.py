@@ -71,6 +71,9 @@ def parse():
     p.add_argument("--loss", default="sum", choices=["sum", "mse"],
                    help="sum: y.sum() as in case6_attention.py:211 (constant cotangent); mse: mean((y - target)^2) "
                         "against a synthetic target (a general, data-dependent cotangent)")
+    p.add_argument("--rules", default="reference",
+                   help="logical-axis rules preset (parallel/tensor.py PRESETS): reference (case6_attention.py:183-187), "
+                        "case5 (embed->data: FSDP-sharded weights, case5_attention_dense.py:109-112), gspmd2d, megatron, dp")
     p.add_argument("--comm-timeout", type=float, default=None,
                    help="seconds a phase may run before the watchdog aborts the communicators and exits "
                         "(default LJS_COMM_TIMEOUT_S or 300)")
@@ -196,7 +199,8 @@ def main():
         mshape = tuple(int(v) for v in args.mesh.split("x"))
     assert mshape[0] * mshape[1] == n, (mshape, n)
     mesh = Mesh(create_device_mesh(mshape), ("data", "model"))
-    rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
+    from learning_jax_sharding_amd.parallel.tensor import rules as _rules_preset
+    rules = _rules_preset(args.rules)
     B = args.batch_per_gpu * n
     S, M = args.seq, args.dim
     if args.model == "layer":
@@ -338,7 +342,7 @@ def main():
         comm = dist.get_backend() + ("+native-rccl" if getattr(c, "_native", None) is not None else "")
     if rank == 0:
         par = f"dp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
-        if args.model == "fsdp":
+        if args.model == "fsdp" or (args.rules in ("case5", "fsdp", "gspmd2d") and mshape[0] > 1):
             par = f"fsdp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
         gemm = "MX-fp8" if args.fp8 else "bf16"
         model_desc = {
@@ -373,7 +377,7 @@ def main():
                        "global_batch": B, "seq_len": S, "parallelism": par, "mode": args.mode,
                        "hip_graph": capture, "graph_segments": segs, "steps_per_graph": G, "mesh": list(mshape),
                        "comm": comm, "grad_wire": os.environ.get("LJS_GRAD_COMM_DTYPE", "fp32"),
-                       "loss": "y.sum()" if args.loss == "sum" else "mean((y - target)^2)"},
+                       "loss": "y.sum()" if args.loss == "sum" else "mean((y - target)^2)", "rules": args.rules},
         }
         print(json.dumps(rec), flush=True)
     if dist_on:

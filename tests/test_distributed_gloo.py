@@ -47,7 +47,7 @@ def job_collectives(ljs):
     return out
 
 
-def job_train(ljs, shapes=((2, 1), (1, 2)), batch=4, seq=32, dtype=torch.bfloat16):
+def job_train(ljs, shapes=((2, 1), (1, 2)), batch=4, seq=32, dtype=torch.bfloat16, rules=None):
     from learning_jax_sharding_amd import nn, optim
     from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
     from learning_jax_sharding_amd.models import MultiHeadAttention
@@ -56,7 +56,8 @@ def job_train(ljs, shapes=((2, 1), (1, 2)), batch=4, seq=32, dtype=torch.bfloat1
     res = {}
     for shape in shapes:
         mesh = Mesh(create_device_mesh(shape), ("data", "model"))
-        rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
+        if rules is None:
+            rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
         model = MultiHeadAttention(64, heads=4, dim_head=16, dtype=dtype)
         x = ljs.random.normal(ljs.random.PRNGKey(0), (batch, seq, 64))
         params = model.init(ljs.random.PRNGKey(1), x)["params"]
@@ -275,3 +276,23 @@ def test_dist_train_fsdp(host_devices):
         for k in pref:
             np.testing.assert_allclose(p[k], pref[k], rtol=1e-4, atol=1e-5)
             np.testing.assert_allclose(p[k], p1[k], rtol=1e-4, atol=1e-5)
+
+
+def job_train_case5(ljs):
+    """The attention block under the case5 rules (embed -> data, case5_attention_dense.py:109-112):
+    Wq/Wk/Wv/Wo sharded FSDP-style over 'data' and gathered at use (bench.py --rules case5)."""
+    from learning_jax_sharding_amd.parallel.tensor import FSDP_RULES
+    return job_train(ljs, ((2, 1), (1, 2)), batch=4, seq=32, dtype=torch.float32, rules=FSDP_RULES)
+
+
+def test_dist_train_case5_rules_matches_unsharded(host_devices):
+    r0, r1 = _run("job_train_case5")
+    host_devices(1)
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd.parallel.tensor import FSDP_RULES
+    l1, p1 = job_train(ljs, ((1, 1),), batch=4, seq=32, dtype=torch.float32, rules=FSDP_RULES)["(1, 1)"]
+    for r in (r0, r1):
+        for shape, (l, p) in r.items():
+            assert abs(l - l1) <= 1e-4 * max(1, abs(l1)), (shape, l, l1)
+            for k in p1:
+                np.testing.assert_allclose(p[k], p1[k], rtol=1e-4, atol=1e-5, err_msg=f"{shape} {k}")
