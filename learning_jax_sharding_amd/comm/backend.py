@@ -41,6 +41,12 @@ def _hip():
     from ..ops import hip
     return hip
 
+def _slots_like(x: torch.Tensor, n: int) -> torch.Tensor:
+    """[n, *x.shape] receive buffer: n dense slots, each with x's strides (x dense)."""
+    base = torch.empty(n * x.numel(), dtype=x.dtype, device=x.device)
+    return base.as_strided((n,) + tuple(x.shape), (x.numel(),) + tuple(x.stride()))
+
+
 class Transfer:
     """Copy ``src_slices`` of device ``src``'s tensor into ``dst_slices`` of device ``dst``'s output."""
 
@@ -110,7 +116,7 @@ class LocalComm:
                     res = grp.all_gather({i: xs[d].contiguous() for i, d in enumerate(g)})
                     gathered = [res[i] for i in range(n)]
                 else:
-                    gathered = nat.all_gather([xs[d].contiguous() for d in g])
+                    gathered = nat.all_gather([_hip().dense(xs[d]) for d in g])
                 for d, buf in zip(g, gathered):
                     out[d] = _hip().from_rank_major(buf, dim)   # rank-major -> gathered layout
                 continue
@@ -150,7 +156,7 @@ class LocalComm:
                 total = v if total is None else total + v
             chunks = total.to(dt).chunk(len(g), dim)
             for i, d in enumerate(g):
-                out[d] = chunks[i].to(xs[d].device).contiguous()
+                out[d] = _hip().dense(chunks[i].to(xs[d].device))
         return out
 
     def all_reduce(self, xs, groups):
@@ -172,7 +178,7 @@ class LocalComm:
                 continue
             nat = self._rccl(g, xs)
             if nat is not None:
-                ts = [xs[d].contiguous() for d in g]
+                ts = [_hip().dense(xs[d]) for d in g]
                 nat.all_reduce(ts)
                 for d, t in zip(g, ts):
                     out[d] = t
@@ -210,7 +216,9 @@ class LocalComm:
                 continue
             for i, d in enumerate(g):
                 dev = xs[d].device
-                out[d] = torch.cat([chunks[s][perm[i]].to(dev) for s in g], concat_dim).contiguous()
+                parts = [chunks[s][perm[i]].to(dev) for s in g]
+                out[d] = _hip().concat_parts(parts, concat_dim) if all(p.device == dev for p in parts) \
+                    else torch.cat(parts, concat_dim).contiguous()
         return out
 
     def watchdog(self, timeout_s: Optional[float] = None):
@@ -326,21 +334,22 @@ class DistComm:
 
     def all_gather(self, xs, groups, dim):
         g, pg = self._group_of(groups)
-        x = xs[self.me].contiguous()
+        x = _hip().dense(xs[self.me])
         if pg is None:
             return {self.me: x.clone()}
         n = len(g)
-        grp = self._p2p(g, pg, x)
+        grp = self._p2p(g, pg, x.contiguous())
         nh = None if grp is not None else self._nat(groups, x)
         if grp is not None:
-            buf = grp.all_gather({grp.rank: x})[grp.rank]
-        elif nh is not None:
-            buf = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-            self._native.all_gather(nh, x, buf)
+            buf = grp.all_gather({grp.rank: x.contiguous()})[grp.rank]
         else:
-            buf = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-            dist.all_gather_into_tensor(buf.view((n * x.shape[0],) + tuple(x.shape[1:])) if x.dim() else buf.view(n),
-                                        x, group=pg)
+            # n slots, each laid out like x (dim order kept: a gather over x's outermost storage
+            # dim is then a view of this buffer, no unpack kernel)
+            buf = _slots_like(x, n)
+            if nh is not None:
+                self._native.all_gather(nh, x, buf)
+            else:
+                dist.all_gather_into_tensor(_hip().flat(buf), _hip().flat(x), group=pg)
         order = None if self._member_order_ok(g) else [sorted(g).index(d) for d in g]
         return {self.me: _hip().from_rank_major(buf, dim, order)}
 
@@ -352,15 +361,15 @@ class DistComm:
         n = len(g)
         # chunk k belongs to member g[k]; the collective hands chunk r to the r-th sorted rank
         xt = _hip().rank_major(x, dim, n, None if self._member_order_ok(g) else [g.index(d) for d in sorted(g)])
-        grp = self._p2p(g, pg, xt, chunked=True)
+        grp = self._p2p(g, pg, xt.contiguous(), chunked=True)
         if grp is not None:
-            return {self.me: grp.reduce_scatter({grp.rank: xt})[grp.rank]}
-        out = torch.empty(xt.shape[1:], dtype=x.dtype, device=x.device)
+            return {self.me: grp.reduce_scatter({grp.rank: xt.contiguous()})[grp.rank]}
+        out = torch.empty_like(xt[0])          # the chunk's own dim order
         nh = self._nat(groups, xt)
         if nh is not None:
             self._native.reduce_scatter(nh, xt, out)
             return {self.me: out}
-        dist.reduce_scatter_tensor(out.view(-1), xt.view(-1), group=pg)
+        dist.reduce_scatter_tensor(_hip().flat(out), _hip().flat(xt), group=pg)
         return {self.me: out}
 
     def all_reduce(self, xs, groups):
@@ -378,7 +387,7 @@ class DistComm:
             elif nh is not None:
                 self._native.all_reduce_(nh, x)
             else:
-                dist.all_reduce(x, group=pg)
+                dist.all_reduce(_hip().flat(x) if _hip().is_dense(x) else x, group=pg)
         return {self.me: x}
 
     def all_to_all(self, xs, groups, split_dim, concat_dim, perms=None):
@@ -392,15 +401,15 @@ class DistComm:
         srt = sorted(g)
         # the chunk sent to group member at tile position i is chunk perm[i]; order sends by sorted rank
         send = _hip().rank_major(x, split_dim, n, [perm[g.index(r)] for r in srt])
-        grp = self._p2p(g, pg, send, chunked=True)
+        grp = self._p2p(g, pg, send.contiguous(), chunked=True)
         nh = None if grp is not None else self._nat(groups, send)
         if grp is not None:
-            recv = grp.all_to_all({grp.rank: send})[grp.rank]
+            recv = grp.all_to_all({grp.rank: send.contiguous()})[grp.rank]
         elif nh is not None:
             recv = self._native.all_to_all(nh, send, torch.empty_like(send), n)
         else:
             recv = torch.empty_like(send)
-            dist.all_to_all_single(recv.view(n, -1), send.view(n, -1), group=pg)
+            dist.all_to_all_single(_hip().flat(recv).view(n, -1), _hip().flat(send).view(n, -1), group=pg)
         # recv[k] came from sorted rank srt[k]; concatenate in member (tile) order
         return {self.me: _hip().from_rank_major(recv, concat_dim, [srt.index(d) for d in g])}
 

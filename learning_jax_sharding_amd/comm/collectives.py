@@ -167,21 +167,41 @@ class _CollectiveFn(torch.autograd.Function):
         ctx.in_meta = {d: (tuple(x.shape), x.dtype, x.device) for d, x in zip(in_devs, xs)}
         out = _run(spec, dict(zip(in_devs, xs)))
         ctx.out_meta = {d: (tuple(out[d].shape), out[d].dtype, out[d].device) for d in out_devs}
+        ctx.out_strides = {d: tuple(out[d].stride()) for d in out_devs}
         return tuple(out[d] for d in out_devs)
 
     @staticmethod
     def backward(ctx, *gs):
         gd = {}
+        from ..ops.hip import is_dense
         for d, g in zip(ctx.out_devs, gs):
             if g is None:
                 shape, dt, dev = ctx.out_meta[d]
                 g = torch.zeros(shape, dtype=dt, device=dev)
-            gd[d] = g.contiguous()
+            elif not is_dense(g):
+                # materialise in the forward output's layout (a seq-major output's gradient then
+                # moves back over the sequence as contiguous blocks)
+                shape, dt, dev = ctx.out_meta[d]
+                st = ctx.out_strides[d]
+                buf = torch.empty_strided(shape, st, dtype=g.dtype, device=dev) if _dense_strides(shape, st) \
+                    else torch.empty(shape, dtype=g.dtype, device=dev)
+                g = buf.copy_(g)
+            gd[d] = g
         tspec = _transpose(ctx.spec, ctx.in_meta)
         kind = "collective_permute" if tspec.kind == "exchange" else tspec.kind
         _plan.record(kind, groups=tspec.groups, note="backward", bytes_in=_per_device_bytes(gd))
         out = _run(tspec, gd)
         return (None, None, None) + tuple(out.get(d) for d in ctx.in_devs)
+
+
+def _dense_strides(shape, strides) -> bool:
+    dims = sorted((i for i in range(len(shape)) if shape[i] > 1), key=lambda i: -strides[i])
+    exp = 1
+    for i in reversed(dims):
+        if strides[i] != exp:
+            return False
+        exp *= shape[i]
+    return True
 
 
 def _apply(spec: _Spec, xs: Dict[int, torch.Tensor], out_devs: Optional[Sequence[int]] = None):

@@ -183,7 +183,8 @@ class NativeRccl:
     def all_gather(self, ts: Sequence[torch.Tensor]):
         """Returns per member a [n, *shape] tensor of every member's block, member-major."""
         n = len(ts)
-        outs = [torch.empty((n,) + tuple(t.shape), dtype=t.dtype, device=t.device) for t in ts]
+        from .backend import _slots_like
+        outs = [_slots_like(t, n) for t in ts]
         h = self.comm(tuple(t.device.index for t in ts))
         rc = runtime().ljs_comm_all_gather(h, _ptrs(ts), _ptrs(outs), ts[0].numel(), _DT[ts[0].dtype], _streams(ts))
         self._check(rc, "all_gather")
@@ -191,7 +192,7 @@ class NativeRccl:
 
     def reduce_scatter(self, ts: Sequence[torch.Tensor]):
         """ts[i] is [n, *chunk] (chunk r destined to member r); returns each member's summed chunk."""
-        outs = [torch.empty(tuple(t.shape[1:]), dtype=t.dtype, device=t.device) for t in ts]
+        outs = [torch.empty_like(t[0]) for t in ts]
         h = self.comm(tuple(t.device.index for t in ts))
         rc = runtime().ljs_comm_reduce_scatter(h, _ptrs(ts), _ptrs(outs), outs[0].numel(), _DT[ts[0].dtype], 0,
                                                _streams(ts))
@@ -295,7 +296,8 @@ class RankRccl:
 
     @staticmethod
     def supports(t: torch.Tensor) -> bool:
-        return t.is_cuda and t.dtype in _DT and t.is_contiguous()
+        from ..ops.hip import is_dense
+        return t.is_cuda and t.dtype in _DT and is_dense(t)
 
     def _one(self, t):
         return (_VP * 1)(t.data_ptr())

@@ -780,11 +780,77 @@ __global__ void rng_kernel(T* __restrict__ out, RngRegion reg, long n, unsigned 
   }
 }
 
+
+// out[s][b][k] = bf16(in[b][s][k]) for a [B][S][K] f32 or bf16 array (K % 8 == 0): the activations'
+// (batch, seq) storage order swapped to seq-major while they are rounded to bf16, so a sequence-
+// sharded layer gathers / scatters whole contiguous blocks (ops/linear.py, ops/hip.py storage_order)
+template <typename T>
+__global__ void swap01_bf16_kernel(const T* __restrict__ in, bf16_t* __restrict__ out, int B, int S, int K8) {
+  const long n8 = (long)B * S * K8;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long o = (long)blockIdx.x * blockDim.x + threadIdx.x; o < n8; o += stride) {
+    const int k8 = (int)(o % K8);
+    const long sb = o / K8;
+    const int b = (int)(sb % B), s = (int)(sb / B);
+    const long i = ((long)b * S + s) * K8 + k8;
+    u32x4 w;
+    if constexpr (sizeof(T) == 4) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(in + i * 8);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(in + i * 8 + 4);
+      w[0] = pack_bf16x2(a[0], a[1]);
+      w[1] = pack_bf16x2(a[2], a[3]);
+      w[2] = pack_bf16x2(c[0], c[1]);
+      w[3] = pack_bf16x2(c[2], c[3]);
+    } else {
+      w = *reinterpret_cast<const u32x4*>(in + i * 8);
+    }
+    *reinterpret_cast<u32x4*>(out + o * 8) = w;
+  }
+}
+
+
+// out[c][r] = in[r][c] for an R x C bf16 matrix (row strides ldi / ldo), 64x64 tiles through LDS:
+// the plain [in][out] shadow of a weight derived from its gathered transposed shadow
+__global__ void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out, int R, int C, long ldi,
+                                      long ldo) {
+  __shared__ bf16_t tile[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? in[(long)r * ldi + c] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) out[(long)c * ldo + r] = tile[tx][i];
+  }
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
 LJS_API int ljs_cast_f32_bf16(const void* in, void* out, long n, hipStream_t s) {
   hipLaunchKernelGGL(cast_f32_bf16, dim3(grid_for(n, 256 * 8)), dim3(256), 0, s, (const float*)in, (bf16_t*)out, n);
+  return (int)hipGetLastError();
+}
+
+LJS_API int ljs_swap01_bf16(const void* in, int in_bf16, void* out, int B, int S, int K, hipStream_t s) {
+  if (K % 8 || (((uintptr_t)in) & 15) || (((uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
+  const long n8 = (long)B * S * (K / 8);
+  const int g = grid_for(n8, 256 * 4);
+  if (in_bf16)
+    hipLaunchKernelGGL(swap01_bf16_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, B, S,
+                       K / 8);
+  else
+    hipLaunchKernelGGL(swap01_bf16_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)in, (bf16_t*)out, B, S,
+                       K / 8);
+  return (int)hipGetLastError();
+}
+
+LJS_API int ljs_transpose_bf16(const void* in, void* out, int R, int C, long ldi, long ldo, hipStream_t s) {
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, R, C, ldi, ldo);
   return (int)hipGetLastError();
 }
 

@@ -57,6 +57,16 @@ class MultiHeadAttention(Module):
                                dtype=self.dtype, name="to_out_0")
         self.dropout_layer = Dropout(rate=self.dropout)
 
+    def _prefetch_out_kernel(self, x: ShardedArray, dt):
+        wo = self.proj_attn.kernel_param(self.dim_head * self.heads)
+        if any(t.is_meta or not t.is_cuda for t in wo.local.values()):
+            return None
+        axis = _fsdp_axis(wo, x)
+        if axis is None:
+            return None
+        from ..parallel.fsdp import Prefetcher
+        return Prefetcher(wo.sharding.mesh, axis, bf16_shadows=dt == torch.bfloat16).prefetch([wo])
+
     def _log(self, *a):
         if self.verbose:
             print(*a)
@@ -70,6 +80,10 @@ class MultiHeadAttention(Module):
         context = hidden_states if context is None else context
         self._log("context.shape: ", context.shape)
         dt = _dt.canonicalize(self.dtype)
+        # FSDP rules (case5_attention_dense.py:109-112: embed -> data) shard the out projection's
+        # kernel over the batch axis: gather it on a side stream NOW, while the QKV projection and
+        # the attention run, instead of at its use (parallel/fsdp.py Prefetcher, bf16 shadows)
+        wo_pf = self._prefetch_out_kernel(hidden_states, dt)
         if self.fused_qkv and self_attn:
             m = hidden_states.shape[-1]
             wq = self.query.kernel_param(m)
@@ -109,15 +123,31 @@ class MultiHeadAttention(Module):
         hidden = core.reshape(hidden, (b, -1, self.heads * self.dim_head))
         hidden = with_logical_constraint(hidden, ("batch", "kv", "heads"))
         drop_id = deterministic or self.dropout == 0.0
+        wo = wo_pf.wait()[0] if wo_pf is not None else None
         if residual is not None and drop_id:
-            hidden = self.proj_attn(hidden, residual=residual)
+            hidden = self.proj_attn(hidden, residual=residual, kernel=wo)
             return with_logical_constraint(hidden, ("batch", "embed"))
-        hidden = self.proj_attn(hidden)
+        hidden = self.proj_attn(hidden, kernel=wo)
         hidden = with_logical_constraint(hidden, ("batch", "embed"))
         hidden = self.dropout_layer(hidden, deterministic=deterministic)
         if residual is not None:
             hidden = core.binary("add", core.convert(residual, dt), hidden)
         return hidden
+
+
+def _fsdp_axis(w: ShardedArray, x: ShardedArray):
+    """The mesh axis sharding both ``w`` and ``x``'s batch dim (the FSDP pattern), else None."""
+    from ..sharding import NamedSharding
+    ws, xs = w.sharding, x.sharding
+    if not isinstance(ws, NamedSharding) or not isinstance(xs, NamedSharding) or not xs.spec:
+        return None
+    b = xs.spec[0]
+    b_axes = set(b) if isinstance(b, tuple) else ({b} if b else set())
+    for e in ws.spec:
+        for a in (e if isinstance(e, tuple) else (e,)):
+            if a is not None and a in b_axes and ws.mesh.shape[a] > 1:
+                return a
+    return None
 
 
 def attention_block_flops(batch: int, seq: int, dim: int, heads: int, dim_head: int, train: bool) -> float:

@@ -45,7 +45,7 @@ class DenseStack(Module):
         if not on_axis or any(t.is_meta for t in w.local.values()):
             return None
         from ..parallel.fsdp import Prefetcher
-        return Prefetcher(sh.mesh, self.fsdp_axis)
+        return Prefetcher(sh.mesh, self.fsdp_axis, bf16_shadows=_dt.canonicalize(self.dtype) == torch.bfloat16)
 
     def __call__(self, x):
         dt = _dt.canonicalize(self.dtype)

@@ -51,10 +51,13 @@ class Dense(Module):
             return None
         return self.param("bias", self.bias_init, (self.features,), _dt.canonicalize(self.param_dtype))
 
-    def __call__(self, inputs: ShardedArray, residual: Optional[ShardedArray] = None) -> ShardedArray:
+    def __call__(self, inputs: ShardedArray, residual: Optional[ShardedArray] = None,
+                 kernel: Optional[ShardedArray] = None) -> ShardedArray:
         """``inputs @ kernel (+ bias)``; ``residual`` is added in the compute dtype (fused into the
-        GEMM epilogue on the MFMA path)."""
-        kernel = self.kernel_param(inputs.shape[-1])
+        GEMM epilogue on the MFMA path).  ``kernel``: this layer's kernel already gathered (an FSDP
+        prefetch, parallel/fsdp.py) in place of the parameter."""
+        if kernel is None:
+            kernel = self.kernel_param(inputs.shape[-1])
         bias = self.bias_param()
         dtype = _dt.canonicalize(self.dtype) or _dt.result_type(inputs.dtype, kernel.dtype)
         return core.dense(inputs, [kernel], bias, compute_dtype=dtype, residual=residual)[0]

@@ -682,6 +682,9 @@ def dot_product_attention(q: ShardedArray, k: ShardedArray, v: ShardedArray, sca
 
 
 # ----------------------------------------------------------------------------- fused dense
+_SEQ_MAJOR = os.environ.get("LJS_SEQ_MAJOR", "1") == "1"
+
+
 def dense(x: ShardedArray, kernels: Sequence[ShardedArray], bias: Optional[ShardedArray] = None,
           compute_dtype=None, relu: bool = False, fp8: bool = False,
           residual: Optional[ShardedArray] = None) -> List[ShardedArray]:
@@ -708,7 +711,14 @@ def dense(x: ShardedArray, kernels: Sequence[ShardedArray], bias: Optional[Shard
     _plan.record("dense", k_source=p.k_source, out_tiles=p.out_tile.tile_shape, n_kernels=len(kernels),
                  **({"fp8": True} if fp8 else {}))
     x2 = reshard_tile(x, p.lhs_tile, note="dense.x")
-    ws = [reshard_tile(k, p.rhs_tile, note="dense.w") for k in kernels]
+    # sharded f32 weights gathered for the GEMM: gather the shards' bf16 shadows instead (half the
+    # bytes, no cast of the gathered copy; parallel/weight_gather.py)
+    from ..parallel import weight_gather as _wg
+    gdim = _wg.eligible(kernels, p.rhs_tile) if (compute_dtype == torch.bfloat16 and not fp8) else None
+    if gdim is not None:
+        ws = _wg.gather_bf16(kernels, p.rhs_tile, gdim, note="dense.w")
+    else:
+        ws = [reshard_tile(k, p.rhs_tile, note="dense.w") for k in kernels]
     partial = p.k_groups is not None
     out_shape = tuple(x.shape[:-1]) + (w0.shape[1],)
     fuse_bias = bias is not None and not partial and len(kernels) == 1
@@ -723,12 +733,19 @@ def dense(x: ShardedArray, kernels: Sequence[ShardedArray], bias: Optional[Shard
             raise ValueError(f"residual shape {residual.shape} != output shape {out_shape}")
         r_loc = reshard_tile(residual, p.out_tile, note="dense.residual").local
     loc_lists = {}
-    for d in x2.local:
-        loc_lists[d] = K.linear(x2.local[d], [w.local[d] for w in ws],
-                                b_loc[d] if fuse_bias else None, compute_dtype,
-                                relu=relu and not partial,
-                                out_dtype=torch.float32 if partial else compute_dtype, fp8=fp8,
-                                residual=r_loc[d] if r_loc is not None else None)
+    # a (batch, seq, features) activation with its sequence sharded: outputs stored seq-major, so
+    # the sequence gathers / scatters that follow (K/V for attention) move whole
+    # contiguous blocks with no pack / unpack kernels (ops/hip.py storage_order)
+    from . import linear as _lin
+    seq_major = x2.ndim == 3 and x2.tile.tile_shape[1] > 1 and x2.shape[0] > x2.tile.tile_shape[0] \
+        and _SEQ_MAJOR
+    with _lin.token_outer(1 if seq_major else None):
+        for d in x2.local:
+            loc_lists[d] = K.linear(x2.local[d], [w.local[d] for w in ws],
+                                    b_loc[d] if fuse_bias else None, compute_dtype,
+                                    relu=relu and not partial,
+                                    out_dtype=torch.float32 if partial else compute_dtype, fp8=fp8,
+                                    residual=r_loc[d] if r_loc is not None else None)
     outs = []
     sh = sharding_from_tile(p.out_tile, like=[x.sharding, w0.sharding])
     for i in range(len(kernels)):

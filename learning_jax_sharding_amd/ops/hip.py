@@ -43,6 +43,8 @@ _SIGS = {
                      c_int, c_void_p],
     "ljs_cast_f32_bf16": [c_void_p, c_void_p, c_long, c_void_p],
     "ljs_cast_bf16_f32": [c_void_p, c_void_p, c_long, c_void_p],
+    "ljs_swap01_bf16": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
+    "ljs_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p],
     "ljs_cast_transpose_f32_bf16": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p],
     "ljs_sum_all": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
@@ -542,6 +544,27 @@ def _cast_raw(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return out
 
 
+def swap01_bf16(x: torch.Tensor) -> torch.Tensor:
+    """bf16 [S][B][K] (contiguous) from a contiguous f32 / bf16 [B][S][K]: the seq-major copy of
+    an activation, rounded in the same pass (one HIP launch)."""
+    B, S, K = x.shape
+    out = torch.empty((S, B, K), dtype=torch.bfloat16, device=x.device)
+    rc = lib().ljs_swap01_bf16(_p(x), int(x.dtype == torch.bfloat16), _p(out), B, S, K, _stream(x))
+    _ck(rc, "swap01_bf16")
+    return out
+
+
+def transpose_bf16(t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[C][R] bf16 transpose of a bf16 [R][C] matrix (unit column stride), one HIP launch."""
+    R, C = t.shape
+    assert t.dtype == torch.bfloat16 and t.stride(1) == 1
+    if out is None:
+        out = torch.empty((C, R), dtype=torch.bfloat16, device=t.device)
+    rc = lib().ljs_transpose_bf16(_p(t), _p(out), R, C, t.stride(0), out.stride(0), _stream(t))
+    _ck(rc, "transpose_bf16")
+    return out
+
+
 def cast_into(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
     """dst[...] = src converted to dst.dtype (f32 <-> bf16 on the HIP kernel; both contiguous)."""
     assert src.numel() == dst.numel() and dst.is_contiguous(), (src.shape, dst.shape)
@@ -769,6 +792,9 @@ def linear(x: torch.Tensor, ws: List[torch.Tensor], b: Optional[torch.Tensor], c
     from . import linear as _lin
     if compute_dtype == torch.bfloat16 and _lin.supported(x, ws, b):
         return _lin.linear(x, list(ws), b, relu, out_dtype, residual=residual)
+    from . import shadow
+    if any(shadow.is_proxy(w) for w in ws):
+        raise RuntimeError("a gathered-weight proxy (bf16 shadow gather) reached a GEMM path that reads f32 weights")
     outs = _linear_any(x, ws, b, compute_dtype, relu, out_dtype)
     if residual is not None:
         outs = [outs[0] + residual.to(outs[0].dtype)] + outs[1:]
@@ -878,55 +904,133 @@ def _pack_ok(*ts) -> bool:
     return all(t.is_cuda for t in ts)
 
 
+def storage_order(t: torch.Tensor):
+    """The permutation of ``t``'s dims from outermost to innermost in memory when ``t`` is DENSE
+    (a permutation of a contiguous tensor: no gaps, no overlap), else None.  Size-1 dims keep
+    their logical position.  Activations whose sharded sequence dim is kept outermost in
+    storage (``seq-major``: (batch, seq, features) stored [seq][batch][features]) gather and
+    scatter over that dim as whole contiguous blocks - no pack / unpack kernels."""
+    if t.dim() == 0:
+        return ()
+    order = sorted(range(t.dim()), key=lambda d: (-t.stride(d) if t.shape[d] > 1 else 0, d))
+    # size-1 dims anywhere: move them to their logical slot (their stride is irrelevant)
+    big = [d for d in order if t.shape[d] > 1]
+    one = [d for d in range(t.dim()) if t.shape[d] <= 1]
+    order = sorted(one + big, key=lambda d: (big.index(d) if d in big else -1, d)) if one else big
+    exp = 1
+    for d in reversed(big):
+        if t.stride(d) != exp:
+            return None
+        exp *= t.shape[d]
+    return tuple(order)
+
+
+def is_dense(t: torch.Tensor) -> bool:
+    return storage_order(t) is not None
+
+
+def dense(t: torch.Tensor) -> torch.Tensor:
+    """``t`` itself when dense (any dim order), else a contiguous copy."""
+    return t if is_dense(t) else t.contiguous()
+
+
+def flat(t: torch.Tensor) -> torch.Tensor:
+    """1-D view of a dense tensor's storage (in memory order)."""
+    assert is_dense(t), "flat() needs a dense tensor"
+    return t.as_strided((t.numel(),), (1,))
+
+
+def _in_order(t: torch.Tensor):
+    """(view of t with dims in storage order - contiguous, the order) for a dense t; else
+    (t.contiguous(), identity)."""
+    o = storage_order(t)
+    if o is None or list(o) == list(range(t.dim())):
+        return t.contiguous(), tuple(range(t.dim()))
+    return t.permute(o), o
+
+
+def _inv(order):
+    inv = [0] * len(order)
+    for i, d in enumerate(order):
+        inv[d] = i
+    return inv
+
+
 def rank_major(x: torch.Tensor, dim: int, n: int, perm=None) -> torch.Tensor:
-    """[.., n*s (dim), ..] -> [n][.., s, ..] contiguous, chunk ``perm[k]`` first-axis slot k (the
-    send buffer of a reduce-scatter / all-to-all), one HIP launch on GPU tensors."""
-    shp = tuple(x.shape)
-    s = shp[dim] // n
-    out_shape = (n,) + shp[:dim] + (s,) + shp[dim + 1:]
+    """[.., n*s (dim), ..] -> [n][.., s, ..], chunk ``perm[k]`` in first-axis slot k (the send
+    buffer of a reduce-scatter / all-to-all): dense, the chunks in x's own dim order.  When
+    ``dim`` is outermost in x's storage (and no perm) this is a VIEW - no kernel; otherwise one
+    HIP launch on GPU tensors."""
+    if perm is not None and list(perm) == list(range(n)):
+        perm = None
+    xs, order = _in_order(x)
+    pdim = order.index(dim)
+    shp = tuple(xs.shape)
+    s = shp[pdim] // n
+    pshape = (n,) + shp[:pdim] + (s,) + shp[pdim + 1:]
+    back = [0] + [1 + i for i in _inv(order)]
+    if all(v == 1 for v in shp[:pdim]) and perm is None:
+        return xs.reshape(pshape).permute(back)
     if not _pack_ok(x) or n > 64:
-        v = x.reshape(shp[:dim] + (n, s) + shp[dim + 1:]).movedim(dim, 0)
-        return (v[list(perm)] if perm is not None else v).contiguous()
-    x = x.contiguous()
-    A = math.prod(shp[:dim])
-    inner = x.element_size() * s * math.prod(shp[dim + 1:])
-    out = torch.empty(out_shape, dtype=x.dtype, device=x.device)
-    _pack_launch([x], out, A, n, inner, 0, perm)
-    return out
+        v = xs.reshape(shp[:pdim] + (n, s) + shp[pdim + 1:]).movedim(pdim, 0)
+        return (v[list(perm)] if perm is not None else v).contiguous().permute(back)
+    A = math.prod(shp[:pdim])
+    inner = xs.element_size() * s * math.prod(shp[pdim + 1:])
+    out = torch.empty(pshape, dtype=x.dtype, device=x.device)
+    _pack_launch([xs], out, A, n, inner, 0, perm)
+    return out.permute(back)
 
 
 def from_rank_major(buf: torch.Tensor, dim: int, perm=None) -> torch.Tensor:
     """[n][.., c (dim), ..] -> [.., n*c, ..]: slot ``perm[k]`` of ``buf`` becomes chunk k along
-    ``dim`` (the receive buffer of an all-gather / all-to-all back in the tensor's layout)."""
+    ``dim`` (the receive buffer of an all-gather / all-to-all back in the tensor's layout).  The
+    result keeps the chunks' dim order; when ``dim`` is outermost in it (and no perm) it is a
+    VIEW of ``buf``."""
     n = buf.shape[0]
-    cs = tuple(buf.shape[1:])
-    out_shape = cs[:dim] + (n * cs[dim],) + cs[dim + 1:]
+    if perm is not None and list(perm) == list(range(n)):
+        perm = None
+    chunk = buf[0]
+    o = storage_order(chunk) if n > 0 else None
+    dense_slots = o is not None and buf.stride(0) == chunk.numel()
+    if not dense_slots:
+        buf, o = buf.contiguous(), tuple(range(buf.dim() - 1))
+    pbuf = buf.permute([0] + [1 + d for d in o])
+    pdim = list(o).index(dim)
+    cs = tuple(pbuf.shape[1:])
+    out_shape = cs[:pdim] + (n * cs[pdim],) + cs[pdim + 1:]
+    inv = _inv(o)
+    if all(v == 1 for v in cs[:pdim]) and perm is None:
+        return pbuf.reshape(out_shape).permute(inv)
     if not _pack_ok(buf) or n > 64:
-        b = buf[list(perm)] if perm is not None else buf
-        return b.movedim(0, dim).reshape(out_shape).contiguous()
-    buf = buf.contiguous()
-    A = math.prod(cs[:dim])
-    inner = buf.element_size() * math.prod(cs[dim:])
+        b = pbuf[list(perm)] if perm is not None else pbuf
+        return b.movedim(0, pdim).reshape(out_shape).contiguous().permute(inv)
+    A = math.prod(cs[:pdim])
+    inner = buf.element_size() * math.prod(cs[pdim:])
     out = torch.empty(out_shape, dtype=buf.dtype, device=buf.device)
-    _pack_launch([buf], out, A, n, inner, 1, perm)
-    return out
+    _pack_launch([pbuf], out, A, n, inner, 1, perm)
+    return out.permute(inv)
 
 
 def concat_parts(parts, dim: int) -> torch.Tensor:
     """``torch.cat(parts, dim)`` of same-shape parts on one GPU in one HIP launch (a loopback
-    all-gather over virtual devices)."""
+    all-gather over virtual devices); the result keeps the parts' dim order when they are dense
+    in a common order."""
     p0 = parts[0]
     n = len(parts)
     if not _pack_ok(*parts) or n > 64 or any(p.shape != p0.shape or p.dtype != p0.dtype or p.device != p0.device
                                             for p in parts):
         return torch.cat(parts, dim)
-    parts = [p.contiguous() for p in parts]
-    cs = tuple(p0.shape)
-    A = math.prod(cs[:dim])
-    inner = p0.element_size() * math.prod(cs[dim:])
-    out = torch.empty(cs[:dim] + (n * cs[dim],) + cs[dim + 1:], dtype=p0.dtype, device=p0.device)
-    _pack_launch(parts, out, A, n, inner, 2, None)
-    return out
+    o = storage_order(p0)
+    if o is None or any(storage_order(p) != o or p.stride() != p0.stride() for p in parts):
+        parts, o = [p.contiguous() for p in parts], tuple(range(p0.dim()))
+    pparts = [p.permute(o) for p in parts]
+    pdim = list(o).index(dim)
+    cs = tuple(pparts[0].shape)
+    A = math.prod(cs[:pdim])
+    inner = p0.element_size() * math.prod(cs[pdim:])
+    out = torch.empty(cs[:pdim] + (n * cs[pdim],) + cs[pdim + 1:], dtype=p0.dtype, device=p0.device)
+    _pack_launch(pparts, out, A, n, inner, 2, None)
+    return out.permute(_inv(o))
 
 
 def bcast_scalar(g: torch.Tensor, C: int, R: int, want_db: bool, db_out: Optional[torch.Tensor] = None,
@@ -982,12 +1086,22 @@ def _strides3(t: torch.Tensor):
     return [t.stride(0), t.stride(1), t.stride(2)]
 
 
+def _bs_like(shape, ref: torch.Tensor) -> torch.Tensor:
+    """Empty bf16 (B, S, H, D) stored like ``ref``'s (batch, seq) dims: seq-major when ref is
+    (the kernels take any batch / seq strides; the result then gathers / scatters over the
+    sequence as contiguous blocks)."""
+    B, S, H, D = shape
+    if B > 1 and S > 1 and ref.stride(1) > ref.stride(0):
+        return torch.empty((S, B, H, D), dtype=torch.bfloat16, device=ref.device).permute(1, 0, 2, 3)
+    return torch.empty(shape, dtype=torch.bfloat16, device=ref.device)
+
+
 class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, scale, causal, q_offset):
         B, Sq, H, D = q.shape
         Sk = k.shape[1]
-        o = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
+        o = _bs_like((B, Sq, H, D), q)
         lse = torch.empty((B, H, Sq), dtype=torch.float32, device=q.device)
         rc = lib().ljs_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), B, Sq, Sk, H, _longs(_strides3(q)),
                                 _longs(_strides3(k)), _longs(_strides3(v)), _longs(_strides3(o)), scale, int(causal),
@@ -1016,9 +1130,9 @@ class _Attention(torch.autograd.Function):
             dqkv = torch.empty((B, Sq, 3, H, D), dtype=torch.bfloat16, device=q.device)
             dq, dk, dv = dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2]
         else:
-            dq = torch.empty((B, Sq, H, D), dtype=torch.bfloat16, device=q.device)
-            dk = torch.empty((B, Sk, H, D), dtype=torch.bfloat16, device=q.device)
-            dv = torch.empty((B, Sk, H, D), dtype=torch.bfloat16, device=q.device)
+            dq = _bs_like((B, Sq, H, D), q)
+            dk = _bs_like((B, Sk, H, D), k)
+            dv = _bs_like((B, Sk, H, D), v)
         delta = torch.empty((B, H, Sq), dtype=torch.float32, device=q.device)
         rc = lib().ljs_attn_bwd(_p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(delta), _p(dq), _p(dk), _p(dv), B, Sq,
                                 Sk, H, _longs(_strides3(q)), _longs(_strides3(k)), _longs(_strides3(v)),

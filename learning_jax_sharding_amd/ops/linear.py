@@ -252,6 +252,50 @@ def _row_view(dy: torch.Tensor, M: int, N: int) -> Tuple[torch.Tensor, int]:
     return d2, d2.stride(0)
 
 
+# ops.core.dense's layout hint: the logical dim to keep OUTERMOST in the outputs' storage
+# (1 = the sequence of a (batch, seq, features) activation whose sequence is sharded)
+_TOKEN_OUTER: List[Optional[int]] = [None]
+
+
+class token_outer:
+    """Context: dense layers called inside produce ``dim``-major outputs (see _row_order)."""
+
+    def __init__(self, dim: Optional[int]):
+        self.dim = dim
+
+    def __enter__(self):
+        self.prev, _TOKEN_OUTER[0] = _TOKEN_OUTER[0], self.dim
+        return self
+
+    def __exit__(self, *exc):
+        _TOKEN_OUTER[0] = self.prev
+        return False
+
+
+def _inv_perm(order):
+    inv = [0] * len(order)
+    for i, d in enumerate(order):
+        inv[d] = i
+    return tuple(inv)
+
+
+def _row_order(x: torch.Tensor):
+    """(dim order with the feature dim last, swap): the order in which x's leading dims are
+    flattened into GEMM rows - x's own storage order when x is dense with its feature dim
+    innermost, else logical order.  ``swap``: x is a contiguous (batch, seq, K) activation and the
+    active hint asks for seq-major rows - it is transposed while being rounded to bf16."""
+    nd = x.dim()
+    ident = tuple(range(nd))
+    o = hip.storage_order(x) if x.is_cuda else None
+    if o is not None and o[-1] == nd - 1 and o != ident:
+        return tuple(o), False
+    hint = _TOKEN_OUTER[0]
+    if (hint == 1 and nd == 3 and x.is_cuda and x.is_contiguous() and x.shape[0] > 1 and x.shape[1] > 1
+            and x.shape[2] % 8 == 0 and x.dtype in (torch.float32, torch.bfloat16) and x.data_ptr() % 16 == 0):
+        return (1, 0, 2), True
+    return ident, False
+
+
 def _bf16(t: torch.Tensor) -> torch.Tensor:
     if t.dtype == torch.bfloat16:
         return t
@@ -265,17 +309,28 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, b, res, relu, out_dtype, *ws):
         lead = x.shape[:-1]
         K = x.shape[-1]
-        x2 = x.reshape(-1, K)
-        M = x2.shape[0]
+        # rows (tokens) in x's STORAGE order: a seq-major activation ((batch, seq, K) stored
+        # [seq][batch][K]) is flattened without a copy and the outputs keep that order
+        order, swap = _row_order(x)
+        x2 = x.permute(order).reshape(-1, K) if not swap else None
+        M = x.numel() // max(1, K)
         nw = len(ws)
         N = ws[0].shape[1]
+        pshape = tuple(x.shape[d] for d in order[:-1])
+        inv = _inv_perm(order)
+        # weight-major outputs ([nw][M][N]: each projection dense on its own) for a seq-major
+        # fused projection, so its K / V gather over the sequence are contiguous blocks
+        wmajor = nw > 1 and order[0] != 0
         # f32 activations (the reference's f32 input under a bf16 Dense): the GEMM rounds them as
         # it reads them and writes the bf16 copy the backward needs -- no separate cast pass
-        cast_on_load = (_CAST_ON_LOAD and x2.is_cuda and x2.dtype == torch.float32 and x2.is_contiguous()
-                        and res is None and b is None and not relu and K % 64 == 0 and N % 8 == 0
-                        and out_dtype == torch.bfloat16 and x2.data_ptr() % 16 == 0
+        cast_on_load = (_CAST_ON_LOAD and not swap and not wmajor and x2.is_cuda and x2.dtype == torch.float32
+                        and x2.is_contiguous() and res is None and b is None and not relu and K % 64 == 0
+                        and N % 8 == 0 and out_dtype == torch.bfloat16 and x2.data_ptr() % 16 == 0
                         and M * nw * N >= (1 << 20))
-        xb = None if cast_on_load else _bf16(x2 if x2.is_contiguous() else x2.contiguous())
+        if swap:   # batch-major x -> seq-major bf16 rows, rounded in the same pass
+            xb = hip.swap01_bf16(x.contiguous()).view(M, K)
+        else:
+            xb = None if cast_on_load else _bf16(x2 if x2.is_contiguous() else x2.contiguous())
         if nw == 1:
             wt = shadow.get(ws[0], "T")
             sB = 0
@@ -284,7 +339,7 @@ class _Linear(torch.autograd.Function):
             wt = shadow.get_stacked(ws)
             sB = N * K
         od = out_dtype if out_dtype in (torch.bfloat16, torch.float32) else torch.float32
-        out = torch.empty((M, nw * N), dtype=od, device=x.device)
+        out = torch.empty((nw, M, N) if wmajor else (M, nw * N), dtype=od, device=x.device)
         bias = None
         if b is not None:
             bias = (b if b.dtype in (torch.float32, torch.bfloat16) else b.float()).contiguous()
@@ -294,7 +349,7 @@ class _Linear(torch.autograd.Function):
         # residual fused into the epilogue (bf16 output, one kernel, 8-column-aligned operand)
         r2, r_ld = None, 0
         if res is not None:
-            r2 = res.reshape(M, N)
+            r2 = res.permute(order).reshape(M, N)
             if r2.dtype not in (torch.bfloat16, torch.float32):
                 r2 = r2.float()
             if not (r2.stride(1) == 1 and r2.stride(0) % 8 == 0 and r2.data_ptr() % 16 == 0):
@@ -309,9 +364,11 @@ class _Linear(torch.autograd.Function):
         else:
             if cast_on_load:  # (a fused output sum wanted: the cast pass, then the plain GEMM)
                 xb = _bf16(x2)
-            cnt = hip.gemm(xb, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=sB, sC=N,
-                           bias=bias, sBias=0, relu=relu, psum=partials, res=r2, res_ld=r_ld)
-        ys = [out[:, i * N:(i + 1) * N].view(tuple(lead) + (N,)) for i in range(nw)]
+            cnt = hip.gemm(xb, wt, out, M, N, K, K, K, N if wmajor else nw * N, True, True, batch=nw, sA=0, sB=sB,
+                           sC=M * N if wmajor else N, bias=bias, sBias=0, relu=relu, psum=partials, res=r2,
+                           res_ld=r_ld)
+        cols = [out[i] if wmajor else out[:, i * N:(i + 1) * N] for i in range(nw)]
+        ys = [c.view(pshape + (N,)).permute(inv) for c in cols]
         if res is not None and r2 is None:
             ys = [ys[0] + res.to(ys[0].dtype)]
             partials = None
@@ -329,18 +386,22 @@ class _Linear(torch.autograd.Function):
         ctx.has_res = res is not None
         ctx.save_for_backward(xb, b, *ws, *(ys if relu else []))
         ctx.meta = (lead, K, M, N, nw, relu, x.dtype, b is not None)
+        ctx.order, ctx.pshape = order, pshape
         return tuple(ys)
 
     @staticmethod
     def backward(ctx, *dys):
         lead, K, M, N, nw, relu, xdtype, has_b = ctx.meta
+        order, pshape = ctx.order, ctx.pshape
         # the residual's gradient is the output gradient itself (y = dense(x) + res)
         dres = dys[0] if (ctx.has_res and ctx.needs_input_grad[2]) else None
+        # every [M][N] view below is in the forward's row (storage) order
+        dys = tuple(None if d is None else d.permute(order) for d in dys)
         saved = ctx.saved_tensors
         xb, b = saved[0], saved[1]
         ctx.bias_leaf = b
         ws = saved[2:2 + nw]
-        ys = saved[2 + nw:] if relu else None
+        ys = tuple(y.permute(order) for y in saved[2 + nw:]) if relu else None
         dev = xb.device
         mats: List[Optional[Tuple[torch.Tensor, int]]] = []
         db_bcast: List[Optional[torch.Tensor]] = [None] * nw
@@ -413,7 +474,7 @@ class _Linear(torch.autograd.Function):
                 wn = shadow.get(ws[i], "N")                  # [K][N]: B[k=n][n'=k], k-contiguous
                 hip.gemm(t, wn, dx, M, K, N, ld, N, K, True, True, accumulate=j > 0,
                          res=xb if premask else None, res_ld=K, res_mode="mask")
-            dx = dx.to(xdtype).view(tuple(lead) + (K,))
+            dx = dx.to(xdtype).view(pshape + (K,)).permute(_inv_perm(order))
             if premask:
                 _register(_PREMASKED, dx, xb.data_ptr())
         # ---- dW (MN-contiguous operands: X^T and dY read in place), on the side stream inside

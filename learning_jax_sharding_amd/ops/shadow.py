@@ -20,16 +20,18 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-__all__ = ["get", "get_stacked", "get_mx", "mx_eligible", "entry", "adopt", "mark_fresh", "kinds_of"]
+__all__ = ["get", "get_stacked", "get_mx", "mx_eligible", "entry", "adopt", "mark_fresh", "kinds_of", "register_proxy",
+           "is_proxy"]
 
 
 class _Entry:
-    __slots__ = ("ref", "bufs", "versions")
+    __slots__ = ("ref", "bufs", "versions", "proxy")
 
     def __init__(self, w: torch.Tensor):
         self.ref = weakref.ref(w)
         self.bufs: Dict[str, torch.Tensor] = {}
         self.versions: Dict[str, int] = {}
+        self.proxy = False
 
 
 _REG: Dict[Tuple, _Entry] = {}
@@ -75,6 +77,15 @@ def _alloc(w: torch.Tensor, kind: str) -> torch.Tensor:
 def _refresh(w: torch.Tensor, e: _Entry, kind: str) -> torch.Tensor:
     from . import hip
     buf = e.bufs[kind]
+    if e.proxy:
+        if e.versions.get(kind) != w._version:
+            if kind == "N" and "T" in e.bufs and e.versions.get("T") == w._version:
+                hip.transpose_bf16(e.bufs["T"], buf)     # derived from the gathered [out][in] shadow
+                e.versions[kind] = w._version
+            else:
+                raise RuntimeError("shadow of a gathered-weight proxy requested that cannot be derived from its "
+                                   f"gathered bf16 copy (kind {kind!r}); the proxy holds no f32 values")
+        return buf
     if e.versions.get(kind) != w._version:
         if kind == "T":
             hip.cast_transpose_bf16(w, buf)
@@ -93,6 +104,39 @@ def get(w: torch.Tensor, kind: str) -> torch.Tensor:
     return _refresh(w, e, kind)
 
 
+def stacked_proxy_T(ws: Sequence[torch.Tensor]) -> bool:
+    """Whether same-shape proxies' "T" shadows already sit in consecutive slices of one buffer."""
+    es = [entry(w, create=False) for w in ws]
+    if any(e is None or not e.proxy or "T" not in e.bufs for e in es):
+        return False
+    K, N = ws[0].shape
+    base = es[0].bufs["T"]
+    return all(e.bufs["T"].data_ptr() == base.data_ptr() + i * N * K * 2 for i, e in enumerate(es))
+
+
+def register_proxy(w: torch.Tensor, t_buf: torch.Tensor) -> None:
+    """``w`` (an uninitialised f32 tensor of the full weight's shape) stands for a weight whose bf16
+    transposed shadow ``t_buf`` [out][in] was all-gathered from the shards' own shadows
+    (parallel/weight_gather.py): the GEMMs read ``t_buf`` (and an "N" shadow transposed from it);
+    asking for anything that needs the f32 values raises."""
+    e = entry(w)
+    e.proxy = True
+    e.bufs["T"] = t_buf
+    e.versions["T"] = w._version
+    # the entry (and the gathered buffers it holds) goes with the proxy
+    weakref.finalize(w, _drop, _key(w), e)
+
+
+def _drop(key, e) -> None:
+    if _REG.get(key) is e:
+        del _REG[key]
+
+
+def is_proxy(w: torch.Tensor) -> bool:
+    e = entry(w, create=False)
+    return e is not None and e.proxy
+
+
 def mx_eligible(w: torch.Tensor) -> bool:
     """Weights whose MX-fp8 shadows the fused Adam can keep (64 x 64 tiles of its 4-wide path)."""
     import os
@@ -108,6 +152,8 @@ def get_mx(w: torch.Tensor, kind: str):
     Adam rewrites them with the weight (``hip.adam_multi``); any other write re-quantizes."""
     from . import fp8
     e = entry(w)
+    if e.proxy:
+        raise RuntimeError("MX-fp8 shadows of a gathered-weight proxy are not available (bf16 gather)")
     K, N = w.shape
     if kind not in e.bufs:
         qs = (N, K) if kind == "QT" else (K, N)
@@ -132,6 +178,8 @@ def get_stacked(ws: Sequence[torch.Tensor]) -> torch.Tensor:
     """
     es = [entry(w) for w in ws]
     K, N = ws[0].shape
+    if any(e.proxy for e in es) and not stacked_proxy_T(ws):
+        raise RuntimeError("gathered-weight proxies must arrive stacked (one gather of the stacked shadows)")
     bufs = [e.bufs.get("T") for e in es]
     base = bufs[0]
     ok = all(b is not None for b in bufs) and base is not None and all(

@@ -84,11 +84,14 @@ class _Handle:
 class Prefetcher:
     """Gathers FSDP-sharded parameters over ``axis`` on a side stream ahead of use."""
 
-    def __init__(self, mesh: Optional[Mesh] = None, axis: str = "data"):
+    def __init__(self, mesh: Optional[Mesh] = None, axis: str = "data", bf16_shadows: bool = False):
+        """``bf16_shadows``: the consumers are bf16 GEMMs - 2-D f32 weights are gathered as their
+        shards' bf16 shadows (parallel/weight_gather.py: half the bytes, no cast kernel)."""
         self.mesh = mesh or current_mesh()
         if self.mesh is None:
             raise ValueError("Prefetcher needs a mesh")
         self.axis = axis
+        self.bf16_shadows = bf16_shadows
         self._streams: Dict[int, torch.cuda.Stream] = {}
 
     def _gather_leaf(self, p: ShardedArray) -> ShardedArray:
@@ -103,7 +106,13 @@ class Prefetcher:
             dims = [d for d in range(p.ndim) if ta.tile_shape[d] > 1]
         if not dims:
             return p
-        return reshard_tile(p, ta.unshard(dims), note="fsdp.prefetch")
+        dst = ta.unshard(dims)
+        if self.bf16_shadows:
+            from . import weight_gather as _wg
+            gdim = _wg.eligible([p], dst)
+            if gdim is not None:
+                return _wg.gather_bf16([p], dst, gdim, note="fsdp.prefetch")[0]
+        return reshard_tile(p, dst, note="fsdp.prefetch")
 
     def prefetch(self, tree: Any) -> _Handle:
         leaves = [l for l in T.tree_leaves(tree, is_leaf=_is_arr) if _is_arr(l)]

@@ -1,0 +1,138 @@
+"""All-gather of sharded weights as their bf16 GEMM shadows.
+
+When a layer's f32 weight is sharded and its GEMM needs it whole - FSDP's gather at use
+(``case5_attention_dense.py:109-112``, ``case3_fully_sharded.py:23-46,57``) or the reference's
+Q/K/V weights sharded over ``model`` (``case6_attention.py:56-59,183-187``) - the partitioner's
+generic plan gathers the f32 master shards and every step then casts + transposes the gathered
+copy for the MFMA GEMM.  But each shard already HAS its bf16 transposed shadow, rewritten by the
+fused Adam in the pass that updates it (``ops/shadow.py``).  Gathering those instead:
+
+* moves half the bytes over xGMI (bf16, not f32);
+* needs no cast kernel on the gathered weight;
+* stacks Q/K/V: one collective of the three shards' stacked shadows ``[3][N][K/n]`` and one
+  unpack into the ``[3][N][K]`` operand of the batched QKV GEMM.
+
+The gathered weight is handed to the layer as an f32 PROXY - an uninitialised tensor of the full
+shape whose shadow registry entry points at the gathered bf16 copy (``shadow.register_proxy``):
+the GEMMs read the bf16 copy; the backward's plain ``[in][out]`` shadow is transposed from it;
+nothing may read the proxy's f32 values (the registry raises).  The proxy is the output of a
+differentiable gather whose backward is the reduce-scatter of the full f32 gradient onto the
+shards - the transposed collective, as for the generic all-gather.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence
+
+import torch
+
+from ..array import ShardedArray
+from ..comm import collectives as C
+from ..sharding.shardings import sharding_from_tile
+from ..sharding.tile import TileAssignment
+from ..spmd import plan as _plan
+
+__all__ = ["eligible", "gather_bf16"]
+
+_ON = os.environ.get("LJS_GATHER_SHADOWS", "1") == "1"
+
+
+def _gather_dim(src: TileAssignment, dst: TileAssignment, shape) -> Optional[int]:
+    """The one dim along which ``dst`` is ``src`` all-gathered (no slicing, no permutation)."""
+    from ..spmd.reshard import plan_reshard
+    p = plan_reshard(tuple(shape), src, dst)
+    if p.kind != "all_gather" or len(p.info["dims"]) != 1:
+        return None
+    dim = p.info["dims"][0]
+    return dim if src.unshard([dim]) == dst else None
+
+
+def eligible(kernels: Sequence[ShardedArray], dst: TileAssignment) -> Optional[int]:
+    """Gather dim when every kernel is a 2-D f32 GPU weight that ``dst`` all-gathers along one dim."""
+    if not _ON or not kernels:
+        return None
+    k0 = kernels[0]
+    if k0.ndim != 2 or k0.dtype != torch.float32 or k0.tile == dst:
+        return None
+    for k in kernels:
+        if k.tile != k0.tile or tuple(k.shape) != tuple(k0.shape) or k.dtype != torch.float32:
+            return None
+        if not k.local or not all(t.is_cuda and t.is_contiguous() for t in k.local.values()):
+            return None
+    dim = _gather_dim(k0.tile, dst, k0.shape)
+    if dim is None:
+        return None
+    n = k0.tile.tile_shape[dim]
+    K, N = k0.shape
+    # the shards' shadows: "T" = [N][K_loc] for dim 0 (gather along its columns), [N_loc][K] for dim 1
+    if (K if dim == 0 else N) % n or (K // n if dim == 0 else N // n) % 8:
+        return None
+    return dim
+
+
+class _GatherBf16(torch.autograd.Function):
+    """All local devices at once (a loopback group holds several): f32 shards -> f32 proxies of
+    the gathered weights (the forward moves the shards' bf16 shadows); backward reduce-scatters
+    the proxies' f32 gradients onto the shards."""
+
+    @staticmethod
+    def forward(ctx, meta, *flat):
+        groups, dim, devs, nw, n = meta
+        from ..ops import hip, shadow
+        t_loc = {}
+        for j, d in enumerate(devs):
+            ws = list(flat[j * nw:(j + 1) * nw])
+            # [nw][N_loc][K_loc] shadows in ONE buffer (the fused Adam keeps them there)
+            t_loc[d] = shadow.get(ws[0], "T").unsqueeze(0) if nw == 1 else shadow.get_stacked(ws)
+        # gather along the shadow's K axis (dim 0 of W) or its N axis (dim 1 of W)
+        gdim = 2 if dim == 0 else 1
+        gathered = C._run(C._Spec("all_gather", groups, dim=gdim), t_loc)
+        K_loc, N_loc = flat[0].shape
+        K, N = (K_loc * n, N_loc) if dim == 0 else (K_loc, N_loc * n)
+        outs = []
+        for j, d in enumerate(devs):
+            g = gathered[d]
+            if not g.is_contiguous():
+                g = g.contiguous()                                   # [nw][N][K] bf16
+            for i in range(nw):
+                p = torch.empty((K, N), dtype=torch.float32, device=flat[j * nw].device)
+                shadow.register_proxy(p, g[i])
+                outs.append(p)
+        ctx.meta = meta
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        groups, dim, devs, nw, n = ctx.meta
+        _plan.record("reduce_scatter", groups=groups, note="backward.bf16_shadow_gather")
+        res = [None] * len(gs)
+        for i in range(nw):
+            xs = {}
+            for j, d in enumerate(devs):
+                g = gs[j * nw + i]
+                if g is not None:
+                    xs[d] = g.contiguous()
+            if len(xs) != len(devs):
+                continue
+            red = C._run(C._Spec("reduce_scatter", groups, dim=dim), xs)
+            for j, d in enumerate(devs):
+                res[j * nw + i] = red[d]
+        return (None,) + tuple(res)
+
+
+def gather_bf16(kernels: Sequence[ShardedArray], dst: TileAssignment, dim: int, note: str = "") -> List[ShardedArray]:
+    """The kernels all-gathered along ``dim`` to ``dst`` as bf16-shadow proxies (see module doc)."""
+    k0 = kernels[0]
+    src = k0.tile
+    groups = src.groups_along([dim])
+    n = src.tile_shape[dim]
+    _plan.record("all_gather", dim=dim, groups=tuple(tuple(g) for g in groups),
+                 bytes_in=sum(next(iter(k.local.values())).numel() * 2 for k in kernels),
+                 note=f"{note}.bf16_shadows", dtype="bfloat16", n_weights=len(kernels))
+    sh = sharding_from_tile(dst, like=[k0.sharding])
+    devs = tuple(sorted(k0.local))
+    nw = len(kernels)
+    flat = [k.local[d] for d in devs for k in kernels]
+    outs = _GatherBf16.apply((tuple(tuple(g) for g in groups), dim, devs, nw, n), *flat)
+    return [ShardedArray(k.shape, k.dtype, sh, {d: outs[j * nw + i] for j, d in enumerate(devs)})
+            for i, k in enumerate(kernels)]

@@ -4,7 +4,10 @@ Launched with torchrun (one rank per device; ``LJS_DIST_BACKEND=gloo`` lets seve
 share one GPU) or as a single process (the reference).  The global batch is fixed, so every
 world size must reach the same parameters.  Used by ``tests/test_distributed_gpu.py``.
 
-usage: python scripts/dp_check.py OUT.npz STEPS CAPTURE(0/1) [GLOBAL_BATCH]
+usage: python scripts/dp_check.py OUT.npz STEPS CAPTURE(0/1) [GLOBAL_BATCH] [MESH DxM]
+
+With MESH (e.g. 1x2 or 2x2) the reference's 2-D layout runs: sequence over 'model', Q/K/V
+weights sharded over 'model' (case6_attention.py:155-162,183-187).
 """
 import os
 import sys
@@ -35,7 +38,9 @@ def main():
     from learning_jax_sharding_amd.training import TrainState
 
     n = ljs.device_count()
-    mesh = Mesh(create_device_mesh((n, 1)), ("data", "model"))
+    mshape = tuple(int(v) for v in sys.argv[5].split("x")) if len(sys.argv) > 5 and world > 1 else (n, 1)
+    assert mshape[0] * mshape[1] == n, (mshape, n)
+    mesh = Mesh(create_device_mesh(mshape), ("data", "model"))
     rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
     model = MultiHeadAttention(640, heads=8, dim_head=64)
     xs = NamedSharding(mesh, P("data", "model"))

@@ -18,16 +18,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCRIPT = os.path.join(ROOT, "scripts", "dp_check.py")
 
 
-def _run(tmp_path, world, capture, steps=3, port=29517, wire="bf16"):
-    out = str(tmp_path / f"w{world}_c{capture}_{wire}.npz")
+def _run(tmp_path, world, capture, steps=3, port=29517, wire="bf16", mesh=None, gb=4):
+    out = str(tmp_path / f"w{world}_c{capture}_{wire}_{mesh}.npz")
     env = dict(os.environ, PYTHONPATH=ROOT, LJS_PLATFORM="gpu", LJS_DIST_BACKEND="gloo", LJS_GRAD_COMM_DTYPE=wire)
     env.pop("LJS_NUM_DEVICES", None)
     if world == 1:
-        cmd = [sys.executable, SCRIPT, out, str(steps), str(int(capture))]
+        cmd = [sys.executable, SCRIPT, out, str(steps), str(int(capture)), str(gb)]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr=127.0.0.1", f"--master-port={port + world + 10 * int(capture)}", SCRIPT, out,
-               str(steps), str(int(capture))]
+               str(steps), str(int(capture)), str(gb)] + ([mesh] if mesh else [])
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     return np.load(out)
@@ -57,3 +57,18 @@ def test_dp2_graph_matches_single_process(tmp_path, wire):
             assert diff.max() <= 6e-3 + 1e-6, (k, diff.max())
             assert np.mean(diff > 2e-4 + 2e-3 * np.abs(ref[k])) < 5e-3, (k, np.mean(diff > 2e-4))
         np.testing.assert_allclose(graph[k], eager[k], rtol=1e-5, atol=1e-6, err_msg=f"graph {k}")
+
+
+@pytest.mark.parametrize("world,mesh", [(2, "1x2"), (4, "2x2")])
+def test_2d_layout_matches_single_process(tmp_path, world, mesh):
+    """The reference's 2-D layout (sequence and Q/K/V weights over 'model', batch over 'data') on
+    ranks sharing the GPU: seq-major activations, K/V / head gathers and the out-projection
+    all-to-all as whole-block collectives (no pack kernels) - same parameters as one process."""
+    ref = _run(tmp_path, 1, False, wire="fp32", gb=4)
+    got = _run(tmp_path, world, False, port=29557 + world, wire="fp32", mesh=mesh, gb=4)
+    for k in ref.files:
+        if k == "step":
+            continue
+        diff = np.abs(got[k] - ref[k])
+        assert diff.max() <= 6e-3 + 1e-6, (k, diff.max())
+        assert np.mean(diff > 2e-4 + 2e-3 * np.abs(ref[k])) < 5e-3, (k, np.mean(diff > 2e-4))
