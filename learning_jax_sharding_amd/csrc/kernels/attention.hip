@@ -48,6 +48,12 @@ struct AttnArgs {
   int causal, q_offset;
   int prio_hi_half;  // 8-wave kernels: s_setprio 1 for waves 4-7 (LJS_ATTN_PRIO)
   int flags32;       // attn_bwd_pair32_kernel's dQ blocks: 128 queries (dq32_body), else 64
+  // forward only: running-output merge across key blocks (ring / blockwise context parallelism).
+  // acc_mode 0: plain (bf16 out + lse); 1: first block -> f32 oacc + lse; 2: merge into oacc + lse
+  // by log-sum-exp; 3: merge, write the FINAL bf16 out (+ lse).  oacc: f32, d contiguous.
+  float* oacc;
+  long oa_sb, oa_ss, oa_sh;
+  int acc_mode;
 };
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -224,6 +230,59 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
   }
 }
 
+
+// forward epilogue of one query row (this lane's 16 d-values of it): normalise, and - for
+// blockwise / ring attention - merge with the running (O, lse) of the key blocks seen so far
+// (log-sum-exp in the log2 domain; +inf lse marks "no unmasked key yet"), all in registers.
+__device__ __forceinline__ void fwd_store(const AttnArgs& a, const f32x4 (&o)[4], float m, float lt, int b, int h,
+                                          int qrow, int lane) {
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const float lse_blk = lt > 0.f ? m + __log2f(lt) : INFINITY;
+  const long lidx = ((long)b * a.H + h) * a.Sq + qrow;
+  const int g = lane >> 4;
+  if (a.acc_mode == 0) {
+    bf16_t* op = a.out + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
+    store_row_T(op, o, inv, lane);
+    if (g == 0 && a.lse) a.lse[lidx] = lse_blk;
+    return;
+  }
+  float* ap = a.oacc + b * a.oa_sb + (long)qrow * a.oa_ss + h * a.oa_sh + 4 * g;
+  if (a.acc_mode == 1) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) *reinterpret_cast<f32x4*>(ap + 16 * dt) = o[dt] * inv;
+    if (g == 0) a.lse[lidx] = lse_blk;
+    return;
+  }
+  const float lp = a.lse[lidx];
+  const float x0 = lp == INFINITY ? -INFINITY : lp, x1 = lse_blk == INFINITY ? -INFINITY : lse_blk;
+  const float mx = fmaxf(x0, x1);
+  float cp = 0.f, cb = 0.f, lnew = INFINITY;
+  if (mx != -INFINITY) {
+    const float wp = fast_exp2(x0 - mx), wb = fast_exp2(x1 - mx), tot = wp + wb;
+    cp = wp / tot;
+    cb = wb / tot * inv;
+    lnew = mx + __log2f(tot);
+  }
+  if (a.acc_mode == 2) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const f32x4 prev = *reinterpret_cast<const f32x4*>(ap + 16 * dt);
+      *reinterpret_cast<f32x4*>(ap + 16 * dt) = prev * cp + o[dt] * cb;
+    }
+  } else {
+    bf16_t* op = a.out + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(ap + 16 * dt) * cp + o[dt] * cb;
+      u32x2 w;
+      w[0] = pack_bf16x2(v[0], v[1]);
+      w[1] = pack_bf16x2(v[2], v[3]);
+      *reinterpret_cast<u32x2*>(op + 16 * dt + 4 * g) = w;
+    }
+  }
+  if (g == 0) a.lse[lidx] = lnew;
+}
+
 // K/V-resident forward for Sk <= 256: the whole K and V of the (batch, head) -- at most 2 x
 // 32 KB -- go to LDS in ONE burst of LDS-DMA pieces (issued from asm, swizzle on the source
 // address), so a block pays the HBM latency once instead of once per 64-key tile behind a
@@ -285,13 +344,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
     }
   }
   float lt = row4_sum(st.l);
-  if (qok) {
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    bf16_t* op = a.out + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
-    store_row_T(op, st.o, inv, lane);
-    if ((lane >> 4) == 0 && a.lse)
-      a.lse[((long)b * a.H + h) * a.Sq + qrow] = lt > 0.f ? st.m + __log2f(lt) : INFINITY;
-  }
+  if (qok) fwd_store(a, st.o, st.m, lt, b, h, qrow, lane);
 }
 
 // Persistent K/V-resident forward (Sk <= 256): one workgroup per CU walks work items (query
@@ -373,13 +426,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_pers_kernel(AttnArgs a, int 
       else fwd_tile<false>(a, st, &Ks[buf][kt * BLK * D], &Vs[buf][kt * BLK * D], qf, kbase, qrow, lane);
     }
     const float lt = row4_sum(st.l);
-    if (qrow < a.Sq) {
-      const float inv = lt > 0.f ? 1.f / lt : 0.f;
-      bf16_t* op = a.out + cur.b * a.o_sb + (long)qrow * a.o_ss + cur.h * a.o_sh;
-      store_row_T(op, st.o, inv, lane);
-      if ((lane >> 4) == 0 && a.lse)
-        a.lse[((long)cur.b * a.H + cur.h) * a.Sq + qrow] = lt > 0.f ? st.m + __log2f(lt) : INFINITY;
-    }
+    if (qrow < a.Sq) fwd_store(a, st.o, st.m, lt, cur.b, cur.h, qrow, lane);
     cur = nw;
   }
 }
@@ -456,13 +503,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     const int qrow = qb * QB + 16 * (4 * sb + wave) + (lane & 15);
     float lt = st[sb].l;
     lt = row4_sum(lt);
-    if (qrow < a.Sq) {
-      const float inv = lt > 0.f ? 1.f / lt : 0.f;
-      bf16_t* op = a.out + b * a.o_sb + (long)qrow * a.o_ss + h * a.o_sh;
-      store_row_T(op, st[sb].o, inv, lane);
-      if ((lane >> 4) == 0 && a.lse)
-        a.lse[((long)b * a.H + h) * a.Sq + qrow] = lt > 0.f ? st[sb].m + __log2f(lt) : INFINITY;
-    }
+    if (qrow < a.Sq) fwd_store(a, st[sb].o, st[sb].m, lt, b, h, qrow, lane);
   }
 }
 
@@ -1503,10 +1544,15 @@ LJS_API void ljs_attn_set_fwd_res(int v) { g_fwd_res = v; }
 LJS_API void ljs_attn_set_fwd_nsub(int v) { g_fwd_nsub = v; }
 
 // strides are in elements, ordered (batch, seq, head); head_dim must be 64 and contiguous.
-LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Sq, int Sk,
+static int attn_fwd_impl(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Sq, int Sk,
                          int H, const long* qs, const long* ks, const long* vs, const long* os, float scale,
-                         int causal, int q_offset, hipStream_t stream) {
+                         int causal, int q_offset, void* oacc, const long* oas, int acc_mode, hipStream_t stream) {
   AttnArgs a = {};
+  a.oacc = (float*)oacc;
+  a.acc_mode = acc_mode;
+  if (oas) {
+    a.oa_sb = oas[0]; a.oa_ss = oas[1]; a.oa_sh = oas[2];
+  }
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.out = (bf16_t*)o;
   a.lse = (float*)lse;
   a.q_sb = qs[0]; a.q_ss = qs[1]; a.q_sh = qs[2];
@@ -1560,6 +1606,25 @@ LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, v
   if (nsub == 2) hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(nqb * H * B), dim3(256), 0, stream, a);
   else hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3(nqb * H * B), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
+}
+
+LJS_API int ljs_attn_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Sq, int Sk,
+                         int H, const long* qs, const long* ks, const long* vs, const long* os, float scale,
+                         int causal, int q_offset, hipStream_t stream) {
+  return attn_fwd_impl(q, k, v, o, lse, B, Sq, Sk, H, qs, ks, vs, os, scale, causal, q_offset, nullptr, nullptr, 0,
+                       stream);
+}
+
+// blockwise forward with the running-output merge (ring attention's hop): acc_mode 1 / 2 / 3 (see
+// AttnArgs); oacc f32 [.., d] with strides oas; lse read (modes 2, 3) and rewritten
+LJS_API int ljs_attn_fwd_acc(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Sq, int Sk,
+                             int H, const long* qs, const long* ks, const long* vs, const long* os, float scale,
+                             int causal, int q_offset, void* oacc, const long* oas, int acc_mode, hipStream_t stream) {
+  if (acc_mode < 1 || acc_mode > 3 || !oacc || !lse || (((uintptr_t)oacc) & 15) || oas[1] % 4 || oas[2] % 4 ||
+      oas[0] % 4)
+    return (int)hipErrorInvalidValue;
+  return attn_fwd_impl(q, k, v, o, lse, B, Sq, Sk, H, qs, ks, vs, os, scale, causal, q_offset, oacc, oas, acc_mode,
+                       stream);
 }
 
 // backward implementation for Sk <= 256: 1 = fused single-pass kernel, 0 = split dQ + dK/dV

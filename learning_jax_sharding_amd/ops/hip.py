@@ -34,10 +34,13 @@ _SIGS = {
                       c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
                       ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p, c_void_p],
     "ljs_sum_partials": [c_void_p, c_int, c_void_p, c_int, c_void_p],
+    "ljs_mse_colsum_ws_bytes": [c_int, c_int],
     "ljs_gemm_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long,
                      c_long, c_long, c_long, c_int, c_void_p],
     "ljs_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, _LP, _LP, _LP, _LP,
                      c_float, c_int, c_int, c_void_p],
+    "ljs_attn_fwd_acc": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, _LP, _LP, _LP,
+                         _LP, c_float, c_int, c_int, c_void_p, _LP, c_int, c_void_p],
     "ljs_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_int, c_int, c_int, c_int, _LP, _LP, _LP, _LP, _LP, _LP, _LP, _LP, c_float, c_int,
                      c_int, c_void_p],
@@ -60,6 +63,8 @@ _SIGS = {
     "ljs_adam_multi": [_LP, c_int, c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float,
                        c_void_p],
     "ljs_mse_loss": [c_void_p, c_void_p, c_int, c_long, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    "ljs_mse_colsum": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                       c_void_p],
     "ljs_rng_fill": [c_void_p, c_int, c_int, _LP, _LP, _LP, c_uint, c_uint, c_int, c_float, c_float, c_float,
                      c_float, c_void_p],
 }
@@ -79,6 +84,7 @@ def lib():
                     fn = getattr(L, name)
                     fn.argtypes = argt
                     fn.restype = c_int
+                L.ljs_mse_colsum_ws_bytes.restype = c_long
                 _LIB = L
     return _LIB
 
@@ -703,38 +709,83 @@ def sum_all(t: torch.Tensor, acc_dtype: torch.dtype) -> torch.Tensor:
     return _SumAll.apply(t, acc_dtype)
 
 
+# gradients whose column sums a producer already computed (the fused MSE): data_ptr ->
+# (weakref, version, f32 [C] sums); the dense backward takes its bias gradient from here
+_COLSUMS = {}
+
+
+def register_colsum(g: torch.Tensor, sums: torch.Tensor) -> None:
+    import weakref
+    key = g.data_ptr()
+    ref = weakref.ref(g, lambda _r, k=key: _COLSUMS.pop(k, None) if _COLSUMS.get(k, (None,))[0] is _r else None)
+    _COLSUMS[key] = (ref, g._version, sums, g.numel())
+
+
+def colsum_for(t: torch.Tensor, C: int) -> Optional[torch.Tensor]:
+    """Precomputed column sums of the [R][C] gradient ``t`` (any view of the registered storage
+    with the same element count), or None."""
+    ent = _COLSUMS.get(t.data_ptr())
+    if ent is None:
+        return None
+    g = ent[0]()
+    if g is None or g._version != ent[1] or ent[3] != t.numel() or ent[2].numel() != C:
+        return None
+    return ent[2]
+
+
 class _MSELoss(torch.autograd.Function):
     """scale * sum((y - t)^2) of one shard (bf16 y, f32 / bf16 t).  When y needs a gradient the
-    SAME kernel pass writes dY = bf16(2 * scale * (y - t)) (csrc/kernels/loss.hip): the loss's
-    backward is then free for the constant seed grad() feeds it, a scalar multiply otherwise."""
+    SAME kernel pass writes dY = bf16(2 * scale * (y - t)) and dY's column sums - the bias gradient
+    of the dense layer that produced y (csrc/kernels/loss.hip): the loss's backward is then free
+    for the constant seed grad() feeds it, a scalar multiply otherwise."""
 
     @staticmethod
     def forward(ctx, y, t, scale):
         want_dy = ctx.needs_input_grad[0]
-        y, t = y.contiguous(), t.contiguous()
+        order = storage_order(y)
+        if order is None or order[-1] != y.dim() - 1:
+            y, order = y.contiguous(), tuple(range(y.dim()))
+        yp = y.permute(order)                                    # contiguous: y's storage order
+        tp = t.permute(order).contiguous()                       # the target in the same order
         out = torch.empty((), dtype=torch.float32, device=y.device)
-        dy = torch.empty_like(y) if want_dy else None
-        ws = _workspace(y.device, "mse", (1024 + 33) * 4)
-        rc = lib().ljs_mse_loss(_p(y), _p(t), int(t.dtype == torch.bfloat16), y.numel(), float(scale), _p(dy),
-                                _p(out), _p(ws), _stream(y))
-        _ck(rc, "mse_loss")
-        ctx.save_for_backward(dy)
+        dy = torch.empty_like(yp).permute(_inv(order)) if want_dy else None
+        C = y.shape[-1]
+        R = y.numel() // max(1, C)
+        sums = None
+        if want_dy and C % 64 == 0 and y.dim() >= 2:
+            sums = torch.empty((C,), dtype=torch.float32, device=y.device)
+            nb = lib().ljs_mse_colsum_ws_bytes(R, C)
+            ws = _workspace(y.device, "mse_colsum", nb)
+            rc = lib().ljs_mse_colsum(_p(yp), _p(tp), int(tp.dtype == torch.bfloat16), R, C, float(scale), _p(dy),
+                                      _p(sums), _p(out), _p(ws), _stream(y))
+            _ck(rc, "mse_colsum")
+        else:
+            ws = _workspace(y.device, "mse", (1024 + 33) * 4)
+            rc = lib().ljs_mse_loss(_p(yp), _p(tp), int(tp.dtype == torch.bfloat16), y.numel(), float(scale),
+                                    _p(dy), _p(out), _p(ws), _stream(y))
+            _ck(rc, "mse_loss")
+        ctx.save_for_backward(dy, sums)
         ctx.t_dtype = t.dtype
         return out
 
     @staticmethod
     def backward(ctx, g):
-        dy, = ctx.saved_tensors
+        dy, sums = ctx.saved_tensors
         if dy is None:
             return None, None, None
-        gy = dy if seed_constant(g) == 1.0 else (dy.float() * g.float()).to(dy.dtype)
+        if seed_constant(g) == 1.0:
+            gy = dy
+            if sums is not None:
+                register_colsum(gy, sums)
+        else:
+            gy = (dy.float() * g.float()).to(dy.dtype)
         gt = (-gy).to(ctx.t_dtype) if ctx.needs_input_grad[1] else None
         return gy, gt, None
 
 
 def mse_loss(y: torch.Tensor, t: torch.Tensor, scale: float) -> torch.Tensor:
     ok = (y.dtype == torch.bfloat16 and t.dtype in (torch.float32, torch.bfloat16) and y.shape == t.shape
-          and y.data_ptr() % 16 == 0 and t.data_ptr() % 16 == 0)
+          and y.data_ptr() % 16 == 0 and t.data_ptr() % 16 == 0 and y.shape[-1] % 8 == 0)
     if not ok:
         return ((y.float() - t.float()) ** 2).sum() * scale
     return _MSELoss.apply(y, t, scale)
@@ -1155,6 +1206,24 @@ def attn_fwd_lse(q, k, v, scale: float, causal: bool = False, q_offset: int = 0)
                             q_offset, _stream(q))
     _ck(rc, "ljs_attn_fwd")
     return o, lse
+
+
+def attn_fwd_acc(q, k, v, scale: float, causal: bool, q_offset: int, oacc: torch.Tensor, lse: torch.Tensor, mode: int,
+                 out: Optional[torch.Tensor] = None):
+    """One key block of a blockwise (ring) forward merged INTO the running result in the kernel's
+    epilogue: mode 1 starts (f32 ``oacc`` [B,Sq,H,D] + ``lse``), 2 merges by log-sum-exp, 3 merges
+    and writes the final bf16 ``out`` (returned).  No per-hop torch merge kernels."""
+    B, Sq, H, D = q.shape
+    Sk = k.shape[1]
+    assert oacc.dtype == torch.float32 and oacc.stride(3) == 1 and lse.dtype == torch.float32
+    if mode == 3 and out is None:
+        out = _bs_like((B, Sq, H, D), q)
+    o = out if out is not None else q   # (unused unless mode 3)
+    rc = lib().ljs_attn_fwd_acc(_p(q), _p(k), _p(v), _p(o), _p(lse), B, Sq, Sk, H, _longs(_strides3(q)),
+                                _longs(_strides3(k)), _longs(_strides3(v)), _longs(_strides3(o)), scale, int(causal),
+                                q_offset, _p(oacc), _longs(_strides3(oacc)), int(mode), _stream(q))
+    _ck(rc, "ljs_attn_fwd_acc")
+    return out
 
 
 def attn_bwd_block(q, k, v, o, do, lse, scale: float, causal: bool = False, q_offset: int = 0):

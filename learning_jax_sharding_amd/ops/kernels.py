@@ -187,6 +187,49 @@ def attention_fwd_lse(q, k, v, scale: float, causal: bool = False, q_offset: int
     return o, lse
 
 
+def attention_fwd_merge(q, k, v, scale: float, causal: bool, q_offset: int, state, last: bool):
+    """One key block of a blockwise forward merged into ``state`` = [o_acc f32, lse] (None before the
+    first block).  On GPU the merge happens in the kernel's epilogue; ``last`` makes it write and
+    return the final output in v's dtype (else returns None)."""
+    if use_hip(q):
+        B, Sq, H, D = q.shape
+        if state[0] is None:
+            state[0] = torch.empty((B, Sq, H, D), dtype=torch.float32, device=q.device)
+            state[1] = torch.empty((B, H, Sq), dtype=torch.float32, device=q.device)
+            mode = 1
+        else:
+            mode = 3 if last else 2
+        if mode == 1 and last:
+            # a single block: the plain forward (bf16 out + lse)
+            o, lse = _hip().attn_fwd_lse(q, k, v, scale, causal, q_offset)
+            state[1] = lse
+            return o
+        out = _hip().attn_fwd_acc(q, k, v, scale, causal, q_offset, state[0], state[1], mode)
+        return out if last else None
+    o_s, l_s = attention_fwd_lse(q, k, v, scale, causal, q_offset)
+    if state[0] is None:
+        state[0], state[1] = o_s.float(), l_s
+    else:
+        state[0], state[1] = _merge_lse(state[0], state[1], o_s, l_s)
+    return state[0].to(v.dtype) if last else None
+
+
+def _merge_lse(o, lse, o_s, lse_s):
+    """Merge two partial attention results (o normalised per part, lse in log2; +inf = no keys)."""
+    neg = torch.full_like(lse, float("-inf"))
+    a = torch.where(torch.isinf(lse) & (lse > 0), neg, lse)
+    b = torch.where(torch.isinf(lse_s) & (lse_s > 0), neg, lse_s)
+    m = torch.maximum(a, b)
+    m0 = torch.where(torch.isinf(m), torch.zeros_like(m), m)
+    wa, wb = torch.exp2(a - m0), torch.exp2(b - m0)
+    tot = wa + wb
+    lse_new = torch.where(tot > 0, m0 + torch.log2(tot), torch.full_like(m, float("inf")))
+    inv = torch.where(tot > 0, 1.0 / tot, torch.zeros_like(tot))
+    ca = (wa * inv).permute(0, 2, 1)[..., None]
+    cb = (wb * inv).permute(0, 2, 1)[..., None]
+    return o.float() * ca + o_s.float() * cb, lse_new
+
+
 def attention_bwd_block(q, k, v, o, do, lse, scale: float, causal: bool = False, q_offset: int = 0):
     """One kv block's (dq, dk, dv) given the final output ``o`` and global (log2) ``lse``."""
     if use_hip(q):

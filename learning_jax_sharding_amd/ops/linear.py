@@ -392,7 +392,10 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *dys):
         lead, K, M, N, nw, relu, xdtype, has_b = ctx.meta
-        order, pshape = ctx.order, ctx.pshape
+        order = getattr(ctx, "order", None)          # (the fp8 dense reuses this backward in row order)
+        pshape = ctx.pshape if order is not None else tuple(lead)
+        if order is None:
+            order = tuple(range(len(lead) + 1))
         # the residual's gradient is the output gradient itself (y = dense(x) + res)
         dres = dys[0] if (ctx.has_res and ctx.needs_input_grad[2]) else None
         # every [M][N] view below is in the forward's row (storage) order
@@ -493,6 +496,10 @@ class _Linear(torch.autograd.Function):
                     tot = db_bcast[i] if tot is None else tot + db_bcast[i]
                     continue
                 t, ld = mats[i]
+                pre = hip.colsum_for(t, N) if ld > 0 else None
+                if pre is not None:   # the loss kernel that produced dY summed its columns already
+                    tot = pre if tot is None else tot + pre
+                    continue
                 tot = hip.colsum_ld(t, M, N, ld, tot)
             db = tot.to(b.dtype)
         if joint is not None:

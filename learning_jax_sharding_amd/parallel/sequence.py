@@ -19,7 +19,10 @@ Two schedules are provided on (batch, seq, heads, head_dim) arrays whose seq dim
 Memory per device is O(S/n) for K/V instead of O(S), the stepping stone to long-context
 training on 288 GB parts; on xGMI the hop is a point-to-point neighbour transfer, one link.
 Each hop's K/V transfer is issued on a side HIP stream before the current block's flash
-kernel and joined after it, so the transfer overlaps the attention compute.
+kernel and joined after it, so the transfer overlaps the attention compute.  The
+partial softmaxes are merged by log-sum-exp INSIDE the forward kernel's epilogue (running f32
+output + lse, ``ops.kernels.attention_fwd_merge``), and in the backward the dK/dV accumulators'
+hops run on the side stream while the next block's backward computes.
 """
 from __future__ import annotations
 
@@ -72,6 +75,7 @@ def _rotate_async(bufs: List[Dict[int, torch.Tensor]], nxt: Dict[int, int]):
     current stream's producers), so the hop overlaps the attention block computed meanwhile on
     the compute stream.  Returns a thunk that makes the compute stream wait for the hop and
     hands back the rotated dicts (host devices: the hop simply runs)."""
+    import contextlib
     t0 = next(iter(bufs[0].values()))
     if not t0.is_cuda:
         out = [_rotate(b, nxt) for b in bufs]
@@ -84,9 +88,11 @@ def _rotate_async(bufs: List[Dict[int, torch.Tensor]], nxt: Dict[int, int]):
             side = _SIDE[g] = torch.cuda.Stream(device=g)
         side.wait_stream(torch.cuda.current_stream(g))
     streams = [_SIDE[g] for g in gpus]
-    # one process drives each GPU's side stream in turn; a single-GPU run (virtual devices or
-    # one rank per GPU) has exactly one
-    with torch.cuda.stream(streams[0]):
+    # every GPU's side stream is made current for its device (a single-controller run drives
+    # several GPUs from this thread; one rank per GPU has exactly one)
+    with contextlib.ExitStack() as es:
+        for st in streams:
+            es.enter_context(torch.cuda.stream(st))
         out = [_rotate(b, nxt) for b in bufs]
         for g, st in zip(gpus, streams):
             ev = torch.cuda.Event()
@@ -104,23 +110,6 @@ def _rotate_async(bufs: List[Dict[int, torch.Tensor]], nxt: Dict[int, int]):
     return join
 
 
-def _merge(o, lse, o_s, lse_s):
-    """Merge two partial attention results (o normalised per part, lse in log2)."""
-    neg = torch.full_like(lse, float("-inf"))
-    a = torch.where(torch.isinf(lse) & (lse > 0), neg, lse)        # +inf marks "no keys"
-    b = torch.where(torch.isinf(lse_s) & (lse_s > 0), neg, lse_s)
-    m = torch.maximum(a, b)
-    m0 = torch.where(torch.isinf(m), torch.zeros_like(m), m)
-    wa, wb = torch.exp2(a - m0), torch.exp2(b - m0)
-    tot = wa + wb
-    lse_new = torch.where(tot > 0, m0 + torch.log2(tot), torch.full_like(m, float("inf")))
-    inv = torch.where(tot > 0, 1.0 / tot, torch.zeros_like(tot))
-    ca = (wa * inv).permute(0, 2, 1)[..., None]                      # [b, q, h, 1]
-    cb = (wb * inv).permute(0, 2, 1)[..., None]
-    o_new = o.float() * ca + o_s.float() * cb
-    return o_new, lse_new
-
-
 class _RingAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, meta, devs, *flat):
@@ -129,39 +118,36 @@ class _RingAttention(torch.autograd.Function):
         q = dict(zip(devs, flat[:nd]))
         kk = dict(zip(devs, flat[nd:2 * nd]))
         vv = dict(zip(devs, flat[2 * nd:]))
-        o = {d: None for d in devs}
-        lse = {d: None for d in devs}
+        # the hops each device computes (causal: blocks entirely above the diagonal are skipped);
+        # the last one writes the final output
+        hops = {d: [s for s in range(n) if not (causal and (pos[d] - s) % n > pos[d])] for d in devs}
+        state = {d: [None, None] for d in devs}            # running (O f32, lse), merged in-kernel
+        out = {}
         kb, vb = dict(kk), dict(vv)
         for s in range(n):
             # hop s+1's K/V transfer runs on the side stream while block s computes
             pending = _rotate_async([kb, vb], nxt) if s + 1 < n else None
             for d in devs:
+                if s not in hops[d]:
+                    continue
                 j = (pos[d] - s) % n                       # global block index of the kv in hand
-                if causal and j > pos[d]:
-                    continue                               # block entirely above the diagonal
-                o_s, l_s = K.attention_fwd_lse(q[d], kb[d], vb[d], scale, causal, (pos[d] - j) * s_loc)
-                if o[d] is None:
-                    o[d], lse[d] = o_s.float(), l_s
-                else:
-                    o[d], lse[d] = _merge(o[d], lse[d], o_s, l_s)
+                r = K.attention_fwd_merge(q[d], kb[d], vb[d], scale, causal, (pos[d] - j) * s_loc, state[d],
+                                          last=s == hops[d][-1])
+                if r is not None:
+                    out[d] = r
             if pending is not None:
                 kb, vb = pending()
-        outs = []
-        for d in devs:
-            if o[d] is None:                                # only possible for n == 0
-                o[d] = torch.zeros_like(q[d], dtype=torch.float32)
-                lse[d] = torch.full(q[d].shape[:1] + q[d].shape[2:3] + q[d].shape[1:2], float("inf"),
-                                    device=q[d].device)
-            outs.append(o[d].to(vv[d].dtype))
+        outs = [out[d] for d in devs]
         ctx.meta = meta
         ctx.devs = devs
-        ctx.save_for_backward(*flat, *outs, *[lse[d] for d in devs])
+        ctx.hops = hops
+        ctx.save_for_backward(*flat, *outs, *[state[d][1] for d in devs])
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *gos):
         scale, causal, pos, n, nxt, prv, s_loc = ctx.meta
-        devs = ctx.devs
+        devs, hops = ctx.devs, ctx.hops
         nd = len(devs)
         saved = ctx.saved_tensors
         q = dict(zip(devs, saved[:nd]))
@@ -170,29 +156,39 @@ class _RingAttention(torch.autograd.Function):
         o = dict(zip(devs, saved[3 * nd:4 * nd]))
         lse = dict(zip(devs, saved[4 * nd:5 * nd]))
         do = {d: (g if g is not None else torch.zeros_like(o[d])) for d, g in zip(devs, gos)}
-        dq = {d: torch.zeros(q[d].shape, dtype=torch.float32, device=q[d].device) for d in devs}
-        dk = {d: torch.zeros(kb[d].shape, dtype=torch.float32, device=kb[d].device) for d in devs}
-        dv = {d: torch.zeros(vb[d].shape, dtype=torch.float32, device=vb[d].device) for d in devs}
+        dq = {d: None for d in devs}
+        acc = None                 # join thunk of the dK/dV accumulators in flight
         for s in range(n):
-            # the next K/V blocks travel on the side stream during this block's backward; the
-            # gradient accumulators follow once this block has added to them
+            # the next K/V blocks travel on the side stream during this block's backward
             pending = _rotate_async([kb, vb], nxt) if s + 1 < n else None
+            contrib = {}
             for d in devs:
-                j = (pos[d] - s) % n
-                if causal and j > pos[d]:
+                if s not in hops[d]:
                     continue
+                j = (pos[d] - s) % n
                 gq, gk, gv = K.attention_bwd_block(q[d], kb[d], vb[d], o[d], do[d], lse[d], scale, causal,
                                                    (pos[d] - j) * s_loc)
-                dq[d] += gq.float()
-                dk[d] += gk.float()
-                dv[d] += gv.float()
-            # the kv blocks and their gradient accumulators travel together; n hops bring
-            # every accumulator back to the block's owner
-            dk, dv = _rotate(dk, nxt), _rotate(dv, nxt)
+                dq[d] = gq.float() if dq[d] is None else dq[d].add_(gq)
+                contrib[d] = (gk, gv)
+            # the dK/dV accumulators travel with their kv blocks; each hop is started as soon as
+            # this block has added to them and lands while the NEXT block computes (only the add
+            # waits for it); n hops bring every accumulator home
+            if acc is None:
+                dk = {d: (contrib[d][0].float() if d in contrib else torch.zeros(kb[d].shape, dtype=torch.float32,
+                                                                                 device=kb[d].device)) for d in devs}
+                dv = {d: (contrib[d][1].float() if d in contrib else torch.zeros(vb[d].shape, dtype=torch.float32,
+                                                                                 device=vb[d].device)) for d in devs}
+            else:
+                dk, dv = acc()
+                for d, (gk, gv) in contrib.items():
+                    dk[d].add_(gk)
+                    dv[d].add_(gv)
+            acc = _rotate_async([dk, dv], nxt)
             if pending is not None:
                 kb, vb = pending()
-        grads = [dq[d].to(q[d].dtype) for d in devs] + [dk[d].to(kb[d].dtype) for d in devs] + \
-            [dv[d].to(vb[d].dtype) for d in devs]
+        dk, dv = acc()
+        grads = [(dq[d] if dq[d] is not None else torch.zeros_like(q[d], dtype=torch.float32)).to(q[d].dtype)
+                 for d in devs] + [dk[d].to(kb[d].dtype) for d in devs] + [dv[d].to(vb[d].dtype) for d in devs]
         return (None, None) + tuple(grads)
 
 

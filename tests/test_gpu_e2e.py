@@ -293,3 +293,30 @@ def test_mse_loss_kernel_matches_torch(gpu_devices):
         assert abs(float(loss) - float(ref)) <= 1e-4 * float(ref)
         ref_g = (2 * scale * (yf - t.float()))
         np.testing.assert_allclose(gy.float().cpu().numpy(), ref_g.cpu().numpy(), rtol=1e-2, atol=1e-9)
+
+
+def test_mse_colsum_kernel_and_bias_grad(gpu_devices):
+    """The fused MSE (value + dY + dY's column sums in one pass) under a dense layer with a bias:
+    value, input gradient and bias gradient vs the f32 torch oracle; also for a seq-major
+    prediction (y stored [seq][batch][features])."""
+    gpu_devices(1)
+    from learning_jax_sharding_amd.ops import hip
+    torch.manual_seed(0)
+    for seq_major in (False, True):
+        x = torch.randn(8, 128, 256, device="cuda")
+        w = (torch.randn(256, 640, device="cuda") * 0.05).requires_grad_(True)
+        b = (torch.randn(640, device="cuda") * 0.1).requires_grad_(True)
+        t = torch.randn(8, 128, 640, device="cuda")
+        xin = x.transpose(0, 1).contiguous().transpose(0, 1) if seq_major else x
+        y = hip.linear(xin, [w], b, torch.bfloat16, False, torch.bfloat16)[0]
+        loss = hip.mse_loss(y, t, 1.0 / y.numel())
+        gw, gb = torch.autograd.grad(loss, (w, b), torch.tensor(1.0, device="cuda"))
+        yr = y.detach().float()
+        ref_loss = ((yr - t) ** 2).mean()
+        dy = (2.0 / y.numel()) * (yr - t)
+        ref_gb = dy.to(torch.bfloat16).float().sum((0, 1))
+        ref_gw = x.reshape(-1, 256).bfloat16().float().t() @ dy.to(torch.bfloat16).float().reshape(-1, 640)
+        assert abs(float(loss) - float(ref_loss)) <= 1e-4 * float(ref_loss)
+        np.testing.assert_allclose(gb.cpu().numpy(), ref_gb.cpu().numpy(), rtol=2e-3, atol=1e-7)
+        np.testing.assert_allclose(gw.cpu().numpy(), ref_gw.cpu().numpy(), rtol=2e-2,
+                                   atol=2e-2 * float(ref_gw.abs().max()))

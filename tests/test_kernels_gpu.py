@@ -839,3 +839,27 @@ def test_linear_f32_input_cast_on_load(hip, monkeypatch):
         res[flag] = [y.clone() for y in ys] + [g.clone() for g in gs]
     for a, b in zip(res[False], res[True]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("sk", [128, 512])
+def test_attention_fwd_inkernel_lse_merge(causal, sk):
+    """Ring attention's forward: key blocks merged by log-sum-exp in the kernel epilogue (f32
+    running output + lse, modes 1 / 2 / 3) == one attention over all keys (f32 oracle), including
+    a causal block that is fully masked for some rows (+inf lse)."""
+    from learning_jax_sharding_amd.ops import hip, kernels as K
+    torch.manual_seed(0)
+    B, Sq, H = 2, 128, 4
+    nblk = 3
+    q = torch.randn(B, Sq, H, 64, device="cuda").bfloat16()
+    k = torch.randn(B, nblk * sk, H, 64, device="cuda").bfloat16()
+    v = torch.randn(B, nblk * sk, H, 64, device="cuda").bfloat16()
+    q_off = sk if causal else 0     # causal: queries aligned with block 1 -> block 2 fully masked (+inf lse)
+    ref = K.attention_reference(q, k, v, 0.125, causal, q_off).float()
+    state = [None, None]
+    out = None
+    for i in range(nblk):
+        kb, vb = k[:, i * sk:(i + 1) * sk], v[:, i * sk:(i + 1) * sk]
+        out = K.attention_fwd_merge(q, kb, vb, 0.125, causal, q_off - i * sk, state, last=i == nblk - 1)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.float().cpu().numpy(), ref.cpu().numpy(), rtol=2e-2, atol=2e-2)
