@@ -338,7 +338,7 @@ class DistComm:
         if pg is None:
             return {self.me: x.clone()}
         n = len(g)
-        grp = self._p2p(g, pg, x.contiguous())
+        grp = self._p2p(g, pg, x)
         nh = None if grp is not None else self._nat(groups, x)
         if grp is not None:
             buf = grp.all_gather({grp.rank: x.contiguous()})[grp.rank]
@@ -361,7 +361,7 @@ class DistComm:
         n = len(g)
         # chunk k belongs to member g[k]; the collective hands chunk r to the r-th sorted rank
         xt = _hip().rank_major(x, dim, n, None if self._member_order_ok(g) else [g.index(d) for d in sorted(g)])
-        grp = self._p2p(g, pg, xt.contiguous(), chunked=True)
+        grp = self._p2p(g, pg, xt, chunked=True)
         if grp is not None:
             return {self.me: grp.reduce_scatter({grp.rank: xt.contiguous()})[grp.rank]}
         out = torch.empty_like(xt[0])          # the chunk's own dim order
@@ -401,7 +401,7 @@ class DistComm:
         srt = sorted(g)
         # the chunk sent to group member at tile position i is chunk perm[i]; order sends by sorted rank
         send = _hip().rank_major(x, split_dim, n, [perm[g.index(r)] for r in srt])
-        grp = self._p2p(g, pg, send.contiguous(), chunked=True)
+        grp = self._p2p(g, pg, send, chunked=True)
         nh = None if grp is not None else self._nat(groups, send)
         if grp is not None:
             recv = grp.all_to_all({grp.rank: send.contiguous()})[grp.rank]

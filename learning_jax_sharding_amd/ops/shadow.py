@@ -35,10 +35,21 @@ class _Entry:
 
 
 _REG: Dict[Tuple, _Entry] = {}
+import os as _os
+_TRACE = _os.environ.get("LJS_SHADOW_TRACE", "0") == "1"
 
 
 def _key(w: torch.Tensor):
     return (w.data_ptr(), w.dtype, tuple(w.shape), tuple(w.stride()), w.device)
+
+
+def _owner_of(w: torch.Tensor) -> torch.Tensor:
+    """The persistent tensor whose storage ``w`` views: the parameter an autograd leaf was
+    detached from (``spmd.api._fresh_leaf`` records it), else ``w`` itself.  Shadows are owned by
+    it, so they survive the per-step leaves (a sharded weight's shadow would otherwise be re-cast
+    every step once the leaf is gone before the optimizer adopts it)."""
+    b = getattr(w, "_ljs_base", None)
+    return b if b is not None and b.data_ptr() == w.data_ptr() else w
 
 
 def entry(w: torch.Tensor, create: bool = True) -> Optional[_Entry]:
@@ -50,7 +61,7 @@ def entry(w: torch.Tensor, create: bool = True) -> Optional[_Entry]:
             e = None
             _REG.pop(k, None)
     if e is None and create:
-        e = _Entry(w)
+        e = _Entry(_owner_of(w))
         _REG[k] = e
     return e
 
@@ -87,6 +98,10 @@ def _refresh(w: torch.Tensor, e: _Entry, kind: str) -> torch.Tensor:
                                    f"gathered bf16 copy (kind {kind!r}); the proxy holds no f32 values")
         return buf
     if e.versions.get(kind) != w._version:
+        if _TRACE:
+            import sys
+            print(f"[shadow] refresh {kind} {tuple(w.shape)} ptr={w.data_ptr():#x} ver={w._version} "
+                  f"had={e.versions.get(kind)} owner_alive={e.ref() is not None}", file=sys.stderr)
         if kind == "T":
             hip.cast_transpose_bf16(w, buf)
         else:

@@ -275,7 +275,9 @@ def _fresh_leaf(x: ShardedArray) -> ShardedArray:
     loc = {}
     for d, t in x.local.items():
         if t.dtype.is_floating_point:
-            loc[d] = t.detach().requires_grad_(True)
+            leaf = t.detach().requires_grad_(True)
+            leaf._ljs_base = t      # the persistent parameter (owner of its bf16 shadows, ops/shadow.py)
+            loc[d] = leaf
         else:
             loc[d] = t
     return ShardedArray(x.shape, x.dtype, x.sharding, loc)
