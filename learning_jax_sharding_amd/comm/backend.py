@@ -349,7 +349,8 @@ class DistComm:
             if nh is not None:
                 self._native.all_gather(nh, x, buf)
             else:
-                dist.all_gather_into_tensor(_hip().flat(buf), _hip().flat(x), group=pg)
+                if not self._fake:   # rehearsal: collectives move nothing (not even torch's fake copies)
+                    dist.all_gather_into_tensor(_hip().flat(buf), _hip().flat(x), group=pg)
         order = None if self._member_order_ok(g) else [sorted(g).index(d) for d in g]
         return {self.me: _hip().from_rank_major(buf, dim, order)}
 
@@ -369,7 +370,8 @@ class DistComm:
         if nh is not None:
             self._native.reduce_scatter(nh, xt, out)
             return {self.me: out}
-        dist.reduce_scatter_tensor(_hip().flat(out), _hip().flat(xt), group=pg)
+        if not self._fake:
+            dist.reduce_scatter_tensor(_hip().flat(out), _hip().flat(xt), group=pg)
         return {self.me: out}
 
     def all_reduce(self, xs, groups):
@@ -387,7 +389,8 @@ class DistComm:
             elif nh is not None:
                 self._native.all_reduce_(nh, x)
             else:
-                dist.all_reduce(_hip().flat(x) if _hip().is_dense(x) else x, group=pg)
+                if not self._fake:
+                    dist.all_reduce(_hip().flat(x) if _hip().is_dense(x) else x, group=pg)
         return {self.me: x}
 
     def all_to_all(self, xs, groups, split_dim, concat_dim, perms=None):
@@ -409,7 +412,8 @@ class DistComm:
             recv = self._native.all_to_all(nh, send, torch.empty_like(send), n)
         else:
             recv = torch.empty_like(send)
-            dist.all_to_all_single(_hip().flat(recv).view(n, -1), _hip().flat(send).view(n, -1), group=pg)
+            if not self._fake:
+                dist.all_to_all_single(_hip().flat(recv).view(n, -1), _hip().flat(send).view(n, -1), group=pg)
         # recv[k] came from sorted rank srt[k]; concatenate in member (tile) order
         return {self.me: _hip().from_rank_major(recv, concat_dim, [srt.index(d) for d in g])}
 

@@ -54,9 +54,11 @@ struct AttnArgs {
   float* oacc;
   long oa_sb, oa_ss, oa_sh;
   int acc_mode;
+  int fwd_prog;      // resident forward: per-key-tile waits (1) or one wait for the whole burst (0)
 };
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 
 // XCD-aware 3-D tile index of a 1-D grid of nx * H * B blocks: blocks sharing an XCD (dealt
 // round-robin by block id) take CONSECUTIVE tiles, so the query blocks of one (batch, head)
@@ -302,10 +304,18 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
   int kend = a.Sk;
   if (a.causal) kend = min(a.Sk, a.q_offset + (qb + 1) * QB);
   const int nkt = (kend + BLK - 1) / BLK;
+  // Q fragments first: the oldest loads, so the per-key-tile waits below never hold a tile's
+  // compute behind them
+  const int qrow = qb * QB + 16 * wave + (lane & 15);
+  const bool qok = qrow < a.Sq;
+  const bf16_t* qp = a.q + b * a.q_sb + (long)qrow * a.q_ss + h * a.q_sh;
+  bf16x8 qf[2];
+  qf[0] = load_row_frag(qp, qok, 0, lane);
+  qf[1] = load_row_frag(qp, qok, 1, lane);
   {
     const u32x4 rk = rsrc_u4(kb, 2 * ((long)(a.Sk - 1) * a.k_ss + D));
     const u32x4 rv = rsrc_u4(vb, 2 * ((long)(a.Sk - 1) * a.v_ss + D));
-    const int npieces = nkt * (BLK / 8);  // 8 rows x 128 B per 1 KiB piece
+    const int npieces = nkt * (BLK / 8);  // 8 rows x 128 B per 1 KiB piece, key-tile major
     for (int pc = wave; pc < npieces; pc += NW) {
       const int row = 8 * pc + (lane >> 3);
       const int c = ((lane & 7) ^ (((row >> 1) & 3) << 1)) * 8;
@@ -314,24 +324,37 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
       dma_lds_x4(rv, ok ? (int)(((long)row * a.v_ss + c) * 2) : 0x7ffffff0, Vs + pc * 512);
     }
   }
-  const int qrow = qb * QB + 16 * wave + (lane & 15);
-  const bool qok = qrow < a.Sq;
-  const bf16_t* qp = a.q + b * a.q_sb + (long)qrow * a.q_ss + h * a.q_sh;
   if (a.prio_hi_half && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  bf16x8 qf[2];
-  qf[0] = load_row_frag(qp, qok, 0, lane);
-  qf[1] = load_row_frag(qp, qok, 1, lane);
   FwdState st;
 #pragma unroll
   for (int i = 0; i < 4; ++i) st.o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   st.m = -INFINITY;
   st.l = 0.f;
+  const int qrow0 = qb * QB + 16 * wave;
+  if constexpr (NW <= 8) {
+    if ((a.Sk % BLK) == 0 && !a.causal && a.fwd_prog) {
+      // no tile needs a mask: one tile instance (with both in the loop the compiler copied the O
+      // accumulators at their join on every key tile).  Each key tile's compute starts as soon
+      // as ITS pieces have landed (counted vmcnt: this wave issued 2 * 8 / NW per tile, in tile
+      // order; the barrier covers the other waves' pieces) while the later tiles still stream in
+      constexpr int PER = 2 * (8 / NW);
+      for (int kt = 0; kt < nkt; ++kt) {
+        const int left = nkt - 1 - kt;
+        if (left >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory");
+        else if (left == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+        else if (left == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kt * BLK, qrow, lane);
+      }
+      float lt = row4_sum(st.l);
+      if (qok) fwd_store(a, st.o, st.m, lt, b, h, qrow, lane);
+      return;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int qrow0 = qb * QB + 16 * wave;
   if ((a.Sk % BLK) == 0 && !a.causal) {
-    // no tile needs a mask: one tile instance (with both in the loop the compiler copied the O
-    // accumulators at their join on every key tile)
     for (int kt = 0; kt < nkt; ++kt)
       fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kt * BLK, qrow, lane);
   } else {
@@ -1548,6 +1571,8 @@ static int attn_fwd_impl(const void* q, const void* k, const void* v, void* o, v
                          int H, const long* qs, const long* ks, const long* vs, const long* os, float scale,
                          int causal, int q_offset, void* oacc, const long* oas, int acc_mode, hipStream_t stream) {
   AttnArgs a = {};
+  static const int prog = getenv("LJS_ATTN_FWD_PROG") ? atoi(getenv("LJS_ATTN_FWD_PROG")) : 1;
+  a.fwd_prog = prog;
   a.oacc = (float*)oacc;
   a.acc_mode = acc_mode;
   if (oas) {

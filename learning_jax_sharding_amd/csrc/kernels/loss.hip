@@ -82,9 +82,18 @@ __global__ void __launch_bounds__(256) mse_kernel(const bf16_t* __restrict__ y, 
   if (lane == 0) last = ticket_last_2lvl(ticket, blockIdx.x, gridDim.x);
   last = __shfl(last, 0, 64);
   if (!last) return;
-  float v = 0.f;
-  for (int k = lane; k < (int)gridDim.x; k += 64) v += sc1_load(partials + k);
-  v = warp_sum64(v);
+  // the last arriver sums the partials with 4 independent loads in flight per lane
+  float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+  const int G = (int)gridDim.x;
+  int k = lane;
+  for (; k + 192 < G; k += 256) {
+    v0 += sc1_load(partials + k);
+    v1 += sc1_load(partials + k + 64);
+    v2 += sc1_load(partials + k + 128);
+    v3 += sc1_load(partials + k + 192);
+  }
+  for (; k < G; k += 64) v0 += sc1_load(partials + k);
+  float v = warp_sum64((v0 + v1) + (v2 + v3));
   if (lane == 0) *out = v * scale;
 }
 
@@ -169,11 +178,12 @@ __global__ void __launch_bounds__(256) mse_colsum_kernel(const bf16_t* __restric
   s = warp_sum64(s);
   if ((threadIdx.x & 63) == 0) lred[threadIdx.x >> 6] = s;
   __syncthreads();
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nblk = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
   unsigned* col_tickets = tickets;                 // one per column block
   unsigned* loss_tickets = tickets + gridDim.x;    // two-level over all blocks
-  __shared__ int last_col;
+  __shared__ int last_col, last_all;
+  __shared__ float fin[4][64];
   if (threadIdx.x < 64) {
     const int c = blockIdx.x * 64 + lane;
     float cs = 0.f;
@@ -181,27 +191,42 @@ __global__ void __launch_bounds__(256) mse_colsum_kernel(const bf16_t* __restric
     if (c < C) sc1_store(col_part + (long)blockIdx.y * C + c, cs);
     if (lane == 0) sc1_store(loss_part + bid, lred[0] + lred[1] + lred[2] + lred[3]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) last_col = ticket_last(col_tickets + blockIdx.x, gridDim.y);
+    if (lane == 0) {
+      last_col = ticket_last(col_tickets + blockIdx.x, gridDim.y);
+      last_all = ticket_last_2lvl(loss_tickets, bid, nblk);
+    }
   }
   __syncthreads();
-  if (last_col && threadIdx.x < 64) {
+  // the last row block of this column block sums its column partials: 4 waves x row slices,
+  // 2 independent loads in flight per lane, then across the waves through LDS
+  if (last_col) {
     const int c = blockIdx.x * 64 + lane;
+    float t0 = 0.f, t1 = 0.f;
     if (c < C) {
-      float t = 0.f;
-      for (int yb = 0; yb < (int)gridDim.y; ++yb) t += sc1_load(col_part + (long)yb * C + c);
-      colsum[c] = t;
+      int yb = w;
+      for (; yb + 4 < (int)gridDim.y; yb += 8) {
+        t0 += sc1_load(col_part + (long)yb * C + c);
+        t1 += sc1_load(col_part + (long)(yb + 4) * C + c);
+      }
+      for (; yb < (int)gridDim.y; yb += 4) t0 += sc1_load(col_part + (long)yb * C + c);
     }
+    fin[w][lane] = t0 + t1;
+    __syncthreads();
+    if (w == 0 && c < C) colsum[c] = (fin[0][lane] + fin[1][lane]) + (fin[2][lane] + fin[3][lane]);
+    __syncthreads();
   }
-  if (threadIdx.x < 64) {
-    int last = 0;
-    if (lane == 0) last = ticket_last_2lvl(loss_tickets, bid, nblk);
-    last = __shfl(last, 0, 64);
-    if (last) {
-      float v = 0.f;
-      for (int k = lane; k < nblk; k += 64) v += sc1_load(loss_part + k);
-      v = warp_sum64(v);
-      if (lane == 0) *out = v * scale;
+  if (last_all) {
+    float v0 = 0.f, v1 = 0.f;
+    int k = threadIdx.x;
+    for (; k + 256 < nblk; k += 512) {
+      v0 += sc1_load(loss_part + k);
+      v1 += sc1_load(loss_part + k + 256);
     }
+    for (; k < nblk; k += 256) v0 += sc1_load(loss_part + k);
+    const float v = warp_sum64(v0 + v1);
+    if (lane == 0) fin[w][0] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) *out = ((fin[0][0] + fin[1][0]) + (fin[2][0] + fin[3][0])) * scale;
   }
 }
 

@@ -36,14 +36,14 @@ cd "$R"
 echo done2
 # MX-fp8 FF GEMMs (T=16384): up projection 640 -> 2560 with the fp8 copy, down projection 2560 -> 640
 cd /tmp
-for cfg in "2560 640 1282 20 qout" "640 2560 1282 20 res" "2560 640 2562 20 qout" "2560 640 1283 20 qout"; do
+for cfg in "2560 640 1282 20 qboth" "2560 640 1282 20 qout" "2560 640 1282 20 plain" "640 2560 1282 20 res" "2560 640 2562 20 qboth" "2560 640 1283 20 qboth"; do
   tag=$(echo $cfg | tr ' ' '_')
   timeout -k 10 120 python3 $R/scripts/fp8_one.py $cfg > $O/f8_$tag.time 2>&1
 done
-run f8_up_1 "$P1" python3 $R/scripts/fp8_one.py 2560 640 1282 10 qout
-run f8_up_2 "$P2" python3 $R/scripts/fp8_one.py 2560 640 1282 10 qout
-run f8_up_3 "$P3" python3 $R/scripts/fp8_one.py 2560 640 1282 10 qout
-run f8_up_4 "$P4" python3 $R/scripts/fp8_one.py 2560 640 1282 10 qout
+run f8_up_1 "$P1" python3 $R/scripts/fp8_one.py 2560 640 1282 10 qboth
+run f8_up_2 "$P2" python3 $R/scripts/fp8_one.py 2560 640 1282 10 qboth
+run f8_up_3 "$P3" python3 $R/scripts/fp8_one.py 2560 640 1282 10 qboth
+run f8_up_4 "$P4" python3 $R/scripts/fp8_one.py 2560 640 1282 10 qboth
 cd "$R"
 for d in gpurun_out/r3ap/f8*/; do python3 scripts/pmc_summary.py "$d**/*counter_collection.csv" > "${d%/}.txt" || true; done
 echo done3
