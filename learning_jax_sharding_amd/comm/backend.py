@@ -150,11 +150,15 @@ class LocalComm:
                 continue
             dev0 = xs[g[0]].device
             dt = xs[g[0]].dtype
-            total = None
-            for d in g:
-                v = xs[d].to(dev0, _acc_dtype(dt))
-                total = v if total is None else total + v
-            chunks = total.to(dt).chunk(len(g), dim)
+            if all(xs[d].device == dev0 for d in g) and dev0.type == "cuda":
+                total = _hip().sum_n([_hip().dense(xs[d]) for d in g])   # one HIP launch, f32 accumulation
+            else:
+                total = None
+                for d in g:
+                    v = xs[d].to(dev0, _acc_dtype(dt))
+                    total = v if total is None else total + v
+                total = total.to(dt)
+            chunks = total.chunk(len(g), dim)
             for i, d in enumerate(g):
                 out[d] = _hip().dense(chunks[i].to(xs[d].device))
         return out
@@ -185,11 +189,14 @@ class LocalComm:
                 continue
             dev0 = xs[g[0]].device
             dt = xs[g[0]].dtype
-            total = None
-            for d in g:
-                v = xs[d].to(dev0, _acc_dtype(dt))
-                total = v if total is None else total + v
-            total = total.to(dt)
+            if all(xs[d].device == dev0 for d in g) and dev0.type == "cuda":
+                total = _hip().sum_n([_hip().dense(xs[d]) for d in g])
+            else:
+                total = None
+                for d in g:
+                    v = xs[d].to(dev0, _acc_dtype(dt))
+                    total = v if total is None else total + v
+                total = total.to(dt)
             for d in g:
                 out[d] = total.to(xs[d].device, copy=True)
         return out

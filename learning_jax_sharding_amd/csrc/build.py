@@ -53,17 +53,19 @@ def _compile(src, obj, extra):
     return obj
 
 
-def build_lib(name: str, sub: str, extra_link=(), force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(LIBDIR, exist_ok=True)
+def build_lib(name: str, sub: str, extra_link=(), force: bool = False, verbose: bool = True,
+              libdir: str = None, defines=()) -> str:
+    libdir = libdir or LIBDIR
+    os.makedirs(libdir, exist_ok=True)
     srcs = _sources(sub)
-    out = os.path.join(LIBDIR, f"lib{name}.so")
+    out = os.path.join(libdir, f"lib{name}.so")
     stamp = out + ".stamp"
-    dig = _digest(srcs)
+    dig = _digest(srcs) + ("/" + " ".join(defines) if defines else "")
     if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read().strip() == dig:
         return out
-    objdir = os.path.join(LIBDIR, "obj", name)
+    objdir = os.path.join(libdir, "obj", name)
     os.makedirs(objdir, exist_ok=True)
-    extra = ["-I", os.path.join(HERE, "kernels")]
+    extra = ["-I", os.path.join(HERE, "kernels")] + list(defines)
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs) or 1)) as ex:
         objs = list(ex.map(lambda s: _compile(s, os.path.join(objdir, os.path.basename(s) + ".o"), extra), srcs))
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + list(extra_link)
@@ -90,5 +92,17 @@ def build_all(force: bool = False, verbose: bool = True):
     return paths
 
 
+def build_variant(tag: str, defines, verbose: bool = True) -> str:
+    """An alternative build of the kernel library (A/B timing of a kernel variant): compiled with
+    ``defines`` (e.g. ``-DLJS_ATTN_PK=0``) into ``_lib/variants/<tag>/``; load it with
+    ``LJS_KERNELS_LIB=<path>``."""
+    return build_lib("ljs_kernels", "kernels", libdir=os.path.join(LIBDIR, "variants", tag), defines=tuple(defines),
+                     verbose=verbose)
+
+
 if __name__ == "__main__":
-    print(build_all(force="--force" in sys.argv))
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        print(build_variant(sys.argv[i + 1], sys.argv[i + 2:]))
+    else:
+        print(build_all(force="--force" in sys.argv))

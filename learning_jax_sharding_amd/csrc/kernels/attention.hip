@@ -59,6 +59,45 @@ struct AttnArgs {
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// f32 pair arithmetic of the softmax / dS: packed v_pk_* (LJS_ATTN_PK=1) or two scalar ops
+// (LJS_ATTN_PK=0; the build adds -fno-slp-vectorize so the compiler does not re-pack them).
+// MI355X_MICROARCH.md prices packed f32 VALU beside MFMAs above the scalar pair; measured A/B in
+// profiles/PERF_NOTES.md.
+#ifndef LJS_ATTN_PK
+#define LJS_ATTN_PK 1
+#endif
+__device__ __forceinline__ f32x2 pk_fms(const f32x2 a, const f32x2 b, const f32x2 c) {  // a * b - c
+#if LJS_ATTN_PK
+  return a * b - c;
+#else
+  f32x2 r;
+  r[0] = fmaf(a[0], b[0], -c[0]);
+  r[1] = fmaf(a[1], b[1], -c[1]);
+  return r;
+#endif
+}
+__device__ __forceinline__ f32x2 pk_mul(const f32x2 a, const f32x2 b) {
+#if LJS_ATTN_PK
+  return a * b;
+#else
+  f32x2 r;
+  r[0] = a[0] * b[0];
+  r[1] = a[1] * b[1];
+  return r;
+#endif
+}
+__device__ __forceinline__ f32x2 pk_add(const f32x2 a, const f32x2 b) {
+#if LJS_ATTN_PK
+  return a + b;
+#else
+  f32x2 r;
+  r[0] = a[0] + b[0];
+  r[1] = a[1] + b[1];
+  return r;
+#endif
+}
+
+
 
 // XCD-aware 3-D tile index of a 1-D grid of nx * H * B blocks: blocks sharing an XCD (dealt
 // round-robin by block id) take CONSECUTIVE tiles, so the query blocks of one (batch, head)
@@ -203,11 +242,11 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
   for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const f32x2 x = f32x2{s[jt][2 * h], s[jt][2 * h + 1]} * sc2 - mm2;
+      const f32x2 x = pk_fms(f32x2{s[jt][2 * h], s[jt][2 * h + 1]}, sc2, mm2);
       const f32x2 pv = {fast_exp2(x[0]), fast_exp2(x[1])};
       s[jt][2 * h] = pv[0];
       s[jt][2 * h + 1] = pv[1];
-      ps2 += pv;
+      ps2 = pk_add(ps2, pv);
     }
   const float psum = ps2[0] + ps2[1];
   // no lane's running max moved (the usual case after the first key tiles): alpha is exactly 1
@@ -218,7 +257,7 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
   const f32x2 al2 = {alpha, alpha};
 #pragma unroll
   for (int dt = 0; dt < 4 && rescale; ++dt) {
-    const f32x2 lo = f32x2{st.o[dt][0], st.o[dt][1]} * al2, hi = f32x2{st.o[dt][2], st.o[dt][3]} * al2;
+    const f32x2 lo = pk_mul(f32x2{st.o[dt][0], st.o[dt][1]}, al2), hi = pk_mul(f32x2{st.o[dt][2], st.o[dt][3]}, al2);
     st.o[dt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
   }
 #pragma unroll
@@ -583,7 +622,7 @@ __device__ __forceinline__ void dkv_tile(const AttnArgs& a, const bf16_t* Qt, co
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - f32x2{rc.lse[t][2 * h], rc.lse[t][2 * h + 1]};
+      const f32x2 x = pk_fms(f32x2{s[2 * h], s[2 * h + 1]}, sc2, f32x2{rc.lse[t][2 * h], rc.lse[t][2 * h + 1]});
       p[t][2 * h] = fast_exp2(x[0]);
       p[t][2 * h + 1] = fast_exp2(x[1]);
     }
@@ -597,7 +636,7 @@ __device__ __forceinline__ void dkv_tile(const AttnArgs& a, const bf16_t* Qt, co
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const f32x2 d = f32x2{p[t][2 * h], p[t][2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+      const f32x2 d = pk_mul(f32x2{p[t][2 * h], p[t][2 * h + 1]}, f32x2{dp[2 * h], dp[2 * h + 1]});
       ds[t][2 * h] = d[0];
       ds[t][2 * h + 1] = d[1];
     }
@@ -754,7 +793,7 @@ __device__ __forceinline__ void dkv32_tile(const AttnArgs& a, const bf16_t* Qt, 
         float pv[4], dsv[4];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - f32x2{lse[2 * h], lse[2 * h + 1]};
+          const f32x2 x = pk_fms(f32x2{s[2 * h], s[2 * h + 1]}, sc2, f32x2{lse[2 * h], lse[2 * h + 1]});
           pv[2 * h] = fast_exp2(x[0]);
           pv[2 * h + 1] = fast_exp2(x[1]);
         }
@@ -768,7 +807,7 @@ __device__ __forceinline__ void dkv32_tile(const AttnArgs& a, const bf16_t* Qt, 
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x2 d = f32x2{pv[2 * h], pv[2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+          const f32x2 d = pk_mul(f32x2{pv[2 * h], pv[2 * h + 1]}, f32x2{dp[2 * h], dp[2 * h + 1]});
           dsv[2 * h] = d[0];
           dsv[2 * h + 1] = d[1];
         }
@@ -940,7 +979,7 @@ __device__ __forceinline__ void dq_tile(const AttnArgs& a, const bf16_t* Kt, con
     float pv[4];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - ls2;
+      const f32x2 x = pk_fms(f32x2{s[2 * h], s[2 * h + 1]}, sc2, ls2);
       pv[2 * h] = fast_exp2(x[0]);
       pv[2 * h + 1] = fast_exp2(x[1]);
     }
@@ -954,7 +993,7 @@ __device__ __forceinline__ void dq_tile(const AttnArgs& a, const bf16_t* Kt, con
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const f32x2 d = f32x2{pv[2 * h], pv[2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+      const f32x2 d = pk_mul(f32x2{pv[2 * h], pv[2 * h + 1]}, f32x2{dp[2 * h], dp[2 * h + 1]});
       ds[jt][2 * h] = d[0];
       ds[jt][2 * h + 1] = d[1];
     }
@@ -1082,7 +1121,7 @@ __device__ __forceinline__ void dq32_tile(const AttnArgs& a, const bf16_t* Kt, c
       float pv[4], dsv[4];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - ls2;
+        const f32x2 x = pk_fms(f32x2{s[2 * h], s[2 * h + 1]}, sc2, ls2);
         pv[2 * h] = fast_exp2(x[0]);
         pv[2 * h + 1] = fast_exp2(x[1]);
       }
@@ -1097,7 +1136,7 @@ __device__ __forceinline__ void dq32_tile(const AttnArgs& a, const bf16_t* Kt, c
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const f32x2 d = f32x2{pv[2 * h], pv[2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+        const f32x2 d = pk_mul(f32x2{pv[2 * h], pv[2 * h + 1]}, f32x2{dp[2 * h], dp[2 * h + 1]});
         dsv[2 * h] = d[0];
         dsv[2 * h + 1] = d[1];
       }
@@ -1300,7 +1339,7 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
         const f32x2 sc2 = {a.scale_log2, a.scale_log2};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x2 x = f32x2{s[2 * h], s[2 * h + 1]} * sc2 - f32x2{lse[2 * h], lse[2 * h + 1]};
+          const f32x2 x = pk_fms(f32x2{s[2 * h], s[2 * h + 1]}, sc2, f32x2{lse[2 * h], lse[2 * h + 1]});
           pv[2 * h] = fast_exp2(x[0]);
           pv[2 * h + 1] = fast_exp2(x[1]);
         }
@@ -1314,7 +1353,7 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x2 d = f32x2{pv[2 * h], pv[2 * h + 1]} * f32x2{dp[2 * h], dp[2 * h + 1]};
+          const f32x2 d = pk_mul(f32x2{pv[2 * h], pv[2 * h + 1]}, f32x2{dp[2 * h], dp[2 * h + 1]});
           dsv[2 * h] = d[0];
           dsv[2 * h + 1] = d[1];
         }

@@ -810,12 +810,45 @@ __global__ void swap01_bf16_kernel(const T* __restrict__ in, bf16_t* __restrict_
 
 
 // out[c][r] = in[r][c] for an R x C bf16 matrix (row strides ldi / ldo), 64x64 tiles through LDS:
-// the plain [in][out] shadow of a weight derived from its gathered transposed shadow
+// the plain [in][out] shadow of a weight derived from its gathered transposed shadow.  16-byte
+// loads (8 columns of one row per lane) and 16-byte stores (8 rows of one output row per lane);
+// the LDS tile rows are padded so the transposed reads spread over the banks.
 __global__ void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out, int R, int C, long ldi,
                                       long ldo) {
-  __shared__ bf16_t tile[64][66];
+  __shared__ unsigned short tile[64][66];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int t = threadIdx.x;                 // 256 threads
+  const bool vec = (C % 8 == 0) && (R % 8 == 0) && (ldi % 8 == 0) && (ldo % 8 == 0) &&
+                   ((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0;
+  if (vec) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {            // 64 rows x 8 chunks of 8 columns
+      const int idx = t + 256 * p, row = idx >> 3, ch = idx & 7;
+      const int r = r0 + row, c = c0 + ch * 8;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (r < R && c < C) v = *reinterpret_cast<const u32x4*>(in + (long)r * ldi + c);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        tile[row][ch * 8 + 2 * k] = (unsigned short)(v[k] & 0xffffu);
+        tile[row][ch * 8 + 2 * k + 1] = (unsigned short)(v[k] >> 16);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {            // 64 output rows (= input columns) x 8 chunks of 8 rows
+      const int idx = t + 256 * p, oc = idx >> 3, ch = idx & 7;
+      const int c = c0 + oc, r = r0 + ch * 8;
+      if (c < C && r < R) {
+        u32x4 v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[k] = (unsigned)tile[ch * 8 + 2 * k][oc] | ((unsigned)tile[ch * 8 + 2 * k + 1][oc] << 16);
+        *reinterpret_cast<u32x4*>(out + (long)c * ldo + r) = v;
+      }
+    }
+    return;
+  }
+  const int tx = t & 63, ty = t >> 6;
   for (int i = ty; i < 64; i += 4) {
     const int r = r0 + i, c = c0 + tx;
     tile[i][tx] = (r < R && c < C) ? in[(long)r * ldi + c] : (bf16_t)0;
@@ -824,6 +857,58 @@ __global__ void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __r
   for (int i = ty; i < 64; i += 4) {
     const int c = c0 + i, r = r0 + tx;
     if (c < C && r < R) out[(long)c * ldo + r] = tile[tx][i];
+  }
+}
+
+// out = sum of n same-shape f32 / bf16 arrays (f32 accumulation, output in the inputs' dtype): the
+// loopback reduce-scatter / all-reduce over virtual devices that share one GPU, in ONE launch
+struct SumPtrs {
+  const void* p[16];
+};
+
+template <typename T>
+__global__ void sum_n_kernel(SumPtrs sp, int n, long count, T* __restrict__ out) {
+  const T* const* ins = reinterpret_cast<const T* const*>(sp.p);
+  constexpr int V = 16 / sizeof(T);
+  const long nv = count / V;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    for (int j = 0; j < n; ++j) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(ins[j] + i * V);
+      if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += __uint_as_float(v[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += __uint_as_float(v[e] << 16);
+          acc[2 * e + 1] += __uint_as_float(v[e] & 0xffff0000u);
+        }
+      }
+    }
+    u32x4 o;
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = __float_as_uint(acc[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[2 * e], acc[2 * e + 1]);
+    }
+    *reinterpret_cast<u32x4*>(out + i * V) = o;
+  }
+  if (blockIdx.x == 0) {
+    for (long j = nv * V + threadIdx.x; j < count; j += blockDim.x) {
+      float a = 0.f;
+      for (int k = 0; k < n; ++k) {
+        if constexpr (sizeof(T) == 4) a += ins[k][j];
+        else a += bf2f(ins[k][j]);
+      }
+      if constexpr (sizeof(T) == 4) out[j] = a;
+      else out[j] = f2bf(a);
+    }
   }
 }
 
@@ -851,6 +936,22 @@ LJS_API int ljs_swap01_bf16(const void* in, int in_bf16, void* out, int B, int S
 LJS_API int ljs_transpose_bf16(const void* in, void* out, int R, int C, long ldi, long ldo, hipStream_t s) {
   dim3 grid((C + 63) / 64, (R + 63) / 64);
   hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, R, C, ldi, ldo);
+  return (int)hipGetLastError();
+}
+
+LJS_API int ljs_sum_n(const void* const* ins, int n, int is_bf16, long count, void* out, hipStream_t s) {
+  // the n input pointers travel BY VALUE in the kernel arguments (graph-capturable, no copy)
+  if (n < 1 || n > 16 || (((uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
+  SumPtrs sp = {};
+  for (int j = 0; j < n; ++j) {
+    if (((uintptr_t)ins[j]) & 15) return (int)hipErrorInvalidValue;
+    sp.p[j] = ins[j];
+  }
+  const int g = grid_for(count / (is_bf16 ? 8 : 4) + 1, 256);
+  if (is_bf16)
+    hipLaunchKernelGGL(sum_n_kernel<bf16_t>, dim3(g), dim3(256), 0, s, sp, n, count, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(sum_n_kernel<float>, dim3(g), dim3(256), 0, s, sp, n, count, (float*)out);
   return (int)hipGetLastError();
 }
 

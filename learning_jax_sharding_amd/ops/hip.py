@@ -48,6 +48,7 @@ _SIGS = {
     "ljs_cast_bf16_f32": [c_void_p, c_void_p, c_long, c_void_p],
     "ljs_swap01_bf16": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
     "ljs_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p],
+    "ljs_sum_n": [ctypes.POINTER(c_void_p), c_int, c_int, c_long, c_void_p, c_void_p],
     "ljs_cast_transpose_f32_bf16": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p],
     "ljs_sum_all": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
@@ -557,6 +558,27 @@ def swap01_bf16(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty((S, B, K), dtype=torch.bfloat16, device=x.device)
     rc = lib().ljs_swap01_bf16(_p(x), int(x.dtype == torch.bfloat16), _p(out), B, S, K, _stream(x))
     _ck(rc, "swap01_bf16")
+    return out
+
+
+def sum_n(ts: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Elementwise sum of same-shape dense f32 / bf16 tensors on one GPU (f32 accumulation) in one
+    launch - the loopback reduction over virtual devices.  Falls back to torch adds otherwise."""
+    t0 = ts[0]
+    ok = (t0.is_cuda and t0.dtype in (torch.float32, torch.bfloat16) and 1 <= len(ts) <= 16
+          and all(t.shape == t0.shape and t.dtype == t0.dtype and t.device == t0.device and is_dense(t)
+                  and t.stride() == t0.stride() and t.data_ptr() % 16 == 0 for t in ts))
+    if not ok:
+        acc = None
+        for t in ts:
+            v = t.float()
+            acc = v if acc is None else acc + v
+        return acc.to(t0.dtype)
+    if out is None:
+        out = torch.empty_like(t0)
+    arr = (c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+    rc = lib().ljs_sum_n(arr, len(ts), int(t0.dtype == torch.bfloat16), t0.numel(), _p(out), _stream(t0))
+    _ck(rc, "sum_n")
     return out
 
 
