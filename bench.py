@@ -244,6 +244,9 @@ def main():
         return model.apply({"params": state.params}, x)
 
     capture = not args.no_graph and torch.cuda.is_available()
+    aten_trace = os.environ.get("LJS_ATEN_TRACE")   # diagnostics: eager steps, one traced (utils/aten_trace.py)
+    if aten_trace:
+        capture = False
     G = max(1, args.graph_steps) if (capture and args.mode == "train") else 1
     if args.mode == "train":
         step = ljs.jit(train_step, in_shardings=(state_sharding, x_sharding), out_shardings=state_sharding,
@@ -304,6 +307,12 @@ def main():
             run(2 * G)
             run(2)
         run(max(1, args.warmup))
+        if aten_trace:
+            from learning_jax_sharding_amd.utils.aten_trace import AtenTrace
+            with AtenTrace() as tr:
+                run(1)
+            if int(os.environ.get("RANK", "0")) == 0:
+                tr.write(aten_trace)
         barrier_sync()
         phase("timed steps")
         t0 = time.perf_counter()

@@ -1610,7 +1610,9 @@ static int attn_fwd_impl(const void* q, const void* k, const void* v, void* o, v
                          int H, const long* qs, const long* ks, const long* vs, const long* os, float scale,
                          int causal, int q_offset, void* oacc, const long* oas, int acc_mode, hipStream_t stream) {
   AttnArgs a = {};
-  static const int prog = getenv("LJS_ATTN_FWD_PROG") ? atoi(getenv("LJS_ATTN_FWD_PROG")) : 1;
+  // per-key-tile progressive waits in the resident forward: measured slower in isolation
+  // (B=64 22.3 vs 23.1 us, B=8 6.6 vs 7.2 us, gpurun_out/r3d kt_prog*), so off by default
+  static const int prog = getenv("LJS_ATTN_FWD_PROG") ? atoi(getenv("LJS_ATTN_FWD_PROG")) : 0;
   a.fwd_prog = prog;
   a.oacc = (float*)oacc;
   a.acc_mode = acc_mode;

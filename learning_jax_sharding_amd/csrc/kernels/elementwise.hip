@@ -863,7 +863,7 @@ __global__ void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __r
 // out = sum of n same-shape f32 / bf16 arrays (f32 accumulation, output in the inputs' dtype): the
 // loopback reduce-scatter / all-reduce over virtual devices that share one GPU, in ONE launch
 struct SumPtrs {
-  const void* p[16];
+  const void* p[64];
 };
 
 template <typename T>
@@ -876,16 +876,25 @@ __global__ void sum_n_kernel(SumPtrs sp, int n, long count, T* __restrict__ out)
     float acc[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[e] = 0.f;
-    for (int j = 0; j < n; ++j) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(ins[j] + i * V);
-      if constexpr (sizeof(T) == 4) {
+    // inputs in groups of 4: four independent 16-byte loads in flight per thread (in order:
+    // the sum is the same left-to-right f32 sum for every group size)
+    for (int j0 = 0; j0 < n; j0 += 4) {
+      u32x4 v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] += __uint_as_float(v[e]);
-      } else {
+      for (int u = 0; u < 4; ++u)
+        if (j0 + u < n) v[u] = *reinterpret_cast<const u32x4*>(ins[j0 + u] + i * V);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc[2 * e] += __uint_as_float(v[e] << 16);
-          acc[2 * e + 1] += __uint_as_float(v[e] & 0xffff0000u);
+      for (int u = 0; u < 4; ++u) {
+        if (j0 + u >= n) break;
+        if constexpr (sizeof(T) == 4) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] += __uint_as_float(v[u][e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc[2 * e] += __uint_as_float(v[u][e] << 16);
+            acc[2 * e + 1] += __uint_as_float(v[u][e] & 0xffff0000u);
+          }
         }
       }
     }
@@ -941,7 +950,7 @@ LJS_API int ljs_transpose_bf16(const void* in, void* out, int R, int C, long ldi
 
 LJS_API int ljs_sum_n(const void* const* ins, int n, int is_bf16, long count, void* out, hipStream_t s) {
   // the n input pointers travel BY VALUE in the kernel arguments (graph-capturable, no copy)
-  if (n < 1 || n > 16 || (((uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
+  if (n < 1 || n > 64 || (((uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
   SumPtrs sp = {};
   for (int j = 0; j < n; ++j) {
     if (((uintptr_t)ins[j]) & 15) return (int)hipErrorInvalidValue;

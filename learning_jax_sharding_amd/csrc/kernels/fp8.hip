@@ -601,6 +601,312 @@ template __global__ void gemm_mx_fp8_kernel<128, 3>(F8Args);
 template __global__ void gemm_mx_fp8_kernel<256, 2>(F8Args);
 template __global__ void gemm_mx_fp8_kernel<256, 3>(F8Args);
 
+// ---------------------------------------------------------------------------- GEMM, 8 waves
+// Large-tile MX-fp8 GEMM: BM x BN output tile, 8 waves (WM x WN, each (BM/WM) x (BN/WN)), BK =
+// 128, a two-stage LDS-DMA ring.  Why not the 4-wave 128x128 kernel above: at T=16384 its
+// 128x128 tiles pull 32 KiB per 512 MFMA cycles per CU from L2 / the Infinity Cache (about the
+// L2's whole bandwidth at the fp8 MFMA rate), the 16-MFMA K-tile is too short to cover the
+// next tile's load latency, and its runtime-flag epilogue costs ~1900 VALU per wave (PMC:
+// 24 VALU per MFMA, MFMA busy 20 %).  Here a 256x256 tile halves the bytes per FLOP, two
+// waves per SIMD interleave, and the epilogue is one pass that writes the finished bf16 tile
+// into an LDS image (the idle ring), followed by cooperative passes for each requested output:
+// the bf16 rows, the row-blocked MX copy and the transposed (token-blocked) MX copy, each read
+// from the image with conflict-free lane mappings and stored as whole 16 / 32-byte pieces.
+// F32: plain (split-K slab) f32 output straight from the accumulators.
+template <int BM, int BN, int WM, bool F32, int NST>
+__global__ __launch_bounds__(512) void gemm_mx8_kernel(F8Args p) {
+  constexpr int NW = 8, WN = NW / WM;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
+  constexpr int A_T = BM * F8_BK, B_T = BN * F8_BK;
+  constexpr int NSA = (BM + 63) / 64, NSB = (BN + 63) / 64;  // 64-row scale-word instructions
+  constexpr int STAGE = A_T + B_T + 256 * (NSA + NSB);
+  constexpr int PA = (BM / 8 + NW - 1) / NW, PB = (BN / 8 + NW - 1) / NW, PS = (NSA + NSB + NW - 1) / NW;
+  constexpr int L = PA + PB + PS;  // DMA instructions per wave per K-tile (uniform: extras repeat)
+  constexpr int RS = BN * 2 + 16;  // image row stride (bytes): padded so 16 rows spread over banks
+  constexpr int SMEM = NST * STAGE > BM * RS ? NST * STAGE : BM * RS;
+  static_assert(SMEM <= 163840 && L * (NST - 1) <= 63, "LDS / vmcnt budget");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int ntiles = ((p.M + BM - 1) / BM) * ntn;
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = item % ntiles, split = item / ntiles;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int KB = p.K / 32;
+  const int kt0 = split * p.kps;
+  const int nk = min(p.K / F8_BK - kt0, p.kps);
+
+  const __amdgpu_buffer_rsrc_t ra = f8_rsrc(p.A, (long)(p.M - 1) * p.lda + p.K);
+  const __amdgpu_buffer_rsrc_t rb = f8_rsrc(p.B, (long)(p.N - 1) * p.ldb + p.K);
+  const __amdgpu_buffer_rsrc_t rsa = f8_rsrc(p.SA, (long)(p.M - 1) * p.ldsa + KB);
+  const __amdgpu_buffer_rsrc_t rsb = f8_rsrc(p.SB, (long)(p.N - 1) * p.ldsb + KB);
+
+  // 1 KiB pieces (8 rows x 128 B): piece q of A / B; waves past the last piece repeat it
+  int voa[PA], vob[PB], vos[PS], dsa[PA], dsb[PB], dss[PS];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int q = min(wave + NW * i, BM / 8 - 1);
+    const int row = 8 * q + (lane >> 3), slot = lane & 7;
+    voa[i] = (m0 + row) * p.lda + 16 * f8_swz(row, slot);
+    dsa[i] = q * 1024;
+  }
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int q = min(wave + NW * i, BN / 8 - 1);
+    const int row = 8 * q + (lane >> 3), slot = lane & 7;
+    vob[i] = (n0 + row) * p.ldb + 16 * f8_swz(row, slot);
+    dsb[i] = A_T + q * 1024;
+  }
+  // scale words (4 B per lane: one row's 4 scale bytes of a K-tile, 64 rows per instruction);
+  // rows past the tile read whatever the buffer holds (or 0 past its end) into unused words
+  bool sis_a[PS];
+#pragma unroll
+  for (int i = 0; i < PS; ++i) {
+    const int si = min(wave + NW * i, NSA + NSB - 1);
+    sis_a[i] = si < NSA;
+    const int r = 64 * (sis_a[i] ? si : si - NSA) + lane;
+    vos[i] = sis_a[i] ? (m0 + r) * p.ldsa : (n0 + r) * p.ldsb;
+    dss[i] = A_T + B_T + 256 * si;
+  }
+
+#define MX8_ISSUE(KT, ST)                                                                         \
+  do {                                                                                            \
+    unsigned char* base_ = smem + (ST) * STAGE;                                                   \
+    _Pragma("unroll") for (int i_ = 0; i_ < PA; ++i_)                                             \
+        f8_dma(ra, base_ + dsa[i_], 16, voa[i_], (kt0 + (KT)) * F8_BK);                           \
+    _Pragma("unroll") for (int i_ = 0; i_ < PB; ++i_)                                             \
+        f8_dma(rb, base_ + dsb[i_], 16, vob[i_], (kt0 + (KT)) * F8_BK);                           \
+    _Pragma("unroll") for (int i_ = 0; i_ < PS; ++i_)                                             \
+        f8_dma(sis_a[i_] ? rsa : rsb, base_ + dss[i_], 4, vos[i_], (kt0 + (KT)) * 4);             \
+  } while (0)
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) MX8_ISSUE(s, s);
+  const int g = lane >> 4, r16 = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
+    // K-tile kt landed (this wave's pieces); younger stages may stay in flight
+    if constexpr (NST >= 3) {
+      if (kt + NST - 2 >= nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const unsigned char* As_ = smem + (kt % NST) * STAGE;
+    const unsigned char* Bs_ = As_ + A_T;
+    const unsigned* Sa = reinterpret_cast<const unsigned*>(As_ + A_T + B_T);
+    const unsigned* Sb = reinterpret_cast<const unsigned*>(As_ + A_T + B_T + 256 * NSA);
+    i32x8 bfr[TN];
+    int sb[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wc * WTN + 16 * j + r16;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs_ + row * 128 + 16 * f8_swz(row, g));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs_ + row * 128 + 16 * f8_swz(row, g + 4));
+      bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      sb[j] = (int)((Sb[row] >> (8 * g)) & 0xff);
+    }
+    // the DMA NST-1 K-tiles ahead once this wave's fragment reads are issued (its stage was
+    // released by every wave at the barrier above)
+    if (kt + NST - 1 < nk) MX8_ISSUE(kt + NST - 1, (kt + NST - 1) % NST);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wr * WTM + 16 * i + r16;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(As_ + row * 128 + 16 * f8_swz(row, g));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(As_ + row * 128 + 16 * f8_swz(row, g + 4));
+      const i32x8 af = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      const int sa = (int)((Sa[row] >> (8 * g)) & 0xff);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f8_mfma(bfr[j], af, acc[i][j], sb[j], sa);
+    }
+  }
+#undef MX8_ISSUE
+
+  // lane (g, r16) holds C[m0 + wr WTM + 16 i + r16][n0 + wc WTN + 16 j + 4 g + e], e = 0..3
+  const bool relu = p.flags & 1, has_bias = p.flags & 2, bias_f32 = p.flags & 4;
+  const int rowb = wr * WTM + r16, colb = wc * WTN + 4 * g;
+  float bv[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int col = n0 + colb + 16 * j + e;
+      bv[j][e] = (has_bias && col < p.N) ? (bias_f32 ? reinterpret_cast<const float*>(p.bias)[col]
+                                                     : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[col]))
+                                         : 0.f;
+    }
+  if constexpr (F32) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = m0 + rowb + 16 * i;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + colb + 16 * j;
+        if (row < p.M && col < p.N) {
+          f32x4 v = acc[i][j];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] += bv[j][e];
+            if (relu) v[e] = fmaxf(v[e], 0.f);
+          }
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.C) + split * p.sC + (long)row * p.ldc + col) = v;
+        }
+      }
+    }
+    return;
+  } else {
+    const bool res_add = p.flags & 64, res_mask = p.flags & 128, qout = p.flags & 256;
+    const bool qtout = p.flags & 512, r_fp8 = p.flags & 1024;
+    __syncthreads();  // every wave is done reading the ring: it becomes the bf16 image
+    const __amdgpu_buffer_rsrc_t rr =
+        f8_rsrc(p.R, (r_fp8 ? 1 : 2) * ((long)(p.M - 1) * p.ldr + p.N) * ((res_add || res_mask) ? 1 : 0));
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int lr = rowb + 16 * i, row = m0 + lr;
+      u32x2 rv[TN];
+      if (res_add || res_mask) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + colb + 16 * j;
+          const bool ok = row < p.M && col < p.N;
+          if (r_fp8) {
+            const unsigned b = __builtin_amdgcn_raw_buffer_load_b32(rr, ok ? (int)((long)row * p.ldr + col) : 0x7ffffff0, 0, 0);
+            rv[j] = u32x2{b, 0u};
+          } else {
+            rv[j] = __builtin_amdgcn_raw_buffer_load_b64(rr, ok ? (int)(((long)row * p.ldr + col) * 2) : 0x7ffffff0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][e] + bv[j][e];
+          if (relu) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (res_mask && r_fp8) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const unsigned byte = (rv[j][0] >> (8 * e)) & 0xffu;
+            v[e] = ((byte & 0x80u) == 0u && byte != 0u) ? v[e] : 0.f;
+          }
+        } else if (res_add || res_mask) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const unsigned w = rv[j][e >> 1];
+            const float r = (e & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+            if (res_add) v[e] = bf2f(f2bf(v[e])) + r;
+            else v[e] = r > 0.f ? v[e] : 0.f;
+          }
+        }
+        *reinterpret_cast<u32x2*>(smem + lr * RS + (colb + 16 * j) * 2) =
+            u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+      }
+    }
+    __syncthreads();
+    if (p.C) {  // bf16 rows: 16 B per lane, consecutive lanes along a row
+      for (int c = tid; c < BM * (BN / 8); c += 512) {
+        const int lr = c / (BN / 8), ch = c % (BN / 8);
+        const int grow = m0 + lr, gcol = n0 + ch * 8;
+        const u32x4 val = *reinterpret_cast<const u32x4*>(smem + lr * RS + ch * 16);
+        if (grow < p.M && gcol < p.N)
+          *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(p.C) + (long)grow * p.ldc + gcol) = val;
+      }
+    }
+    if (qout) {  // row-blocked MX copy: lane = (row, 32-column block), rows consecutive across lanes
+      for (int it = tid; it < BM * (BN / 32); it += 512) {
+        const int lr = it % BM, b = it / BM;
+        const int grow = m0 + lr, gcol = n0 + 32 * b;
+        float v[32];
+        float amax = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const u32x4 w = *reinterpret_cast<const u32x4*>(smem + lr * RS + b * 64 + k * 16);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[8 * k + 2 * e] = __uint_as_float(w[e] << 16);
+            v[8 * k + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 32; ++e) amax = fmaxf(amax, fabsf(v[e]));
+        const int x = mx_exponent(amax);
+        const float inv = ldexpf(1.f, -x);
+        u32x4 o[2];
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          o[c >> 2][c & 3] = pack4_e4m3(v[4 * c] * inv, v[4 * c + 1] * inv, v[4 * c + 2] * inv, v[4 * c + 3] * inv);
+        if (grow < p.M && gcol < p.N) {
+          u32x4* dst = reinterpret_cast<u32x4*>(p.QC + (long)grow * p.N + gcol);
+          dst[0] = o[0];
+          dst[1] = o[1];
+          p.SC[(long)grow * (p.N / 32) + gcol / 32] = (unsigned char)(x + 127);
+        }
+      }
+    }
+    if (qtout) {  // transposed MX copy: lane = (column pair, 32-row block), pairs consecutive across lanes
+      for (int it = tid; it < (BN / 2) * (BM / 32); it += 512) {
+        const int cp = it % (BN / 2), tb = it / (BN / 2);
+        float v0[32], v1[32];
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+          const unsigned h2 = *reinterpret_cast<const unsigned*>(smem + (tb * 32 + k) * RS + cp * 4);
+          v0[k] = __uint_as_float(h2 << 16);
+          v1[k] = __uint_as_float(h2 & 0xffff0000u);
+          a0 = fmaxf(a0, fabsf(v0[k]));
+          a1 = fmaxf(a1, fabsf(v1[k]));
+        }
+        const int x0 = mx_exponent(a0), x1 = mx_exponent(a1);
+        const float i0 = ldexpf(1.f, -x0), i1 = ldexpf(1.f, -x1);
+        u32x4 o0[2], o1[2];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          o0[k >> 2][k & 3] = pack4_e4m3(v0[4 * k] * i0, v0[4 * k + 1] * i0, v0[4 * k + 2] * i0, v0[4 * k + 3] * i0);
+          o1[k >> 2][k & 3] = pack4_e4m3(v1[4 * k] * i1, v1[4 * k + 1] * i1, v1[4 * k + 2] * i1, v1[4 * k + 3] * i1);
+        }
+        const int gcol = n0 + 2 * cp, grow = m0 + tb * 32;
+        if (grow < p.M) {  // M % 32 == 0 (launcher): blocks are whole; N % 8: pairs are whole
+          if (gcol < p.N) {
+            u32x4* dst = reinterpret_cast<u32x4*>(p.QT + (long)gcol * p.ldqt + grow);
+            dst[0] = o0[0];
+            dst[1] = o0[1];
+            p.ST[(long)gcol * (p.ldqt / 32) + grow / 32] = (unsigned char)(x0 + 127);
+          }
+          if (gcol + 1 < p.N) {
+            u32x4* dst = reinterpret_cast<u32x4*>(p.QT + (long)(gcol + 1) * p.ldqt + grow);
+            dst[0] = o1[0];
+            dst[1] = o1[1];
+            p.ST[(long)(gcol + 1) * (p.ldqt / 32) + grow / 32] = (unsigned char)(x1 + 127);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int NST = 2>
+hipError_t launch_mx8(const F8Args& a, int tiles, hipStream_t s) {
+  if (a.flags & 32)
+    hipLaunchKernelGGL((gemm_mx8_kernel<BM, BN, WM, true, NST>), dim3(tiles), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_mx8_kernel<BM, BN, WM, false, NST>), dim3(tiles), dim3(512), 0, s, a);
+  return hipGetLastError();
+}
+
 template <int BM, int NST>
 hipError_t launch_f8(const F8Args& a, int tiles, hipStream_t s) {
   hipLaunchKernelGGL((gemm_mx_fp8_kernel<BM, NST>), dim3(tiles), dim3(BM * 2), 0, s, a);
@@ -707,11 +1013,25 @@ LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const 
   a.ldsb = b_bcast ? 0 : K / 32;
   a.QT = (unsigned char*)QT; a.ST = (unsigned char*)ST; a.ldqt = ldqt;
   a.kps = kps; a.nsplit = nsplit; a.sC = sC;
-  if (tile == 0) {
-    // 128x128, 2 stages, 2 blocks per CU: with the LDS-staged epilogue it beats the 256-row
-    // tiles at every FF shape (scripts/fp8_one.py: up-projection + MX copy 70.5 vs 76.0 us,
-    // dA with mask + MX copy 83.9 vs 89.5, down-projection 50.1 vs 54.4)
-    tile = 1282;
+  if (tile == 0) tile = 1282;
+  if (tile >= 10000) {  // 8-wave large tiles: tile = BM * 1000 + BN (+ 1000000 * 3: three stages)
+    const int t6 = tile % 1000000;
+    const int bm = t6 / 1000, bn = t6 % 1000;
+    const int tl = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * nsplit;
+    switch (tile) {
+      case 256256: return (int)launch_mx8<256, 256, 2>(a, tl, stream);
+      case 256128: return (int)launch_mx8<256, 128, 2>(a, tl, stream);
+      case 256160: return (int)launch_mx8<256, 160, 4>(a, tl, stream);
+      case 128320: return (int)launch_mx8<128, 320, 2>(a, tl, stream);
+      case 128256: return (int)launch_mx8<128, 256, 2>(a, tl, stream);
+      case 128128: return (int)launch_mx8<128, 128, 2>(a, tl, stream);
+      case 128160: return (int)launch_mx8<128, 160, 4>(a, tl, stream);
+      case 3128128: return (int)launch_mx8<128, 128, 2, 3>(a, tl, stream);
+      case 3128160: return (int)launch_mx8<128, 160, 4, 3>(a, tl, stream);
+      case 3128256: return (int)launch_mx8<128, 256, 2, 3>(a, tl, stream);
+      case 3256128: return (int)launch_mx8<256, 128, 2, 3>(a, tl, stream);
+      default: return (int)hipErrorInvalidValue;
+    }
   }
   const int bm = tile / 10 >= 256 ? 256 : 128;
   const int tiles = ((M + bm - 1) / bm) * ((N + 127) / 128) * nsplit;

@@ -565,7 +565,7 @@ def sum_n(ts: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> tor
     """Elementwise sum of same-shape dense f32 / bf16 tensors on one GPU (f32 accumulation) in one
     launch - the loopback reduction over virtual devices.  Falls back to torch adds otherwise."""
     t0 = ts[0]
-    ok = (t0.is_cuda and t0.dtype in (torch.float32, torch.bfloat16) and 1 <= len(ts) <= 16
+    ok = (t0.is_cuda and t0.dtype in (torch.float32, torch.bfloat16) and 1 <= len(ts) <= 64
           and all(t.shape == t0.shape and t.dtype == t0.dtype and t.device == t0.device and is_dense(t)
                   and t.stride() == t0.stride() and t.data_ptr() % 16 == 0 for t in ts))
     if not ok:
@@ -578,6 +578,17 @@ def sum_n(ts: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> tor
         out = torch.empty_like(t0)
     arr = (c_void_p * len(ts))(*[t.data_ptr() for t in ts])
     rc = lib().ljs_sum_n(arr, len(ts), int(t0.dtype == torch.bfloat16), t0.numel(), _p(out), _stream(t0))
+    _ck(rc, "sum_n")
+    return out
+
+
+def sum_ptrs(ptrs: Sequence[int], out: torch.Tensor) -> torch.Tensor:
+    """out (dense f32 / bf16) = sum of ``len(ptrs)`` <= 64 dense arrays of out's dtype and element
+    count at the given device addresses (16-byte aligned) - e.g. every device's split-K weight
+    gradient slabs, summed in one pass (parallel/weight_gather.py)."""
+    assert 1 <= len(ptrs) <= 64 and out.is_cuda and is_dense(out) and all(p % 16 == 0 for p in ptrs)
+    arr = (c_void_p * len(ptrs))(*ptrs)
+    rc = lib().ljs_sum_n(arr, len(ptrs), int(out.dtype == torch.bfloat16), out.numel(), _p(out), _stream(out))
     _ck(rc, "sum_n")
     return out
 

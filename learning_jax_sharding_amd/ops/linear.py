@@ -102,12 +102,23 @@ _DEFER_ON = os.environ.get("LJS_DEFER_WGRAD", "1") == "1"
 
 
 def _key(t: torch.Tensor):
+    fn = t.grad_fn
+    if fn is not None and type(fn).__name__ in _SLAB_CONSUMERS:
+        # an output of a node that consumes its gradient as slabs (a gathered-weight proxy,
+        # parallel/weight_gather.py): keyed by (node, output index)
+        return ("node", id(fn), t.output_nr)
     return (t.data_ptr(), tuple(t.shape))
 
 
-def defer_safe_leaves(outs) -> set:
-    """Keys of leaf tensors reached from ``outs`` by exactly one autograd edge, and that edge from
-    a _Linear backward (so autograd passes that Function's gradient through untouched)."""
+# autograd nodes that take their outputs' gradients uncombined (parallel/weight_gather.py: the
+# loopback reduce-scatter of a gathered weight sums every device's split-K slabs in one pass)
+_SLAB_CONSUMERS = ("_GatherBf16Backward",)
+
+
+def defer_safe_leaves(outs, leaves: bool = True) -> set:
+    """Keys of leaf tensors (``leaves``) and of slab-consumer outputs reached from ``outs`` by
+    exactly one autograd edge, and that edge from a _Linear backward (so autograd passes that
+    Function's gradient through untouched)."""
     counts, prod, seen = {}, {}, set()
     stack = [t.grad_fn for t in outs if t.grad_fn is not None]
     while stack:
@@ -115,15 +126,19 @@ def defer_safe_leaves(outs) -> set:
         if id(fn) in seen:
             continue
         seen.add(id(fn))
-        for nxt, _ in fn.next_functions:
+        for nxt, idx in fn.next_functions:
             if nxt is None:
                 continue
             var = getattr(nxt, "variable", None)
+            k = None
             if var is not None:
-                k = _key(var)
+                k = _key(var) if leaves else None
+            elif type(nxt).__name__ in _SLAB_CONSUMERS:
+                k = ("node", id(nxt), idx)
+            if k is not None:
                 counts[k] = counts.get(k, 0) + 1
                 prod[k] = fn
-            elif id(nxt) not in seen:
+            if var is None and id(nxt) not in seen:
                 stack.append(nxt)
     return {k for k, c in counts.items() if c == 1 and type(prod[k]).__name__ in _DEFER_NODES}
 
@@ -149,10 +164,14 @@ def defer_slabs(w: torch.Tensor, out: torch.Tensor, ld: int, offset: int = 0):
 class defer_wgrads:
     """Context manager around one autograd.grad call (spmd.api.value_and_grad)."""
 
-    def __init__(self, outs, enabled: bool):
+    def __init__(self, outs, enabled: bool, proxies: bool = False):
+        """``enabled``: leaves' gradients may stay slabs (one device, the fused Adam sums them);
+        ``proxies``: only slab-consumer outputs' may (several devices)."""
         self.state = None
-        if enabled and _DEFER_ON and not _streams.enabled():
-            self.state = {"safe": defer_safe_leaves(outs), "pending": {}}
+        if (enabled or proxies) and _DEFER_ON and not _streams.enabled():
+            safe = defer_safe_leaves(outs, leaves=enabled)
+            if safe:
+                self.state = {"safe": safe, "pending": {}}
 
     def __enter__(self):
         global _DEFER

@@ -25,13 +25,14 @@ __all__ = ["get", "get_stacked", "get_mx", "mx_eligible", "entry", "adopt", "mar
 
 
 class _Entry:
-    __slots__ = ("ref", "bufs", "versions", "proxy")
+    __slots__ = ("ref", "bufs", "versions", "proxy", "shared")
 
     def __init__(self, w: torch.Tensor):
         self.ref = weakref.ref(w)
         self.bufs: Dict[str, torch.Tensor] = {}
         self.versions: Dict[str, int] = {}
         self.proxy = False
+        self.shared = None   # proxies of ONE gathered buffer (virtual devices of a GPU): derived shadows
 
 
 _REG: Dict[Tuple, _Entry] = {}
@@ -93,6 +94,8 @@ def _refresh(w: torch.Tensor, e: _Entry, kind: str) -> torch.Tensor:
             if kind == "N" and "T" in e.bufs and e.versions.get("T") == w._version:
                 hip.transpose_bf16(e.bufs["T"], buf)     # derived from the gathered [out][in] shadow
                 e.versions[kind] = w._version
+                if e.shared is not None:
+                    e.shared[kind] = buf
             else:
                 raise RuntimeError("shadow of a gathered-weight proxy requested that cannot be derived from its "
                                    f"gathered bf16 copy (kind {kind!r}); the proxy holds no f32 values")
@@ -113,6 +116,8 @@ def _refresh(w: torch.Tensor, e: _Entry, kind: str) -> torch.Tensor:
 def get(w: torch.Tensor, kind: str) -> torch.Tensor:
     """bf16 copy of the 2-D f32 weight ``w`` (``kind`` "T": transposed, "N": plain)."""
     e = entry(w)
+    if e.proxy and e.shared is not None and kind in e.shared:
+        return e.shared[kind]                 # derived once for every proxy sharing the buffer
     if kind not in e.bufs:
         e.bufs[kind] = _alloc(w, kind)
         e.versions[kind] = -1
@@ -129,13 +134,16 @@ def stacked_proxy_T(ws: Sequence[torch.Tensor]) -> bool:
     return all(e.bufs["T"].data_ptr() == base.data_ptr() + i * N * K * 2 for i, e in enumerate(es))
 
 
-def register_proxy(w: torch.Tensor, t_buf: torch.Tensor) -> None:
+def register_proxy(w: torch.Tensor, t_buf: torch.Tensor, shared: Optional[dict] = None) -> None:
     """``w`` (an uninitialised f32 tensor of the full weight's shape) stands for a weight whose bf16
     transposed shadow ``t_buf`` [out][in] was all-gathered from the shards' own shadows
     (parallel/weight_gather.py): the GEMMs read ``t_buf`` (and an "N" shadow transposed from it);
-    asking for anything that needs the f32 values raises."""
+    asking for anything that needs the f32 values raises.  ``shared``: one dict for all the
+    proxies standing for the same ``t_buf`` (virtual devices of one GPU): shadows derived from it
+    are computed once."""
     e = entry(w)
     e.proxy = True
+    e.shared = shared
     e.bufs["T"] = t_buf
     e.versions["T"] = w._version
     # the entry (and the gathered buffers it holds) goes with the proxy

@@ -70,6 +70,53 @@ def eligible(kernels: Sequence[ShardedArray], dst: TileAssignment) -> Optional[i
     return dim
 
 
+def _loopback(groups, xs) -> bool:
+    """Every group's members are virtual devices of ONE GPU under the single-process backend (the
+    collective is a local copy / sum, no RCCL)."""
+    from ..comm.backend import get_comm
+    if get_comm().kind != "local":
+        return False
+    for g in groups:
+        ts = [xs.get(d) for d in g]
+        if any(t is None for t in ts) or not ts[0].is_cuda or any(t.device != ts[0].device for t in ts):
+            return False
+    return True
+
+
+def _slab_sum(groups, dim, devs, ents, shape):
+    """Loopback reduce-scatter of uncombined weight gradients: per group, ONE pass sums every
+    member's split-K slabs (hip.SlabGrad, contiguous [K][N] each) into the full gradient, whose
+    chunks along ``dim`` are the members' shards - no per-device slab combine, no second sum."""
+    from ..ops import hip
+    out = {}
+    for g in groups:
+        ptrs = []
+        for d in g:
+            sg = ents[d][0]
+            base = sg.slabs.data_ptr() + 4 * sg.offset
+            ptrs += [base + 4 * s * sg.slab_stride for s in range(sg.S)]
+        total = torch.empty(shape, dtype=torch.float32, device=ents[g[0]][0].slabs.device)
+        hip.sum_ptrs(ptrs, total)
+        for i, ch in enumerate(total.chunk(len(g), dim)):
+            out[g[i]] = hip.dense(ch)
+    return out
+
+
+def _slabs_ok(ents, devs, shape) -> bool:
+    if len(ents) != len(devs):
+        return False
+    sgs = [ents[d][0] for d in devs]
+    return (all(isinstance(sg, _hip_cls("SlabGrad")) for sg in sgs) and all(
+        tuple(sg.shape) == tuple(shape) and sg.ld == shape[1] and sg.slabs.dtype == torch.float32
+        and (sg.slabs.data_ptr() + 4 * sg.offset) % 16 == 0 and (4 * sg.slab_stride) % 16 == 0 for sg in sgs)
+        and sum(sg.S for sg in sgs) <= 64)
+
+
+def _hip_cls(name):
+    from ..ops import hip
+    return getattr(hip, name)
+
+
 class _GatherBf16(torch.autograd.Function):
     """All local devices at once (a loopback group holds several): f32 shards -> f32 proxies of
     the gathered weights (the forward moves the shards' bf16 shadows); backward reduce-scatters
@@ -86,17 +133,29 @@ class _GatherBf16(torch.autograd.Function):
             t_loc[d] = shadow.get(ws[0], "T").unsqueeze(0) if nw == 1 else shadow.get_stacked(ws)
         # gather along the shadow's K axis (dim 0 of W) or its N axis (dim 1 of W)
         gdim = 2 if dim == 0 else 1
-        gathered = C._run(C._Spec("all_gather", groups, dim=gdim), t_loc)
+        if _loopback(groups, t_loc):
+            # virtual devices of one GPU: ONE concatenation per group, shared by its members
+            # (the proxies are read-only stand-ins; nothing writes the gathered shadow)
+            gathered = {}
+            for grp in groups:
+                buf = hip.concat_parts([t_loc[d] for d in grp], gdim)
+                for d in grp:
+                    gathered[d] = buf
+        else:
+            gathered = C._run(C._Spec("all_gather", groups, dim=gdim), t_loc)
         K_loc, N_loc = flat[0].shape
         K, N = (K_loc * n, N_loc) if dim == 0 else (K_loc, N_loc * n)
         outs = []
+        dense = {}
+        holders = {}
         for j, d in enumerate(devs):
             g = gathered[d]
-            if not g.is_contiguous():
-                g = g.contiguous()                                   # [nw][N][K] bf16
+            if id(g) not in dense:
+                dense[id(g)] = g if g.is_contiguous() else g.contiguous()   # [nw][N][K] bf16
+            gid, g = id(g), dense[id(g)]
             for i in range(nw):
                 p = torch.empty((K, N), dtype=torch.float32, device=flat[j * nw].device)
-                shadow.register_proxy(p, g[i])
+                shadow.register_proxy(p, g[i], shared=holders.setdefault((gid, i), {}))
                 outs.append(p)
         ctx.meta = meta
         return tuple(outs)
@@ -105,13 +164,26 @@ class _GatherBf16(torch.autograd.Function):
     def backward(ctx, *gs):
         groups, dim, devs, nw, n = ctx.meta
         _plan.record("reduce_scatter", groups=groups, note="backward.bf16_shadow_gather")
+        from ..ops import linear as _lin
         res = [None] * len(gs)
+        pend = _lin._DEFER["pending"] if _lin._DEFER is not None else None
         for i in range(nw):
-            xs = {}
+            xs, ents = {}, {}
             for j, d in enumerate(devs):
                 g = gs[j * nw + i]
                 if g is not None:
-                    xs[d] = g.contiguous()
+                    ent = pend.pop(g.data_ptr(), None) if pend is not None else None
+                    if ent is not None:
+                        ents[d] = ent
+                    xs[d] = g
+            if ents and len(xs) == len(devs) and _loopback(groups, xs) and _slabs_ok(ents, devs, xs[devs[0]].shape):
+                red = _slab_sum(groups, dim, devs, ents, tuple(xs[devs[0]].shape))
+                for j, d in enumerate(devs):
+                    res[j * nw + i] = red[d]
+                continue
+            for ent in ents.values():
+                ent[1]()                                   # combine the slabs the usual way
+            xs = {d: g.contiguous() for d, g in xs.items()}
             if len(xs) != len(devs):
                 continue
             red = C._run(C._Spec("reduce_scatter", groups, dim=dim), xs)

@@ -444,7 +444,7 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
                 # fused Adam (ops/linear.defer_wgrads)
                 one_dev = side and all(len(l.local) == 1 for l in all_leaves) and len(
                     {d for l in all_leaves for d in l.local}) == 1 and not _multi_process()
-                dfr = _lin.defer_wgrads(outs, one_dev)
+                dfr = _lin.defer_wgrads(outs, one_dev, proxies=side and not _multi_process())
                 with torch.autograd.set_multithreading_enabled(_graphs.current() is None), \
                         _streams.wgrad_scope(side), dfr:
                     gs = torch.autograd.grad(outs, inputs, seeds, allow_unused=True)

@@ -863,3 +863,66 @@ def test_attention_fwd_inkernel_lse_merge(causal, sk):
         out = K.attention_fwd_merge(q, kb, vb, 0.125, causal, q_off - i * sk, state, last=i == nblk - 1)
     torch.cuda.synchronize()
     np.testing.assert_allclose(out.float().cpu().numpy(), ref.cpu().numpy(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("shape", [(640, 1920), (64, 8), (100, 264), (3, 8)])
+def test_transpose_bf16_and_swap01(hip, shape):
+    """Vectorised LDS transpose and the (a, b, c) -> (b, a, c) swap == torch (bit-exact, ragged
+    edges included)."""
+    x = torch.randn(shape, device="cuda").bfloat16()
+    assert torch.equal(hip.transpose_bf16(x), x.t().contiguous())
+    y = torch.randn(4, shape[0], 8, device="cuda").bfloat16()
+    assert torch.equal(hip.swap01_bf16(y), y.transpose(0, 1).contiguous())
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 7])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sum_n(hip, n, dtype):
+    """One-launch n-way sum (f32 accumulation, pointers by value) == the f32 torch sum."""
+    xs = [torch.randn(1000 + 8 * n, 24, device="cuda").to(dtype) for _ in range(n)]
+    ref = torch.stack([x.float() for x in xs]).sum(0)
+    out = hip.sum_n(xs)
+    torch.cuda.synchronize()
+    tol = 0 if dtype == torch.float32 and n <= 2 else 1e-2
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("tile", [256256, 256128, 256160, 128320, 128256, 128128, 128160, 3128128, 3128160, 3128256, 3256128])
+@pytest.mark.parametrize("mode", ["qboth", "qmask8", "res_bias", "f32split"])
+def test_fp8_gemm_8wave_tiles_match_4wave(hip, tile, mode):
+    """The 8-wave large-tile MX GEMM runs the same MFMA sequence per output element as the 4-wave
+    128x128 kernel: every output (bf16 rows, row-blocked and transposed MX copies, f32 split-K
+    slabs) must be bit-identical, edges included (M, N not multiples of the tile)."""
+    from learning_jax_sharding_amd.ops import fp8 as F
+    g = torch.Generator(device="cpu").manual_seed(tile % 997)
+    T, N, K = 1056, 640, 512
+    x = torch.randn(T, K, generator=g).bfloat16().to(dev)
+    w = torch.randn(N, K, generator=g).bfloat16().to(dev)
+    qa, sa = F.quant_rows(x)
+    qb, sb = F.quant_rows(w)
+    r = torch.randn(T, N, generator=g).bfloat16().to(dev)
+    r8, _ = F.quant_rows(r)
+    bias = torch.randn(N, generator=g).to(dev)
+
+    def run(t):
+        if mode in ("qboth", "qmask8"):
+            o = [torch.full((T, N), 7, dtype=torch.uint8, device=dev), torch.zeros((T, N // 32), dtype=torch.uint8, device=dev),
+                 torch.full((N, T), 7, dtype=torch.uint8, device=dev), torch.zeros((N, T // 32), dtype=torch.uint8, device=dev)]
+            if mode == "qboth":
+                F.gemm_mx(qa, sa, qb, sb, T, N, K, None, relu=True, qout=(o[0], o[1]), qtout=(o[2], o[3]), tile=t)
+            else:
+                F.gemm_mx(qa, sa, qb, sb, T, N, K, None, res=r8, res_mode="mask", qout=(o[0], o[1]),
+                          qtout=(o[2], o[3]), tile=t)
+            return o
+        if mode == "f32split":
+            c = torch.zeros((2, T, N), dtype=torch.float32, device=dev)
+            F.gemm_mx(qa, sa, qb, sb, T, N, K, c, nsplit=2, tile=t)
+            return [c]
+        c = torch.zeros((T, N), dtype=torch.bfloat16, device=dev)
+        F.gemm_mx(qa, sa, qb, sb, T, N, K, c, bias=bias, relu=True, res=r, tile=t)
+        return [c]
+
+    ref, out = run(1282), run(tile)
+    torch.cuda.synchronize()
+    for a, b in zip(ref, out):
+        assert torch.equal(a, b)
