@@ -863,7 +863,7 @@ __global__ void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __r
 // out = sum of n same-shape f32 / bf16 arrays (f32 accumulation, output in the inputs' dtype): the
 // loopback reduce-scatter / all-reduce over virtual devices that share one GPU, in ONE launch
 struct SumPtrs {
-  const void* p[64];
+  const void* p[128];
 };
 
 template <typename T>
@@ -950,7 +950,7 @@ LJS_API int ljs_transpose_bf16(const void* in, void* out, int R, int C, long ldi
 
 LJS_API int ljs_sum_n(const void* const* ins, int n, int is_bf16, long count, void* out, hipStream_t s) {
   // the n input pointers travel BY VALUE in the kernel arguments (graph-capturable, no copy)
-  if (n < 1 || n > 64 || (((uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
+  if (n < 1 || n > 128 || (((uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
   SumPtrs sp = {};
   for (int j = 0; j < n; ++j) {
     if (((uintptr_t)ins[j]) & 15) return (int)hipErrorInvalidValue;

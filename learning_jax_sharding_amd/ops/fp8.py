@@ -20,6 +20,8 @@ from __future__ import annotations
 import ctypes
 from typing import Optional, Tuple
 
+import os
+
 import torch
 
 from . import hip
@@ -191,11 +193,30 @@ def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: Optional[torch.Tensor],
         flags |= 512
     ldc = (od.stride(-2) if od is not None else N)
     sC = od.stride(0) if (od is not None and nsplit > 1) else 0
+    if tile == 0:
+        tile = _auto_tile(M, N, K, flags, nsplit)
     rc = _lib().ljs_gemm_mx_fp8(hip._p(qa), hip._p(sa), hip._p(qb), hip._p(sb), hip._p(od), hip._p(bias), M, N, K,
                                 ldc, flags, hip._p(res), ldr, hip._p(q_o), hip._p(s_o), tile, int(a_bcast),
                                 int(b_bcast), hip._p(qt_o), hip._p(st_o), M, nsplit, sC, hip._stream(qa))
     hip._ck(rc, "gemm_mx_fp8")
     return out
+
+
+# tile choice (scripts/fp8_tiles.py, gpurun_out/r3d/fp8_tiles.log, T=16384): the 8-wave 256x160
+# tile for the N=640 GEMMs of the FF block (down projection + residual 42.9 vs 53.2 us, dX 36.0
+# vs 49.0 us: one round of 256 tiles, a third fewer bytes per FLOP); the epilogue-heavy K=640
+# GEMMs (up projection / dA with both MX copies) stay on the 4-wave 128x128 kernel, whose two
+# blocks per CU overlap one block's epilogue with the other's K-loop.  LJS_F8_AUTO=0: always 1282.
+_F8_AUTO = os.environ.get("LJS_F8_AUTO", "1") == "1"
+
+
+def _auto_tile(M: int, N: int, K: int, flags: int, nsplit: int) -> int:
+    if not _F8_AUTO:
+        return 0
+    quant_out = flags & (256 | 512)
+    if not quant_out and nsplit == 1 and N % 160 == 0 and N <= 1280 and M >= 4096 and K >= 1024:
+        return 256160
+    return 0
 
 
 class _Fp8Linear(torch.autograd.Function):

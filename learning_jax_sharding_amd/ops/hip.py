@@ -12,7 +12,7 @@ import ctypes
 import math
 import os
 import threading
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
@@ -565,7 +565,7 @@ def sum_n(ts: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> tor
     """Elementwise sum of same-shape dense f32 / bf16 tensors on one GPU (f32 accumulation) in one
     launch - the loopback reduction over virtual devices.  Falls back to torch adds otherwise."""
     t0 = ts[0]
-    ok = (t0.is_cuda and t0.dtype in (torch.float32, torch.bfloat16) and 1 <= len(ts) <= 64
+    ok = (t0.is_cuda and t0.dtype in (torch.float32, torch.bfloat16) and 1 <= len(ts) <= 128
           and all(t.shape == t0.shape and t.dtype == t0.dtype and t.device == t0.device and is_dense(t)
                   and t.stride() == t0.stride() and t.data_ptr() % 16 == 0 for t in ts))
     if not ok:
@@ -583,10 +583,10 @@ def sum_n(ts: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> tor
 
 
 def sum_ptrs(ptrs: Sequence[int], out: torch.Tensor) -> torch.Tensor:
-    """out (dense f32 / bf16) = sum of ``len(ptrs)`` <= 64 dense arrays of out's dtype and element
+    """out (dense f32 / bf16) = sum of ``len(ptrs)`` <= 128 dense arrays of out's dtype and element
     count at the given device addresses (16-byte aligned) - e.g. every device's split-K weight
     gradient slabs, summed in one pass (parallel/weight_gather.py)."""
-    assert 1 <= len(ptrs) <= 64 and out.is_cuda and is_dense(out) and all(p % 16 == 0 for p in ptrs)
+    assert 1 <= len(ptrs) <= 128 and out.is_cuda and is_dense(out) and all(p % 16 == 0 for p in ptrs)
     arr = (c_void_p * len(ptrs))(*ptrs)
     rc = lib().ljs_sum_n(arr, len(ptrs), int(out.dtype == torch.bfloat16), out.numel(), _p(out), _stream(out))
     _ck(rc, "sum_n")
@@ -1310,11 +1310,12 @@ def adam(p, g, m, v, step, lr, b1, b2, eps, wd, inplace):
 class SlabGrad:
     """A weight gradient not yet combined: element (r, c) is the sum over s < S of
     ``slabs.view(-1)[offset + s * slab_stride + r * ld + c]`` (the split-K slabs of its GEMM)."""
-    __slots__ = ("slabs", "S", "offset", "ld", "slab_stride", "shape")
+    __slots__ = ("slabs", "S", "offset", "ld", "slab_stride", "shape", "ready")
 
     def __init__(self, slabs, S, offset, ld, slab_stride, shape):
         self.slabs, self.S, self.offset, self.ld, self.slab_stride = slabs, S, offset, ld, slab_stride
         self.shape = tuple(shape)
+        self.ready = None   # event recorded after the producing GEMM (early optimizer launches)
 
 
 class ConstGrad:
@@ -1360,6 +1361,7 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
         assert step.dtype == torch.int32 and step.is_contiguous()
     step_i = step if step.dtype == torch.int32 else step.to(torch.int32)
     ticket = _workspace(step_i.device, "adam_ticket", 64 << 10) if increment_step else None  # two-level tickets
+    rows = _early_adam(rows, step_i, lr, b1, b2, eps, wd, increment_step)
     for i in range(0, len(rows), 32):
         chunk = rows[i:i + 32]
         tab = np.asarray([r[0] for r in chunk], dtype=np.int64).reshape(-1)
@@ -1371,6 +1373,53 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
         _ck(rc, "ljs_adam_multi")
     for p, _, _, _ in entries:
         shadow.mark_fresh(p)
+
+
+# Early optimizer launches: a weight whose gradient is still split-K slabs produced well before
+# the backward ends (the out-projection's dW, computed before the attention backward) is updated
+# on a side stream as soon as its GEMM has run (an event recorded after it), concurrent with the
+# rest of the backward; the main launch waits for it (it reads the same step counter).  In a
+# captured step the side launch is a parallel branch of the graph.  LJS_EARLY_ADAM=0: one launch.
+_EARLY_ADAM = os.environ.get("LJS_EARLY_ADAM", "1") == "1"
+_ADAM_SIDE: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _early_adam(rows, step_i, lr, b1, b2, eps, wd, increment_step):
+    """Launch the rows whose slab gradient became ready before the latest one on a side stream
+    (joined into the current stream before returning); the rest are returned for the main
+    launch."""
+    if not _EARLY_ADAM or not step_i.is_cuda or not increment_step:
+        # (without the folded increment the step counter may be written by an op still queued
+        # on the main stream)
+        return rows
+    evs = [r[1].ready for r in rows if isinstance(r[1], SlabGrad) and r[1].ready is not None]
+    if len(evs) < 2:
+        return rows
+    last = evs[-1]
+    early = [r for r in rows if isinstance(r[1], SlabGrad) and r[1].ready is not None and r[1].ready is not last]
+    if not early or len(early) > 32:
+        return rows
+    main = torch.cuda.current_stream(step_i.device)
+    side = _ADAM_SIDE.get(step_i.device.index)
+    if side is None:
+        side = _ADAM_SIDE[step_i.device.index] = torch.cuda.Stream(step_i.device)
+    seen = set()
+    for r in early:
+        ev = r[1].ready
+        if id(ev) not in seen:
+            seen.add(id(ev))
+            side.wait_event(ev)
+        r[1].slabs.record_stream(side)
+    import numpy as np
+    tab = np.asarray([r[0] for r in early], dtype=np.int64).reshape(-1)
+    arr = (ctypes.c_long * tab.size)(*tab.tolist())
+    with torch.cuda.stream(side):
+        rc = lib().ljs_adam_multi(arr, len(early), _p(step_i), int(increment_step), None, lr, b1, b2, eps, wd,
+                                  ctypes.c_void_p(side.cuda_stream))
+    _ck(rc, "ljs_adam_multi (early)")
+    main.wait_stream(side)
+    ids = {id(r) for r in early}
+    return [r for r in rows if id(r) not in ids]
 
 
 # ============================================================================ RNG

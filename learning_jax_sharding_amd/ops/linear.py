@@ -238,6 +238,13 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
             hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
     if defer is not None:
         defer(slabs, S, materialize)
+        if _DEFER is not None and slabs.is_cuda and hip._EARLY_ADAM:
+            # the optimizer may update this weight as soon as its slabs exist (hip._early_adam)
+            ev = torch.cuda.Event()
+            ev.record()
+            for desc, _ in _DEFER["pending"].values():
+                if isinstance(desc, hip.SlabGrad) and desc.slabs is slabs:
+                    desc.ready = ev
     else:
         materialize()
 

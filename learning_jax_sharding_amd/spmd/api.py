@@ -445,7 +445,9 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
                 one_dev = side and all(len(l.local) == 1 for l in all_leaves) and len(
                     {d for l in all_leaves for d in l.local}) == 1 and not _multi_process()
                 dfr = _lin.defer_wgrads(outs, one_dev, proxies=side and not _multi_process())
-                with torch.autograd.set_multithreading_enabled(_graphs.current() is None), \
+                # (LJS_ATEN_TRACE: on this thread, so the tracer sees the backward's call sites)
+                mt = _graphs.current() is None and not os.environ.get("LJS_ATEN_TRACE")
+                with torch.autograd.set_multithreading_enabled(mt), \
                         _streams.wgrad_scope(side), dfr:
                     gs = torch.autograd.grad(outs, inputs, seeds, allow_unused=True)
             else:

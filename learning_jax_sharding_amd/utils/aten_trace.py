@@ -54,14 +54,44 @@ def _desc(a) -> str:
     return ""
 
 
+# framework (ops.hip) helpers whose launches are data movement or glue rather than the step's
+# math: traced by call site too (they are ctypes calls, invisible to the dispatcher)
+_HIP_GLUE = ("rank_major", "from_rank_major", "concat_parts", "slab_reduce", "cast_transpose_bf16", "swap01_bf16",
+             "transpose_bf16", "colsum_ld", "sum_n", "sum_ptrs", "cast", "cast_into", "bcast_scalar")
+
+
 class AtenTrace(TorchDispatchMode):
-    """Record kernel-launching aten calls: ``(op, operand shapes, call site) -> count``."""
+    """Record kernel-launching aten calls (and the framework's glue kernels, ``_HIP_GLUE``):
+    ``(op, operand shapes, call site) -> count``."""
 
     def __init__(self, cuda_only: bool = True, depth: int = 6):
         super().__init__()
         self.cuda_only = cuda_only
         self.depth = depth
         self.calls: Dict[Tuple[str, str, Tuple[str, ...]], int] = collections.Counter()
+        self._saved = {}
+
+    def __enter__(self):
+        from ..ops import hip
+        for name in _HIP_GLUE:
+            fn = getattr(hip, name, None)
+            if fn is None:
+                continue
+            self._saved[name] = fn
+
+            def wrap(*a, _fn=fn, _name=name, **k):
+                shapes = " ".join(s for s in (_desc(x) for x in a) if s)
+                self.calls[("hip." + _name, shapes, _site(self.depth))] += 1
+                return _fn(*a, **k)
+            setattr(hip, name, wrap)
+        return super().__enter__()
+
+    def __exit__(self, *exc):
+        from ..ops import hip
+        for name, fn in self._saved.items():
+            setattr(hip, name, fn)
+        self._saved.clear()
+        return super().__exit__(*exc)
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}

@@ -352,7 +352,10 @@ def test_fsdp_stack_virtual_devices_matches_host(host_devices, gpu_devices):
     host_devices(4)
     vh, gh = _run_fsdp_stack(4)
     gpu_devices(4)
+    from learning_jax_sharding_amd.parallel import weight_gather as wg
+    n0 = wg.STATS["slab_sum"]
     vg, gg = _run_fsdp_stack(4)
+    assert wg.STATS["slab_sum"] > n0, wg.STATS          # the one-pass slab reduce-scatter ran
     assert abs(vh - vg) <= 3e-2 * max(1.0, abs(vh)), (vh, vg)
     for k in gh:
         for name in gh[k]:

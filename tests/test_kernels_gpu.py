@@ -875,7 +875,7 @@ def test_transpose_bf16_and_swap01(hip, shape):
     assert torch.equal(hip.swap01_bf16(y), y.transpose(0, 1).contiguous())
 
 
-@pytest.mark.parametrize("n", [1, 2, 4, 7])
+@pytest.mark.parametrize("n", [1, 2, 4, 7, 100])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_sum_n(hip, n, dtype):
     """One-launch n-way sum (f32 accumulation, pointers by value) == the f32 torch sum."""
