@@ -575,7 +575,7 @@ gemm_dma_kernel(
   float tsum = 0.f;
   const bool slabs = OUT_F32 && (p.flags & kSlabs);
   const __amdgpu_buffer_rsrc_t rc = make_rsrc(
-      p.C, (OUT_F32 ? 4 : 2) * ((long)((slabs ? p.splitk : p.batch) - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
+      p.C, (OUT_F32 ? 4 : 2) * ((long)((slabs ? p.splitk * p.batch : p.batch) - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
   bool after_epi = false;
 
   // K-tile g landed in LDS for every wave, and every wave's fragment reads of tile g - 1
@@ -788,7 +788,9 @@ gemm_dma_kernel(
     } else {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]
       const bool vec = (p.ldc & 3) == 0 && (p.sC & 3) == 0 && ((((uintptr_t)p.C) & 15) == 0);
-      const long cb = (long)(slabs ? w.split : w.b) * p.sC;  // this item's output block
+      // this item's output block (slab mode: slab (split, batch b) = split * batch + b, so the
+      // slabs of a batch of weight gradients are [S][batch][M][N]: one slab_reduce combines all)
+      const long cb = (long)(slabs ? w.split * p.batch + w.b : w.b) * p.sC;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + j * 16 + 4 * g;
@@ -1027,7 +1029,7 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   // K-tiles and operands addressable with 32-bit byte offsets.
   const int nkt64 = K / BK;
   const bool slabs = flags & kSlabs;
-  if (slabs && (!out_f32 || a_kc || b_kc || batch != 1 || (flags & (8 | 16)) || K % BK ||
+  if (slabs && (!out_f32 || a_kc || b_kc || (flags & (8 | 16)) || K % BK ||
                 a.splitk != splitk || !(tile > 1000 || tile == 643 || tile == 644)))
     return (int)hipErrorInvalidValue;  // the caller's slab count must be the launched split count
   const long k_ext = slabs ? (long)a.splitk * a.kt_per_split * BK : K;  // K-rows the splits address

@@ -222,8 +222,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     ``A`` may be f32 (k-contiguous, bf16 output, no split / epilogue operand / fused sum): the
     GEMM rounds it to bf16 as it reads it (the activation cast fused in) and, with ``acopy`` (bf16
     [M][K]), also writes that rounding for the backward.
-    ``slabs`` (f32 C, m/n-contiguous operands, batch 1, an LDS-DMA tile): split s of the K range
-    writes its own slab ``C + s * sC``; ``splitk`` must be :func:`slab_count`-consistent (the
+    ``slabs`` (f32 C, m/n-contiguous operands, an LDS-DMA tile): split s of batch b's K range
+    writes its own slab ``C + (s * batch + b) * sC``; ``splitk`` must be :func:`slab_count`-consistent (the
     last split may run past K, where it reads zeros), so the split need not divide the K-tiles.
     """
     assert A.dtype in (torch.bfloat16, torch.float32) and B.dtype == torch.bfloat16, (A.dtype, B.dtype)

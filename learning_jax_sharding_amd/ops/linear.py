@@ -208,6 +208,41 @@ def _defer_ok(*ts) -> bool:
     return d is not None and all(t is not None and t.dtype == torch.float32 and _key(t) in d["safe"] for t in ts)
 
 
+def _dw_slabs_wmajor(xb: torch.Tensor, dys: torch.Tensor, T: int, K: int, N: int, ws, pend):
+    """The weight gradients xb^T @ dys[i] of weight-major cotangents dys [nw][T][N] (a seq-major
+    fused projection, ops.linear.token_outer) as ONE slab-mode launch (batch i, split s -> slab
+    [s][i] of [S][nw][K][N]) and, when combined, ONE slab_reduce into views of one [nw][K][N]
+    buffer (so a reduce-scatter / bucket takes them without a concatenation).  Each gradient is
+    deferred as slabs when allowed (``pend``).  None when the slab-mode kernel does not apply."""
+    nw = len(ws)
+    tile, S, slab_mode = hip.pick_dw_slabs(K, nw * N, T)
+    if not slab_mode or (_DW_SPLIT and T % (64 * _DW_SPLIT) == 0):
+        return None
+    slabs = torch.empty((S, nw, K, N), dtype=torch.float32, device=xb.device)
+    out = torch.empty((nw, K, N), dtype=torch.float32, device=xb.device)
+    hip.gemm(xb, dys, slabs, K, N, T, K, N, N, False, False, batch=nw, sA=0, sB=T * N, sC=K * N, splitk=S,
+             tile=tile, slabs=True)
+    done = []
+
+    def materialize():
+        if not done:
+            done.append(True)
+            hip.slab_reduce(slabs.view(S, nw * K, N), out.view(nw * K, N), N, 0)
+    ev = None
+    for i, w in enumerate(ws):
+        if pend is not None and _defer_ok(w):
+            sg = hip.SlabGrad(slabs, S, i * K * N, N, nw * K * N, (K, N))
+            if hip._EARLY_ADAM:
+                if ev is None:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                sg.ready = ev
+            pend[out[i].data_ptr()] = (sg, materialize)
+        else:
+            materialize()
+    return [out[i] for i in range(nw)]
+
+
 def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: int, out: torch.Tensor, cb: int,
               out_bs: int, twin: Optional[torch.Tensor] = None, tail=None, defer=None) -> None:
     """out (column blocks of width cb, out_bs apart) = xb^T @ dy for xb [T][K], dy [T][Nt] (row
@@ -581,6 +616,11 @@ def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, 
                 _dp.register_wire_twin(dW, twin)
             for i in want:
                 dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
+        elif (_WMAJOR_BATCH and len(want) == nw and nw > 1 and ld0 == N and not wire and all(
+                mats[i][1] == N and mats[i][0].data_ptr() == t0.data_ptr() + i * M * N * 2 for i in want)
+                and (wm := _dw_slabs_wmajor(xb, t0, M, K, N, [ws[i] for i in want], pend)) is not None):
+            for j, i in enumerate(want):
+                dws[i] = wm[j] if ws[i].dtype == torch.float32 else wm[j].to(ws[i].dtype)
         else:
             for i in want:
                 t, ld = mats[i]
@@ -610,6 +650,11 @@ def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, 
                 sk = _splitk(K, N, M, 1, tile)
                 hip.gemm(xb, t, dW, K, N, M, K, ld, N, False, False, splitk=sk, tile=tile, zero_c=True)
                 dws[i] = dW if ws[i].dtype == torch.float32 else dW.to(ws[i].dtype)
+
+
+# the weight-major (seq-major fused projection) weight gradients as one batched slab-mode launch
+# instead of one GEMM per weight (LJS_WMAJOR_DW_BATCH=0: per weight)
+_WMAJOR_BATCH = os.environ.get("LJS_WMAJOR_DW_BATCH", "1") == "1"
 
 
 def supported(x: torch.Tensor, ws: Sequence[torch.Tensor], b) -> bool:

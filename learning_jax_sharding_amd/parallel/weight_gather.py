@@ -36,7 +36,7 @@ __all__ = ["eligible", "gather_bf16"]
 
 _ON = os.environ.get("LJS_GATHER_SHADOWS", "1") == "1"
 # how the backward reduce-scatters ran (tests / diagnostics): one-pass slab sums vs combined grads
-STATS = {"slab_sum": 0, "combined": 0}
+STATS = {"slab_sum": 0, "combined": 0, "stacked": 0}
 
 
 def _gather_dim(src: TileAssignment, dst: TileAssignment, shape) -> Optional[int]:
@@ -114,6 +114,27 @@ def _slabs_ok(ents, devs, shape) -> bool:
         and sum(sg.S for sg in sgs) <= 128)
 
 
+def _stacked_grads(gs, devs, nw, pend):
+    """{device: [nw][K][N] view} when every device's nw gradients are consecutive [K][N] slices of
+    one f32 buffer and none is still uncombined (``pend``); else None."""
+    if nw < 2:
+        return None
+    out = {}
+    for j, d in enumerate(devs):
+        g0 = gs[j * nw]
+        if g0 is None or g0.dtype != torch.float32 or not g0.is_contiguous() or g0.dim() != 2:
+            return None
+        K, N = g0.shape
+        for i in range(nw):
+            g = gs[j * nw + i]
+            if (g is None or not g.is_contiguous() or tuple(g.shape) != (K, N) or g.dtype != g0.dtype
+                    or g.data_ptr() != g0.data_ptr() + i * K * N * 4
+                    or (pend is not None and g.data_ptr() in pend)):
+                return None
+        out[d] = torch.as_strided(g0, (nw, K, N), (K * N, N, 1))
+    return out
+
+
 def _hip_cls(name):
     from ..ops import hip
     return getattr(hip, name)
@@ -169,6 +190,17 @@ class _GatherBf16(torch.autograd.Function):
         from ..ops import linear as _lin
         res = [None] * len(gs)
         pend = _lin._DEFER["pending"] if _lin._DEFER is not None else None
+        stacked = _stacked_grads(gs, devs, nw, pend)
+        if stacked is not None and not _loopback(groups, stacked):
+            # the nw gradients are slices of one [nw][K][N] buffer on every device (a batched
+            # weight-gradient launch): ONE reduce-scatter of the stack, whose shards are slices of
+            # one buffer in turn (a gradient bucket takes them without concatenating)
+            STATS["stacked"] += 1
+            red = C._run(C._Spec("reduce_scatter", groups, dim=dim + 1), stacked)
+            for j, d in enumerate(devs):
+                for i in range(nw):
+                    res[j * nw + i] = red[d][i]
+            return (None,) + tuple(res)
         for i in range(nw):
             xs, ents = {}, {}
             for j, d in enumerate(devs):

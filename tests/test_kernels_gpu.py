@@ -926,3 +926,21 @@ def test_fp8_gemm_8wave_tiles_match_4wave(hip, tile, mode):
     torch.cuda.synchronize()
     for a, b in zip(ref, out):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("tile", [1282, 12883, 12884, 2563])
+def test_gemm_slab_mode_batched_weights(hip, tile):
+    """Slab mode over a batch of weight-major cotangents (shared X, dY_i at stride T*N): slab
+    [s][i] = split s of weight i, bit-identical to the one-weight launches."""
+    T, K, N, nw = 4096, 640, 512, 3
+    S = 4
+    assert hip.slab_count(T // 64, S) == S
+    x = _rand(T, K, seed=80)
+    dys = _rand(nw * T, N, seed=81).view(nw, T, N)
+    slabs = torch.full((S, nw, K, N), float("nan"), dtype=torch.float32, device=dev)
+    hip.gemm(x, dys, slabs, K, N, T, K, N, N, False, False, batch=nw, sA=0, sB=T * N, sC=K * N, splitk=S,
+             tile=tile, slabs=True)
+    for i in range(nw):
+        one = torch.full((S, K, N), float("nan"), dtype=torch.float32, device=dev)
+        hip.gemm(x, dys[i], one, K, N, T, K, N, N, False, False, sC=K * N, splitk=S, tile=tile, slabs=True)
+        assert torch.equal(slabs[:, i], one)
