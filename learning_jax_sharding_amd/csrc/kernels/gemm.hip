@@ -39,6 +39,7 @@ struct GemmArgs {
   long ldr, sR;
   bf16_t* acopy;    // f32-A kernels: the bf16 rounding of A ([M][K], dense), written by the items of
                     // batch 0 / tile column 0 (the operand the backward's weight gradient reads)
+  const bf16_t* bptr[4];  // flags & kBPtrs (slab mode): batch b's B operand (instead of B + b * sB)
 };
 
 constexpr int kResAdd = 64, kResMask = 128, kResF32 = 256;
@@ -49,6 +50,9 @@ constexpr int kSlabs = 512;
 // item order with the tile-row fastest (set by the launcher when there are fewer tile rows
 // than tile columns; see decode_item)
 constexpr int kMFast = 1024;
+// B operand of batch b taken from bptr[b] (up to 4 separate tensors, e.g. the q / k / v
+// cotangents of a weight-major fused projection) -- slab-mode LDS-DMA kernels only
+constexpr int kBPtrs = 4096;
 
 // Epilogue operand R applied to 8 consecutive output values (after bias / ReLU, f32):
 //   residual add: out = bf16(bf16(v) + bf16(R))   (the unfused "y = dense(x); y + R" in bf16:
@@ -527,7 +531,7 @@ gemm_dma_kernel(
   auto load_item = [&](int k) {
     const WorkItem w = decode_item(p, slot + G * k, ntm, ntn);
     ra = make_rsrc(reinterpret_cast<const unsigned char*>(p.A) + (long)w.b * p.sA * AES, a_bytes);
-    rb = make_rsrc(p.B + (long)w.b * p.sB, b_bytes);
+    rb = make_rsrc((p.flags & kBPtrs) ? p.bptr[w.b] : p.B + (long)w.b * p.sB, b_bytes);
     a_off = __builtin_amdgcn_readfirstlane(
         (int)((A_KC ? (long)w.m0 * BM * p.lda : (long)w.m0 * BM) * AES + w.kt0 * a_kt));
     b_off = __builtin_amdgcn_readfirstlane(
@@ -996,6 +1000,15 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   a.ldr = ldr;
   a.sR = sR;
   a.acopy = (bf16_t*)acopy;
+  if (flags & kBPtrs) {
+    // B is a HOST array of `batch` (<= 4) device pointers, one B operand per batch
+    if (batch < 1 || batch > 4 || !(flags & kSlabs)) return (int)hipErrorInvalidValue;
+    const void* const* bp = (const void* const*)B;
+    for (int i = 0; i < 4; ++i) a.bptr[i] = (const bf16_t*)(i < batch ? bp[i] : bp[0]);
+    a.B = a.bptr[0];
+  } else {
+    for (int i = 0; i < 4; ++i) a.bptr[i] = nullptr;
+  }
   if (flags & kAF32) {
     // f32 A: the 8-wave 128x128 LDS-DMA kernel only (bf16 output, k-contiguous operands, no
     // split, no epilogue operand / fused sum); every condition is the caller's to meet

@@ -207,7 +207,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
          accumulate: bool = False, splitk: int = 1, tile: Optional[int] = None, a_off: int = 0, b_off: int = 0,
          c_off: int = 0, zero_c: bool = False, psum: Optional[torch.Tensor] = None,
          res: Optional[torch.Tensor] = None, res_ld: int = 0, res_mode: str = "add", sR: int = 0,
-         slabs: bool = False, acopy: Optional[torch.Tensor] = None) -> int:
+         slabs: bool = False, acopy: Optional[torch.Tensor] = None,
+         b_list: Optional[Sequence[torch.Tensor]] = None) -> int:
     """Raw launcher.  A/B bf16; C bf16 or f32 (split-K/accumulate need f32 C).
 
     ``lda``/``ldb`` may be 0 for an operand that repeats one row (a broadcast gradient).
@@ -222,6 +223,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     ``A`` may be f32 (k-contiguous, bf16 output, no split / epilogue operand / fused sum): the
     GEMM rounds it to bf16 as it reads it (the activation cast fused in) and, with ``acopy`` (bf16
     [M][K]), also writes that rounding for the backward.
+    ``b_list`` (slab mode, batch <= 4): batch b's B operand is ``b_list[b]`` (separate tensors).
     ``slabs`` (f32 C, m/n-contiguous operands, an LDS-DMA tile): split s of batch b's K range
     writes its own slab ``C + (s * batch + b) * sC``; ``splitk`` must be :func:`slab_count`-consistent (the
     last split may run past K, where it reads zeros), so the split need not divide the K-tiles.
@@ -239,7 +241,14 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc)
     eA = A.element_size()
     cnt = c_int(0)
-    rc = lib().ljs_gemm_bf16(ctypes.c_void_p(A.data_ptr() + a_off * eA), ctypes.c_void_p(B.data_ptr() + b_off * eA),
+    b_arg = ctypes.c_void_p(B.data_ptr() + b_off * eA)
+    if b_list is not None:
+        # slab mode over a batch of separate B tensors (each laid out like B): pointers by value
+        assert slabs and len(b_list) == batch <= 4 and all(t.dtype == torch.bfloat16 for t in b_list)
+        flags |= 4096
+        b_keep = (c_void_p * len(b_list))(*[t.data_ptr() + b_off * eA for t in b_list])
+        b_arg = ctypes.cast(b_keep, c_void_p)
+    rc = lib().ljs_gemm_bf16(ctypes.c_void_p(A.data_ptr() + a_off * eA), b_arg,
                              ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb,
                              ldc, sA, sB, sC, sBias, batch, int(a_kc), int(b_kc), int(out_f32), flags, alpha,
                              splitk, tile, _p(psum), ctypes.byref(cnt), _p(res), res_ld, sR, _p(acopy), _stream(C))
@@ -1380,7 +1389,9 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
 # on a side stream as soon as its GEMM has run (an event recorded after it), concurrent with the
 # rest of the backward; the main launch waits for it (it reads the same step counter).  In a
 # captured step the side launch is a parallel branch of the graph.  LJS_EARLY_ADAM=0: one launch.
-_EARLY_ADAM = os.environ.get("LJS_EARLY_ADAM", "1") == "1"
+# Measured: b8 0.1003 vs 0.0875 ms, b64 0.2605-0.2625 vs 0.2459-0.2472 ms (gpurun_out/r3g): the
+# side branch costs more than the overlap buys -- off by default.
+_EARLY_ADAM = os.environ.get("LJS_EARLY_ADAM", "0") == "1"
 _ADAM_SIDE: Dict[int, "torch.cuda.Stream"] = {}
 
 

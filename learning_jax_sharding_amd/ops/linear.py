@@ -208,7 +208,7 @@ def _defer_ok(*ts) -> bool:
     return d is not None and all(t is not None and t.dtype == torch.float32 and _key(t) in d["safe"] for t in ts)
 
 
-def _dw_slabs_wmajor(xb: torch.Tensor, dys: torch.Tensor, T: int, K: int, N: int, ws, pend):
+def _dw_slabs_wmajor(xb: torch.Tensor, dys, T: int, K: int, N: int, ws, pend):
     """The weight gradients xb^T @ dys[i] of weight-major cotangents dys [nw][T][N] (a seq-major
     fused projection, ops.linear.token_outer) as ONE slab-mode launch (batch i, split s -> slab
     [s][i] of [S][nw][K][N]) and, when combined, ONE slab_reduce into views of one [nw][K][N]
@@ -220,8 +220,10 @@ def _dw_slabs_wmajor(xb: torch.Tensor, dys: torch.Tensor, T: int, K: int, N: int
         return None
     slabs = torch.empty((S, nw, K, N), dtype=torch.float32, device=xb.device)
     out = torch.empty((nw, K, N), dtype=torch.float32, device=xb.device)
-    hip.gemm(xb, dys, slabs, K, N, T, K, N, N, False, False, batch=nw, sA=0, sB=T * N, sC=K * N, splitk=S,
-             tile=tile, slabs=True)
+    # dys: the nw [T][N] cotangents (separate tensors: q's from the attention backward, k's and
+    # v's from the sequence gather's reduce-scatter), read through per-batch B pointers
+    hip.gemm(xb, dys[0], slabs, K, N, T, K, N, N, False, False, batch=nw, sA=0, sC=K * N, splitk=S,
+             tile=tile, slabs=True, b_list=dys)
     done = []
 
     def materialize():
@@ -616,9 +618,10 @@ def _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, 
                 _dp.register_wire_twin(dW, twin)
             for i in want:
                 dws[i] = dW[i] if ws[i].dtype == torch.float32 else dW[i].to(ws[i].dtype)
-        elif (_WMAJOR_BATCH and len(want) == nw and nw > 1 and ld0 == N and not wire and all(
-                mats[i][1] == N and mats[i][0].data_ptr() == t0.data_ptr() + i * M * N * 2 for i in want)
-                and (wm := _dw_slabs_wmajor(xb, t0, M, K, N, [ws[i] for i in want], pend)) is not None):
+        elif (_WMAJOR_BATCH and len(want) == nw and 1 < nw <= 4 and not wire and all(
+                mats[i][1] == N and mats[i][0].stride(-1) == 1 and mats[i][0].data_ptr() % 16 == 0 for i in want)
+                and (wm := _dw_slabs_wmajor(xb, [mats[i][0] for i in want], M, K, N, [ws[i] for i in want],
+                                            pend)) is not None):
             for j, i in enumerate(want):
                 dws[i] = wm[j] if ws[i].dtype == torch.float32 else wm[j].to(ws[i].dtype)
         else:

@@ -125,12 +125,16 @@ def _stacked_grads(gs, devs, nw, pend):
         if g0 is None or g0.dtype != torch.float32 or not g0.is_contiguous() or g0.dim() != 2:
             return None
         K, N = g0.shape
+        st = g0.untyped_storage()
         for i in range(nw):
             g = gs[j * nw + i]
             if (g is None or not g.is_contiguous() or tuple(g.shape) != (K, N) or g.dtype != g0.dtype
+                    or g.untyped_storage().data_ptr() != st.data_ptr()
                     or g.data_ptr() != g0.data_ptr() + i * K * N * 4
                     or (pend is not None and g.data_ptr() in pend)):
                 return None
+        if (g0.storage_offset() + nw * K * N) * 4 > st.nbytes():
+            return None
         out[d] = torch.as_strided(g0, (nw, K, N), (K * N, N, 1))
     return out
 

@@ -940,7 +940,13 @@ def test_gemm_slab_mode_batched_weights(hip, tile):
     slabs = torch.full((S, nw, K, N), float("nan"), dtype=torch.float32, device=dev)
     hip.gemm(x, dys, slabs, K, N, T, K, N, N, False, False, batch=nw, sA=0, sB=T * N, sC=K * N, splitk=S,
              tile=tile, slabs=True)
+    # the same batch from separate B tensors (per-batch pointers)
+    sep = [dys[i].clone() for i in range(nw)]
+    slabs2 = torch.full((S, nw, K, N), float("nan"), dtype=torch.float32, device=dev)
+    hip.gemm(x, sep[0], slabs2, K, N, T, K, N, N, False, False, batch=nw, sA=0, sC=K * N, splitk=S,
+             tile=tile, slabs=True, b_list=sep)
     for i in range(nw):
         one = torch.full((S, K, N), float("nan"), dtype=torch.float32, device=dev)
         hip.gemm(x, dys[i], one, K, N, T, K, N, N, False, False, sC=K * N, splitk=S, tile=tile, slabs=True)
         assert torch.equal(slabs[:, i], one)
+        assert torch.equal(slabs2[:, i], one)
