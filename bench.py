@@ -309,7 +309,8 @@ def main():
         run(max(1, args.warmup))
         if aten_trace:
             from learning_jax_sharding_amd.utils.aten_trace import AtenTrace
-            with AtenTrace() as tr:
+            with AtenTrace(cuda_only=not os.environ.get("LJS_ATEN_TRACE_ALL"),
+                           depth=int(os.environ.get("LJS_ATEN_TRACE_DEPTH", "6"))) as tr:
                 run(1)
             if int(os.environ.get("RANK", "0")) == 0:
                 tr.write(aten_trace)

@@ -374,6 +374,31 @@ def _seed(t: torch.Tensor, value: float) -> torch.Tensor:
     return s
 
 
+_SEED_HOIST = os.environ.get("LJS_SEED_HOIST", "1") == "1"
+
+
+def _through_permutations(ts: List[torch.Tensor]) -> List[torch.Tensor]:
+    """The tensors to seed with a summed loss's constant cotangent: when ``ts`` are ALL the
+    outputs of one all-to-all (a permutation of elements over the devices - e.g. the reference's
+    final ``("batch", "length", "embed")`` constraint on the block output), the all-to-all's inputs
+    instead, repeatedly.  The sum is the same either way, and the backward then runs no transposed
+    all-to-all on a materialised constant (a copy, a pack and a column-sum kernel per step)."""
+    if not _SEED_HOIST:
+        return ts
+    while ts:
+        fn = ts[0].grad_fn
+        if fn is None or type(fn).__name__ != "_CollectiveFnBackward" or getattr(fn, "perm_inputs", None) is None:
+            return ts
+        ins = fn.perm_inputs
+        if len(ts) != len(ins) or any(t.grad_fn is not fn for t in ts) or \
+                sorted(t.output_nr for t in ts) != list(range(len(ins))):
+            return ts
+        if not all(x.requires_grad for x in ins):
+            return ts
+        ts = list(ins)
+    return ts
+
+
 def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
     multi = isinstance(argnums, (tuple, list))
     argnums_t = tuple(argnums) if multi else (argnums,)
@@ -401,7 +426,7 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
             # out = sum(x) whose value nobody has read: seed x with the broadcast cotangent
             # (gsize / n_holders in x's dtype, all strides 0 - what the sum's backward returns)
             xs, gsize = sum_inputs
-            for d, t in xs.items():
+            for t in _through_permutations([t for t in xs.values()]):
                 outs.append(t)
                 seeds.append(_seed(t.new_empty(()), gsize / n_holders).expand(t.shape))
         elif partials is not None and not _SEED_THROUGH_ALLREDUCE:
