@@ -922,7 +922,37 @@ __global__ void debug_mfma_f8_kernel(const i32x8* a, const i32x8* b, const int* 
 
 }  // namespace
 
+// semantics probe of the gfx950 scaled conversion v_cvt_scalef32_pk_fp8_bf16 against the
+// reference path (bf16 -> f32, times 2^-x, RNE to e4m3): per element i (bf16 pair in[i], block
+// exponent x[i]): out[4 i + 0..1] = reference bytes, out[4 i + 2] = scalef32 with scale 2^x,
+// out[4 i + 3] = scalef32 with scale 2^-x (low bytes of each)
+__global__ void debug_cvt_scalef_kernel(const unsigned* in, const int* xs, unsigned* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned w = in[i];
+  const int x = xs[i];
+  const float a = __uint_as_float(w << 16), b = __uint_as_float(w & 0xffff0000u);
+  const float inv = ldexpf(1.f, -x);
+  const unsigned ref = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(a * inv, b * inv, 0, false) & 0xffffu;
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  const bf2 v = __builtin_bit_cast(bf2, w);
+  s2 o1 = {0, 0}, o2 = {0, 0};
+  o1 = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(o1, v, ldexpf(1.f, x), false);
+  o2 = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(o2, v, inv, false);
+  out[4 * i] = ref;
+  out[4 * i + 1] = 0;
+  out[4 * i + 2] = __builtin_bit_cast(unsigned, o1) & 0xffffu;
+  out[4 * i + 3] = __builtin_bit_cast(unsigned, o2) & 0xffffu;
+}
+
 // a, b: 64 lanes x 32 bytes; sa, sb: 64 ints (scale byte in bits 0-7); c: 64 lanes x 4 floats
+LJS_API int ljs_debug_cvt_scalef(const void* in, const void* xs, void* out, int n, hipStream_t stream) {
+  hipLaunchKernelGGL(debug_cvt_scalef_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, (const unsigned*)in,
+                     (const int*)xs, (unsigned*)out, n);
+  return (int)hipGetLastError();
+}
+
 LJS_API int ljs_debug_mfma_f8(const void* a, const void* b, const void* sa, const void* sb, void* c,
                               hipStream_t stream) {
   hipLaunchKernelGGL(debug_mfma_f8_kernel, dim3(1), dim3(64), 0, stream, (const i32x8*)a, (const i32x8*)b,
