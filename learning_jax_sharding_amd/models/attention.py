@@ -67,6 +67,25 @@ class MultiHeadAttention(Module):
         from ..parallel.fsdp import Prefetcher
         return Prefetcher(wo.sharding.mesh, axis, bf16_shadows=dt == torch.bfloat16).prefetch([wo])
 
+    def _prefetch_qkv(self, x: ShardedArray, ws, dt):
+        from ..sharding import NamedSharding
+        w0 = ws[0]
+        if dt != torch.bfloat16 or any(t.is_meta or not t.is_cuda for w in ws for t in w.local.values()):
+            return None
+        sh, xs = w0.sharding, x.sharding
+        if not isinstance(sh, NamedSharding) or not isinstance(xs, NamedSharding) or not sh.spec:
+            return None
+        if any(w.sharding != sh for w in ws):
+            return None
+        axis = sh.spec[0]
+        if not isinstance(axis, str) or sh.mesh.shape[axis] < 2 or (len(sh.spec) > 1 and sh.spec[1] is not None):
+            return None
+        xspec = tuple(xs.spec) + (None,) * (x.ndim - len(xs.spec))
+        if xspec[-1] is not None:
+            return None
+        from ..parallel.fsdp import Prefetcher
+        return Prefetcher(sh.mesh, axis, bf16_shadows=True).prefetch_joint(ws)
+
     def _log(self, *a):
         if self.verbose:
             print(*a)
@@ -89,7 +108,20 @@ class MultiHeadAttention(Module):
             wq = self.query.kernel_param(m)
             wk = self.key.kernel_param(m)
             wv = self.value.kernel_param(m)
-            query_proj, key_proj, value_proj = core.dense(hidden_states, [wq, wk, wv], None, compute_dtype=dt)
+            # Q/K/V kernels sharded over their input features (the reference's 2-D rules: embed
+            # -> model) while the activation's features are whole: their one stacked bf16 gather
+            # runs on a side stream, and the projection GEMM waits for it only after queueing
+            # the activation's cast pass (ops/linear.defer_wait)
+            qkv_pf = self._prefetch_qkv(hidden_states, [wq, wk, wv], dt)
+            if qkv_pf is not None:
+                from ..ops import linear as _lin
+                _lin.defer_wait(qkv_pf)
+                ws = qkv_pf.tree()
+            else:
+                ws = [wq, wk, wv]
+            query_proj, key_proj, value_proj = core.dense(hidden_states, ws, None, compute_dtype=dt)
+            if qkv_pf is not None:
+                qkv_pf.wait()
         else:
             query_proj = self.query(hidden_states)
             key_proj = self.key(context)

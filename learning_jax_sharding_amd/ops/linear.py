@@ -394,6 +394,9 @@ class _Linear(torch.autograd.Function):
             xb = hip.swap01_bf16(x.contiguous()).view(M, K)
         else:
             xb = None if cast_on_load else _bf16(x2 if x2.is_contiguous() else x2.contiguous())
+        # weights gathered on a side stream (parallel/fsdp.Prefetcher.prefetch(defer_wait=True)):
+        # the stream waits for them only now, after the activation's cast pass was queued
+        take_pending_waits(x.device)
         if nw == 1:
             wt = shadow.get(ws[0], "T")
             sB = 0
@@ -571,6 +574,22 @@ class _Linear(torch.autograd.Function):
             if joint_bf16 is not None:
                 _dp.register_wire_twin(joint, joint_bf16)
         return (dx, db, dres, None, None, *dws)
+
+
+# side-stream gathers whose completion the next _Linear forward waits for after its input cast
+_PENDING_WAITS: List = []
+
+
+def defer_wait(handle) -> None:
+    """Register a prefetch handle (parallel/fsdp._Handle) to be waited on by the next dense GEMM
+    after it has queued its activation pass; the caller still calls ``handle.wait()`` after the
+    dense (a no-op for the stream by then) in case no GEMM consumed it."""
+    _PENDING_WAITS.append(handle)
+
+
+def take_pending_waits(dev) -> None:
+    while _PENDING_WAITS:
+        _PENDING_WAITS.pop().wait()
 
 
 def twin_free(joint_bf16, wire) -> bool:

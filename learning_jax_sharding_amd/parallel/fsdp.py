@@ -67,17 +67,32 @@ class _Handle:
         self._tree = tree
         self._event = event
         self._stream = stream
+        self._waited = False
+
+    def tree(self):
+        """The gathered tree WITHOUT ordering the current stream after the gathers (the consumer
+        must call :meth:`wait` before any kernel reads it - ops.linear.defer_wait)."""
+        return self._tree
 
     def wait(self):
         """The gathered tree, ordered after the side-stream gathers on the current stream."""
+        if self._waited:
+            return self._tree
+        self._waited = True
         if self._event is not None:
             cur = torch.cuda.current_stream()
             cur.wait_event(self._event)
+            from ..ops import shadow as _shadow
             for leaf in T.tree_leaves(self._tree, is_leaf=_is_arr):
                 if _is_arr(leaf):
                     for t in leaf.local.values():
                         if t.is_cuda:
                             t.record_stream(cur)
+                            if t.dim() == 2 and _shadow.is_proxy(t):
+                                # a gathered-weight proxy: its data is the bf16 buffer the side
+                                # stream allocated (kept by the shadow registry)
+                                for buf in _shadow.kinds_of(t).values():
+                                    buf.record_stream(cur)
         return self._tree
 
 
@@ -113,6 +128,38 @@ class Prefetcher:
             if gdim is not None:
                 return _wg.gather_bf16([p], dst, gdim, note="fsdp.prefetch")[0]
         return reshard_tile(p, dst, note="fsdp.prefetch")
+
+    def prefetch_joint(self, ws) -> _Handle:
+        """Gather same-sharded 2-D weights (e.g. Q/K/V) as ONE collective of their stacked bf16
+        shadows on the side stream (per weight when that does not apply)."""
+        ws = list(ws)
+        w0 = ws[0]
+        dims = self._dims(w0)
+        if not dims or any(w.tile != w0.tile or tuple(w.shape) != tuple(w0.shape) for w in ws):
+            return self.prefetch(ws)
+        dst = w0.tile.unshard(dims)
+        from . import weight_gather as _wg
+        gdim = _wg.eligible(ws, dst) if self.bf16_shadows else None
+        if gdim is None:
+            return self.prefetch(ws)
+        devs = sorted({t.device.index for w in ws for t in w.local.values() if t.is_cuda})
+        dev = devs[0]
+        s = self._streams.get(dev)
+        if s is None:
+            s = self._streams[dev] = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            out = _wg.gather_bf16(ws, dst, gdim, note="prefetch.joint")
+            ev = torch.cuda.Event()
+            ev.record(s)
+        return _Handle(out, ev, s)
+
+    def _dims(self, p: ShardedArray):
+        sh = p.sharding
+        if isinstance(sh, NamedSharding):
+            spec = tuple(sh.spec) + (None,) * (p.ndim - len(sh.spec))
+            return [d for d, e in enumerate(spec) if e == self.axis or (isinstance(e, tuple) and self.axis in e)]
+        return [d for d in range(p.ndim) if p.tile.tile_shape[d] > 1]
 
     def prefetch(self, tree: Any) -> _Handle:
         leaves = [l for l in T.tree_leaves(tree, is_leaf=_is_arr) if _is_arr(l)]
