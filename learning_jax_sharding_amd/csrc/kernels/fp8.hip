@@ -260,7 +260,15 @@ __device__ __forceinline__ f32x4 f8_mfma(const i32x8& a, const i32x8& b, const f
 // BM x 128 output tile, BM / 64 x 2 waves of 64 x 64 (BM = 128: 4 waves; 256: 8 waves, two per
 // SIMD), BK = 128 (one MFMA K step per K-tile), an NST-deep ring of LDS-DMA stages (A and B
 // tiles + the per-row scale words), counted vmcnt, one raw barrier per K-tile.
-template <int BM, int NST>
+// FIX: the epilogue's flags as compile-time constants for the FF block's two epilogue-heavy
+// GEMMs (1: up projection = ReLU + both MX copies, no bf16 output; 2: dA = e4m3 ReLU mask +
+// both MX copies, no bf16 output); 0 reads p.flags at run time
+template <int FIX>
+__device__ __forceinline__ int f8_flags(const F8Args& p) {
+  return FIX == 1 ? (1 | 256 | 512) : FIX == 2 ? (128 | 1024 | 256 | 512) : p.flags;
+}
+
+template <int BM, int NST, int FIX = 0>
 __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   constexpr int NW = BM / 32;                      // waves (BM / 64 rows x 2 cols)
   constexpr int A_TILE = BM * F8_BK, B_TILE = 128 * F8_BK;
@@ -378,9 +386,11 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   // epilogue: lane holds C[row 16 i + r16][cols 16 j + 4 g .. +3]; lane pairs (g, g^1) trade
   // halves -> 8 consecutive columns per lane -> one 16-byte (bf16) / 2 x 16-byte (f32) store.
   // A 32-column MX block of a row sits in the 4 lanes r16, r16 + 16, + 32, + 48 (g = 0..3).
-  const bool relu = p.flags & 1, has_bias = p.flags & 2, bias_f32 = p.flags & 4, out_f32 = p.flags & 32;
-  const bool res_add = p.flags & 64, res_mask = p.flags & 128, qout = p.flags & 256;
-  const bool qtout = p.flags & 512, r_fp8 = p.flags & 1024;
+  const int flags = f8_flags<FIX>(p);
+  const bool relu = flags & 1, has_bias = flags & 2, bias_f32 = flags & 4, out_f32 = flags & 32;
+  const bool res_add = flags & 64, res_mask = flags & 128, qout = flags & 256;
+  const bool qtout = flags & 512, r_fp8 = flags & 1024;
+  void* const Cp = FIX ? nullptr : p.C;   // (the fixed epilogues write no bf16 output)
   const bool even = (g & 1) == 0;
   // the epilogue operand's 8 chunks per lane are all requested before the first is used (one
   // exposed latency per item instead of one per 16-row block); rows / columns outside the
@@ -491,7 +501,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
         }
       }
       if (staged) {
-        if (p.C || qtout) {  // (the transposed MX copy is formed from this bf16 image)
+        if (Cp || qtout) {  // (the transposed MX copy is formed from this bf16 image)
           u32x4 pk;
 #pragma unroll
           for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
@@ -502,28 +512,28 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
       }
       if (!ok) continue;
       if (out_f32) {
-        float* C = reinterpret_cast<float*>(p.C) + split * p.sC + (long)row * p.ldc + col;
+        float* C = reinterpret_cast<float*>(Cp) + split * p.sC + (long)row * p.ldc + col;
         *reinterpret_cast<f32x4*>(C) = f32x4{v[0], v[1], v[2], v[3]};
         *reinterpret_cast<f32x4*>(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
-      } else if (p.C) {
+      } else if (Cp) {
         u32x4 pk;
 #pragma unroll
         for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
-        *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(p.C) + (long)row * p.ldc + col) = pk;
+        *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(Cp) + (long)row * p.ldc + col) = pk;
       }
     }
   }
   if (!staged) return;
   __syncthreads();
   constexpr int NT = BM * 2;  // threads
-  if (p.C) {
+  if (Cp) {
 #pragma unroll
     for (int r = 0; r < BM * 16 / NT; ++r) {
       const int c = tid + NT * r, lr = c >> 4, ch = c & 15;
       const int grow = m0 + lr, gcol = n0 + ch * 8;
       const u32x4 val = *reinterpret_cast<const u32x4*>(Cs + lr * 256 + ((ch ^ (lr & 15)) << 4));
       if (grow < p.M && gcol < p.N)
-        *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(p.C) + (long)grow * p.ldc + gcol) = val;
+        *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(Cp) + (long)grow * p.ldc + gcol) = val;
     }
   }
   if (qout) {
@@ -596,10 +606,12 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
 }
 
 #undef F8_ISSUE
-template __global__ void gemm_mx_fp8_kernel<128, 2>(F8Args);
-template __global__ void gemm_mx_fp8_kernel<128, 3>(F8Args);
-template __global__ void gemm_mx_fp8_kernel<256, 2>(F8Args);
-template __global__ void gemm_mx_fp8_kernel<256, 3>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<128, 2, 0>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<128, 3, 0>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<256, 2, 0>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<256, 3, 0>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<128, 2, 1>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<128, 2, 2>(F8Args);
 
 // ---------------------------------------------------------------------------- GEMM, 8 waves
 // Large-tile MX-fp8 GEMM: BM x BN output tile, 8 waves (WM x WN, each (BM/WM) x (BN/WN)), BK =
@@ -909,7 +921,18 @@ hipError_t launch_mx8(const F8Args& a, int tiles, hipStream_t s) {
 
 template <int BM, int NST>
 hipError_t launch_f8(const F8Args& a, int tiles, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_mx_fp8_kernel<BM, NST>), dim3(tiles), dim3(BM * 2), 0, s, a);
+  // the FF block's up projection / dA epilogues get their compile-time specialisations
+  if (BM == 128 && NST == 2 && a.C == nullptr && a.bias == nullptr && a.nsplit == 1) {
+    if (a.flags == (1 | 256 | 512)) {
+      hipLaunchKernelGGL((gemm_mx_fp8_kernel<128, 2, 1>), dim3(tiles), dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
+    if (a.flags == (128 | 1024 | 256 | 512)) {
+      hipLaunchKernelGGL((gemm_mx_fp8_kernel<128, 2, 2>), dim3(tiles), dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((gemm_mx_fp8_kernel<BM, NST, 0>), dim3(tiles), dim3(BM * 2), 0, s, a);
   return hipGetLastError();
 }
 
