@@ -584,6 +584,24 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
 #pragma unroll
         for (int q = 0; q < NQ; ++q) gv[q] += (v[q][0] + v[q][1]) + (v[q][2] + v[q][3]);
       }
+      // the 1-3 remaining slabs: their loads issued together (one round trip, not one each),
+      // added one by one in slab_reduce's order
+      if (NQ <= 2 && s < T.gS) {   // (64-row tiles: registers would halve the occupancy)
+        f32x4 r[NQ][3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          if (s + j < T.gS) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) r[q][j] = *reinterpret_cast<const f32x4*>(G + (s + j) * T.g_ss + gix[q]);
+          }
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          if (s + j < T.gS) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) gv[q] += r[q][j];
+          }
+        s = T.gS;
+      }
       for (; s < T.gS; ++s) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) gv[q] += *reinterpret_cast<const f32x4*>(G + s * T.g_ss + gix[q]);

@@ -15,6 +15,8 @@ step $O/case5_4.log env LJS_NUM_DEVICES=4 timeout -k 10 300 python bench.py --me
 step $O/layer8.log timeout -k 10 200 python bench.py --model layer --fp8
 step $O/layer.log timeout -k 10 200 python bench.py --model layer
 step $O/fp8_tiles.log timeout -k 10 300 python scripts/fp8_tiles.py 20 1282,256160,3128256
+for r in 16 32 64; do step $O/b8_rows$r.log env LJS_ADAM_ROWS=$r timeout -k 10 200 python bench.py --batch-per-gpu 8; done
+step $O/b64.log timeout -k 10 200 python bench.py
 cd /tmp
 step $O/prof_v2x2.log env LJS_NUM_DEVICES=4 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_v2x2 -o run -- python3 $R/bench.py --mesh 2x2 --steps 24 --warmup 6
 step $O/prof_case5.log env LJS_NUM_DEVICES=4 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_case5 -o run -- python3 $R/bench.py --mesh 4x1 --rules case5 --steps 24 --warmup 6
