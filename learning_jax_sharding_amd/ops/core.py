@@ -670,15 +670,104 @@ def dot_product_attention(q: ShardedArray, k: ShardedArray, v: ShardedArray, sca
         q = reshard_tile(q, qt.unshard([3]), note="attn.q")
         qt = q.tile
     kv_tile = qt.unshard([1])
-    k2 = reshard_tile(k, kv_tile, note="attn.k") if k.tile != kv_tile else k
-    v2 = reshard_tile(v, kv_tile, note="attn.v") if v.tile != kv_tile else v
     q_offsets = {}
     ss = qt.shard_shape(q.shape)
     for d in q.local:
         q_offsets[d] = qt.coords[d][1] * ss[1]
+    if _local_first_ok(q, k, v, kv_tile):
+        return _attention_local_first(q, k, v, kv_tile, scale, causal, q_offsets)
+    k2 = reshard_tile(k, kv_tile, note="attn.k") if k.tile != kv_tile else k
+    v2 = reshard_tile(v, kv_tile, note="attn.v") if v.tile != kv_tile else v
     _plan.record("attention", q_tiles=qt.tile_shape)
     loc = {d: K.attention(q.local[d], k2.local[d], v2.local[d], scale, causal, q_offsets[d]) for d in q.local}
     return ShardedArray(q.shape, v.dtype, q.sharding, loc)
+
+
+# Local-first all-gather attention (SURVEY §5 "start with local keys while remote keys arrive"):
+# the K/V sequence gathers run on a side stream while the flash kernel processes the device's OWN
+# K/V block; the remote blocks follow, merged by log-sum-exp in the kernel epilogue
+# (hip.attn_fwd_acc).  The backward is one flash backward over the gathered K/V with the final O
+# and log-sum-exp (blockwise-separable).  Worth it when the gather is a real transfer (one process
+# per GPU over RCCL: "auto"); over loopback / rehearsal transfers it only adds launches.
+# LJS_KV_LOCAL_FIRST = auto | 1 | 0.
+_KV_LOCAL_FIRST = os.environ.get("LJS_KV_LOCAL_FIRST", "auto")
+
+
+def _local_first_ok(q, k, v, kv_tile) -> bool:
+    if _KV_LOCAL_FIRST == "0" or k.tile == kv_tile or k.tile != v.tile or k.tile != q.tile:
+        return False
+    if k.tile.unshard([1]) != kv_tile:
+        return False
+    if _KV_LOCAL_FIRST == "auto":
+        if not all(t.is_cuda for t in k.local.values()):
+            return False
+        from ..comm.backend import get_comm
+        c = get_comm()
+        return c.kind == "dist" and not getattr(c, "_fake", False)
+    return True
+
+
+class _LocalFirstAttention(torch.autograd.Function):
+    """Per device: forward over the local K/V block, then (after the gathers' event) the remote
+    blocks of the gathered K/V, merged in the kernel; backward = the flash backward over the
+    gathered K/V (gradients flow to q and to the gathered k/v, whose collective transposes them)."""
+
+    @staticmethod
+    def forward(ctx, meta, q, kg, vg, kl, vl):
+        scale, causal, q_off, n, me, ev = meta
+        st = [None, None]
+        Sl = kl.shape[1]
+        K.attention_fwd_merge(q, kl, vl, scale, causal, q_off - me * Sl, st, last=False)
+        if ev is not None:
+            torch.cuda.current_stream(q.device).wait_event(ev)
+        out = None
+        others = [j for j in range(n) if j != me]
+        for i, j in enumerate(others):
+            out = K.attention_fwd_merge(q, kg[:, j * Sl:(j + 1) * Sl], vg[:, j * Sl:(j + 1) * Sl], scale, causal,
+                                        q_off - j * Sl, st, last=i == len(others) - 1)
+        ctx.save_for_backward(q, kg, vg, out, st[1])
+        ctx.meta = (scale, causal, q_off)
+        return out
+
+    @staticmethod
+    def backward(ctx, do):
+        q, kg, vg, o, lse = ctx.saved_tensors
+        scale, causal, q_off = ctx.meta
+        dq, dk, dv = K.attention_bwd_block(q, kg, vg, o, do, lse, scale, causal, q_off)
+        return None, dq.to(q.dtype), dk.to(kg.dtype), dv.to(vg.dtype), None, None
+
+
+def _attention_local_first(q, k, v, kv_tile, scale, causal, q_offsets):
+    n = k.tile.tile_shape[1]
+    devs = sorted(k.local)
+    dev0 = k.local[devs[0]].device
+    ev = None
+    if dev0.type == "cuda":
+        side = _LF_STREAMS.get(dev0.index)
+        if side is None:
+            side = _LF_STREAMS[dev0.index] = torch.cuda.Stream(dev0)
+        cur = torch.cuda.current_stream(dev0)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            k2 = reshard_tile(k, kv_tile, note="attn.k.local_first")
+            v2 = reshard_tile(v, kv_tile, note="attn.v.local_first")
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for t in list(k2.local.values()) + list(v2.local.values()):
+            t.record_stream(cur)
+    else:
+        k2 = reshard_tile(k, kv_tile, note="attn.k.local_first")
+        v2 = reshard_tile(v, kv_tile, note="attn.v.local_first")
+    _plan.record("attention", q_tiles=q.tile.tile_shape, local_first=True)
+    loc = {}
+    for d in q.local:
+        me = k.tile.coords[d][1]
+        loc[d] = _LocalFirstAttention.apply((scale, causal, q_offsets[d], n, me, ev), q.local[d], k2.local[d],
+                                            v2.local[d], k.local[d], v.local[d])
+    return ShardedArray(q.shape, v.dtype, q.sharding, loc)
+
+
+_LF_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
 
 
 # ----------------------------------------------------------------------------- fused dense

@@ -361,3 +361,19 @@ def test_fsdp_stack_virtual_devices_matches_host(host_devices, gpu_devices):
         for name in gh[k]:
             a, b = gh[k][name], gg[k][name]
             np.testing.assert_allclose(b, a, rtol=5e-2, atol=5e-2 * np.abs(a).max(), err_msg=f"{k}/{name}")
+
+
+def test_block_gpu_local_first_kv_gather(host_devices, gpu_devices, monkeypatch):
+    """2x2 virtual mesh with the local-first all-gather attention forced (own K/V block first on
+    the compute stream while the gathers run on a side stream, in-kernel LSE merges) == host."""
+    host_devices(4)
+    vh, gh = _run_block((2, 2))
+    gpu_devices(4)
+    from learning_jax_sharding_amd.ops import core
+    monkeypatch.setattr(core, "_KV_LOCAL_FIRST", "1")
+    vg, gg = _run_block((2, 2))
+    assert abs(vh - vg) <= 3e-2 * max(1.0, abs(vh)), (vh, vg)
+    for k in gh:
+        for name in gh[k]:
+            a, b = gh[k][name], gg[k][name]
+            np.testing.assert_allclose(b, a, rtol=5e-2, atol=5e-2 * np.abs(a).max(), err_msg=f"{k}/{name}")
