@@ -180,6 +180,20 @@ __device__ __forceinline__ int mx_exponent(float amax) {
 // the whole block inside [-448, 448] - m <= 0.875 gives at most 448, a larger mantissa raises
 // the exponent and gives at most 256 -- so the 8 min/max a clamp costs per 4 values would never
 // change a finite result)
+// 4 e4m3 bytes of two packed bf16 pairs divided by 2^x, in two gfx950 scaled conversions
+// (v_cvt_scalef32_pk_fp8_bf16 with scale 2^x: bit-identical to rounding v * 2^-x with
+// pack4_e4m3, measured on 2^20 pairs by scripts/cvt_scalef_probe.py).  x = -127 (an all-zero
+// block) converts with scale 1 (the values are 0 either way; 2^-127 would be an f32 denormal).
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+typedef short s16x2v_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float mx_scale_pow2(int x) { return x == -127 ? 1.f : ldexpf(1.f, x); }
+__device__ __forceinline__ unsigned cvt4_e4m3_bf16(unsigned lo2, unsigned hi2, float sc) {
+  s16x2v_t o = {0, 0};
+  o = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(o, __builtin_bit_cast(bf16x2v_t, lo2), sc, false);
+  o = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(o, __builtin_bit_cast(bf16x2v_t, hi2), sc, true);
+  return __builtin_bit_cast(unsigned, o);
+}
+
 __device__ __forceinline__ unsigned pack4_e4m3(float a, float b, float c, float d) {
   int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);   // bytes 0,1
   int hi = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, lo, true);   // bytes 2,3

@@ -123,22 +123,25 @@ __global__ __launch_bounds__(256) void quant_mx_cols_tiled_kernel(const bf16_t* 
   }
   __syncthreads();
   const int n = tid >> 2, kb = tid & 3;
-  float v[32];
-  float amax = 0.f;
+  // the column's 32 bf16 re-paired along k, amax as an integer max of the magnitude bits, then
+  // the gfx950 scaled conversions (cvt4_e4m3_bf16; bit-identical to the multiply + pack4 path)
+  unsigned pr[16];
+  unsigned mx = 0u;
 #pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const int r = kb * 32 + i;
-    const unsigned short h =
+  for (int i = 0; i < 16; ++i) {
+    const int r = kb * 32 + 2 * i;
+    const unsigned lo =
         *reinterpret_cast<const unsigned short*>(tile + r * 128 + (((n >> 3) ^ kb) << 4) + ((n & 7) << 1));
-    v[i] = __uint_as_float((unsigned)h << 16);
-    amax = fmaxf(amax, fabsf(v[i]));
+    const unsigned hi =
+        *reinterpret_cast<const unsigned short*>(tile + (r + 1) * 128 + (((n >> 3) ^ kb) << 4) + ((n & 7) << 1));
+    pr[i] = lo | (hi << 16);
+    mx = max(mx, max(lo & 0x7fffu, hi & 0x7fffu));
   }
-  const int x = mx_exponent(amax);
-  const float inv = ldexpf(1.f, -x);
+  const int x = mx_exponent(__uint_as_float(mx << 16));
+  const float sc = mx_scale_pow2(x);
   u32x4 o[2];
 #pragma unroll
-  for (int c = 0; c < 8; ++c)
-    o[c >> 2][c & 3] = pack4_e4m3(v[4 * c] * inv, v[4 * c + 1] * inv, v[4 * c + 2] * inv, v[4 * c + 3] * inv);
+  for (int c = 0; c < 8; ++c) o[c >> 2][c & 3] = cvt4_e4m3_bf16(pr[2 * c], pr[2 * c + 1], sc);
   u32x4* qo = reinterpret_cast<u32x4*>(q + (long)(n0 + n) * K + k0 + kb * 32);
   qo[0] = o[0];
   qo[1] = o[1];
@@ -146,25 +149,24 @@ __global__ __launch_bounds__(256) void quant_mx_cols_tiled_kernel(const bf16_t* 
   if (qr) {
     // row blocks: thread (tile row r, 32-column half hb) -- 4 x 16 B LDS chunks
     const int r = tid >> 1, hb = tid & 1;
-    float w[32];
-    float am = 0.f;
+    u32x4 raw[4];
+    unsigned mr = 0u;
 #pragma unroll
     for (int c4 = 0; c4 < 4; ++c4) {
       const int ch = hb * 4 + c4;
-      const u32x4 raw = *reinterpret_cast<const u32x4*>(tile + r * 128 + ((ch ^ ((r >> 5) & 3)) << 4));
+      raw[c4] = *reinterpret_cast<const u32x4*>(tile + r * 128 + ((ch ^ ((r >> 5) & 3)) << 4));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        w[8 * c4 + 2 * e] = __uint_as_float(raw[e] << 16);
-        w[8 * c4 + 2 * e + 1] = __uint_as_float(raw[e] & 0xffff0000u);
-        am = fmaxf(am, fmaxf(fabsf(w[8 * c4 + 2 * e]), fabsf(w[8 * c4 + 2 * e + 1])));
+        const unsigned a = raw[c4][e] & 0x7fff7fffu;
+        mr = max(mr, max(a & 0xffffu, a >> 16));
       }
     }
-    const int xr = mx_exponent(am);
-    const float ir = ldexpf(1.f, -xr);
+    const int xr = mx_exponent(__uint_as_float(mr << 16));
+    const float sr = mx_scale_pow2(xr);
     u32x4 orr[2];
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      orr[c >> 2][c & 3] = pack4_e4m3(w[4 * c] * ir, w[4 * c + 1] * ir, w[4 * c + 2] * ir, w[4 * c + 3] * ir);
+      orr[c >> 2][c & 3] = cvt4_e4m3_bf16(raw[c >> 1][2 * (c & 1)], raw[c >> 1][2 * (c & 1) + 1], sr);
     u32x4* qd = reinterpret_cast<u32x4*>(qr + (long)(k0 + r) * N + n0 + hb * 32);
     qd[0] = orr[0];
     qd[1] = orr[1];
@@ -476,6 +478,28 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
           }
         }
       }
+      if (qout && staged) {
+        // MX-fp8 copy of the bf16-rounded outputs from their packed bf16 pairs: block amax over
+        // the 4 lanes of the block (rounding is monotonic: max of the rounded values = the
+        // rounded max), then the scaled conversions; lane g = 0 stores the e8m0 scale
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+        amax = bf2f(f2bf(amax));
+        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        const int x = mx_exponent(amax);
+        const float sc = mx_scale_pow2(x);
+        u32x4 pb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pb[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+        const u32x2 qq = u32x2{cvt4_e4m3_bf16(pb[0], pb[1], sc), cvt4_e4m3_bf16(pb[2], pb[3], sc)};
+        const int lr = row - m0, lc = col - n0;
+        *reinterpret_cast<u32x2*>(Qs + lr * 128 + (((lc >> 4) ^ (lr & 7)) << 4) + (((lc >> 3) & 1) << 3)) = qq;
+        if (g == 0) Ss[lr * 4 + (lc >> 5)] = (unsigned char)(x + 127);
+        if (Cp || qtout) *reinterpret_cast<u32x4*>(Cs + lr * 256 + (((lc >> 3) ^ (lr & 15)) << 4)) = pb;
+        continue;
+      }
       if (qout) {
         // MX-fp8 copy of the bf16-rounded outputs: block amax over the 4 lanes of the block,
         // then each lane stores its 8 e4m3 bytes and lane g = 0 the block's e8m0 scale
@@ -566,25 +590,30 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
 #pragma unroll
     for (int r = 0; r < 64 * NB / NT; ++r) {
       const int w = tid + NT * r, c = 2 * (w / NB), tb = w % NB;
-      float v0[32], v1[32];
-      float a0 = 0.f, a1 = 0.f;
+      // 32 rows of the column pair (c, c + 1) as packed bf16 words; the block amax of each column
+      // as an integer max of the magnitude bits (both columns at once), then the rows re-paired
+      // along the column for the scaled conversions
+      unsigned h[32];
+      unsigned mx = 0u;
 #pragma unroll
       for (int k = 0; k < 32; ++k) {
         const int lr = tb * 32 + k;
-        const unsigned h2 =
-            *reinterpret_cast<const unsigned*>(Cs + lr * 256 + (((c >> 3) ^ (lr & 15)) << 4) + ((c & 7) << 1));
-        v0[k] = __uint_as_float(h2 << 16);
-        v1[k] = __uint_as_float(h2 & 0xffff0000u);
-        a0 = fmaxf(a0, fabsf(v0[k]));
-        a1 = fmaxf(a1, fabsf(v1[k]));
+        h[k] = *reinterpret_cast<const unsigned*>(Cs + lr * 256 + (((c >> 3) ^ (lr & 15)) << 4) + ((c & 7) << 1));
+        const unsigned a = h[k] & 0x7fff7fffu;
+        mx = max(mx & 0xffffu, a & 0xffffu) | max(mx & 0xffff0000u, a & 0xffff0000u);
       }
+      const float a0 = __uint_as_float(mx << 16), a1 = __uint_as_float(mx & 0xffff0000u);
       const int x0 = mx_exponent(a0), x1 = mx_exponent(a1);
-      const float i0 = ldexpf(1.f, -x0), i1 = ldexpf(1.f, -x1);
+      const float s0 = mx_scale_pow2(x0), s1 = mx_scale_pow2(x1);
       u32x4 o0[2], o1[2];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        o0[k >> 2][k & 3] = pack4_e4m3(v0[4 * k] * i0, v0[4 * k + 1] * i0, v0[4 * k + 2] * i0, v0[4 * k + 3] * i0);
-        o1[k >> 2][k & 3] = pack4_e4m3(v1[4 * k] * i1, v1[4 * k + 1] * i1, v1[4 * k + 2] * i1, v1[4 * k + 3] * i1);
+        const unsigned p00 = (h[4 * k] & 0xffffu) | (h[4 * k + 1] << 16);
+        const unsigned p01 = (h[4 * k + 2] & 0xffffu) | (h[4 * k + 3] << 16);
+        const unsigned p10 = (h[4 * k] >> 16) | (h[4 * k + 1] & 0xffff0000u);
+        const unsigned p11 = (h[4 * k + 2] >> 16) | (h[4 * k + 3] & 0xffff0000u);
+        o0[k >> 2][k & 3] = cvt4_e4m3_bf16(p00, p01, s0);
+        o1[k >> 2][k & 3] = cvt4_e4m3_bf16(p10, p11, s1);
       }
       const int gcol = n0 + c, grow = m0 + tb * 32;
       if (grow < p.M) {  // M % 32 == 0 (launcher): blocks are whole; N % 8: pairs are whole
@@ -842,25 +871,24 @@ __global__ __launch_bounds__(512) void gemm_mx8_kernel(F8Args p) {
       for (int it = tid; it < BM * (BN / 32); it += 512) {
         const int lr = it % BM, b = it / BM;
         const int grow = m0 + lr, gcol = n0 + 32 * b;
-        float v[32];
-        float amax = 0.f;
+        // 32 bf16 of the row as 16 packed words: amax as an integer max of the magnitude bits,
+        // then the scaled conversions straight from the pairs
+        u32x4 w[4];
+        unsigned mx = 0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const u32x4 w = *reinterpret_cast<const u32x4*>(smem + lr * RS + b * 64 + k * 16);
+          w[k] = *reinterpret_cast<const u32x4*>(smem + lr * RS + b * 64 + k * 16);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            v[8 * k + 2 * e] = __uint_as_float(w[e] << 16);
-            v[8 * k + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+            const unsigned a = w[k][e] & 0x7fff7fffu;
+            mx = max(mx, max(a & 0xffffu, a >> 16));
           }
         }
-#pragma unroll
-        for (int e = 0; e < 32; ++e) amax = fmaxf(amax, fabsf(v[e]));
-        const int x = mx_exponent(amax);
-        const float inv = ldexpf(1.f, -x);
+        const int x = mx_exponent(__uint_as_float(mx << 16));
+        const float sc = mx_scale_pow2(x);
         u32x4 o[2];
 #pragma unroll
-        for (int c = 0; c < 8; ++c)
-          o[c >> 2][c & 3] = pack4_e4m3(v[4 * c] * inv, v[4 * c + 1] * inv, v[4 * c + 2] * inv, v[4 * c + 3] * inv);
+        for (int c = 0; c < 8; ++c) o[c >> 2][c & 3] = cvt4_e4m3_bf16(w[c >> 1][2 * (c & 1)], w[c >> 1][2 * (c & 1) + 1], sc);
         if (grow < p.M && gcol < p.N) {
           u32x4* dst = reinterpret_cast<u32x4*>(p.QC + (long)grow * p.N + gcol);
           dst[0] = o[0];
@@ -872,23 +900,23 @@ __global__ __launch_bounds__(512) void gemm_mx8_kernel(F8Args p) {
     if (qtout) {  // transposed MX copy: lane = (column pair, 32-row block), pairs consecutive across lanes
       for (int it = tid; it < (BN / 2) * (BM / 32); it += 512) {
         const int cp = it % (BN / 2), tb = it / (BN / 2);
-        float v0[32], v1[32];
-        float a0 = 0.f, a1 = 0.f;
+        unsigned h[32];
+        unsigned mx = 0u;
 #pragma unroll
         for (int k = 0; k < 32; ++k) {
-          const unsigned h2 = *reinterpret_cast<const unsigned*>(smem + (tb * 32 + k) * RS + cp * 4);
-          v0[k] = __uint_as_float(h2 << 16);
-          v1[k] = __uint_as_float(h2 & 0xffff0000u);
-          a0 = fmaxf(a0, fabsf(v0[k]));
-          a1 = fmaxf(a1, fabsf(v1[k]));
+          h[k] = *reinterpret_cast<const unsigned*>(smem + (tb * 32 + k) * RS + cp * 4);
+          const unsigned a = h[k] & 0x7fff7fffu;
+          mx = max(mx & 0xffffu, a & 0xffffu) | max(mx & 0xffff0000u, a & 0xffff0000u);
         }
-        const int x0 = mx_exponent(a0), x1 = mx_exponent(a1);
-        const float i0 = ldexpf(1.f, -x0), i1 = ldexpf(1.f, -x1);
+        const int x0 = mx_exponent(__uint_as_float(mx << 16)), x1 = mx_exponent(__uint_as_float(mx & 0xffff0000u));
+        const float s0 = mx_scale_pow2(x0), s1 = mx_scale_pow2(x1);
         u32x4 o0[2], o1[2];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          o0[k >> 2][k & 3] = pack4_e4m3(v0[4 * k] * i0, v0[4 * k + 1] * i0, v0[4 * k + 2] * i0, v0[4 * k + 3] * i0);
-          o1[k >> 2][k & 3] = pack4_e4m3(v1[4 * k] * i1, v1[4 * k + 1] * i1, v1[4 * k + 2] * i1, v1[4 * k + 3] * i1);
+          o0[k >> 2][k & 3] = cvt4_e4m3_bf16((h[4 * k] & 0xffffu) | (h[4 * k + 1] << 16),
+                                             (h[4 * k + 2] & 0xffffu) | (h[4 * k + 3] << 16), s0);
+          o1[k >> 2][k & 3] = cvt4_e4m3_bf16((h[4 * k] >> 16) | (h[4 * k + 1] & 0xffff0000u),
+                                             (h[4 * k + 2] >> 16) | (h[4 * k + 3] & 0xffff0000u), s1);
         }
         const int gcol = n0 + 2 * cp, grow = m0 + tb * 32;
         if (grow < p.M) {  // M % 32 == 0 (launcher): blocks are whole; N % 8: pairs are whole

@@ -18,6 +18,7 @@ reference's literal einsum/softmax formulation (used by the parity tests).
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Optional
 
 import torch
@@ -70,7 +71,7 @@ class MultiHeadAttention(Module):
     def _prefetch_qkv(self, x: ShardedArray, ws, dt):
         from ..sharding import NamedSharding
         w0 = ws[0]
-        if dt != torch.bfloat16 or any(t.is_meta or not t.is_cuda for w in ws for t in w.local.values()):
+        if not _QKV_PREFETCH or dt != torch.bfloat16 or any(t.is_meta or not t.is_cuda for w in ws for t in w.local.values()):
             return None
         sh, xs = w0.sharding, x.sharding
         if not isinstance(sh, NamedSharding) or not isinstance(xs, NamedSharding) or not sh.spec:
@@ -165,6 +166,9 @@ class MultiHeadAttention(Module):
         if residual is not None:
             hidden = core.binary("add", core.convert(residual, dt), hidden)
         return hidden
+
+
+_QKV_PREFETCH = os.environ.get("LJS_QKV_PREFETCH", "1") == "1"
 
 
 def _fsdp_axis(w: ShardedArray, x: ShardedArray):
