@@ -162,11 +162,11 @@ __global__ __launch_bounds__(256) void quant_mx_cols_tiled_kernel(const bf16_t* 
       }
     }
     const int xr = mx_exponent(__uint_as_float(mr << 16));
-    const float sr = mx_scale_pow2(xr);
+    const float scr = mx_scale_pow2(xr);
     u32x4 orr[2];
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      orr[c >> 2][c & 3] = cvt4_e4m3_bf16(raw[c >> 1][2 * (c & 1)], raw[c >> 1][2 * (c & 1) + 1], sr);
+      orr[c >> 2][c & 3] = cvt4_e4m3_bf16(raw[c >> 1][2 * (c & 1)], raw[c >> 1][2 * (c & 1) + 1], scr);
     u32x4* qd = reinterpret_cast<u32x4*>(qr + (long)(k0 + r) * N + n0 + hb * 32);
     qd[0] = orr[0];
     qd[1] = orr[1];
