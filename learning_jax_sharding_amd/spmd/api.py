@@ -249,6 +249,11 @@ class Jitted:
                             sig = self._signature(*self._split(args))
                         return self._capture(sig, args, alias=False)
                     copies.append((t, s))
+        if copies and _REPLAY_TRACE and not getattr(cap, "_traced", False):
+            cap._traced = True
+            import sys
+            print(f"[ljs replay] {len(copies)} input copies per replay: "
+                  + ", ".join(f"{s.dtype}{list(s.shape)}" for _, s in copies[:40]), file=sys.stderr)
         for t, s in copies:
             t.copy_(s)
         cap.graph.replay()
@@ -375,6 +380,7 @@ def _seed(t: torch.Tensor, value: float) -> torch.Tensor:
 
 
 _SEED_HOIST = os.environ.get("LJS_SEED_HOIST", "1") == "1"
+_REPLAY_TRACE = os.environ.get("LJS_REPLAY_TRACE", "0") == "1"
 
 
 def _through_permutations(ts: List[torch.Tensor]) -> List[torch.Tensor]:
