@@ -168,7 +168,11 @@ class MultiHeadAttention(Module):
         return hidden
 
 
-_QKV_PREFETCH = os.environ.get("LJS_QKV_PREFETCH", "1") == "1"
+# Measured: the gather overlaps the activation cast (profiles/r3k_v2x2_prefetch_overlap.md), but
+# the side-stream branch costs more than it hides on one GPU: 2-D rehearsal 0.3378-0.3404 vs
+# 0.3165-0.3172 ms, 4 virtual devices 1.79-1.80 vs 1.62 ms (gpurun_out/r3k) -- off by default
+# (with RCCL over xGMI the gather is a real transfer worth hiding: LJS_QKV_PREFETCH=1)
+_QKV_PREFETCH = os.environ.get("LJS_QKV_PREFETCH", "0") == "1"
 
 
 def _fsdp_axis(w: ShardedArray, x: ShardedArray):

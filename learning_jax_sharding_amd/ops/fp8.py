@@ -215,8 +215,11 @@ def _auto_tile(M: int, N: int, K: int, flags: int, nsplit: int) -> int:
         return 0
     quant_out = flags & (256 | 512)
     if not quant_out and nsplit == 1 and N % 160 == 0 and N <= 1280 and M >= 4096 and K >= 1024:
-        return 256160
+        return _F8_N640_TILE
     return 0
+
+
+_F8_N640_TILE = int(os.environ.get("LJS_F8_N640_TILE", "256160"))
 
 
 class _Fp8Linear(torch.autograd.Function):
