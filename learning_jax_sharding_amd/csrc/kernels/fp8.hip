@@ -236,6 +236,8 @@ struct F8Args {
   int ldb, ldsb;        // B / SB row strides in bytes (K, K / 32; both 0: one broadcast row)
   int kps, nsplit;      // split-K: K-tiles per split, splits (split s -> f32 slab C + s * sC)
   long sC;
+  float* csum;          // flags & 2048 (8-wave kernel, bf16 output): per-row-tile column sums of the
+                        // bf16 output, csum[tile row][N] (summed over tile rows by the caller)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t f8_rsrc(const void* base, long bytes) {
@@ -666,7 +668,9 @@ __global__ __launch_bounds__(512) void gemm_mx8_kernel(F8Args p) {
   constexpr int PA = (BM / 8 + NW - 1) / NW, PB = (BN / 8 + NW - 1) / NW, PS = (NSA + NSB + NW - 1) / NW;
   constexpr int L = PA + PB + PS;  // DMA instructions per wave per K-tile (uniform: extras repeat)
   constexpr int RS = BN * 2 + 16;  // image row stride (bytes): padded so 16 rows spread over banks
-  constexpr int SMEM = NST * STAGE > BM * RS ? NST * STAGE : BM * RS;
+  constexpr int CSP = 512 / BN;    // column-sum partials per column (threads per column)
+  constexpr int IMG = BM * RS + 4 * CSP * BN;
+  constexpr int SMEM = NST * STAGE > IMG ? NST * STAGE : IMG;
   static_assert(SMEM <= 163840 && L * (NST - 1) <= 63, "LDS / vmcnt budget");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -858,6 +862,25 @@ __global__ __launch_bounds__(512) void gemm_mx8_kernel(F8Args p) {
       }
     }
     __syncthreads();
+    if (p.flags & 2048) {
+      // column sums of the bf16 output tile (a bias gradient downstream): CSP threads per column
+      // over row ranges, partials through LDS, one f32 per column and tile row to csum
+      float* part = reinterpret_cast<float*>(smem + BM * RS);
+      if (tid < CSP * BN) {
+        const int c = tid % BN, pr = tid / BN;
+        const int r0 = pr * BM / CSP, r1 = min((pr + 1) * BM / CSP, p.M - m0);
+        float acc = 0.f;
+        for (int r = r0; r < r1; ++r) acc += bf2f(*reinterpret_cast<const bf16_t*>(smem + r * RS + c * 2));
+        part[pr * BN + c] = acc;
+      }
+      __syncthreads();
+      if (tid < BN && n0 + tid < p.N) {
+        float a = 0.f;
+#pragma unroll
+        for (int pr = 0; pr < CSP; ++pr) a += part[pr * BN + tid];
+        p.csum[(long)(m0 / BM) * p.N + n0 + tid] = a;
+      }
+    }
     if (p.C) {  // bf16 rows: 16 B per lane, consecutive lanes along a row
       for (int c = tid; c < BM * (BN / 8); c += 512) {
         const int lr = c / (BN / 8), ch = c % (BN / 8);
@@ -1069,7 +1092,7 @@ LJS_API int ljs_quant_mx_cols(const void* in, int is_bf16, long ld, int K, int N
 LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const void* SB, void* C, const void* bias,
                             int M, int N, int K, long ldc, int flags, const void* R, long ldr, void* QC, void* SC,
                             int tile, int a_bcast, int b_bcast, void* QT, void* ST, long ldqt, int nsplit, long sC,
-                            hipStream_t stream) {
+                            void* csum, hipStream_t stream) {
   if (K % F8_BK || N % 8 || ldc % 8 || (long)M * K >= (1L << 31) || (long)N * K >= (1L << 31))
     return (int)hipErrorInvalidValue;
   if ((flags & (64 | 128)) && (!R || ldr % 8 || (((uintptr_t)R) & 15) || (flags & 32)))
@@ -1094,6 +1117,9 @@ LJS_API int ljs_gemm_mx_fp8(const void* A, const void* SA, const void* B, const 
   a.ldsb = b_bcast ? 0 : K / 32;
   a.QT = (unsigned char*)QT; a.ST = (unsigned char*)ST; a.ldqt = ldqt;
   a.kps = kps; a.nsplit = nsplit; a.sC = sC;
+  a.csum = (float*)csum;
+  // fused column sums: the 8-wave kernels' bf16 epilogue only
+  if ((flags & 2048) && (!csum || tile < 10000 || (flags & 32))) return (int)hipErrorInvalidValue;
   if (tile == 0) tile = 1282;
   if (tile >= 10000) {  // 8-wave large tiles: tile = BM * 1000 + BN (+ 1000000 * 3: three stages)
     const int t6 = tile % 1000000;

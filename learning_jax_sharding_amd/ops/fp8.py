@@ -49,7 +49,7 @@ _SIGS = {
                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int,
                         ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int,
-                        ctypes.c_long, ctypes.c_void_p],
+                        ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p],
 }
 _bound = False
 
@@ -162,7 +162,8 @@ def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: Optional[torch.Tensor],
             relu: bool = False, res: Optional[torch.Tensor] = None, res_mode: str = "add",
             qout: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, tile: int = 0,
             a_bcast: bool = False, b_bcast: bool = False,
-            qtout: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, nsplit: int = 1) -> Optional[torch.Tensor]:
+            qtout: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, nsplit: int = 1,
+            colsum: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """out[M][N] = qa . qb^T (MX-fp8 operands, f32 accumulation) (+bias)(relu); epilogue options:
     ``res`` (bf16 [M][N]) added as a residual (``res_mode="add"``, bit-exact with the unfused bf16
     add) or used as a ReLU mask (``"mask"``: keep where res > 0); ``qout = (q, s)`` also receives
@@ -195,9 +196,14 @@ def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: Optional[torch.Tensor],
     sC = od.stride(0) if (od is not None and nsplit > 1) else 0
     if tile == 0:
         tile = _auto_tile(M, N, K, flags, nsplit)
+    if colsum is not None:
+        # ``colsum`` f32 [ceil(M / BM)][N]: per-row-tile column sums of the bf16 output (8-wave
+        # tiles only; the caller sums the rows)
+        assert tile >= 10000 and colsum.dtype == torch.float32 and colsum.shape == (-(-M // (tile % 1000000 // 1000)), N)
+        flags |= 2048
     rc = _lib().ljs_gemm_mx_fp8(hip._p(qa), hip._p(sa), hip._p(qb), hip._p(sb), hip._p(od), hip._p(bias), M, N, K,
                                 ldc, flags, hip._p(res), ldr, hip._p(q_o), hip._p(s_o), tile, int(a_bcast),
-                                int(b_bcast), hip._p(qt_o), hip._p(st_o), M, nsplit, sC, hip._stream(qa))
+                                int(b_bcast), hip._p(qt_o), hip._p(st_o), M, nsplit, sC, hip._p(colsum), hip._stream(qa))
     hip._ck(rc, "gemm_mx_fp8")
     return out
 
@@ -474,8 +480,19 @@ class _FFBlockFp8(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             qwi_r, swi_r = _weight_q_rows(w_in)     # Win [M][F] rows: blocks along F
             dx = torch.empty((T, M), dtype=torch.bfloat16, device=dev)
-            # the skip path's dY summed in the epilogue (bf16(bf16(dx) + dY), the unfused add)
-            gemm_mx(qdA, sdA, qwi_r, swi_r, T, M, F, dx, res=t if fold else None, res_mode="add")
+            # the skip path's dY summed in the epilogue (bf16(bf16(dx) + dY), the unfused add);
+            # on the 8-wave tiles the epilogue also writes dx's column sums per row tile: the bias
+            # gradient of the dense that produced x (a transformer layer's out projection) is then
+            # one small reduction, computed only if that backward asks (hip.colsum_for)
+            tile = _auto_tile(T, M, F, 64 if fold else 0, 1)
+            cs = None
+            if tile >= 10000 and _FUSED_COLSUM:
+                bm = tile % 1000000 // 1000
+                cs = torch.empty((-(-T // bm), M), dtype=torch.float32, device=dev)
+            gemm_mx(qdA, sdA, qwi_r, swi_r, T, M, F, dx, res=t if fold else None, res_mode="add", tile=tile,
+                    colsum=cs)
+            if cs is not None:
+                hip.register_colsum(dx, _lazy_rows_sum(cs))
             out["dx"] = dx.view(tuple(lead) + (M,))
         if ctx.needs_input_grad[2]:
             # dY blocked along tokens: one constant row for a broadcast scalar, else a column pass
@@ -490,6 +507,23 @@ class _FFBlockFp8(torch.autograd.Function):
             out["wi"] = _mx_wgrad(qxT, sxT, qdAT, sdAT, M, F, T, w=w_in)
         dres = dy if (has_res and ctx.needs_input_grad[3] and not fold) else None
         return out.get("dx"), out.get("wi"), out.get("wo"), dres
+
+
+_FUSED_COLSUM = os.environ.get("LJS_F8_FUSED_COLSUM", "1") == "1"
+
+
+def _lazy_rows_sum(cs: torch.Tensor):
+    """f32 [N] = sum over the rows of ``cs`` [R][N], computed on first use (one slab_reduce)."""
+    done = []
+
+    def get():
+        if not done:
+            R, N = cs.shape
+            out = torch.empty((N,), dtype=torch.float32, device=cs.device)
+            hip.slab_reduce(cs.view(R, 1, N), out.view(1, N), N, 0)
+            done.append(out)
+        return done[0]
+    return get
 
 
 def _bcast_grad_mx2(dy2: torch.Tensor, n: int):

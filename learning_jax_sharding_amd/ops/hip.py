@@ -770,9 +770,10 @@ def colsum_for(t: torch.Tensor, C: int) -> Optional[torch.Tensor]:
     if ent is None:
         return None
     g = ent[0]()
-    if g is None or g._version != ent[1] or ent[3] != t.numel() or ent[2].numel() != C:
+    if g is None or g._version != ent[1] or ent[3] != t.numel():
         return None
-    return ent[2]
+    sums = ent[2]() if callable(ent[2]) else ent[2]   # (a lazy reduction, computed on first use)
+    return sums if sums.numel() == C else None
 
 
 class _MSELoss(torch.autograd.Function):

@@ -9,5 +9,9 @@ step $O/smoke.log timeout -k 10 300 python -c "import __graft_entry__ as g; g.sm
 for t in 256160 128160 128320; do
   step $O/layer8_$t.log env LJS_F8_N640_TILE=$t timeout -k 10 200 python bench.py --model layer --fp8
 done
+for i in 1 2; do
+  step $O/layer8_cs1_$i.log env LJS_F8_FUSED_COLSUM=1 timeout -k 10 200 python bench.py --model layer --fp8
+  step $O/layer8_cs0_$i.log env LJS_F8_FUSED_COLSUM=0 timeout -k 10 200 python bench.py --model layer --fp8
+done
 step $O/b64.log timeout -k 10 200 python bench.py
 echo done

@@ -950,3 +950,24 @@ def test_gemm_slab_mode_batched_weights(hip, tile):
         hip.gemm(x, dys[i], one, K, N, T, K, N, N, False, False, sC=K * N, splitk=S, tile=tile, slabs=True)
         assert torch.equal(slabs[:, i], one)
         assert torch.equal(slabs2[:, i], one)
+
+
+@pytest.mark.parametrize("tile", [256160, 128160, 256256])
+def test_fp8_gemm_fused_column_sums(hip, tile):
+    """The 8-wave MX GEMM's epilogue column sums (per row tile, of the bf16 output including the
+    residual add) == the f32 column sums of the output it wrote."""
+    from learning_jax_sharding_amd.ops import fp8 as F
+    g = torch.Generator(device="cpu").manual_seed(5)
+    T, N, K = 1056, 640, 512
+    qa, sa = F.quant_rows(torch.randn(T, K, generator=g).bfloat16().to(dev))
+    qb, sb = F.quant_rows(torch.randn(N, K, generator=g).bfloat16().to(dev))
+    r = torch.randn(T, N, generator=g).bfloat16().to(dev)
+    c = torch.empty((T, N), dtype=torch.bfloat16, device=dev)
+    bm = tile // 1000
+    cs = torch.full((-(-T // bm), N), float("nan"), dtype=torch.float32, device=dev)
+    F.gemm_mx(qa, sa, qb, sb, T, N, K, c, res=r, tile=tile, colsum=cs)
+    torch.cuda.synchronize()
+    ref = c.float().sum(0)
+    torch.testing.assert_close(cs.sum(0), ref, rtol=1e-4, atol=1e-3 * ref.abs().max().item())
+    sums = F._lazy_rows_sum(cs)()
+    torch.testing.assert_close(sums, ref, rtol=1e-4, atol=1e-3 * ref.abs().max().item())
