@@ -402,7 +402,11 @@ def _through_permutations(ts: List[torch.Tensor]) -> List[torch.Tensor]:
         if not all(x.requires_grad for x in ins):
             return ts
         ts = list(ins)
+        HOIST_STATS["hoisted"] += 1
     return ts
+
+
+HOIST_STATS = {"hoisted": 0}
 
 
 def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):

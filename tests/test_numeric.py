@@ -397,3 +397,20 @@ def test_attention_local_first_kv_gather_matches_unsharded(host_devices, mesh_sh
         for name in g1[k]:
             a, b = g1[k][name], gn[k][name]
             np.testing.assert_allclose(b, a, rtol=3e-2, atol=3e-2 * np.abs(a).max(), err_msg=f"{k}/{name}")
+
+
+def test_loss_seed_hoisted_through_output_all_to_all(host_devices, monkeypatch):
+    """The reference's final ('batch', 'embed') constraint is an all-to-all; grad() of the block's
+    sum seeds the all-to-all's inputs instead (the sum is permutation-invariant): same value and
+    gradients as seeding the outputs."""
+    from learning_jax_sharding_amd.spmd import api
+    host_devices(4)
+    n0 = api.HOIST_STATS["hoisted"]
+    v1, g1 = _block_loss_and_grads((2, 2))
+    assert api.HOIST_STATS["hoisted"] > n0
+    monkeypatch.setattr(api, "_SEED_HOIST", False)
+    v0, g0 = _block_loss_and_grads((2, 2))
+    assert abs(v1 - v0) <= 1e-3 * max(1.0, abs(v0))
+    for k in g0:
+        for name in g0[k]:
+            np.testing.assert_allclose(g1[k][name], g0[k][name], rtol=1e-4, atol=1e-5, err_msg=f"{k}/{name}")
