@@ -804,12 +804,12 @@ __global__ void rng_kernel(T* __restrict__ out, RngRegion reg, long n, unsigned 
 // sharded layer gathers / scatters whole contiguous blocks (ops/linear.py, ops/hip.py storage_order)
 template <typename T>
 __global__ void swap01_bf16_kernel(const T* __restrict__ in, bf16_t* __restrict__ out, int B, int S, int K8) {
-  const long n8 = (long)B * S * K8;
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long o = (long)blockIdx.x * blockDim.x + threadIdx.x; o < n8; o += stride) {
-    const int k8 = (int)(o % K8);
-    const long sb = o / K8;
-    const int b = (int)(sb % B), s = (int)(sb / B);
+  // blockIdx.y = output row s (no 64-bit divisions per element); x covers its B * K8 chunks
+  const int s = blockIdx.y;
+  const int nbk = B * K8;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nbk; j += gridDim.x * blockDim.x) {
+    const int b = j / K8, k8 = j - b * K8;
+    const long o = (long)s * nbk + j;
     const long i = ((long)b * S + s) * K8 + k8;
     u32x4 w;
     if constexpr (sizeof(T) == 4) {
@@ -949,13 +949,14 @@ LJS_API int ljs_cast_f32_bf16(const void* in, void* out, long n, hipStream_t s) 
 
 LJS_API int ljs_swap01_bf16(const void* in, int in_bf16, void* out, int B, int S, int K, hipStream_t s) {
   if (K % 8 || (((uintptr_t)in) & 15) || (((uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
-  const long n8 = (long)B * S * (K / 8);
-  const int g = grid_for(n8, 256 * 4);
+  const long nbk = (long)B * (K / 8);
+  if (S > 65535 || nbk >= (1L << 31)) return (int)hipErrorInvalidValue;
+  const dim3 g((unsigned)((nbk + 255) / 256 < 64 ? (nbk + 255) / 256 : 64), (unsigned)S);
   if (in_bf16)
-    hipLaunchKernelGGL(swap01_bf16_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, B, S,
+    hipLaunchKernelGGL(swap01_bf16_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, B, S,
                        K / 8);
   else
-    hipLaunchKernelGGL(swap01_bf16_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)in, (bf16_t*)out, B, S,
+    hipLaunchKernelGGL(swap01_bf16_kernel<float>, g, dim3(256), 0, s, (const float*)in, (bf16_t*)out, B, S,
                        K / 8);
   return (int)hipGetLastError();
 }
