@@ -487,8 +487,8 @@ class _FFBlockFp8(torch.autograd.Function):
             tile = _auto_tile(T, M, F, 64 if fold else 0, 1)
             cs = None
             if tile >= 10000 and _FUSED_COLSUM:
-                bm = tile % 1000000 // 1000
-                cs = torch.empty((-(-T // bm), M), dtype=torch.float32, device=dev)
+                rows = tile % 1000000 // 1000
+                cs = torch.empty((-(-T // rows), M), dtype=torch.float32, device=dev)
             gemm_mx(qdA, sdA, qwi_r, swi_r, T, M, F, dx, res=t if fold else None, res_mode="add", tile=tile,
                     colsum=cs)
             if cs is not None:

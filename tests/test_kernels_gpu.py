@@ -971,3 +971,39 @@ def test_fp8_gemm_fused_column_sums(hip, tile):
     torch.testing.assert_close(cs.sum(0), ref, rtol=1e-4, atol=1e-3 * ref.abs().max().item())
     sums = F._lazy_rows_sum(cs)()
     torch.testing.assert_close(sums, ref, rtol=1e-4, atol=1e-3 * ref.abs().max().item())
+
+
+def test_fp8_transformer_layer_large_tiles_and_fused_colsum(gpu_devices):
+    """At 4096 tokens the fp8 FF block's N=640 GEMMs take the 8-wave tiles and its dX GEMM writes
+    the column sums the attention out-projection's bias gradient reads: that bias gradient ==
+    the column sums of the same step with the fused sums off (LJS_F8_FUSED_COLSUM path), and
+    every gradient is finite."""
+    gpu_devices(1)
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd.models import TransformerLayer
+    from learning_jax_sharding_amd.ops import fp8 as F
+    model = TransformerLayer(640, heads=8, dim_head=64, ff_dim=1024, fp8=True)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (16, 256, 640))
+    params = model.init(ljs.random.PRNGKey(1), x)["params"]
+
+    def grads():
+        _, g = ljs.value_and_grad(lambda p: model.apply({"params": p}, x).sum())(params)
+        torch.cuda.synchronize()
+        return {"/".join(map(str, k)): v.to_torch().float().cpu()
+                for k, v in ljs.tree_util.tree_flatten_with_path(ljs.nn.unbox(g))[0]} \
+            if hasattr(ljs.tree_util, "tree_flatten_with_path") else \
+            [l.to_torch().float().cpu() for l in ljs.tree_util.tree_leaves(ljs.nn.unbox(g))]
+
+    assert F._auto_tile(4096, 640, 1024, 64, 1) >= 10000
+    g1 = grads()
+    old = F._FUSED_COLSUM
+    F._FUSED_COLSUM = False
+    try:
+        g0 = grads()
+    finally:
+        F._FUSED_COLSUM = old
+    items = g1.items() if isinstance(g1, dict) else enumerate(g1)
+    for k, a in items:
+        b = g0[k]
+        assert torch.isfinite(a).all(), k
+        torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-3 * max(1.0, b.abs().max().item()))
