@@ -1400,13 +1400,22 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
 
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
+  // K and V land by LDS-DMA (swizzle on the source address, rows past Sk read zeros), in flight
+  // together with the first query block's Q / dO / O below: one exposed latency, not two (the
+  // register-staged copy waited for K / V before the first block's DMA was even issued)
+  {
+    const u32x4 rk = rsrc_u4(kb, 2 * ((long)(a.Sk - 1) * a.k_ss + D));
+    const u32x4 rv = rsrc_u4(vb, 2 * ((long)(a.Sk - 1) * a.v_ss + D));
+    constexpr int NWF = FT / 64;
 #pragma unroll
-  for (int i = 0; i < FK * 8 / FT; ++i) {
-    int c = tid + FT * i, row = c >> 3, c16 = c & 7;
-    u32x4 x = row < a.Sk ? *reinterpret_cast<const u32x4*>(kb + (long)row * a.k_ss + c16 * 8) : u32x4{0, 0, 0, 0};
-    u32x4 y = row < a.Sk ? *reinterpret_cast<const u32x4*>(vb + (long)row * a.v_ss + c16 * 8) : u32x4{0, 0, 0, 0};
-    *reinterpret_cast<u32x4*>(Ks + img16(row, c16)) = x;
-    *reinterpret_cast<u32x4*>(Vs + img16(row, c16)) = y;
+    for (int i = 0; i < FK / 8 / NWF; ++i) {
+      const int pc = wave + NWF * i;
+      const int row = 8 * pc + (lane >> 3);
+      const int c = ((lane & 7) ^ (((row >> 1) & 3) << 1)) * 8;
+      const bool ok = row < a.Sk;
+      dma_lds_x4(rk, ok ? (int)(((long)row * a.k_ss + c) * 2) : 0x7ffffff0, Ks + pc * 512);
+      dma_lds_x4(rv, ok ? (int)(((long)row * a.v_ss + c) * 2) : 0x7ffffff0, Vs + pc * 512);
+    }
   }
 
   const bf16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
