@@ -513,15 +513,14 @@ _FUSED_COLSUM = os.environ.get("LJS_F8_FUSED_COLSUM", "1") == "1"
 
 
 def _lazy_rows_sum(cs: torch.Tensor):
-    """f32 [N] = sum over the rows of ``cs`` [R][N], computed on first use (one slab_reduce)."""
+    """f32 [N] = sum over the rows of ``cs`` [R][N], computed on first use (one column-sum pass)."""
     done = []
 
     def get():
         if not done:
-            R, N = cs.shape
-            out = torch.empty((N,), dtype=torch.float32, device=cs.device)
-            hip.slab_reduce(cs.view(R, 1, N), out.view(1, N), N, 0)
-            done.append(out)
+            # (one column-sum pass over the few row-tile partials; slab_reduce would run these 640
+            # columns on a single workgroup)
+            done.append(hip.colsum(cs))
         return done[0]
     return get
 
