@@ -983,6 +983,38 @@ LJS_API int ljs_sum_n(const void* const* ins, int n, int is_bf16, long count, vo
   return (int)hipGetLastError();
 }
 
+// out[c] = sum_r in[r][c] for a SHORT f32 matrix (the per-row-tile partials a GEMM epilogue wrote):
+// one workgroup per 64 columns, its 4 waves take every 4th row with all of a lane's loads issued
+// before the first add, then one LDS combine -- one memory round trip instead of the column-sum
+// kernels' long-R loop (3 workgroups, ~21 us for 64 x 640) or slab_reduce's one workgroup
+__global__ __launch_bounds__(256) void rows_sum_f32_kernel(const float* __restrict__ in, int R, int C, long ld,
+                                                          float* __restrict__ out) {
+  __shared__ float part[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < C) {
+    int r = w;
+    for (; r + 28 < R; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = in[(long)(r + 4 * i) * ld + c];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc += v[i];
+    }
+    for (; r < R; r += 4) acc += in[(long)r * ld + c];
+  }
+  part[w][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (w == 0 && c < C) out[c] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+}
+
+LJS_API int ljs_rows_sum_f32(const void* in, int R, int C, long ld, void* out, hipStream_t s) {
+  if (R < 1 || C < 1 || ld < C) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(rows_sum_f32_kernel, dim3((C + 63) / 64), dim3(256), 0, s, (const float*)in, R, C, ld,
+                     (float*)out);
+  return (int)hipGetLastError();
+}
+
 LJS_API int ljs_cast_bf16_f32(const void* in, void* out, long n, hipStream_t s) {
   hipLaunchKernelGGL(cast_bf16_f32, dim3(grid_for(n, 256 * 8)), dim3(256), 0, s, (const bf16_t*)in, (float*)out, n);
   return (int)hipGetLastError();

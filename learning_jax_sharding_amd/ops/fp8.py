@@ -513,14 +513,14 @@ _FUSED_COLSUM = os.environ.get("LJS_F8_FUSED_COLSUM", "1") == "1"
 
 
 def _lazy_rows_sum(cs: torch.Tensor):
-    """f32 [N] = sum over the rows of ``cs`` [R][N], computed on first use (one column-sum pass)."""
+    """f32 [N] = sum over the rows of ``cs`` [R][N], computed on first use (one short-matrix row sum)."""
     done = []
 
     def get():
         if not done:
-            # (one column-sum pass over the few row-tile partials; slab_reduce would run these 640
-            # columns on a single workgroup)
-            done.append(hip.colsum(cs))
+            # (one short-matrix pass over the row-tile partials: the long-R column-sum kernel ran
+            # 3 workgroups for 21 us here, slab_reduce one workgroup for 10 us)
+            done.append(hip.rows_sum(cs))
         return done[0]
     return get
 

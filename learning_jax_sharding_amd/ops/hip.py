@@ -49,6 +49,7 @@ _SIGS = {
     "ljs_swap01_bf16": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
     "ljs_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p],
     "ljs_sum_n": [ctypes.POINTER(c_void_p), c_int, c_int, c_long, c_void_p, c_void_p],
+    "ljs_rows_sum_f32": [c_void_p, c_int, c_int, c_long, c_void_p, c_void_p],
     "ljs_cast_transpose_f32_bf16": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p],
     "ljs_sum_all": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
     "ljs_colsum": [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p],
@@ -588,6 +589,21 @@ def sum_n(ts: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> tor
     arr = (c_void_p * len(ts))(*[t.data_ptr() for t in ts])
     rc = lib().ljs_sum_n(arr, len(ts), int(t0.dtype == torch.bfloat16), t0.numel(), _p(out), _stream(t0))
     _ck(rc, "sum_n")
+    return out
+
+
+def rows_sum(t2d: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """f32 [C] = sum over the rows of a SHORT f32 [R][C] (e.g. per-row-tile partial column sums a
+    GEMM epilogue wrote): one memory round trip (rows_sum_f32_kernel); torch on the CPU."""
+    R, C = t2d.shape
+    if not t2d.is_cuda:
+        s = t2d.float().sum(0)
+        return s if out is None else out.copy_(s)
+    assert t2d.dtype == torch.float32 and t2d.stride(1) == 1
+    if out is None:
+        out = torch.empty((C,), dtype=torch.float32, device=t2d.device)
+    rc = lib().ljs_rows_sum_f32(_p(t2d), R, C, t2d.stride(0), _p(out), _stream(t2d))
+    _ck(rc, "rows_sum_f32")
     return out
 
 

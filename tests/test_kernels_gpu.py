@@ -887,6 +887,16 @@ def test_sum_n(hip, n, dtype):
     torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("R,C", [(1, 5), (3, 64), (64, 640), (37, 1000), (200, 130)])
+def test_rows_sum(hip, R, C):
+    """Short-matrix row sum (the fused column-sum partials) == the f32 torch sum; a strided view too."""
+    base = torch.randn(R, C + 8, device="cuda")
+    x = base[:, :C]
+    out = hip.rows_sum(x)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, x.double().sum(0).float(), rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("tile", [256256, 256128, 256160, 128320, 128256, 128128, 128160, 3128128, 3128160, 3128256, 3256128])
 @pytest.mark.parametrize("mode", ["qboth", "qmask8", "res_bias", "f32split"])
 def test_fp8_gemm_8wave_tiles_match_4wave(hip, tile, mode):
