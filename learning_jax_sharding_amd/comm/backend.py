@@ -280,15 +280,35 @@ class DistComm:
 
     _GRAPH_KINDS = ("all_gather", "reduce_scatter", "all_reduce", "all_to_all")
 
-    def graph_safe(self, kind: str, x: Optional[torch.Tensor] = None) -> bool:
+    def graph_safe(self, kind: str, x: Optional[torch.Tensor] = None, groups: Optional[Groups] = None) -> bool:
         """Whether this collective can be captured inside a HIP graph (no capture cut): native
         RCCL rank communicators, or the rehearsal backend ('fake': collectives move nothing)."""
-        from . import p2p
-        if kind not in self._GRAPH_KINDS or p2p.enabled():
+        if kind not in self._GRAPH_KINDS:
             return False
         if self._fake:
             return True
+        # the ipc-mode peer-memory collectives are stream-ordered kernels + one D2D copy, and their
+        # flag barrier takes its sequence number from a device-side counter, so a replayed graph
+        # keeps the members in step: capturable once the group exists (its construction is a
+        # host-side handle exchange, done by the eager warm-up call)
+        if x is not None and groups is not None and self._p2p_ready(kind, x, groups):
+            return True
         return self._native is not None and (x is None or self._native.supports(x))
+
+    def _p2p_ready(self, kind: str, x: torch.Tensor, groups: Groups) -> bool:
+        """Whether this collective will take an already-built peer-memory group (the routing
+        rule of :meth:`_p2p`, evaluated without building anything)."""
+        from . import p2p
+        if not p2p.enabled() or not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16):
+            return False
+        nbytes = x.numel() * x.element_size()
+        if nbytes > p2p.max_bytes():
+            return False
+        mine = [tuple(int(v) for v in g) for g in groups if self.me in g]
+        if not mine or len(mine[0]) < 2:
+            return False
+        grp = self._p2p_groups.get(tuple(sorted(mine[0])))
+        return grp is not None and grp.fits(nbytes, kind in ("reduce_scatter", "all_to_all"))
 
     def _nat(self, groups, x) -> Optional[int]:
         if self._native is None or not self._native.supports(x):
@@ -309,6 +329,8 @@ class DistComm:
         srt = tuple(sorted(g))
         grp = self._p2p_groups.get(srt)
         if grp is None:
+            if torch.cuda.is_current_stream_capturing():
+                return None   # the handle exchange cannot run inside a capture: bulk path
             devs = [x.device if r == self.me else torch.device("cuda", 0) for r in srt]
             grp = self._p2p_groups[srt] = p2p.P2PGroup(devs, p2p.max_bytes(), rank=srt.index(self.me), pg=pg)
         return grp if grp.fits(nbytes, chunked) else None

@@ -17,7 +17,11 @@ by every other member; in single-controller runs they are peer-mapped.  Synchron
 * ``local`` mode: HIP events between the members' streams.
 
 Opt-in: ``LJS_P2P=1`` routes collectives of at most ``LJS_P2P_MAX_KB`` (default 1024) KiB per
-member through here; RCCL keeps everything else.
+member through here; RCCL keeps everything else.  In ``ipc`` mode every collective is a staging
+copy plus stream-ordered kernels whose barrier sequence comes from a device-side counter, so it
+is captured into HIP graphs like a native RCCL call (``DistComm.graph_safe``) once the group
+exists; the group itself (an IPC-handle exchange) is built by the eager warm-up call, never
+inside a capture (``scripts/p2p_check.py`` replays a captured all-reduce + all-gather).
 """
 from __future__ import annotations
 

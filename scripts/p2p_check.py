@@ -64,6 +64,35 @@ def main():
     y = comm.all_reduce({comm.me: x}, [tuple(range(n))])[comm.me]
     assert torch.all(y == n * (n + 1) / 2), y
     assert comm._p2p_groups, "DistComm did not take the p2p path"
+    # ... and, once built, the route is capturable (no graph cut at this collective)
+    assert comm.graph_safe("all_reduce", x, [tuple(range(n))]), "p2p all-reduce not graph-safe"
+    assert not comm.graph_safe("all_reduce", torch.empty(4 << 20, device=dev), [tuple(range(n))]) or \
+        comm._native is not None
+
+    # HIP-graph capture of the ipc collectives: replays keep advancing the device-side barrier
+    # counter, so captured members stay in step; results follow the (re-filled) static input
+    xin = torch.zeros(4096, device=dev)
+    xg = torch.zeros(2 * 1024, dtype=torch.bfloat16, device=dev)
+    grp.all_reduce({rank: xin})
+    torch.cuda.synchronize()
+    dist.barrier()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        yout = grp.all_reduce({rank: xin})[rank]
+        gout = grp.all_gather({rank: xg})[rank]
+    torch.cuda.synchronize()
+    dist.barrier()
+    for it in range(3):
+        xin.fill_(float(rank + 1 + it))
+        xg.fill_(float(rank - it))
+        graph.replay()
+        torch.cuda.synchronize()
+        want = float(sum(r + 1 + it for r in range(n)))
+        assert torch.all(yout == want), (it, yout[:4])
+        for r in range(n):
+            assert torch.all(gout[r] == float(r - it)), (it, r)
+    grp.check_error()
+    dist.barrier()
 
     # failure detection: a barrier nobody else joins times out into the error word, no hang
     dist.barrier()

@@ -172,3 +172,37 @@ def test_localcomm_native_glue_matches_copy_path(monkeypatch, groups):
     # one native call per device group and collective
     assert sorted(set(k for k, _ in fake.groups)) == ["a2a", "ag", "ar", "rs"]
     assert len(fake.groups) == 4 * len(groups)
+
+
+class _Msg:
+    """Tensor stand-in with the attributes DistComm's routing reads (a CPU box has no GPU tensors)."""
+    def __init__(self, nbytes, dtype=torch.float32):
+        self.is_cuda, self.dtype, self._n = True, dtype, nbytes // 4 if dtype == torch.float32 else nbytes // 2
+
+    def numel(self):
+        return self._n
+
+    def element_size(self):
+        return 4 if self.dtype == torch.float32 else 2
+
+
+def test_p2p_route_graph_safe_only_when_group_built(monkeypatch):
+    """The ipc peer-memory collectives are capturable (device-side barrier counter); DistComm
+    reports a collective graph-safe only if it will take an already-built group that fits."""
+    from learning_jax_sharding_amd.comm.backend import DistComm
+    from learning_jax_sharding_amd.comm.p2p import P2PGroup
+    monkeypatch.setenv("LJS_P2P", "1")
+    c = object.__new__(DistComm)
+    c.me, c._fake, c._native, c._p2p_groups = 1, False, None, {}
+    groups = [(0, 1), (2, 3)]
+    assert not c.graph_safe("all_reduce", _Msg(4096), groups)          # no group yet: torch path, cut
+    grp = object.__new__(P2PGroup)
+    grp.n, grp.cap, grp.oneshot_max = 2, 1 << 20, 256 << 10
+    c._p2p_groups[(0, 1)] = grp
+    assert c.graph_safe("all_reduce", _Msg(4096), groups)
+    assert c.graph_safe("reduce_scatter", _Msg(4096), groups)
+    assert not c.graph_safe("all_reduce", _Msg(2 << 20), groups)       # above LJS_P2P_MAX_KB
+    assert not c.graph_safe("all_reduce", _Msg(4096), [(1, 2), (0, 3)])  # a different group
+    assert not c.graph_safe("send", _Msg(4096), groups)
+    monkeypatch.setenv("LJS_P2P", "0")
+    assert not c.graph_safe("all_reduce", _Msg(4096), groups)
