@@ -55,6 +55,8 @@ struct AttnArgs {
   long oa_sb, oa_ss, oa_sh;
   int acc_mode;
   int fwd_prog;      // resident forward: per-key-tile waits (1) or one wait for the whole burst (0)
+  int vst;           // outputs 16-byte aligned with row strides % 8 == 0: row tiles leave through an
+                     // LDS image as full 128-byte rows (stage_rows16 / flush_rows), LJS_ATTN_VST
 };
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -197,6 +199,41 @@ __device__ __forceinline__ void store_row_T(bf16_t* rowp, const f32x4 (&acc)[4],
   }
 }
 
+// The same row tile through LDS: store_row_T issues 4 dwordx2 per lane, each covering 32 bytes of
+// 16 different rows, and a wave's stores of a tile queue behind each other (the epilogue store tail
+// is store-ISSUE bound, MI355X_MICROARCH "attention epilogue store tail").  Staged into a wave-
+// private [rows][64] bf16 image (16-byte chunk c of local row r at chunk c ^ (r & 7): the 16 rows
+// of a ds_write_b64 spread over 8 chunk positions) and read back as 16-byte row chunks, the tile
+// leaves as dwordx4 stores of 8 whole 128-byte rows each (half the store instructions).
+// Local row of this lane: rbase + (lane & 15).
+__device__ __forceinline__ void stage_rows16(bf16_t* img, int rbase, const f32x4 (&acc)[4], float mul, int lane) {
+  const int r = rbase + (lane & 15), g = lane >> 4;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    u32x2 w;
+    w[0] = pack_bf16x2(acc[dt][0] * mul, acc[dt][1] * mul);
+    w[1] = pack_bf16x2(acc[dt][2] * mul, acc[dt][3] * mul);
+    const int c = (2 * dt + (g >> 1)) ^ (r & 7);
+    *reinterpret_cast<u32x2*>(img + r * D + c * 8 + 4 * (g & 1)) = w;
+  }
+}
+// NR staged rows -> global rows row0 + r (row stride ld elements; rows >= rlim skipped)
+template <int NR>
+__device__ __forceinline__ void flush_rows(const bf16_t* img, bf16_t* base, long ld, int row0, int rlim, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's image writes done (wave-private)
+  u32x4 v[NR / 8];
+#pragma unroll
+  for (int i = 0; i < NR / 8; ++i) {
+    const int r = 8 * i + (lane >> 3), c = lane & 7;
+    v[i] = *reinterpret_cast<const u32x4*>(img + r * D + ((c ^ (r & 7)) << 3));
+  }
+#pragma unroll
+  for (int i = 0; i < NR / 8; ++i) {
+    const int r = 8 * i + (lane >> 3), c = lane & 7;
+    if (row0 + r < rlim) *reinterpret_cast<u32x4*>(base + (long)(row0 + r) * ld + c * 8) = v[i];
+  }
+}
+
 // ============================================================================ forward
 struct FwdState {
   f32x4 o[4];
@@ -324,6 +361,17 @@ __device__ __forceinline__ void fwd_store(const AttnArgs& a, const f32x4 (&o)[4]
   if (g == 0) a.lse[lidx] = lnew;
 }
 
+// acc_mode 0 epilogue of a wave's 16 query rows through the LDS image img (2 KiB, wave-private)
+__device__ __forceinline__ void fwd_store_vst(const AttnArgs& a, const f32x4 (&o)[4], float m, float lt, int b, int h,
+                                              int qrow0, int lane, bf16_t* img) {
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const int qrow = qrow0 + (lane & 15);
+  if ((lane >> 4) == 0 && a.lse && qrow < a.Sq)
+    a.lse[((long)b * a.H + h) * a.Sq + qrow] = lt > 0.f ? m + __log2f(lt) : INFINITY;
+  stage_rows16(img, 0, o, inv, lane);
+  flush_rows<16>(img, a.out + b * a.o_sb + h * a.o_sh, a.o_ss, qrow0, a.Sq, lane);
+}
+
 // K/V-resident forward for Sk <= 256: the whole K and V of the (batch, head) -- at most 2 x
 // 32 KB -- go to LDS in ONE burst of LDS-DMA pieces (issued from asm, swizzle on the source
 // address), so a block pays the HBM latency once instead of once per 64-key tile behind a
@@ -387,7 +435,12 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
         fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kt * BLK, qrow, lane);
       }
       float lt = row4_sum(st.l);
-      if (qok) fwd_store(a, st.o, st.m, lt, b, h, qrow, lane);
+      if (a.vst && a.acc_mode == 0) {
+        __syncthreads();  // every wave is done with the K / V images
+        fwd_store_vst(a, st.o, st.m, lt, b, h, qrow0, lane, Ks + wave * 16 * D);
+      } else if (qok) {
+        fwd_store(a, st.o, st.m, lt, b, h, qrow, lane);
+      }
       return;
     }
   }
@@ -406,7 +459,12 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
     }
   }
   float lt = row4_sum(st.l);
-  if (qok) fwd_store(a, st.o, st.m, lt, b, h, qrow, lane);
+  if (a.vst && a.acc_mode == 0) {
+    __syncthreads();  // every wave is done with the K / V images
+    fwd_store_vst(a, st.o, st.m, lt, b, h, qrow0, lane, Ks + wave * 16 * D);
+  } else if (qok) {
+    fwd_store(a, st.o, st.m, lt, b, h, qrow, lane);
+  }
 }
 
 // Persistent K/V-resident forward (Sk <= 256): one workgroup per CU walks work items (query
@@ -944,6 +1002,22 @@ __device__ __forceinline__ void dkv32_body(const AttnArgs& a, int kblk, int h, i
   };
   if (wave_mask) sweep(std::true_type{});
   else sweep(std::false_type{});
+  if (a.vst) {
+    // every wave passed the sweep's last barrier and no DMA is in flight: the Q / dO buffers are
+    // free; this wave's 32 key rows of dK / dV go through its own 4 KiB of them each
+    if (active) {
+      bf16_t* ik = QO + wave * 32 * D;
+      bf16_t* iv = QO + (4 + wave) * 32 * D;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        stage_rows16(ik, 16 * j, dk[j], a.scale, lane);
+        stage_rows16(iv, 16 * j, dv[j], 1.f, lane);
+      }
+      flush_rows<32>(ik, a.out + b * a.out_sb + h * a.out_sh, a.out_ss, key0, a.Sk, lane);
+      flush_rows<32>(iv, a.out2 + b * a.out2_sb + h * a.out2_sh, a.out2_ss, key0, a.Sk, lane);
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int key = key0 + 16 * j + (lane & 15);
@@ -1550,6 +1624,20 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   };
   if (wave_mask) sweep(std::true_type{});
   else sweep(std::false_type{});
+  if (a.vst) {
+    // every wave passed the sweep's last barrier: the K / V images are free; this wave's 32 key
+    // rows of dK / dV go through its own rows of them
+    if (active) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        stage_rows16(Ks + key0 * D, 16 * j, dk[j], a.scale, lane);
+        stage_rows16(Vs + key0 * D, 16 * j, dv[j], 1.f, lane);
+      }
+      flush_rows<32>(Ks + key0 * D, a.out + b * a.out_sb + h * a.out_sh, a.out_ss, key0, a.Sk, lane);
+      flush_rows<32>(Vs + key0 * D, a.out2 + b * a.out2_sb + h * a.out2_sh, a.out2_ss, key0, a.Sk, lane);
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     int key = key0 + 16 * j + (lane & 15);
@@ -1607,6 +1695,20 @@ static int attn_prio() {
   return v;
 }
 
+// row tiles stored through LDS as whole 128-byte rows (LJS_ATTN_VST=0: per-lane 8-byte stores)
+static int g_vst = -1;  // -1 = read LJS_ATTN_VST at the next call
+LJS_API void ljs_attn_set_vst(int v) { g_vst = v; }
+static int attn_vst() {
+  if (g_vst < 0) {
+    const char* e = getenv("LJS_ATTN_VST");
+    g_vst = e ? atoi(e) : 1;
+  }
+  return g_vst;
+}
+static bool vst_ok(const void* p, const long* st) {
+  return (((uintptr_t)p) & 15) == 0 && st[0] % 8 == 0 && st[1] % 8 == 0 && st[2] % 8 == 0;
+}
+
 // forward sub-tiles per wave: 1 or 2 forces it; 0 = automatic; -1 = read LJS_ATTN_FWD_NSUB
 static int g_fwd_nsub = -1;
 // K/V-resident forward (Sk <= 256): 0 off, 4 / 8 / 16 waves per block; -1 = read LJS_ATTN_FWD_RES
@@ -1638,6 +1740,7 @@ static int attn_fwd_impl(const void* q, const void* k, const void* v, void* o, v
   a.scale = scale; a.scale_log2 = scale * LOG2E;
   a.causal = causal; a.q_offset = q_offset;
   a.prio_hi_half = attn_prio();
+  a.vst = attn_vst() && vst_ok(o, os);
   // queries per block: as many sub-tiles per wave as keep >= ~2 blocks per CU resident
   if (g_fwd_nsub < 0) {
     const char* e = getenv("LJS_ATTN_FWD_NSUB");
@@ -1740,6 +1843,7 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
     f.out = (bf16_t*)dk; f.out_sb = dks[0]; f.out_ss = dks[1]; f.out_sh = dks[2];
     f.out2 = (bf16_t*)dv; f.out2_sb = dvs[0]; f.out2_ss = dvs[1]; f.out2_sh = dvs[2];
     f.out3 = (bf16_t*)dq; f.out3_sb = dqs[0]; f.out3_ss = dqs[1]; f.out3_sh = dqs[2];
+    f.vst = attn_vst() && vst_ok(dk, dks) && vst_ok(dv, dvs);
     hipLaunchKernelGGL(attn_bwd_fused_kernel, dim3(H, B), dim3(FT), 0, stream, f);
     return (int)hipGetLastError();
   }
@@ -1748,6 +1852,7 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
   AttnArgs b = a;
   b.out = (bf16_t*)dk; b.out_sb = dks[0]; b.out_ss = dks[1]; b.out_sh = dks[2];
   b.out2 = (bf16_t*)dv; b.out2_sb = dvs[0]; b.out2_ss = dvs[1]; b.out2_sh = dvs[2];
+  b.vst = attn_vst() && vst_ok(dk, dks) && vst_ok(dv, dvs);  // (the 128-key dK/dV blocks use it)
   const long nq = (Sq + BLK - 1) / BLK, nk = (Sk + BLK - 1) / BLK;
   if (attn_dkv32(Sk) && (nq + (Sk + 127) / 128) * H * B < (1L << 30)) {
     const long nk128 = (Sk + 127) / 128;

@@ -100,6 +100,16 @@ def set_attention_fwd_resident(waves: int):
     fn(int(waves))
 
 
+def set_attention_vst(enabled: Optional[bool]):
+    """Attention output row tiles (forward O, backward dK / dV) stored through an LDS image as
+    whole 128-byte rows with 16-byte stores (True), or per lane as 8-byte pieces (False); None
+    re-reads ``LJS_ATTN_VST`` (default on).  Bit-identical either way."""
+    fn = lib().ljs_attn_set_vst
+    fn.argtypes = [c_int]
+    fn.restype = None
+    fn(-1 if enabled is None else int(bool(enabled)))
+
+
 def set_attention_bwd_fused(enabled: Optional[bool]):
     """Select the attention backward for key lengths <= 256: the single-pass fused kernel
     (True), the split dQ + dK/dV kernels (False; always used above 256 keys), or None for the

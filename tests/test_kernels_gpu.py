@@ -174,6 +174,26 @@ def test_attention_fwd_bwd(hip, attn_bwd_impl, attn_fwd_nsub, B, S, H, causal):
         assert err <= 3e-2 * max(1.0, b_.abs().max().item()), (name, err)
 
 
+@pytest.mark.parametrize("B,S,H,causal", [(16, 256, 8, False), (2, 256, 8, False), (16, 200, 8, True),
+                                           (3, 100, 3, False), (1, 320, 2, True)])
+def test_attention_vst_bit_exact(hip, B, S, H, causal):
+    """Row tiles stored through the LDS image (16-byte whole-row stores: resident forward, fused
+    and 128-key split backward) == the per-lane 8-byte stores, bit for bit, with ragged Sq."""
+    D = 64
+    qkv = _rand(B, S, 3 * H * D, seed=11).reshape(B, S, 3, H, D)
+    g = _rand(B, S, H, D, seed=12)
+    res = {}
+    for vst in (True, False):
+        hip.set_attention_vst(vst)
+        q, k, v = (qkv[:, :, i].detach().clone().requires_grad_() for i in range(3))
+        o = hip.attention(q, k, v, D ** -0.5, causal)
+        (o.float() * g.float()).sum().backward()
+        res[vst] = (o.detach(), q.grad, k.grad, v.grad)
+    hip.set_attention_vst(None)
+    for a, b_, name in zip(res[True], res[False], ("o", "dq", "dk", "dv")):
+        assert torch.equal(a, b_), name
+
+
 @pytest.mark.parametrize("Sq,Sk,causal,q_offset", [(192, 128, False, 0), (130, 256, True, 64), (64, 100, True, 0)])
 def test_attention_bwd_block_fused_matches_split(hip, attn_fwd_nsub, Sq, Sk, causal, q_offset):
     """Block backward (ring attention's kernel: external O / lse, Sq != Sk, causal offset):
