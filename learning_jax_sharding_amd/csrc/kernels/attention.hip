@@ -1312,6 +1312,17 @@ __device__ __forceinline__ void dq32_body(const AttnArgs& a, int qb, int h, int 
   };
   if (wave_mask) sweep(std::true_type{});
   else sweep(std::false_type{});
+  if (a.vst) {
+    // after the sweep's last barrier (no load in flight) the K / V tiles are free: this wave's 32
+    // query rows of dQ leave through its own 4 KiB of them as whole-row stores
+    if (active) {
+      bf16_t* img = smem + wave * 32 * D;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) stage_rows16(img, 16 * i, dq[i], a.scale, lane);
+      flush_rows<32>(img, a.out + b * a.out_sb + h * a.out_sh, a.out_ss, qrow0, a.Sq, lane);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int qrow = qrow0 + 16 * i + (lane & 15);
@@ -1466,6 +1477,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t QO[4 * BLK * D];  // Q[2], dO[2]
   __shared__ __attribute__((aligned(16))) bf16_t Os[BLK * D];      // next block's O (delta only)
   __shared__ __attribute__((aligned(16))) float rowc[2][2][BLK];    // [buf][lse, delta][query]
+  __shared__ __attribute__((aligned(16))) bf16_t dQs[BLK * D];      // a query block's dQ (a.vst)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int h = blockIdx.x, b = blockIdx.y;
   const int key0 = wave * 32;
@@ -1570,8 +1582,10 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   // in one loop the compiler allocated dK / dV differently in each and copied all 64 accumulator
   // registers at their join on every query block.  Same trip count and barriers in both.
   const bool wave_mask = (a.Sq % BLK) != 0 || key0 + 32 > a.Sk || a.causal;
-  auto sweep = [&](auto wm) {
+  auto sweep = [&](auto wm, auto vs) {
     constexpr bool WM = decltype(wm)::value;
+    constexpr bool VS = decltype(vs)::value;  // dQ through dQs (compile-time: a runtime branch in
+                                              // the sweep cost the loop its register allocation)
     for (int it = 0; it < nqt; ++it) {
       const int cur = it & 1;
       const int q0 = it * BLK;
@@ -1609,7 +1623,19 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
         }
       }
       const int qrow = q0 + 16 * qt + (lane & 15);
-      if (qrow < a.Sq) {
+      if constexpr (VS) {
+        // the block's dQ is split over wave pairs (d halves): staged in dQs (16-byte chunk XOR
+        // row), written as whole 128-byte rows after the barrier below
+        const int r = 16 * qt + (lane & 15);
+  #pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          u32x2 w;
+          w[0] = pack_bf16x2(dq[i][0] * a.scale, dq[i][1] * a.scale);
+          w[1] = pack_bf16x2(dq[i][2] * a.scale, dq[i][3] * a.scale);
+          const int c = (2 * (dt0 + i) + (g >> 1)) ^ (r & 7);
+          *reinterpret_cast<u32x2*>(dQs + r * D + c * 8 + 4 * (g & 1)) = w;
+        }
+      } else if (qrow < a.Sq) {
         bf16_t* rowp = a.out3 + b * a.out3_sb + (long)qrow * a.out3_ss + h * a.out3_sh;
   #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -1620,10 +1646,23 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
         }
       }
       __syncthreads();
+      if constexpr (VS) {
+        // one 16-byte chunk per thread (64 rows x 8 chunks); the read completes before this
+        // thread's store issues, i.e. before the next block's mid-sweep barrier (dQs reuse)
+        const int r = tid >> 3, c = tid & 7;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(dQs + r * D + ((c ^ (r & 7)) << 3));
+        if (q0 + r < a.Sq)
+          *reinterpret_cast<u32x4*>(a.out3 + b * a.out3_sb + (long)(q0 + r) * a.out3_ss + h * a.out3_sh + c * 8) = v;
+      }
     }
   };
-  if (wave_mask) sweep(std::true_type{});
-  else sweep(std::false_type{});
+  if (a.vst == 1) {  // (LJS_ATTN_VST=2: dK / dV staged, dQ per lane -- A/B)
+    if (wave_mask) sweep(std::true_type{}, std::true_type{});
+    else sweep(std::false_type{}, std::true_type{});
+  } else {
+    if (wave_mask) sweep(std::true_type{}, std::false_type{});
+    else sweep(std::false_type{}, std::false_type{});
+  }
   if (a.vst) {
     // every wave passed the sweep's last barrier: the K / V images are free; this wave's 32 key
     // rows of dK / dV go through its own rows of them
@@ -1843,12 +1882,13 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
     f.out = (bf16_t*)dk; f.out_sb = dks[0]; f.out_ss = dks[1]; f.out_sh = dks[2];
     f.out2 = (bf16_t*)dv; f.out2_sb = dvs[0]; f.out2_ss = dvs[1]; f.out2_sh = dvs[2];
     f.out3 = (bf16_t*)dq; f.out3_sb = dqs[0]; f.out3_ss = dqs[1]; f.out3_sh = dqs[2];
-    f.vst = attn_vst() && vst_ok(dk, dks) && vst_ok(dv, dvs);
+    f.vst = vst_ok(dk, dks) && vst_ok(dv, dvs) && vst_ok(dq, dqs) ? attn_vst() : 0;
     hipLaunchKernelGGL(attn_bwd_fused_kernel, dim3(H, B), dim3(FT), 0, stream, f);
     return (int)hipGetLastError();
   }
   AttnArgs c = a;
   c.out = (bf16_t*)dq; c.out_sb = dqs[0]; c.out_ss = dqs[1]; c.out_sh = dqs[2];
+  c.vst = attn_vst() && vst_ok(dq, dqs);  // (the 128-query dQ blocks use it)
   AttnArgs b = a;
   b.out = (bf16_t*)dk; b.out_sb = dks[0]; b.out_ss = dks[1]; b.out_sh = dks[2];
   b.out2 = (bf16_t*)dv; b.out2_sb = dvs[0]; b.out2_ss = dvs[1]; b.out2_sh = dvs[2];
