@@ -93,7 +93,8 @@ def _run(spec: _Spec, xs: Dict[int, torch.Tensor]) -> Dict[int, torch.Tensor]:
         from ..spmd import graphs
         x0 = next(iter(xs.values()))
         if graphs.current() is not None and not comm.graph_safe(spec.kind, x0, spec.groups):
-            out = graphs.run_collective(lambda: _run_local(comm, spec, xs))[0]
+            out = graphs.run_collective(lambda: _run_local(comm, spec, xs),
+                                        what=f"{spec.kind} {tuple(x0.shape)} {x0.dtype}")[0]
     if out is None:
         out = _run_local(comm, spec, xs)
     if _DEBUG:

@@ -207,7 +207,9 @@ class GradReducer:
         _plan.record("all_reduce", groups=tuple(groups), note="grad.bucket", dtype=str(buf.dtype).replace("torch.", ""),
                      bytes_in=buf.numel() * buf.element_size(), overlapped=True)
         comm = get_comm()
-        _, handle = graphs.run_collective(fn, async_=True, capturable=comm.graph_safe("all_reduce", buf))
+        _, handle = graphs.run_collective(fn, async_=True,
+                                          capturable=comm.graph_safe("all_reduce", buf, [tuple(g) for g in groups]),
+                                          what=f"grad bucket all_reduce {tuple(buf.shape)} {buf.dtype}")
         self.launched.append((idxs, flat32, wire, handle))
 
     # ------------------------------------------------------------------ result

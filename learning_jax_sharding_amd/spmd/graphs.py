@@ -23,6 +23,8 @@ replays as a single graph.  The cut path remains for torch process-group collect
 """
 from __future__ import annotations
 
+import os
+import sys
 import warnings
 from typing import Any, Callable, Dict, List, Optional
 
@@ -155,7 +157,7 @@ class _Fork:
         self.ev = ev
 
 
-def run_collective(fn: Callable[[], Any], async_: bool = False, capturable: bool = False):
+def run_collective(fn: Callable[[], Any], async_: bool = False, capturable: bool = False, what: str = ""):
     """Issue a cross-process collective: directly (eager), as a cut point of the active
     segmented capture, or - when ``capturable`` (native RCCL on the current stream) - as part
     of the capture itself, forked onto a side stream when ``async_`` so it overlaps the rest of
@@ -182,7 +184,18 @@ def run_collective(fn: Callable[[], Any], async_: bool = False, capturable: bool
             ev.record(cs)
             return out, ev
         return fn(), None
+    if _CUT_TRACE:
+        # diagnostics (LJS_GRAPH_CUT_TRACE=1): where a capture is cut, i.e. which collective took a
+        # path that cannot be captured
+        import traceback
+        fr = [f for f in traceback.extract_stack(limit=8)[:-1] if "spmd/graphs.py" not in f.filename]
+        print(f"[ljs graph cut] {what or 'collective'} at " + " <- ".join(f"{f.filename.rsplit('/', 2)[-1]}:{f.lineno}"
+                                                                           for f in reversed(fr[-4:])),
+              file=sys.stderr, flush=True)
     return seg.collective(fn, async_)
+
+
+_CUT_TRACE = os.environ.get("LJS_GRAPH_CUT_TRACE", "0") == "1"
 
 
 def join(handle) -> None:

@@ -57,6 +57,19 @@ def test_real_spawn_two_gloo_ranks_on_one_gpu():
     assert rec["config"]["graph_segments"] > 1, rec["config"]
 
 
+def test_two_ranks_one_gpu_tp_p2p_single_graph():
+    """The reference's model (TP) axis over two real ranks sharing GPU 0, every collective of the
+    step (weight gathers, K/V gathers, the out-projection all-to-all, gradient reduce-scatters)
+    through the IPC peer-memory kernels (LJS_P2P=1): bytes really move between the processes and
+    the whole step is ONE captured graph (no gloo cut)."""
+    r = _bench_raw({"LJS_DIST_BACKEND": "gloo", "LJS_P2P": "1", "LJS_P2P_MAX_KB": "65536", "LJS_COMM_TIMEOUT_S": "90"}, "--gpus", "2",
+                   "--mesh", "1x2", "--steps", "8", "--warmup", "2", "--batch-per-gpu", "8", "--graph-steps", "1")
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["config"]["mesh"] == [1, 2]
+    assert rec["config"]["graph_segments"] == 1, rec["config"]
+
+
 def test_fake_8rank_2d_mesh_single_graph():
     """The reference's 2-D DP x TP layout at 8 ranks ((4, 2) mesh): every collective of the step
     (weight all-gathers, K/V gathers, out-projection all-to-all, gradient reductions) is captured
