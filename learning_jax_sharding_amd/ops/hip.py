@@ -344,6 +344,8 @@ _DW_TRAFFIC_W = float(os.environ.get("LJS_DW_TRAFFIC_W", "1"))
 # weight-grad tile above 4096 tokens: 1282 (cost-model split count) or, as an A/B switch, 644 /
 # 12884 with one round of slabs
 _DW_BIG_TILE = int(os.environ.get("LJS_DW_BIG_TILE", "1282"))
+# (A/B) rounds of resident blocks the 644 / 12884 split fills (more, shorter slabs)
+_DW_BIG_ROUNDS = int(os.environ.get("LJS_DW_BIG_ROUNDS", "1"))
 
 
 def slab_count(nkt: int, S: int) -> int:
@@ -379,7 +381,7 @@ def pick_dw_slabs(K: int, N: int, T: int):
         nkt = T // 64
         bm = 64 if _DW_BIG_TILE == 644 else 128
         tiles = -(-K // bm) * -(-N // bm)
-        slots = (2 if _DW_BIG_TILE == 644 else 1) * _cus()
+        slots = (2 if _DW_BIG_TILE == 644 else 1) * _cus() * _DW_BIG_ROUNDS
         S = max(1, min(nkt, slots // max(1, tiles)))
         while S > 1 and slab_count(nkt, S) != S:
             S -= 1
