@@ -53,6 +53,9 @@ constexpr int kMFast = 1024;
 // B operand of batch b taken from bptr[b] (up to 4 separate tensors, e.g. the q / k / v
 // cotangents of a weight-major fused projection) -- slab-mode LDS-DMA kernels only
 constexpr int kBPtrs = 4096;
+// slab mode, the block's LAST item: its f32 tile leaves through the (then idle) LDS ring as whole
+// 256-byte rows (16-byte chunk XOR row), not as 64-byte pieces of 16 rows per store instruction
+constexpr int kSlabVst = 8192;
 
 // Epilogue operand R applied to 8 consecutive output values (after bias / ReLU, f32):
 //   residual add: out = bf16(bf16(v) + bf16(R))   (the unfused "y = dense(x); y + R" in bf16:
@@ -792,6 +795,39 @@ gemm_dma_kernel(
     } else {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]
       const bool vec = (p.ldc & 3) == 0 && (p.sC & 3) == 0 && ((((uintptr_t)p.C) & 15) == 0);
+      if constexpr (BN / WN == 64 && WM * WN * (BM / WM) * 256 <= NST * STAGE * 2) {
+        if (slabs && vec && (p.flags & kSlabVst) && it + 1 == my_items && !has_bias && !relu && !accumulate) {
+          // no DMA is in flight after the block's last item: once every wave's last fragment reads
+          // are done the ring holds this wave's 64-column f32 rows (wave-private image)
+          __syncthreads();
+          unsigned char* img = reinterpret_cast<unsigned char*>(smem) + wave * (BM / WM) * 256;
+#pragma unroll
+          for (int ii = 0; ii < TM; ++ii) {
+            const int r = ii * 16 + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              *reinterpret_cast<f32x4*>(img + r * 256 + (((4 * j + g) ^ (r & 7)) << 4)) = acc[ii][j] * p.alpha;
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const long cb = (long)(w.split * p.batch + w.b) * p.sC;
+#pragma unroll
+          for (int q = 0; q < (BM / WM) / 4; ++q) {
+            const int r = 4 * q + (lane >> 4), c = lane & 15;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + ((c ^ (r & 7)) << 4));
+            const int row = m0 + r, col = n0 + 4 * c;
+            if (row < p.M && col + 4 <= p.N) {
+              const u32x4 bits = __builtin_bit_cast(u32x4, v);
+              __builtin_amdgcn_raw_buffer_store_b128(bits, rc, (int)((cb + (long)row * p.ldc + col) * 4), 0, 0);
+            } else if (row < p.M) {
+              float* C = reinterpret_cast<float*>(p.C) + cb + (long)row * p.ldc + col;
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (col + e < p.N) C[e] = v[e];
+            }
+          }
+          continue;  // the block's last item: nothing follows
+        }
+      }
       // this item's output block (slab mode: slab (split, batch b) = split * batch + b, so the
       // slabs of a batch of weight gradients are [S][batch][M][N]: one slab_reduce combines all)
       const long cb = (long)(slabs ? w.split * p.batch + w.b : w.b) * p.sC;

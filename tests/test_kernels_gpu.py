@@ -1037,3 +1037,23 @@ def test_fp8_transformer_layer_large_tiles_and_fused_colsum(gpu_devices):
         b = g0[k]
         assert torch.isfinite(a).all(), k
         torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-3 * max(1.0, b.abs().max().item()))
+
+
+@pytest.mark.parametrize("T,K,N,tile,S", [(16384, 640, 1536, 1282, 8), (16384, 512, 640, 1282, 24),
+                                          (4096, 192, 328, 1282, 4), (8192, 640, 1536, 2563, 4)])
+def test_slab_gemm_staged_epilogue_bit_exact(hip, T, K, N, tile, S):
+    """Weight-gradient slab GEMMs: the last item's f32 tile through LDS as whole rows
+    (kSlabVst) == the per-lane 16-byte stores, bit for bit (ragged M / N included)."""
+    x = _rand(T, K, seed=21)
+    dy = _rand(T, N, seed=22)
+    assert hip.slab_count(T // 64, S) == S
+    outs = []
+    for vst in (True, False):
+        hip._SLAB_VST = vst
+        slabs = torch.full((S, K, N), float("nan"), dtype=torch.float32, device=dev)
+        hip.gemm(x, dy, slabs, K, N, T, K, N, N, False, False, sC=K * N, splitk=S, tile=tile, slabs=True)
+        outs.append(slabs)
+    hip._SLAB_VST = os.environ.get("LJS_SLAB_VST", "1") == "1"
+    assert torch.equal(outs[0], outs[1])
+    ref = (x.float().t() @ dy.float())
+    torch.testing.assert_close(outs[0].sum(0), ref, rtol=2e-2, atol=2e-1)
