@@ -1,4 +1,5 @@
 """HIP kernel numerics vs plain PyTorch fp32 references (run on a real MI355X: -m gpu)."""
+import os
 import math
 
 import numpy as np
