@@ -56,8 +56,6 @@ constexpr int kBPtrs = 4096;
 // slab mode, the block's LAST item: its f32 tile leaves through the (then idle) LDS ring as whole
 // 256-byte rows (16-byte chunk XOR row), not as 64-byte pieces of 16 rows per store instruction
 constexpr int kSlabVst = 8192;
-// the same for a bf16 output without epilogue operand / fused sum: whole 128-byte wave-tile rows
-constexpr int kBf16Vst = 16384;
 
 // Epilogue operand R applied to 8 consecutive output values (after bias / ReLU, f32):
 //   residual add: out = bf16(bf16(v) + bf16(R))   (the unfused "y = dense(x); y + R" in bf16:
@@ -701,53 +699,6 @@ gemm_dma_kernel(
           }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    if constexpr (!OUT_F32 && RES == 0 && BN / WN == 64 && WM * WN * (BM / WM) * 128 <= NST * STAGE * 2) {
-      if ((p.flags & kBf16Vst) && !psum_on && it + 1 == my_items) {
-        // the block's last item: no DMA in flight, so after every wave's last fragment reads the
-        // ring holds this wave's 64-column bf16 rows (16-byte chunk XOR row), stored as whole rows
-        __syncthreads();
-        unsigned char* img = reinterpret_cast<unsigned char*>(smem) + wave * (BM / WM) * 128;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = n0 + 16 * j + 4 * g;
-          float bv[4] = {0.f, 0.f, 0.f, 0.f};
-          if (has_bias) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if (col + e >= p.N) continue;
-              const long bo = (long)w.b * p.sBias + col + e;
-              bv[e] = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo]
-                               : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo]);
-            }
-          }
-#pragma unroll
-          for (int ii = 0; ii < TM; ++ii) {
-            const int r = ii * 16 + (lane & 15);
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              v[e] = acc[ii][j][e] * p.alpha + bv[e];
-              if (relu) v[e] = fmaxf(v[e], 0.f);
-            }
-            const int c8 = 4 * j + g;
-            *reinterpret_cast<u32x2*>(img + r * 128 + ((((c8 >> 1) ^ (r & 7))) << 4) + ((c8 & 1) << 3)) =
-                u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int q = 0; q < (BM / WM) / 8; ++q) {
-          const int r = 8 * q + (lane >> 3), c = lane & 7;
-          const u32x4 v = *reinterpret_cast<const u32x4*>(img + r * 128 + ((c ^ (r & 7)) << 4));
-          const int row = m0 + r, col = n0 + 8 * c;
-          const int off = (row < p.M && col < p.N) ? (int)(((long)w.b * p.sC + (long)row * p.ldc + col) * 2)
-                                                   : 0x7ffffff0;
-          if (st_sc1) __builtin_amdgcn_raw_buffer_store_b128(v, rc, off, 0, kSC1);
-          else __builtin_amdgcn_raw_buffer_store_b128(v, rc, off, 0, 0);
-        }
-        continue;  // the block's last item: nothing follows
       }
     }
     if constexpr (!OUT_F32) {

@@ -244,8 +244,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
         (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0) | (512 if slabs else 0) | \
-        (2048 if A.dtype == torch.float32 else 0) | (8192 if (slabs and _SLAB_VST) else 0) | \
-        (16384 if (_GEMM_VST and not out_f32) else 0)
+        (2048 if A.dtype == torch.float32 else 0) | (8192 if (slabs and _SLAB_VST) else 0)
     if res is not None:
         assert not out_f32 and res.dtype in (torch.bfloat16, torch.float32), (C.dtype, res.dtype)
         flags |= (64 if res_mode == "add" else 128) | (256 if res.dtype == torch.float32 else 0)
@@ -306,9 +305,6 @@ def _psum_for(t: torch.Tensor):
 _TILE_2561 = os.environ.get("LJS_GEMM_TILE2561", "1") == "1"
 # slab-mode GEMMs: the last item's f32 tile leaves through LDS as whole rows (kSlabVst)
 _SLAB_VST = os.environ.get("LJS_SLAB_VST", "1") == "1"
-# (A/B) bf16-output LDS-DMA GEMMs without epilogue operand / fused sum: the same for the block's
-# last item (kBf16Vst)
-_GEMM_VST = os.environ.get("LJS_GEMM_VST", "0") == "1"
 
 
 # 128x160 tiles when they (and not 128x128 tiles) fill whole rounds of 512 resident blocks

@@ -1058,23 +1058,3 @@ def test_slab_gemm_staged_epilogue_bit_exact(hip, T, K, N, tile, S):
     assert torch.equal(outs[0], outs[1])
     ref = (x.float().t() @ dy.float())
     torch.testing.assert_close(outs[0].sum(0), ref, rtol=2e-2, atol=2e-1)
-
-
-@pytest.mark.parametrize("T,K,N,tile,bias", [(16384, 640, 1536, 2561, True), (16384, 640, 512, 1282, False),
-                                             (4096, 512, 640, 1282, True), (1000, 640, 328, 1282, False)])
-def test_bf16_gemm_staged_epilogue_bit_exact(hip, T, K, N, tile, bias):
-    """bf16-output LDS-DMA GEMMs: the block's last item through LDS as whole rows (kBf16Vst) ==
-    the paired-lane 16-byte stores, bit for bit (bias, ragged M / N)."""
-    x = _rand(T, K, seed=31)
-    w = _rand(N, K, seed=32)
-    b = _rand(N, seed=33) if bias else None
-    outs = []
-    for vst in (True, False):
-        hip._GEMM_VST = vst
-        c = torch.full((T, N), float("nan"), dtype=torch.bfloat16, device=dev)
-        hip.gemm(x, w, c, T, N, K, K, K, N, True, True, bias=b, tile=tile)
-        outs.append(c)
-    hip._GEMM_VST = os.environ.get("LJS_GEMM_VST", "0") == "1"
-    assert torch.equal(outs[0], outs[1])
-    ref = x.float() @ w.float().t() + (b.float() if bias else 0)
-    torch.testing.assert_close(outs[0].float(), ref, rtol=2e-2, atol=2e-1)
