@@ -1470,6 +1470,7 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
   }
 }
 
+template <bool KVDMA>
 __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[FK * D];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[FK * D];
@@ -1489,7 +1490,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   // K and V land by LDS-DMA (swizzle on the source address, rows past Sk read zeros), in flight
   // together with the first query block's Q / dO / O below: one exposed latency, not two (the
   // register-staged copy waited for K / V before the first block's DMA was even issued)
-  {
+  if constexpr (KVDMA) {
     const u32x4 rk = rsrc_u4(kb, 2 * ((long)(a.Sk - 1) * a.k_ss + D));
     const u32x4 rv = rsrc_u4(vb, 2 * ((long)(a.Sk - 1) * a.v_ss + D));
     constexpr int NWF = FT / 64;
@@ -1501,6 +1502,17 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       const bool ok = row < a.Sk;
       dma_lds_x4(rk, ok ? (int)(((long)row * a.k_ss + c) * 2) : 0x7ffffff0, Ks + pc * 512);
       dma_lds_x4(rv, ok ? (int)(((long)row * a.v_ss + c) * 2) : 0x7ffffff0, Vs + pc * 512);
+    }
+  } else {
+    // register-staged copy (the default: 45.98 vs 47.01 us for the LDS-DMA form at B=64,
+    // gpurun_out/r3aj; LJS_ATTN_BWD_KV_DMA=1 selects the DMA form)
+#pragma unroll
+    for (int i = 0; i < FK * 8 / FT; ++i) {
+      int c = tid + FT * i, row = c >> 3, c16 = c & 7;
+      u32x4 x = row < a.Sk ? *reinterpret_cast<const u32x4*>(kb + (long)row * a.k_ss + c16 * 8) : u32x4{0, 0, 0, 0};
+      u32x4 y = row < a.Sk ? *reinterpret_cast<const u32x4*>(vb + (long)row * a.v_ss + c16 * 8) : u32x4{0, 0, 0, 0};
+      *reinterpret_cast<u32x4*>(Ks + img16(row, c16)) = x;
+      *reinterpret_cast<u32x4*>(Vs + img16(row, c16)) = y;
     }
   }
 
@@ -1883,7 +1895,9 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
     f.out2 = (bf16_t*)dv; f.out2_sb = dvs[0]; f.out2_ss = dvs[1]; f.out2_sh = dvs[2];
     f.out3 = (bf16_t*)dq; f.out3_sb = dqs[0]; f.out3_ss = dqs[1]; f.out3_sh = dqs[2];
     f.vst = vst_ok(dk, dks) && vst_ok(dv, dvs) && vst_ok(dq, dqs) ? attn_vst() : 0;
-    hipLaunchKernelGGL(attn_bwd_fused_kernel, dim3(H, B), dim3(FT), 0, stream, f);
+    static const int kv_dma = getenv("LJS_ATTN_BWD_KV_DMA") ? atoi(getenv("LJS_ATTN_BWD_KV_DMA")) : 0;
+    if (kv_dma) hipLaunchKernelGGL(attn_bwd_fused_kernel<true>, dim3(H, B), dim3(FT), 0, stream, f);
+    else hipLaunchKernelGGL(attn_bwd_fused_kernel<false>, dim3(H, B), dim3(FT), 0, stream, f);
     return (int)hipGetLastError();
   }
   AttnArgs c = a;

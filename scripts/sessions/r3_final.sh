@@ -1,7 +1,7 @@
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R=$PWD
-O=$R/gpurun_out/r3final2
+O=$R/gpurun_out/r3final3
 mkdir -p $O
 step() { local log=$1; shift; "$@" > "$log" 2>&1; local rc=$?; if [ $rc -ne 0 ]; then echo "rc=$rc: $*" >> $O/rc.log; case $rc in 1|2) ;; *) exit $rc;; esac; fi; }
 step $O/gpu_tests.log timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/
