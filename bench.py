@@ -313,8 +313,17 @@ def main():
             run(2 * G)
             run(2)
         run(max(1, args.warmup))
-        if multi is not None and args.warmup % G:
-            run(G)  # (untimed) the train state back in the G-step graph's buffers before timing
+        warm_run = max(1, args.warmup)
+        # untimed: at least LJS_BENCH_MIN_WARM steps in all (a fixed count, so every rank runs the
+        # same collectives) - after only W = 5 steps the GPU clock has not ramped: --steps 20
+        # --warmup 5 read 0.255-0.262 ms where --warmup 40 read 0.233-0.237 (gpurun_out/r3al) -
+        # ending in the G-step graph so the timed steps start in its buffers
+        extra = max(0, int(os.environ.get("LJS_BENCH_MIN_WARM", "48")) - warm_run)
+        if multi is not None and (warm_run + extra) % G:
+            extra += G - (warm_run + extra) % G
+        if extra:
+            run(extra)
+            warm_run += extra
         if aten_trace:
             from learning_jax_sharding_amd.utils.aten_trace import AtenTrace
             with AtenTrace(cuda_only=not os.environ.get("LJS_ATEN_TRACE_ALL"),
@@ -393,7 +402,8 @@ def main():
             "data": "synthetic (random normal x, random-init weights)",
             "config": {"model": model_desc,
                        "global_batch": B, "seq_len": S, "parallelism": par, "mode": args.mode,
-                       "hip_graph": capture, "graph_segments": segs, "steps_per_graph": G, "mesh": list(mshape),
+                       "hip_graph": capture, "graph_segments": segs, "steps_per_graph": G,
+                       "warmup_steps_run": warm_run, "mesh": list(mshape),
                        "comm": comm, "grad_wire": os.environ.get("LJS_GRAD_COMM_DTYPE", "fp32"),
                        "loss": "y.sum()" if args.loss == "sum" else "mean((y - target)^2)", "rules": args.rules},
         }
