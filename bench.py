@@ -49,6 +49,10 @@ def parse():
                    help="GPUs (= ranks); default: WORLD_SIZE under torchrun, else 1")
     p.add_argument("--steps", type=int, default=48)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--min-warmup", type=int, default=int(os.environ.get("LJS_BENCH_MIN_WARM", "64")),
+                   help="untimed steps in all before the timed region, at least (the GPU clock has not ramped "
+                        "after a few ms of work: --steps 20 --warmup 5 read 0.255-0.262 ms where --warmup 40 read "
+                        "0.233-0.237, gpurun_out/r3al); the JSON 'warmup' reports the total that ran")
     p.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("LJS_BENCH_BPG", "64")))
     p.add_argument("--seq", type=int, default=256)
     p.add_argument("--dim", type=int, default=640)
@@ -308,19 +312,21 @@ def main():
 
     with mesh, nn.axis_rules(rules):
         phase("capture + warmup")
+        warm_run = 0   # every untimed step, capture steps included
         if multi is not None:
             # both graphs captured before the timed region, whatever W is
             run(2 * G)
             run(2)
+            warm_run += 2 * G + 2
         run(max(1, args.warmup))
-        warm_run = max(1, args.warmup)
-        # untimed: at least LJS_BENCH_MIN_WARM steps in all (a fixed count, so every rank runs the
+        warm_run += max(1, args.warmup)
+        # untimed: at least --min-warmup steps in all (a fixed count, so every rank runs the
         # same collectives) - after only W = 5 steps the GPU clock has not ramped: --steps 20
         # --warmup 5 read 0.255-0.262 ms where --warmup 40 read 0.233-0.237 (gpurun_out/r3al) -
         # ending in the G-step graph so the timed steps start in its buffers
-        extra = max(0, int(os.environ.get("LJS_BENCH_MIN_WARM", "48")) - warm_run)
-        if multi is not None and (warm_run + extra) % G:
-            extra += G - (warm_run + extra) % G
+        extra = max(0, args.min_warmup - warm_run)
+        if multi is not None and extra % G:
+            extra += G - extra % G   # whole G-step graphs: the timed steps start in its buffers
         if extra:
             run(extra)
             warm_run += extra
@@ -390,7 +396,10 @@ def main():
             "n_gpus": n_gpus if cuda else n,
             "n_devices": n,
             "steps": args.steps,
-            "warmup": args.warmup,
+            # the untimed steps actually run before the timed region: --warmup plus the clock-ramp
+            # minimum (--min-warmup), so the field says what ran
+            "warmup": warm_run,
+            "warmup_requested": args.warmup,
             "ms_per_step": round(ms, 4),
             "tflops_per_gpu": round(tflops_total / max(1, n_gpus if cuda else n), 3),
             "tokens_per_s": round(tokens_per_s, 1),

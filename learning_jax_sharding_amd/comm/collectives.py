@@ -166,10 +166,13 @@ class _CollectiveFn(torch.autograd.Function):
         ctx.in_devs = in_devs
         ctx.out_devs = out_devs
         ctx.in_meta = {d: (tuple(x.shape), x.dtype, x.device) for d, x in zip(in_devs, xs)}
-        # a pure permutation of elements over the devices: keep the inputs so a constant
+        # a pure permutation of elements over the devices: keep the inputs' METADATA so a constant
         # cotangent on every output can be moved to them without running the transpose
-        # (spmd.api.value_and_grad: the seed of a summed loss; the sum is permutation-invariant)
-        ctx.perm_inputs = tuple(xs) if spec.kind == "all_to_all" and tuple(in_devs) == tuple(out_devs) else None
+        # (spmd.api.value_and_grad: the seed of a summed loss; the sum is permutation-invariant).
+        # Not the tensors - an activation held to the backward would only cost memory: the seed
+        # goes to the inputs' gradient edges (this node's next_functions)
+        ctx.perm_inputs = tuple((tuple(x.shape), x.dtype, x.device, x.requires_grad) for x in xs) \
+            if spec.kind == "all_to_all" and tuple(in_devs) == tuple(out_devs) else None
         out = _run(spec, dict(zip(in_devs, xs)))
         ctx.out_meta = {d: (tuple(out[d].shape), out[d].dtype, out[d].device) for d in out_devs}
         ctx.out_strides = {d: tuple(out[d].stride()) for d in out_devs}

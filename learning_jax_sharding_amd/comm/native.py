@@ -255,6 +255,10 @@ class RankRccl:
         self._world_h = self._init_world()
         self._parts: Dict[Tuple[Tuple[int, ...], ...], Optional[int]] = {}
         self._log: Dict[int, Dict[str, Tuple[int, int]]] = {}
+        # the watchdog thread (comm/watchdog.py) reads _parts / _log while the main thread adds
+        # partitions and collective kinds: both sides go through this lock and readers iterate
+        # snapshots
+        self._mu = threading.Lock()
 
     def _init_world(self) -> int:
         import torch.distributed as dist
@@ -291,7 +295,8 @@ class RankRccl:
             NativeRccl._check(runtime().ljs_comm_split_rank(self._world_h, color, key, ctypes.byref(out)),
                               "ncclCommSplit")
             h = out.value if color >= 0 else None
-        self._parts[groups] = h
+        with self._mu:
+            self._parts[groups] = h
         return h
 
     @staticmethod
@@ -333,7 +338,9 @@ class RankRccl:
 
     def _handles(self):
         hs = [self._world_h] if self._world_h else []
-        for v in self._parts.values():
+        with self._mu:
+            parts = list(self._parts.values())
+        for v in parts:
             if v and v not in hs:
                 hs.append(v)
         return hs
@@ -341,7 +348,9 @@ class RankRccl:
     def _name(self, h) -> str:
         if h == self._world_h:
             return f"world ({self.world} ranks)"
-        for groups, v in self._parts.items():
+        with self._mu:
+            items = list(self._parts.items())
+        for groups, v in items:
             if v == h:
                 mine = next((g for g in groups if self.rank in g), ())
                 return f"partition {list(map(list, groups))} (this rank's group {list(mine)})"
@@ -360,7 +369,8 @@ class RankRccl:
         counts, bytes per call) - what a hang diagnosis prints (comm/watchdog.py)."""
         out = []
         for h in self._handles():
-            ops = self._log.get(h, {})
+            with self._mu:
+                ops = dict(self._log.get(h, {}))
             ops_s = ", ".join(f"{k} x{n} ({b / 1e6:.3g} MB/call)" for k, (n, b) in sorted(ops.items())) or "idle"
             out.append(f"{self._name(h)}: {ops_s}")
         return out
@@ -374,11 +384,13 @@ class RankRccl:
         """Destroy the partition communicators, then the world one (ncclCommDestroy)."""
         for h in self._handles()[::-1]:
             runtime().ljs_comm_destroy(h)
-        self._parts.clear()
-        self._world_h = None
-        self._log.clear()
+        with self._mu:
+            self._parts.clear()
+            self._world_h = None
+            self._log.clear()
 
     def _note(self, h, kind: str, nbytes: int) -> None:
-        ops = self._log.setdefault(h, {})
-        n, b = ops.get(kind, (0, 0))
-        ops[kind] = (n + 1, max(b, nbytes))
+        with self._mu:
+            ops = self._log.setdefault(h, {})
+            n, b = ops.get(kind, (0, 0))
+            ops[kind] = (n + 1, max(b, nbytes))

@@ -76,8 +76,9 @@ def _rt():
         L.ljs_p2p_free.argtypes = [_VP]
         L.ljs_p2p_close.argtypes = [_VP]
         L.ljs_p2p_enable_peer.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.ljs_rt_capture_id.argtypes = [_VP, ctypes.POINTER(ctypes.c_ulonglong)]
         for f in (L.ljs_p2p_alloc, L.ljs_p2p_open, L.ljs_p2p_free, L.ljs_p2p_close, L.ljs_p2p_enable_peer,
-                  L.ljs_rt_ipc_handle_size):
+                  L.ljs_rt_ipc_handle_size, L.ljs_rt_capture_id):
             f.restype = ctypes.c_int
         L._p2p_sigs = True
     return L
@@ -90,6 +91,15 @@ def _ck(rc, what):
 
 def _stream(dev: torch.device) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _capture_id(stream: int) -> int:
+    """The capture sequence id of ``stream`` (0 when it is not capturing)."""
+    cid = ctypes.c_ulonglong(0)
+    rc = _rt().ljs_rt_capture_id(stream, ctypes.byref(cid))
+    if rc < 0:
+        raise RuntimeError(f"hipStreamGetCaptureInfo failed with hipError {-rc}")
+    return int(cid.value)
 
 
 class P2PGroup:
@@ -147,6 +157,13 @@ class P2PGroup:
                 _ck(rt.ljs_p2p_open(me.index, ctypes.cast(h, _VP), ctypes.byref(q)), "ipc_open")
                 self.base.append(q.value)
                 self._opened.append(q.value)
+        # per member: (stream, event, capture id) of the last collective's completion.  A group has
+        # ONE staging buffer and ONE device-side barrier sequence, so two of its collectives must
+        # never run concurrently: one issued on another stream (a side-stream weight prefetch next
+        # to the compute stream's gathers, an async gradient bucket) first waits for the previous
+        # one.  Every member issues its collectives in the same program order, so the executions -
+        # and the barrier sequence numbers - line up on every member.
+        self._last: Dict[int, tuple] = {}
         self.flags = (_VP * self.n)(*self.base)
         self.ins = (_VP * self.n)(*[b + FLAG_BYTES for b in self.base])
         self.res = (_VP * self.n)(*[b + FLAG_BYTES + self.cap for b in self.base])
@@ -154,6 +171,24 @@ class P2PGroup:
     # ------------------------------------------------------------------ plumbing
     def _members(self) -> List[int]:
         return list(range(self.n)) if self.mode == "local" else [self.rank]
+
+    def _enter(self):
+        """Order this collective after the group's previous one when that ran on another stream
+        (within the same capture, or both eager)."""
+        for m in self._members():
+            s = torch.cuda.current_stream(self.devices[m])
+            last = self._last.get(m)
+            if last is None or last[0] == s.cuda_stream:
+                continue
+            if last[2] == _capture_id(s.cuda_stream):
+                s.wait_event(last[1])
+
+    def _exit(self):
+        for m in self._members():
+            s = torch.cuda.current_stream(self.devices[m])
+            ev = torch.cuda.Event()
+            ev.record(s)
+            self._last[m] = (s.cuda_stream, ev, _capture_id(s.cuda_stream))
 
     def _barrier(self):
         L = _kern()
@@ -209,6 +244,7 @@ class P2PGroup:
         dt = _DT[x0.dtype]
         out = out if out is not None else {m: torch.empty_like(xs[m]) for m in self._members()}
         L = _kern()
+        self._enter()
         self._stage(xs, nbytes)
         self._barrier()
         if nbytes <= self.oneshot_max:
@@ -228,6 +264,7 @@ class P2PGroup:
                     _ck(L.ljs_p2p_gather(self.res, self.n, 0, out[m].data_ptr(), chunk, _stream(self.devices[m])),
                         "gather")
         self._barrier()
+        self._exit()
         return out
 
     def all_gather(self, xs: Dict[int, torch.Tensor]):
@@ -237,6 +274,7 @@ class P2PGroup:
         out = {m: torch.empty((self.n,) + tuple(xs[m].shape), dtype=xs[m].dtype, device=xs[m].device)
                for m in self._members()}
         L = _kern()
+        self._enter()
         self._stage(xs, nbytes)
         self._barrier()
         for m in self._members():
@@ -244,6 +282,7 @@ class P2PGroup:
                 _ck(L.ljs_p2p_gather(self.ins, self.n, 0, out[m].data_ptr(), nbytes, _stream(self.devices[m])),
                     "gather")
         self._barrier()
+        self._exit()
         return out
 
     def reduce_scatter(self, xs: Dict[int, torch.Tensor]):
@@ -254,6 +293,7 @@ class P2PGroup:
         out = {m: torch.empty(tuple(xs[m].shape[1:]), dtype=xs[m].dtype, device=xs[m].device)
                for m in self._members()}
         L = _kern()
+        self._enter()
         self._stage(xs, nbytes)
         self._barrier()
         for m in self._members():
@@ -261,6 +301,7 @@ class P2PGroup:
                 _ck(L.ljs_p2p_reduce(self.ins, self.n, m * chunk, out[m].data_ptr(), chunk, _DT[x0.dtype],
                                      _stream(self.devices[m])), "reduce")
         self._barrier()
+        self._exit()
         return out
 
     def all_to_all(self, xs: Dict[int, torch.Tensor]):
@@ -270,6 +311,7 @@ class P2PGroup:
         chunk = nbytes // self.n
         out = {m: torch.empty_like(xs[m]) for m in self._members()}
         L = _kern()
+        self._enter()
         self._stage(xs, nbytes)
         self._barrier()
         for m in self._members():
@@ -277,6 +319,7 @@ class P2PGroup:
                 _ck(L.ljs_p2p_gather(self.ins, self.n, m * chunk, out[m].data_ptr(), chunk, _stream(self.devices[m])),
                     "gather")
         self._barrier()
+        self._exit()
         return out
 
     def close(self):

@@ -103,8 +103,11 @@ class CommWatchdog:
                  f"[ljs watchdog] phase: {self._phase!r}, {time.monotonic() - self._t0:.1f} s in"]
         nat = self._native()
         if nat is not None:
-            for desc in nat.describe():
-                lines.append(f"[ljs watchdog]   {desc}")
+            try:   # a diagnostic: whatever it raises, the abort and the exit below still run
+                for desc in nat.describe():
+                    lines.append(f"[ljs watchdog]   {desc}")
+            except Exception as e:  # pragma: no cover - defensive
+                lines.append(f"[ljs watchdog] describe failed: {e!r}")
             try:
                 nat.abort()
                 lines.append("[ljs watchdog] every RCCL communicator aborted (ncclCommAbort)")

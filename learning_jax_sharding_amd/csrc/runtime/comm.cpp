@@ -316,3 +316,16 @@ LJS_RT_API int ljs_p2p_enable_peer(int dev, int peer) {
 }
 
 LJS_RT_API int ljs_rt_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// capture state of a stream: 0 not capturing, 1 capturing (*id = the capture sequence id, unique
+// per capture in this process), < 0 a HIP error.  The p2p groups use it to chain their same-group
+// collectives across streams only within one capture (an event recorded outside the capture may
+// not be waited on inside it).
+LJS_RT_API int ljs_rt_capture_id(void* stream, unsigned long long* id) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  hipError_t e = hipStreamGetCaptureInfo(static_cast<hipStream_t>(stream), &st, &cid);
+  if (e != hipSuccess) return -(int)e;
+  *id = st == hipStreamCaptureStatusActive ? cid : 0;
+  return st == hipStreamCaptureStatusActive ? 1 : 0;
+}

@@ -828,7 +828,10 @@ class _MSELoss(torch.autograd.Function):
         if want_dy and C % 64 == 0 and y.dim() >= 2:
             sums = torch.empty((C,), dtype=torch.float32, device=y.device)
             nb = lib().ljs_mse_colsum_ws_bytes(R, C)
-            ws = _workspace(y.device, "mse_colsum", nb)
+            # keyed by geometry: the ticket words sit at an offset that depends on (R, C), so a
+            # workspace shared across geometries could hand a call a non-zero "ticket" left in
+            # another call's partial-sum area (the last arriver would never be found)
+            ws = _workspace(y.device, f"mse_colsum/{R}x{C}", nb)
             rc = lib().ljs_mse_colsum(_p(yp), _p(tp), int(tp.dtype == torch.bfloat16), R, C, float(scale), _p(dy),
                                       _p(sums), _p(out), _p(ws), _stream(y))
             _ck(rc, "mse_colsum")
@@ -918,11 +921,29 @@ def linear(x: torch.Tensor, ws: List[torch.Tensor], b: Optional[torch.Tensor], c
         return _lin.linear(x, list(ws), b, relu, out_dtype, residual=residual)
     from . import shadow
     if any(shadow.is_proxy(w) for w in ws):
-        raise RuntimeError("a gathered-weight proxy (bf16 shadow gather) reached a GEMM path that reads f32 weights")
+        # a gathered-weight proxy holds no f32 values; a shape the fused path does not take (M, K
+        # or N not a multiple of 8) reads the f32 values bf16(w) recovered from the gathered bf16
+        # copy - exactly what a bf16-compute GEMM would round the f32 weight to
+        ws = [_ProxyValues.apply(w) if shadow.is_proxy(w) else w for w in ws]
     outs = _linear_any(x, ws, b, compute_dtype, relu, out_dtype)
     if residual is not None:
         outs = [outs[0] + residual.to(outs[0].dtype)] + outs[1:]
     return outs
+
+
+class _ProxyValues(torch.autograd.Function):
+    """f32 values of a gathered-weight proxy (``parallel/weight_gather.py``) from its gathered bf16
+    copy (the "T" shadow, [N][K]); the gradient passes through unchanged to the proxy, whose
+    backward reduce-scatters it onto the shards."""
+
+    @staticmethod
+    def forward(ctx, w):
+        from . import shadow
+        return shadow.get(w, "T").t().float().contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
 
 
 def _linear_any(x, ws, b, compute_dtype, relu, out_dtype):

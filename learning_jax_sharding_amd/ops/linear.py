@@ -120,7 +120,8 @@ def defer_safe_leaves(outs, leaves: bool = True) -> set:
     exactly one autograd edge, and that edge from a _Linear backward (so autograd passes that
     Function's gradient through untouched)."""
     counts, prod, seen = {}, {}, set()
-    stack = [t.grad_fn for t in outs if t.grad_fn is not None]
+    # (outs may hold autograd GradientEdges: a seed hoisted through an all-to-all, spmd.api)
+    stack = [fn for fn in (t.grad_fn if isinstance(t, torch.Tensor) else t.node for t in outs) if fn is not None]
     while stack:
         fn = stack.pop()
         if id(fn) in seen:

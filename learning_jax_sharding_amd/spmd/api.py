@@ -383,27 +383,41 @@ _SEED_HOIST = os.environ.get("LJS_SEED_HOIST", "1") == "1"
 _REPLAY_TRACE = os.environ.get("LJS_REPLAY_TRACE", "0") == "1"
 
 
-def _through_permutations(ts: List[torch.Tensor]) -> List[torch.Tensor]:
-    """The tensors to seed with a summed loss's constant cotangent: when ``ts`` are ALL the
-    outputs of one all-to-all (a permutation of elements over the devices - e.g. the reference's
-    final ``("batch", "length", "embed")`` constraint on the block output), the all-to-all's inputs
-    instead, repeatedly.  The sum is the same either way, and the backward then runs no transposed
-    all-to-all on a materialised constant (a copy, a pack and a column-sum kernel per step)."""
+def _edge_node(t):
+    """The autograd node a seed target feeds: a tensor's grad_fn, or a GradientEdge's node."""
+    return t.grad_fn if isinstance(t, torch.Tensor) else t.node
+
+
+def _edge_nr(t):
+    return t.output_nr if isinstance(t, torch.Tensor) else t.output_nr
+
+
+def _through_permutations(ts: List[torch.Tensor]):
+    """The targets to seed with a summed loss's constant cotangent, as ``(target, shape, dtype,
+    device)``: when ``ts`` are ALL the outputs of one all-to-all (a permutation of elements over the
+    devices - e.g. the reference's final ``("batch", "length", "embed")`` constraint on the block
+    output), the all-to-all's inputs instead - their gradient edges, the node keeps only their
+    metadata - repeatedly.  The sum is the same either way, and the backward then runs no
+    transposed all-to-all on a materialised constant (a copy, a pack and a column-sum kernel per
+    step)."""
+    from torch.autograd.graph import GradientEdge
+    tgt = [(t, tuple(t.shape), t.dtype, t.device) for t in ts]
     if not _SEED_HOIST:
-        return ts
-    while ts:
-        fn = ts[0].grad_fn
+        return tgt
+    while tgt:
+        fn = _edge_node(tgt[0][0])
         if fn is None or type(fn).__name__ != "_CollectiveFnBackward" or getattr(fn, "perm_inputs", None) is None:
-            return ts
-        ins = fn.perm_inputs
-        if len(ts) != len(ins) or any(t.grad_fn is not fn for t in ts) or \
-                sorted(t.output_nr for t in ts) != list(range(len(ins))):
-            return ts
-        if not all(x.requires_grad for x in ins):
-            return ts
-        ts = list(ins)
+            return tgt
+        meta = fn.perm_inputs
+        if len(tgt) != len(meta) or any(_edge_node(t) is not fn for t, *_ in tgt) or \
+                sorted(_edge_nr(t) for t, *_ in tgt) != list(range(len(meta))):
+            return tgt
+        edges = fn.next_functions
+        if not all(m[3] for m in meta) or len(edges) != len(meta) or any(e[0] is None for e in edges):
+            return tgt
+        tgt = [(GradientEdge(e[0], e[1]), m[0], m[1], m[2]) for e, m in zip(edges, meta)]
         HOIST_STATS["hoisted"] += 1
-    return ts
+    return tgt
 
 
 HOIST_STATS = {"hoisted": 0}
@@ -436,9 +450,9 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
             # out = sum(x) whose value nobody has read: seed x with the broadcast cotangent
             # (gsize / n_holders in x's dtype, all strides 0 - what the sum's backward returns)
             xs, gsize = sum_inputs
-            for t in _through_permutations([t for t in xs.values()]):
+            for t, shape, dt, dev in _through_permutations([t for t in xs.values()]):
                 outs.append(t)
-                seeds.append(_seed(t.new_empty(()), gsize / n_holders).expand(t.shape))
+                seeds.append(_seed(torch.empty((), dtype=dt, device=dev), gsize / n_holders).expand(shape))
         elif partials is not None and not _SEED_THROUGH_ALLREDUCE:
             # out = all_reduce(partials) over groups of size G (replicated over n_holders / G
             # groups): seeding each partial with G / n_holders is exactly what the all-reduce's

@@ -94,6 +94,46 @@ def main():
     grp.check_error()
     dist.barrier()
 
+    # same-group collectives issued alternately on the compute stream and a side stream (a weight
+    # prefetch next to the activation gathers): the group orders each after the previous one, so
+    # the one staging buffer and the barrier sequence are never shared by two in flight - eager and
+    # inside one capture
+    side = torch.cuda.Stream(device=dev)
+    ins = [torch.full((8192,), float(rank + 10 * j), device=dev) for j in range(6)]
+
+    def alternate():
+        outs = []
+        for j, t in enumerate(ins):
+            if j % 2:
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    outs.append(grp.all_gather({rank: t})[rank])
+                # (no join here: the next compute-stream collective is ordered by the group)
+            else:
+                outs.append(grp.all_gather({rank: t})[rank])
+        torch.cuda.current_stream(dev).wait_stream(side)
+        return outs
+
+    def check_alt(outs):
+        for j, o in enumerate(outs):
+            for r in range(n):
+                assert torch.all(o[r] == float(r + 10 * j)), ("two-stream all_gather", j, r)
+
+    check_alt(alternate())
+    torch.cuda.synchronize()
+    dist.barrier()
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2):
+        alt_out = alternate()
+    torch.cuda.synchronize()
+    dist.barrier()
+    for _ in range(2):
+        g2.replay()
+        torch.cuda.synchronize()
+        check_alt(alt_out)
+    grp.check_error()
+    dist.barrier()
+
     # failure detection: a barrier nobody else joins times out into the error word, no hang
     dist.barrier()
     if rank == 0:

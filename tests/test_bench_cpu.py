@@ -8,7 +8,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TINY = ["--batch-per-gpu", "2", "--seq", "32", "--dim", "64", "--heads", "2", "--dim-head", "32",
-        "--ff-dim", "128", "--steps", "2", "--warmup", "1"]
+        "--ff-dim", "128", "--steps", "2", "--warmup", "1", "--min-warmup", "0"]
 
 
 @pytest.mark.parametrize("model", ["attention", "layer", "ff", "fsdp"])
@@ -25,6 +25,8 @@ def test_bench_json_contract(model):
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in rec, k
     assert rec["n_gpus"] == 1 and rec["steps"] == 2 and rec["warmup"] == 1
+    # the JSON 'warmup' is the number of untimed steps that actually ran
+    assert rec["warmup"] == rec["config"]["warmup_steps_run"] and rec["warmup_requested"] == 1
     assert rec["value"] >= 0 and rec["ms_per_step"] > 0  # value is rounded: ~0 TFLOPS on host
     assert rec["config"]["global_batch"] == 2 and rec["config"]["seq_len"] == 32
     assert rec["config"]["parallelism"] == ("fsdp1" if model == "fsdp" else "dp1")
@@ -49,6 +51,21 @@ def test_bench_spawns_ranks(gpus, mesh, par):
     assert rec["config"]["global_batch"] == 2 * gpus  # weak scaling: batch-per-gpu x N
     assert rec["config"]["comm"].startswith("gloo")
     assert rec["dtype"] == "bf16"
+    assert rec["warmup"] == rec["config"]["warmup_steps_run"]
+    # value is the whole-job aggregate (the driver's contract); the per-GPU rate the metric names
+    # is tflops_per_gpu = value / n_gpus
+    assert abs(rec["value"] - rec["tflops_per_gpu"] * gpus) <= 1e-3 * gpus
+
+
+def test_bench_min_warmup_counts_every_untimed_step():
+    env = dict(os.environ, LJS_NUM_DEVICES="1")
+    env.pop("LJS_PLATFORM", None)
+    args = [a if a != "0" else "6" for a in TINY]  # --min-warmup 6
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["warmup"] == 6 == rec["config"]["warmup_steps_run"] and rec["warmup_requested"] == 1
 
 
 def test_bench_rejects_world_mismatch():

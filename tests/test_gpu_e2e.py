@@ -12,14 +12,14 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run_block(mesh_shape, B=4, S=128, M=640, heads=8, dh=64):
+def _run_block(mesh_shape, B=4, S=128, M=640, heads=8, dh=64, rules=None):
     import learning_jax_sharding_amd as ljs
     from learning_jax_sharding_amd import nn
     from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
     from learning_jax_sharding_amd.models import MultiHeadAttention
     from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
     mesh = Mesh(create_device_mesh(mesh_shape), ("data", "model"))
-    rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))
+    rules = rules or (("batch", "data"), ("embed", "model"), ("hidden", "model"))
     model = MultiHeadAttention(M, heads=heads, dim_head=dh)
     x = ljs.random.normal(ljs.random.PRNGKey(0), (B, S, M))
     params = model.init(ljs.random.PRNGKey(1), x)["params"]
@@ -44,6 +44,22 @@ def test_block_gpu_matches_host(host_devices, gpu_devices, mesh_shape):
     from learning_jax_sharding_amd.ops import hip
     hip.lib()
     vg, gg = _run_block(mesh_shape)
+    assert abs(vh - vg) <= 3e-2 * max(1.0, abs(vh)), (vh, vg)
+    for k in gh:
+        for name in gh[k]:
+            a, b = gh[k][name], gg[k][name]
+            np.testing.assert_allclose(b, a, rtol=5e-2, atol=5e-2 * np.abs(a).max(), err_msg=f"{k}/{name}")
+
+
+def test_block_gpu_case5_rules_odd_tokens(host_devices, gpu_devices):
+    """case5 rules (embed -> data: Wq/Wk/Wv/Wo FSDP-sharded, gathered as bf16-shadow proxies) with
+    20 local tokens per device (not a multiple of 8): the dense layers take the padded path and
+    read the proxies' values from the gathered bf16 copies instead of raising."""
+    rules = (("batch", "data"), ("embed", "data"), ("hidden", "model"))
+    host_devices(4)
+    vh, gh = _run_block((2, 2), B=4, S=20, rules=rules)
+    gpu_devices(4)
+    vg, gg = _run_block((2, 2), B=4, S=20, rules=rules)
     assert abs(vh - vg) <= 3e-2 * max(1.0, abs(vh)), (vh, vg)
     for k in gh:
         for name in gh[k]:

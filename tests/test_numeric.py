@@ -414,3 +414,18 @@ def test_loss_seed_hoisted_through_output_all_to_all(host_devices, monkeypatch):
     for k in g0:
         for name in g0[k]:
             np.testing.assert_allclose(g1[k][name], g0[k][name], rtol=1e-4, atol=1e-5, err_msg=f"{k}/{name}")
+
+
+def test_all_to_all_node_keeps_no_activation(host_devices):
+    """The all-to-all's autograd node keeps only its inputs' metadata for the seed hoist (the
+    activations themselves are not held until the backward)."""
+    import torch
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd.comm import collectives as C
+    host_devices(2)
+    xs = {d: torch.randn(4, 6, requires_grad=True) * 1.0 for d in (0, 1)}
+    spec = C._Spec("all_to_all", [(0, 1)], split_dim=0, concat_dim=1)
+    outs = C._CollectiveFn.apply(spec, (0, 1), (0, 1), xs[0], xs[1])
+    meta = outs[0].grad_fn.perm_inputs
+    assert meta is not None and not any(isinstance(v, torch.Tensor) for m in meta for v in m)
+    assert meta[0][0] == (4, 6)
