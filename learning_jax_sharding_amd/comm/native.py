@@ -249,6 +249,7 @@ class RankRccl:
     as ONE graph (no capture cuts, no per-collective Python)."""
 
     _SEQ = [0]
+    _mu = threading.Lock()   # (class default for instances built without __init__: test doubles)
 
     def __init__(self, rank: int, world: int, device: int):
         self.rank, self.world, self.device = rank, world, device

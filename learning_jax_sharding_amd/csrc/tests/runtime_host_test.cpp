@@ -53,6 +53,7 @@ int ljs_p2p_free(void* ptr);
 int ljs_p2p_open(int dev, const void* ipc_handle, void** ptr);
 int ljs_p2p_close(void* ptr);
 int ljs_p2p_enable_peer(int dev, int peer);
+int ljs_rt_capture_id(void* stream, unsigned long long* id);
 int ljs_rt_ipc_handle_size();
 }
 
@@ -290,6 +291,11 @@ hipError_t hipIpcCloseMemHandle(void*) { return hipSuccess; }
 hipError_t hipDeviceSynchronize() { return hipSuccess; }
 hipError_t hipDeviceEnablePeerAccess(int, unsigned int) { return hipErrorPeerAccessAlreadyEnabled; }
 hipError_t hipGetLastError() { return hipSuccess; }
+hipError_t hipStreamGetCaptureInfo(hipStream_t, hipStreamCaptureStatus* st, unsigned long long* id) {
+  *st = hipStreamCaptureStatusNone;
+  if (id) *id = 0;
+  return hipSuccess;
+}
 
 // ------------------------------------------------------------------ tests
 namespace {
@@ -424,6 +430,10 @@ void test_p2p_buffers() {
   EXPECT(ljs_p2p_open(1, ipc.data(), &q) == 0 && q == p);
   EXPECT(ljs_p2p_close(q) == 0);
   EXPECT(ljs_p2p_enable_peer(0, 1) == 0);  // "already enabled" is success
+  {
+    unsigned long long cid = 7;
+    EXPECT(ljs_rt_capture_id(nullptr, &cid) == 0 && cid == 0);  // not capturing
+  }
   EXPECT(ljs_p2p_free(p) == 0);
 }
 }  // namespace

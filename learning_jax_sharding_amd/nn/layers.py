@@ -95,8 +95,9 @@ class FeedForward(Module):
     declared rule ``('hidden','model')`` (``case6_attention.py:186``) shards the
     hidden dim Megatron-style.  ``fp8=True`` runs the GEMMs on CDNA4's MX-fp8 block-scaled MFMA
     (e4m3 elements, e8m0 scales per 32 elements along K): with replicated weights the fused
-    block of :func:`ops.fp8.ff_block` (forward and backward-dX GEMMs in fp8), otherwise the two
-    forward GEMMs in fp8 with a bf16 backward.
+    block of :func:`ops.fp8.ff_block`, with the hidden dim split over a device group the
+    tensor-parallel fused block :func:`ops.fp8.ff_block_tp` (every FF GEMM in fp8 either way);
+    any other layout runs the two forward GEMMs in fp8 with a bf16 backward.
     """
 
     hidden_dim: int
@@ -113,10 +114,13 @@ class FeedForward(Module):
         w_out = self.param("w_out", with_logical_partitioning(init.lecun_normal(), ("hidden", "embed")),
                            (self.hidden_dim, d), torch.float32)
         dt = _dt.canonicalize(self.dtype)
-        replicated = w_in.tile.is_fully_replicated and w_out.tile.is_fully_replicated
         loc = next(iter(x.local.values())) if x.local else None
         tokens_ok = loc is not None and (loc.numel() // max(1, d)) % 128 == 0
-        if dt == torch.bfloat16 and replicated and (residual is None or residual is x) \
+        # weights not split along the hidden dim (replicated, or only M split - the reference
+        # rules map 'embed' before 'hidden', case6_attention.py:183-187): gathered, and every
+        # device runs the fused block on its own tokens (no activation moves)
+        hidden_split = w_in.tile.tile_shape[1] > 1 or w_out.tile.tile_shape[0] > 1
+        if dt == torch.bfloat16 and not hidden_split and (residual is None or residual is x) \
                 and (d % 128 == 0 and self.hidden_dim % 128 == 0 and tokens_ok if self.fp8 else True):
             # replicated weights (data-parallel / single device): the fused block - one autograd
             # node, epilogue fusions across its GEMMs; fp8: every FF GEMM (forward, dX and the
@@ -124,6 +128,21 @@ class FeedForward(Module):
             # quantized operands written by their producers' epilogues
             from ..ops.fp8 import ff_block
             return ff_block(x, w_in, w_out, residual=residual, fp8=self.fp8)
+        if dt == torch.bfloat16 and (d % 128 == 0 and self.hidden_dim % 128 == 0 if self.fp8 else True):
+            # the hidden dim split over a device group (rule ('hidden', 'model')): the
+            # tensor-parallel fused block - x's token blocks gathered over the group, W_in
+            # column- / W_out row-parallel, the partial outputs reduce-scattered (fp8: every FF
+            # GEMM on the MX MFMA, as in the replicated case)
+            from ..ops.fp8 import ff_block_tp, ff_block_tp_plan
+            xg = x
+            if x.tile.tile_shape[-1] > 1:
+                from ..spmd.reshard import reshard_tile
+                xg = reshard_tile(x, x.tile.unshard([x.ndim - 1]), note="ff.x")
+            plan = ff_block_tp_plan(xg, w_in, w_out)
+            tp = len(plan[0][0]) if plan is not None else 1
+            if plan is not None and self._tp_tokens_ok(xg, plan) and (
+                    not self.fp8 or (self.hidden_dim // tp) % 128 == 0):
+                return ff_block_tp(xg, w_in, w_out, residual=residual, fp8=self.fp8, plan=plan)
         if self.fp8:
             from ..ops.fp8 import fp8_dense
             h = fp8_dense(x, w_in, relu=True, out_dtype=dt)
@@ -133,6 +152,17 @@ class FeedForward(Module):
         h = core.dense(x, [w_in], None, compute_dtype=dt, relu=True)[0]
         h = with_logical_constraint(h, ("batch", "length", "hidden"))
         return core.dense(h, [w_out], None, compute_dtype=dt, residual=residual)[0]
+
+
+    @staticmethod
+    def _tp_tokens_ok(x: ShardedArray, plan) -> bool:
+        """The gathered token count per device is a multiple of 128 (the MX weight gradients
+        contract over tokens in 128-deep K-tiles)."""
+        groups, k = plan
+        loc = next(iter(x.local.values()), None)
+        if loc is None:
+            return False
+        return (loc.numel() // max(1, x.shape[-1]) * len(groups[0])) % 128 == 0
 
 
 class Embed(Module):

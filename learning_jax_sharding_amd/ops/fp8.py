@@ -659,3 +659,83 @@ def ff_block(x, w_in, w_out, residual=None, fp8: bool = True):
             h = K.linear(xl, [wil], None, torch.bfloat16, relu=True)[0]
             loc[d] = K.linear(h, [wol], None, torch.bfloat16, residual=rl)[0]
     return ShardedArray(tuple(x.shape), torch.bfloat16, sharding_from_tile(xt, like=[x.sharding]), loc)
+
+
+# ----------------------------------------------------------------------------- tensor-parallel FF block
+def ff_block_tp_plan(x, w_in, w_out):
+    """``(groups, token_dim)`` when the FF hidden dim is split over a device group: ``w_out``
+    ``[F][M]`` tiled ``(tp, *)`` (rule ``('hidden', 'model')``, ``case6_attention.py:186``; a split of
+    M as well, e.g. the GSPMD-paper 2-D rules, is gathered) and x
+    sharded along one token dim ``token_dim`` tp ways by groups whose members hold all tp hidden
+    blocks (the reference's sequence-over-``model`` layout, ``case6_attention.py:161``); else None."""
+    wt = w_out.tile
+    if wt.ndim != 2 or wt.tile_shape[0] < 2:
+        return None
+    tp = wt.tile_shape[0]
+    xt = x.tile
+    if xt.tile_shape[-1] != 1 or set(xt.device_ids) != set(wt.device_ids) or set(w_in.tile.device_ids) != set(
+            wt.device_ids):
+        return None
+    fblk = {d: wt.coords[d][0] for d in wt.device_ids}
+    for k in range(x.ndim - 1):
+        if xt.tile_shape[k] != tp:
+            continue
+        gs = xt.groups_along([k])
+        if all(sorted(fblk[d] for d in g) == list(range(tp)) for g in gs):
+            return gs, k
+    return None
+
+
+def ff_block_tp(x, w_in, w_out, residual=None, fp8: bool = True, plan=None):
+    """Global-view FF block with the hidden dim split over a group of tp devices (Megatron-style
+    tensor parallelism with a sequence-parallel activation, SURVEY §2.4 "FF-layer TP"):
+
+    * x's token blocks all-gathered over the group (``[.., S/tp, M] -> [.., S, M]``);
+    * ``W_in`` column-parallel (``[M][F/tp]``, resharded to the hidden block each device's
+      ``W_out`` row block holds), ``W_out`` row-parallel (``[F/tp][M]``, its own layout);
+    * every device runs the fused FF block on its hidden slice - with ``fp8`` every GEMM
+      (forward, dX and both weight gradients) on the MX-fp8 MFMA, the hidden activation kept only
+      in fp8 (:class:`_FFBlockFp8`) - producing a bf16 partial of y;
+    * the partials are reduce-scattered over the group back to x's token blocks; the residual is
+      added after.
+
+    The backward is the transpose: dY all-gathered over the group, the local block's backward,
+    dX reduce-scattered; the weight gradients stay on their hidden slices (``W_in``'s flows back
+    through its reshard)."""
+    from ..array import ShardedArray
+    from ..comm import collectives as C
+    from ..sharding.tile import TileAssignment
+    from ..spmd.reshard import reshard_tile
+    from . import core
+    from . import linear as L
+    if plan is None:
+        plan = ff_block_tp_plan(x, w_in, w_out)
+    if plan is None:
+        raise ValueError("ff_block_tp: no tensor-parallel layout for these shardings")
+    groups, k = plan
+    wt = w_out.tile
+    tp = wt.tile_shape[0]
+    devs = wt.device_ids
+    fblk = {d: wt.coords[d][0] for d in devs}
+    col = TileAssignment.from_coords({d: (0, fblk[d]) for d in devs}, (1, tp))
+    row = TileAssignment.from_coords({d: (fblk[d], 0) for d in devs}, (tp, 1))
+    core._plan.record("ff_block_tp", fp8=fp8, tp=tp, token_dim=k, groups=tuple(tuple(g) for g in groups))
+    xg = reshard_tile(x, x.tile.unshard([k]), note="ff_tp.x")
+    wi = reshard_tile(w_in, col, note="ff_tp.w_in")
+    wo = reshard_tile(w_out, row, note="ff_tp.w_out")
+    part = {}
+    for d in xg.local:
+        xl, wil, wol = xg.local[d], wi.local[d], wo.local[d]
+        if fp8:
+            part[d] = ff_block_local(xl, wil, wol, None)
+        elif xl.is_cuda and L.ff_block_supported(xl, wil, wol):
+            part[d] = L.ff_block(xl, wil, wol, False)
+        else:
+            from . import kernels as K
+            h = K.linear(xl, [wil], None, torch.bfloat16, relu=True)[0]
+            part[d] = K.linear(h, [wol], None, torch.bfloat16)[0]
+    loc = C.reduce_scatter(part, groups, dim=k, note="ff_tp.partial_sum")
+    y = ShardedArray(tuple(x.shape), torch.bfloat16, x.sharding, loc)
+    if residual is not None:
+        y = core.binary("add", core.convert(residual, torch.bfloat16), y)
+    return y

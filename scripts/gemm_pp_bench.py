@@ -1,0 +1,99 @@
+"""A/B timing of the ping-pong GEMM (gemm_pp.hip, tile codes >= 30000) against the LDS-DMA
+kernels at the headline step's shapes (T = 16384 tokens), interleaved rounds in one process.
+
+    python scripts/gemm_pp_bench.py [case ...]     cases: qkv out dh dwqkv dwo (default: all)
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from learning_jax_sharding_amd.ops import hip  # noqa: E402
+
+dev = torch.device("cuda")
+T = int(os.environ.get("T", "16384"))
+PP = hip._PP_BASE
+
+
+def timeit(fn, iters=20):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def cases():
+    out = {}
+    x = torch.randn(T, 640, device=dev).bfloat16()
+    wqkv = torch.randn(3, 512, 640, device=dev).bfloat16()
+    qkv = torch.empty(T, 1536, device=dev).bfloat16()
+
+    def qkv_fn(tile):
+        return lambda: hip.gemm(x, wqkv, qkv, T, 512, 640, 640, 640, 1536, True, True, batch=3, sA=0, sB=512 * 640,
+                                sC=512, tile=tile)
+    out["qkv"] = (qkv_fn, [PP + 1, 2561], 2 * T * 640 * 1536)
+
+    h = torch.randn(T, 512, device=dev).bfloat16()
+    wo = torch.randn(640, 512, device=dev).bfloat16()
+    bo = torch.randn(640, device=dev)
+    y = torch.empty(T, 640, device=dev).bfloat16()
+    ps = torch.empty(hip.psum_slots(T, 640), device=dev)
+
+    def out_fn(tile):
+        return lambda: hip.gemm(h, wo, y, T, 640, 512, 512, 512, 640, True, True, bias=bo, psum=ps, tile=tile)
+    out["out"] = (out_fn, [PP + 2, 1602], 2 * T * 512 * 640)
+
+    dy = torch.randn(T, 640, device=dev).bfloat16()
+    won = torch.randn(512, 640, device=dev).bfloat16()
+    dh = torch.empty(T, 512, device=dev).bfloat16()
+
+    def dh_fn(tile):
+        return lambda: hip.gemm(dy, won, dh, T, 512, 640, 640, 640, 512, True, True, tile=tile)
+    out["dh"] = (dh_fn, [PP + 3, PP + 4, 1282], 2 * T * 512 * 640)
+
+    dq = [torch.randn(T, 512, device=dev).bfloat16() for _ in range(3)]
+
+    def dwqkv_fn(tile, S=8):
+        nkt = T // 64
+        Se = hip.slab_count(nkt, S)
+        sl = torch.empty(Se, 3, 640, 512, device=dev)
+        return lambda: hip.gemm(x, dq[0], sl, 640, 512, T, 640, 512, 512, False, False, batch=3, sA=0,
+                                sC=640 * 512, splitk=Se, tile=tile, slabs=True, b_list=dq)
+    out["dwqkv"] = (dwqkv_fn, [PP + 11, PP + 12, 1282], 2 * T * 640 * 1536)
+
+    def dwo_fn(tile, S=24):
+        nkt = T // 64
+        Se = hip.slab_count(nkt, S)
+        sl = torch.empty(Se, 512, 640, device=dev)
+        return lambda: hip.gemm(h, dy, sl, 512, 640, T, 512, 640, 640, False, False, sC=512 * 640, splitk=Se,
+                                tile=tile, slabs=True)
+    out["dwo"] = (dwo_fn, [PP + 12, PP + 11, 1282], 2 * T * 512 * 640)
+    return out
+
+
+def main():
+    want = sys.argv[1:] or ["qkv", "out", "dh", "dwqkv", "dwo"]
+    cs = cases()
+    for name in want:
+        mk, tiles, flops = cs[name]
+        fns = {t: mk(t) for t in tiles}
+        res = {t: [] for t in tiles}
+        for _ in range(5):
+            for t in tiles:
+                res[t].append(timeit(fns[t]))
+        line = [f"{name:6s}"]
+        for t in tiles:
+            v = sorted(res[t])
+            med = v[len(v) // 2]
+            line.append(f"tile {t}: {med:7.2f} us ({flops / med / 1e6:6.0f} TF, min {v[0]:.2f})")
+        print("  ".join(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
