@@ -87,6 +87,8 @@ class LocalComm:
         ts = [xs[d] for d in g]
         if not all(t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) for t in ts):
             return None
+        if not p2p.wanted(len({t.device.index for t in ts}) == len(ts)):
+            return None
         nbytes = ts[0].numel() * ts[0].element_size()
         if nbytes > p2p.max_bytes():
             return None
@@ -95,6 +97,14 @@ class LocalComm:
         if grp is None:
             grp = self._p2p_groups[key] = p2p.P2PGroup([t.device for t in ts], p2p.max_bytes())
         return grp if grp.fits(nbytes, chunked) else None
+
+    def real_transfers(self, devices=None) -> bool:
+        """Collectives over ``devices`` (torch devices of the members) cross between distinct
+        GPUs (single controller over several physical GPUs)."""
+        if not devices:
+            return False
+        devs = list(devices)
+        return all(d.type == "cuda" for d in devs) and len({d.index for d in devs}) > 1
 
     def _rccl(self, g, xs):
         from . import native
@@ -301,6 +311,8 @@ class DistComm:
         from . import p2p
         if not p2p.enabled() or not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16):
             return False
+        if p2p.mode() == "auto" and not self._distinct_gpus():
+            return False
         nbytes = x.numel() * x.element_size()
         if nbytes > p2p.max_bytes():
             return False
@@ -308,7 +320,16 @@ class DistComm:
         if not mine or len(mine[0]) < 2:
             return False
         grp = self._p2p_groups.get(tuple(sorted(mine[0])))
-        return grp is not None and grp.fits(nbytes, kind in ("reduce_scatter", "all_to_all"))
+        return bool(grp) and grp.fits(nbytes, kind in ("reduce_scatter", "all_to_all"))
+
+    def _distinct_gpus(self) -> bool:
+        """Every rank drives its own GPU: an RCCL ('nccl') job (a communicator cannot hold one
+        GPU twice); gloo / fake rehearsals may share one GPU among ranks."""
+        return not self._fake and dist.get_backend() == "nccl"
+
+    def real_transfers(self) -> bool:
+        """Collectives move bytes between distinct GPUs (not a rehearsal backend)."""
+        return self._distinct_gpus()
 
     def _nat(self, groups, x) -> Optional[int]:
         if self._native is None or not self._native.supports(x):
@@ -323,6 +344,8 @@ class DistComm:
         from . import p2p
         if pg is None or not p2p.enabled() or not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16):
             return None
+        if p2p.mode() == "auto" and not self._distinct_gpus():
+            return None
         nbytes = x.numel() * x.element_size()
         if nbytes > p2p.max_bytes():
             return None
@@ -332,7 +355,15 @@ class DistComm:
             if torch.cuda.is_current_stream_capturing():
                 return None   # the handle exchange cannot run inside a capture: bulk path
             devs = [x.device if r == self.me else torch.device("cuda", 0) for r in srt]
-            grp = self._p2p_groups[srt] = p2p.P2PGroup(devs, p2p.max_bytes(), rank=srt.index(self.me), pg=pg)
+            try:
+                grp = p2p.P2PGroup(devs, p2p.max_bytes(), rank=srt.index(self.me), pg=pg)
+            except p2p.P2PUnavailable as e:   # every member raised: the group stays on RCCL
+                import warnings
+                warnings.warn(f"peer-memory collectives unavailable for ranks {srt} ({e}); using RCCL")
+                grp = False
+            self._p2p_groups[srt] = grp
+        if grp is False:
+            return None
         return grp if grp.fits(nbytes, chunked) else None
 
     def _group_of(self, groups: Groups) -> Tuple[Tuple[int, ...], object]:

@@ -16,8 +16,11 @@ by every other member; in single-controller runs they are peer-mapped.  Synchron
   every member's flag array, device-side sequence counter, timeout -> error word, no hang);
 * ``local`` mode: HIP events between the members' streams.
 
-Opt-in: ``LJS_P2P=1`` routes collectives of at most ``LJS_P2P_MAX_KB`` (default 1024) KiB per
-member through here; RCCL keeps everything else.  In ``ipc`` mode every collective is a staging
+Routing (:func:`wanted`): by default every group whose members are distinct GPUs sends its
+collectives of at most ``LJS_P2P_MAX_KB`` (default 1024) KiB per member through here - the
+case6 2-D plan's K/V and head gathers and the out-projection all-to-all - and RCCL
+keeps everything else; ``LJS_P2P=1`` forces the path on (virtual devices of one GPU too, for
+tests), ``LJS_P2P=0`` off.  In ``ipc`` mode every collective is a staging
 copy plus stream-ordered kernels whose barrier sequence comes from a device-side counter, so it
 is captured into HIP graphs like a native RCCL call (``DistComm.graph_safe``) once the group
 exists; the group itself (an IPC-handle exchange) is built by the eager warm-up call, never
@@ -34,15 +37,37 @@ import torch
 from ..ops import hip as _hip
 from . import native as _native
 
-__all__ = ["P2PGroup", "enabled", "max_bytes"]
+__all__ = ["P2PGroup", "P2PUnavailable", "enabled", "wanted", "mode", "max_bytes"]
+
+
+class P2PUnavailable(RuntimeError):
+    """The group could not be built on some member (raised on EVERY member alike)."""
 
 FLAG_BYTES = 4096          # 64 u32 arrival slots | word 64: sequence counter | word 65: error
 _VP = ctypes.c_void_p
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
 
+def mode() -> str:
+    """``LJS_P2P``: "1" every eligible small collective, "0" never, "auto" (default) only groups
+    whose members are distinct physical GPUs - where the message crosses xGMI links."""
+    v = os.environ.get("LJS_P2P", "auto").lower()
+    return v if v in ("0", "1") else "auto"
+
+
 def enabled() -> bool:
-    return os.environ.get("LJS_P2P", "0") == "1"
+    """The peer-memory path may be taken at all (see :func:`wanted` for the per-group rule)."""
+    return mode() != "0"
+
+
+def wanted(distinct_gpus: bool) -> bool:
+    """Whether a group's small collectives go through the peer-memory kernels: forced on / off
+    by ``LJS_P2P``, else exactly when every member is a distinct GPU (virtual devices sharing one
+    GPU keep the copy-based loopback path; ranks of a gloo rehearsal share GPUs or have none)."""
+    m = mode()
+    if m == "0":
+        return False
+    return m == "1" or bool(distinct_gpus)
 
 
 def max_bytes() -> int:
@@ -134,29 +159,44 @@ class P2PGroup:
                 for b in idx:
                     _ck(rt.ljs_p2p_enable_peer(a, b), "enable_peer")
         else:
+            # every step that can fail on one member is followed by an exchange of every member's
+            # status, so the members agree: all of them raise P2PUnavailable (the caller routes
+            # the group to RCCL) or none does - a lone failure never leaves peers waiting
             import torch.distributed as dist
             me = self.devices[rank]
             p = _VP()
             if rt.ljs_rt_ipc_handle_size() > 64:
                 raise RuntimeError("unexpected IPC handle size")
             hbuf = (ctypes.c_uint8 * 64)()
-            _ck(rt.ljs_p2p_alloc(me.index, self.total, ctypes.byref(p), hbuf), "alloc")
-            self._own.append(p.value)
+            ok = rt.ljs_p2p_alloc(me.index, self.total, ctypes.byref(p), hbuf) == 0
+            if ok:
+                self._own.append(p.value)
             on_gpu = dist.get_backend(pg) == "nccl"
-            mine = torch.tensor(list(hbuf), dtype=torch.uint8, device=me if on_gpu else "cpu")
-            allh = torch.empty(self.n * 64, dtype=torch.uint8, device=mine.device)
+            mine = torch.tensor(list(hbuf) + [1 if ok else 0], dtype=torch.uint8, device=me if on_gpu else "cpu")
+            allh = torch.empty(self.n * 65, dtype=torch.uint8, device=mine.device)
             dist.all_gather_into_tensor(allh, mine, group=pg)
-            allh = allh.cpu().view(self.n, 64)
+            allh = allh.cpu().view(self.n, 65)
+            if not bool(allh[:, 64].all()):
+                self._release()
+                raise P2PUnavailable(f"staging allocation failed on member(s) {allh[:, 64].eq(0).nonzero().flatten().tolist()}")
             self.base = []
+            ok = True
             for r in range(self.n):
                 if r == rank:
                     self.base.append(p.value)
                     continue
                 h = (ctypes.c_uint8 * 64)(*allh[r].tolist()[:64])
                 q = _VP()
-                _ck(rt.ljs_p2p_open(me.index, ctypes.cast(h, _VP), ctypes.byref(q)), "ipc_open")
+                if rt.ljs_p2p_open(me.index, ctypes.cast(h, _VP), ctypes.byref(q)) != 0:
+                    ok = False
+                    break
                 self.base.append(q.value)
                 self._opened.append(q.value)
+            st = torch.tensor([1 if ok else 0], dtype=torch.int32, device=mine.device)
+            dist.all_reduce(st, op=dist.ReduceOp.MIN, group=pg)
+            if int(st.item()) != 1:
+                self._release()
+                raise P2PUnavailable("opening a peer's IPC staging buffer failed")
         # per member: (stream, event, capture id) of the last collective's completion.  A group has
         # ONE staging buffer and ONE device-side barrier sequence, so two of its collectives must
         # never run concurrently: one issued on another stream (a side-stream weight prefetch next
@@ -322,12 +362,15 @@ class P2PGroup:
         self._exit()
         return out
 
-    def close(self):
+    def _release(self):
         rt = _rt()
-        for m in self._members():
-            torch.cuda.current_stream(self.devices[m]).synchronize()
         for p in self._opened:
             rt.ljs_p2p_close(p)
         for p in self._own:
             rt.ljs_p2p_free(p)
         self._opened, self._own = [], []
+
+    def close(self):
+        for m in self._members():
+            torch.cuda.current_stream(self.devices[m]).synchronize()
+        self._release()

@@ -71,7 +71,9 @@ class MultiHeadAttention(Module):
     def _prefetch_qkv(self, x: ShardedArray, ws, dt):
         from ..sharding import NamedSharding
         w0 = ws[0]
-        if not _QKV_PREFETCH or dt != torch.bfloat16 or any(t.is_meta or not t.is_cuda for w in ws for t in w.local.values()):
+        if dt != torch.bfloat16 or any(t.is_meta or not t.is_cuda for w in ws for t in w.local.values()):
+            return None
+        if not qkv_prefetch_wanted(w0):
             return None
         sh, xs = w0.sharding, x.sharding
         if not isinstance(sh, NamedSharding) or not isinstance(xs, NamedSharding) or not sh.spec:
@@ -169,10 +171,22 @@ class MultiHeadAttention(Module):
 
 
 # Measured: the gather overlaps the activation cast (profiles/r3k_v2x2_prefetch_overlap.md), but
-# the side-stream branch costs more than it hides on one GPU: 2-D rehearsal 0.3378-0.3404 vs
-# 0.3165-0.3172 ms, 4 virtual devices 1.79-1.80 vs 1.62 ms (gpurun_out/r3k) -- off by default
-# (with RCCL over xGMI the gather is a real transfer worth hiding: LJS_QKV_PREFETCH=1)
-_QKV_PREFETCH = os.environ.get("LJS_QKV_PREFETCH", "0") == "1"
+# the side-stream branch costs more than it hides when the "gather" moves no bytes between GPUs:
+# 2-D rehearsal 0.3378-0.3404 vs 0.3165-0.3172 ms, 4 virtual devices 1.79-1.80 vs 1.62 ms
+# (gpurun_out/r3k).  Over xGMI it is a real transfer worth hiding.  LJS_QKV_PREFETCH: "1" on,
+# "0" off, "auto" (default): on exactly when the gather crosses between distinct GPUs.
+_QKV_PREFETCH = os.environ.get("LJS_QKV_PREFETCH", "auto").lower()
+
+
+def qkv_prefetch_wanted(w: ShardedArray) -> bool:
+    """Whether the Q/K/V weight gather of ``w``'s layout is prefetched on a side stream."""
+    if _QKV_PREFETCH in ("0", "1"):
+        return _QKV_PREFETCH == "1"
+    from ..comm.backend import get_comm
+    c = get_comm()
+    if c.kind == "dist":
+        return c.real_transfers()
+    return c.real_transfers([t.device for t in w.local.values()])
 
 
 def _fsdp_axis(w: ShardedArray, x: ShardedArray):

@@ -206,3 +206,85 @@ def test_p2p_route_graph_safe_only_when_group_built(monkeypatch):
     assert not c.graph_safe("send", _Msg(4096), groups)
     monkeypatch.setenv("LJS_P2P", "0")
     assert not c.graph_safe("all_reduce", _Msg(4096), groups)
+
+
+def test_p2p_auto_routing_follows_distinct_gpus(monkeypatch):
+    """LJS_P2P unset ("auto"): small collectives take the peer-memory kernels exactly when every
+    group member is a distinct GPU - an RCCL job's ranks, or a single controller's groups over
+    several physical GPUs - and never for virtual devices of one GPU or a gloo / fake rehearsal."""
+    import torch.distributed as dist
+    from learning_jax_sharding_amd.comm import p2p
+    from learning_jax_sharding_amd.comm.backend import DistComm, LocalComm
+    from learning_jax_sharding_amd.comm.p2p import P2PGroup
+    monkeypatch.delenv("LJS_P2P", raising=False)
+    assert p2p.mode() == "auto" and p2p.wanted(True) and not p2p.wanted(False)
+    monkeypatch.setenv("LJS_P2P", "1")
+    assert p2p.wanted(False)
+    monkeypatch.setenv("LJS_P2P", "0")
+    assert not p2p.wanted(True)
+    monkeypatch.delenv("LJS_P2P", raising=False)
+
+    grp = object.__new__(P2PGroup)
+    grp.n, grp.cap, grp.oneshot_max = 2, 1 << 20, 256 << 10
+    groups = [(0, 1), (2, 3)]
+    for backend, fake, want in [("nccl", False, True), ("gloo", False, False), ("nccl", True, False)]:
+        c = object.__new__(DistComm)
+        c.me, c._fake, c._native, c._p2p_groups = 1, fake, None, {(0, 1): grp}
+        monkeypatch.setattr(dist, "get_backend", lambda *a, b=backend: b)
+        assert c.graph_safe("all_reduce", _Msg(4096), groups) == want or fake, (backend, fake)
+        assert c._p2p_ready("all_gather", _Msg(4096), groups) == want, (backend, fake)
+        assert c.real_transfers() == want
+
+    class _T:
+        def __init__(self, idx):
+            self.is_cuda, self.dtype, self.device = True, torch.float32, torch.device("cuda", idx)
+
+        def numel(self):
+            return 1024
+
+        def element_size(self):
+            return 4
+
+    lc = LocalComm()
+    built = []
+    monkeypatch.setattr(p2p, "P2PGroup", lambda devs, cap: built.append(devs) or grp)
+    assert lc._p2p((0, 1), {0: _T(0), 1: _T(0)}) is None               # virtual devices of one GPU
+    assert lc._p2p((0, 1), {0: _T(0), 1: _T(1)}) is grp                # two GPUs
+    assert len(built) == 1
+    assert lc.real_transfers([torch.device("cuda", 0), torch.device("cuda", 1)])
+    assert not lc.real_transfers([torch.device("cuda", 0), torch.device("cuda", 0)])
+
+
+def test_qkv_prefetch_auto_only_for_real_transfers(monkeypatch):
+    """The Q/K/V weight gather's side-stream prefetch (models/attention.py) is on by default
+    exactly when the gather crosses GPUs (LJS_QKV_PREFETCH overrides)."""
+    from learning_jax_sharding_amd.models import attention as A
+    from learning_jax_sharding_amd.comm import backend as B
+
+    class _W:
+        def __init__(self, idxs):
+            self.local = {i: type("t", (), {"device": torch.device("cuda", j)})() for i, j in enumerate(idxs)}
+
+    class _Dist:
+        kind = "dist"
+
+        def __init__(self, real):
+            self._real = real
+
+        def real_transfers(self, devices=None):
+            return self._real
+
+    monkeypatch.setattr(A, "_QKV_PREFETCH", "auto")
+    lc = B.LocalComm()
+    monkeypatch.setattr(B, "get_comm", lambda: lc)
+    assert not A.qkv_prefetch_wanted(_W([0, 0, 0, 0]))      # 4 virtual devices, one GPU
+    assert A.qkv_prefetch_wanted(_W([0, 1, 2, 3]))          # single controller over 4 GPUs
+    monkeypatch.setattr(B, "get_comm", lambda: _Dist(True))
+    assert A.qkv_prefetch_wanted(_W([0]))                   # RCCL ranks
+    monkeypatch.setattr(B, "get_comm", lambda: _Dist(False))
+    assert not A.qkv_prefetch_wanted(_W([0]))               # fake / gloo rehearsal
+    monkeypatch.setattr(A, "_QKV_PREFETCH", "1")
+    assert A.qkv_prefetch_wanted(_W([0]))
+    monkeypatch.setattr(A, "_QKV_PREFETCH", "0")
+    monkeypatch.setattr(B, "get_comm", lambda: _Dist(True))
+    assert not A.qkv_prefetch_wanted(_W([0]))
