@@ -49,6 +49,7 @@ struct PPArgs {
   int flags;              // kRelu | kBias | kBiasF32 | kSC1Out | kSlabs | kMFast | kBPtrs
   const bf16_t* bptr[4];  // flags & kBPtrs: batch b's B operand
   float* psum;            // bf16 out: per (item, wave) sum of the stored values (the fused loss sum), or null
+  bf16_t* acopy;          // AF32: the bf16 rounding of A ([M][K], dense) for the backward, or null
 };
 
 constexpr int kRelu = 1, kBias = 2, kBiasF32 = 4, kSC1Out = 32, kSlabs = 512, kMFast = 1024, kBPtrs = 4096;
@@ -93,6 +94,24 @@ __device__ __forceinline__ long piece_src(int q, int lane, long ld) {
     const int krow = KPP * q + lane / CPR, slot = lane % CPR;
     return (long)krow * ld + 8 * (slot ^ swzmn16<R>(krow));
   }
+}
+
+// f32 k-contiguous operand (AF32): rows of 64 f32 = 256 B, 1 KiB pieces of 4 rows; 16-byte chunk
+// c of row r lands at chunk c ^ (r & 15), so the 2 x ds_read_b128 of a fragment are conflict-free
+__device__ __forceinline__ long piece_src_f32(int q, int lane, long ld) {
+  const int row = 4 * q + (lane >> 4), slot = lane & 15;
+  return (long)row * ld + 4 * (slot ^ (row & 15));
+}
+// bf16 MFMA operand (8 consecutive k of row rb + lane & 15, k-step ks) from the f32 image, rounded
+// to nearest-even like cast_f32_bf16; also returns the packed bits (the backward's bf16 copy)
+__device__ __forceinline__ u32x4 frag_f32_bits(const bf16_t* lds, int rb, int ks, int lane) {
+  const int row = rb + (lane & 15);
+  const int kc = ks * 4 + (lane >> 4);
+  const unsigned char* base = reinterpret_cast<const unsigned char*>(lds) + row * 256;
+  const f32x4 lo = *reinterpret_cast<const f32x4*>(base + (((2 * kc) ^ (row & 15)) << 4));
+  const f32x4 hi = *reinterpret_cast<const f32x4*>(base + (((2 * kc + 1) ^ (row & 15)) << 4));
+  return u32x4{pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
+               pack_bf16x2(hi[2], hi[3])};
 }
 
 // 64 lanes x 16 B from rsrc + soff + voff (per lane) to LDS [lds, lds + 1 KiB); invisible to the
@@ -145,7 +164,11 @@ __device__ __forceinline__ void wait_vm() {
 // DMA pieces issued from asm) and drain the whole ring at every epilogue.
 constexpr int kBiasMax = 4096;
 
-template <int BM, int BN, bool GSN, int WVM, int NST, bool A_KC, bool B_KC, bool OUT_F32, bool BIAS = false>
+// AF32: A is f32 (k-contiguous), rounded to bf16 as the fragments are read (the activation cast
+// fused into the GEMM: the reference's f32 input under a bf16 Dense, case6_attention.py:96-99);
+// the items of tile column 0 also write A's bf16 rounding from those registers (p.acopy).
+template <int BM, int BN, bool GSN, int WVM, int NST, bool A_KC, bool B_KC, bool OUT_F32, bool BIAS = false,
+          bool AF32 = false>
 __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
   constexpr int GM = GSN ? BM : BM / 2, GN = GSN ? BN / 2 : BN;
   constexpr int WVN = 4 / WVM;
@@ -154,10 +177,13 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
   static_assert(WVM * WVN == 4 && WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
   static_assert(BM % 64 == 0 && BN % 64 == 0, "DMA pieces split evenly over 8 waves");
   static_assert(OUT_F32 || TN % 2 == 0, "bf16 output: column blocks pair up into 16-byte row chunks");
-  constexpr int A_TILE = BM * BK, B_TILE = BN * BK, STAGE = A_TILE + B_TILE;  // elements
-  constexpr int LA = BM / 64, LB = BN / 64, L = LA + LB;                     // DMA pieces per wave per K-tile
+  static_assert(!AF32 || (A_KC && !OUT_F32), "f32 A: k-contiguous, bf16 output");
+  constexpr int AES = AF32 ? 4 : 2;                                          // A element bytes
+  constexpr int A_TILE = BM * BK * AES / 2, B_TILE = BN * BK, STAGE = A_TILE + B_TILE;  // bf16 units
+  constexpr int LA = BM * AES / 128, LB = BN / 64, L = LA + LB;              // DMA pieces per wave per K-tile
   constexpr int S_EPI = OUT_F32 ? TM * TN : TM * TN / 2;                     // epilogue stores per wave
-  static_assert(L * (NST - 1) + S_EPI + 1 <= 63, "vmcnt immediate range");
+  constexpr int S_AC = AF32 ? 2 * TM : 0;                                    // acopy stores per wave per K-tile
+  static_assert(L * (NST - 1) + S_EPI + S_AC + 1 <= 63, "vmcnt immediate range");
   __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE + (BIAS ? 2 * kBiasMax : 0)];
   float* bias_lds = reinterpret_cast<float*>(smem + NST * STAGE);
 
@@ -177,13 +203,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
   const int total = my_items * nk;
 
   // ---- DMA: per-lane source offsets of this wave's pieces (A piece wave + 8 i, B likewise)
-  const long a_bytes = 2 * (A_KC ? (long)(p.M - 1) * p.lda + p.K : (long)(p.K - 1) * p.lda + p.M);
+  const long a_bytes = AES * (A_KC ? (long)(p.M - 1) * p.lda + p.K : (long)(p.K - 1) * p.lda + p.M);
   const long b_bytes = 2 * (B_KC ? (long)(p.N - 1) * p.ldb + p.K : (long)(p.K - 1) * p.ldb + p.N);
-  const int a_step = A_KC ? BK * 2 : (int)(BK * p.lda * 2);
+  const int a_step = A_KC ? BK * AES : (int)(BK * p.lda * 2);
   const int b_step = B_KC ? BK * 2 : (int)(BK * p.ldb * 2);
   int va[LA], vb[LB];
 #pragma unroll
-  for (int i = 0; i < LA; ++i) va[i] = (int)(2 * piece_src<BM, A_KC>(wave + 8 * i, lane, p.lda));
+  for (int i = 0; i < LA; ++i) {
+    if constexpr (AF32) va[i] = (int)(4 * piece_src_f32(wave + 8 * i, lane, p.lda));
+    else va[i] = (int)(2 * piece_src<BM, A_KC>(wave + 8 * i, lane, p.lda));
+  }
 #pragma unroll
   for (int i = 0; i < LB; ++i) vb[i] = (int)(2 * piece_src<BN, B_KC>(wave + 8 * i, lane, p.ldb));
 
@@ -191,11 +220,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
   u32x4 ra, rb;
   auto load_item = [&](int k) {
     const Item w = decode(p, slot + G * k, ntm, ntn);
-    ra = rsrc_u4(p.A + (long)w.b * p.sA, a_bytes);
+    ra = rsrc_u4(reinterpret_cast<const unsigned char*>(p.A) + (long)w.b * p.sA * AES, a_bytes);
     rb = rsrc_u4((p.flags & kBPtrs) ? p.bptr[w.b] : p.B + (long)w.b * p.sB, b_bytes);
     const int kt0 = w.split * nk;
     a_off = __builtin_amdgcn_readfirstlane(
-        (int)((A_KC ? (long)w.tm * BM * p.lda : (long)w.tm * BM) * 2 + (long)kt0 * a_step));
+        (int)((A_KC ? (long)w.tm * BM * p.lda : (long)w.tm * BM) * AES + (long)kt0 * a_step));
     b_off = __builtin_amdgcn_readfirstlane(
         (int)((B_KC ? (long)w.tn * BN * p.ldb : (long)w.tn * BN) * 2 + (long)kt0 * b_step));
   };
@@ -221,13 +250,32 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 fa[TM], fb[TN];
 
-  auto read_frags = [&](int st, int ks) {
+  // AF32 bf16 copy of A: written by group 0's waves of the first wave column (each A row read once
+  // per block tile) in the items of tile column 0 (each A row block once in all)
+  __amdgpu_buffer_rsrc_t rac;
+  if constexpr (AF32) rac = make_rsrc(p.acopy, p.acopy ? 2 * (long)p.M * p.K : 0);
+  const bool ac_wave = AF32 && p.acopy != nullptr && grp == 0 && wn == 0;
+  int ac_row0 = 0, ac_k0 = 0;   // the current item's first A row and K-tile (AF32 copy)
+  auto read_frags = [&](int st, int ks, bool ac) {
     const bf16_t* As = smem + st * STAGE;
     const bf16_t* Bs = As + A_TILE;
 #pragma unroll
     for (int j = 0; j < TN; ++j) fb[j] = frag<BN, B_KC>(Bs, c0w + 16 * j, ks, lane);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) fa[i] = frag<BM, A_KC>(As, r0w + 16 * i, ks, lane);
+    for (int i = 0; i < TM; ++i) {
+      if constexpr (AF32) {
+        const u32x4 bits = frag_f32_bits(As, r0w + 16 * i, ks, lane);
+        fa[i] = __builtin_bit_cast(bf16x8, bits);
+        if (ac) {
+          const int row = ac_row0 + r0w + 16 * i + (lane & 15);
+          const int k = ac_k0 + ks * 32 + (lane >> 4) * 8;
+          const int off = row < p.M ? (int)(((long)row * p.K + k) * 2) : 0x7ffffff0;
+          __builtin_amdgcn_raw_buffer_store_b128(bits, rac, off, 0, 0);
+        }
+      } else {
+        fa[i] = frag<BM, A_KC>(As, r0w + 16 * i, ks, lane);
+      }
+    }
   };
   auto mfmas = [&]() {
     __builtin_amdgcn_s_setprio(1);
@@ -345,7 +393,15 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
 
   // tile f + 1 has landed (this wave's pieces of it; counted: younger tiles' pieces and, right
   // after an epilogue, its stores may stay in flight)
-  auto wait_next = [&](bool after_epi) {
+  auto wait_next = [&](bool after_epi, bool ac) {
+    if constexpr (AF32) {
+      if (ac) {   // this tile's bf16 copy stores (both k-steps) are younger than the next tile's pieces
+        if (after_epi && psum_on) wait_vm<L * (NST - 2) + S_EPI + 1 + S_AC>();
+        else if (after_epi) wait_vm<L * (NST - 2) + S_EPI + S_AC>();
+        else wait_vm<L * (NST - 2) + S_AC>();
+        return;
+      }
+    }
     if (after_epi && psum_on) wait_vm<L * (NST - 2) + S_EPI + 1>();
     else if (after_epi) wait_vm<L * (NST - 2) + S_EPI>();
     else wait_vm<L * (NST - 2)>();
@@ -378,27 +434,41 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
       if (f + NST - 1 < total) issue_next((f + NST - 1) % NST);
       const bool epi = kk == 0 && it > 0;
       if (epi) epilogue(it - 1);
-      read_frags(st, 0);
+      bool ac = false;
+      if constexpr (AF32) {
+        if (ac_wave) {
+          if (kk == 0) {
+            const Item w = decode(p, slot + G * it, ntm, ntn);
+            ac_row0 = w.tn == 0 && w.b == 0 ? w.tm * BM : -1;
+            ac_k0 = w.split * nk * BK;
+          }
+          ac = ac_row0 >= 0;
+        }
+      }
+      read_frags(st, 0, ac);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       bar();
       // M(f, 0)
       mfmas();
       bar();
       // R(f, 1)
-      read_frags(st, 1);
+      read_frags(st, 1, ac);
+      if constexpr (AF32) {
+        if (ac) ac_k0 += BK;   // the copy's next K-tile
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const bool more = f + 1 < total;
       if (grp == 1 && more) {
         // the tail: fewer younger tiles in flight than NST - 2
         if (f + NST - 1 >= total) wait_vm<0>();
-        else wait_next(epi);
+        else wait_next(epi, ac);
       }
       bar();
       // M(f, 1)
       mfmas();
       if (grp == 0 && more) {
         if (f + NST - 1 >= total) wait_vm<0>();
-        else wait_next(epi);
+        else wait_next(epi, ac);
       }
       bar();
     }
@@ -413,6 +483,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
 LJS_PP_INST(128, 384, true, 2, 2, true, true, false)   // QKV projection  [T x 640] x [640 x 1536]
 LJS_PP_INST(128, 320, true, 4, 2, true, true, false)   // out-projection  [T x 512] x [512 x 640]
 template __global__ void gemm_pp_kernel<128, 320, true, 4, 2, true, true, false, true>(PPArgs);
+// f32 A (the activation cast fused in): QKV projection of the reference's f32 input, 160 KiB LDS
+template __global__ void gemm_pp_kernel<128, 384, true, 2, 2, true, true, false, false, true>(PPArgs);
 LJS_PP_INST(128, 256, true, 2, 3, true, true, false)   // dh              [T x 640] x [640 x 512]
 LJS_PP_INST(128, 256, true, 2, 2, true, true, false)
 LJS_PP_INST(256, 256, false, 1, 2, true, true, false)  // 4096-class GEMMs
@@ -424,7 +496,8 @@ LJS_PP_INST(128, 128, true, 4, 3, false, false, true)
 
 int g_cus = 0;
 
-template <int BM, int BN, bool GSN, int WVM, int NST, bool AK, bool BKc, bool OF, bool BIAS = false>
+template <int BM, int BN, bool GSN, int WVM, int NST, bool AK, bool BKc, bool OF, bool BIAS = false,
+          bool AF32 = false>
 hipError_t launch(PPArgs a, hipStream_t s) {
   if (!g_cus) {
     int dev = 0;
@@ -437,7 +510,7 @@ hipError_t launch(PPArgs a, hipStream_t s) {
   if (ntm < ntn) a.flags |= kMFast;
   const int grid = items < g_cus ? items : g_cus;
   if (grid <= 0) return hipSuccess;
-  hipLaunchKernelGGL((gemm_pp_kernel<BM, BN, GSN, WVM, NST, AK, BKc, OF, BIAS>), dim3(grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((gemm_pp_kernel<BM, BN, GSN, WVM, NST, AK, BKc, OF, BIAS, AF32>), dim3(grid), dim3(512), 0, s, a);
   return hipGetLastError();
 }
 
@@ -450,8 +523,17 @@ hipError_t launch(PPArgs a, hipStream_t s) {
 // divides the K-tiles unless slab mode, operand extents < 2^31 bytes, 16-byte aligned bases.
 LJS_API int ljs_gemm_pp(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, long lda,
                         long ldb, long ldc, long sA, long sB, long sC, long sBias, int batch, int flags, float alpha,
-                        int splitk, int cfg, void* psum, int* psum_count, hipStream_t stream) {
+                        int splitk, int cfg, void* psum, int* psum_count, void* acopy, hipStream_t stream) {
   if (psum_count) *psum_count = 0;
+  const bool af32 = cfg == 21;   // f32 A: the QKV configuration with the cast fused in
+  if (af32) {
+    if (lda % 4 || (((uintptr_t)A) & 15) || batch != 1 || (flags & (kBias | kSlabs | kBPtrs)) || splitk > 1 ||
+        (long)M * lda * 4 >= (1L << 31))
+      return (int)hipErrorInvalidValue;
+    cfg = 1;
+  } else if (acopy) {
+    return (int)hipErrorInvalidValue;
+  }
   const bool kc = cfg < 10;
   const bool out_f32 = !kc;
   if (K % BK || N % 8 || lda % 8 || ldb % 8 || batch < 1) return (int)hipErrorInvalidValue;
@@ -470,6 +552,7 @@ LJS_API int ljs_gemm_pp(const void* A, const void* B, void* C, const void* bias,
   a.alpha = alpha;
   a.flags = flags & ~kMFast;
   a.psum = out_f32 ? nullptr : (float*)psum;
+  a.acopy = (bf16_t*)acopy;
   if (flags & kBPtrs) {
     if (batch > 4 || !(flags & kSlabs)) return (int)hipErrorInvalidValue;
     const void* const* bp = (const void* const*)B;
@@ -489,7 +572,9 @@ LJS_API int ljs_gemm_pp(const void* A, const void* B, void* C, const void* bias,
   if (!slabs && a.splitk > 1) return (int)hipErrorInvalidValue;  // no atomics here: slabs only
   const long k_ext = slabs ? (long)a.splitk * a.kt_per_split * BK : K;
   const long ea = kc ? (long)M * lda : k_ext * lda, eb = kc ? (long)N * ldb : k_ext * ldb;
-  if (2 * (ea + (long)(batch - 1) * sA) >= (1L << 31) || 2 * eb >= (1L << 31)) return (int)hipErrorInvalidValue;
+  if ((af32 ? 4 : 2) * (ea + (long)(batch - 1) * sA) >= (1L << 31) || 2 * eb >= (1L << 31))
+    return (int)hipErrorInvalidValue;
+  if (af32) return (int)launch<128, 384, true, 2, 2, true, true, false, false, true>(a, stream);
   if (!(flags & kBPtrs) && 2 * (eb + (long)(batch - 1) * sB) >= (1L << 31)) return (int)hipErrorInvalidValue;
   if (a.psum && psum_count) {
     // one partial per (item, wave): items of the configuration's tile

@@ -35,7 +35,7 @@ _SIGS = {
                       ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p, c_void_p],
     "ljs_gemm_pp": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
                     c_long, c_long, c_long, c_int, c_int, c_float, c_int, c_int, c_void_p, ctypes.POINTER(c_int),
-                    c_void_p],
+                    c_void_p, c_void_p],
     "ljs_sum_partials": [c_void_p, c_int, c_void_p, c_int, c_void_p],
     "ljs_mse_colsum_ws_bytes": [c_int, c_int],
     "ljs_gemm_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long,
@@ -249,7 +249,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
                          zero_c, psum, res, acopy, slabs, sA, sB, sC, ldb)
     if tile >= _PP_BASE:
         rc, cnt = _gemm_pp(A, B, C, M, N, K, lda, ldb, ldc, a_kc, b_kc, batch, sA, sB, sC, bias, sBias, relu, alpha,
-                           splitk, tile - _PP_BASE, a_off, b_off, c_off, slabs, b_list, psum)
+                           splitk, tile - _PP_BASE, a_off, b_off, c_off, slabs, b_list, psum, acopy)
         if rc == 0:
             return cnt
         tile = None   # a shape / option the ping-pong kernel does not take: the LDS-DMA kernels
@@ -283,13 +283,15 @@ _PP_BASE = 30000   # tile codes >= _PP_BASE: the ping-pong kernel (csrc/kernels/
 
 
 def _gemm_pp(A, B, C, M, N, K, lda, ldb, ldc, a_kc, b_kc, batch, sA, sB, sC, bias, sBias, relu, alpha, splitk,
-             cfg, a_off, b_off, c_off, slabs, b_list, psum=None):
+             cfg, a_off, b_off, c_off, slabs, b_list, psum=None, acopy=None):
     """Launch the ping-pong GEMM; returns (HIP status, fused-sum partials written); a non-zero
-    status means the configuration was not taken (nothing launched)."""
-    if A.dtype != torch.bfloat16 or (cfg < 10) != (a_kc and b_kc and C.dtype == torch.bfloat16) or \
-            (cfg >= 10 and (a_kc or b_kc or C.dtype != torch.float32)):
+    status means the configuration was not taken (nothing launched).  cfg 21: f32 A (rounded in
+    the GEMM; ``acopy`` receives its bf16 copy)."""
+    kc_cfg = cfg < 10 or cfg == 21
+    if (A.dtype == torch.float32) != (cfg == 21) or kc_cfg != (a_kc and b_kc and C.dtype == torch.bfloat16) or \
+            (not kc_cfg and (a_kc or b_kc or C.dtype != torch.float32)) or (acopy is not None and cfg != 21):
         return -1, 0
-    if batch > 1 and cfg < 10 and sA == 0 and sB == N * ldb and sC == N and bias is None and ldc == batch * N:
+    if batch > 1 and kc_cfg and sA == 0 and sB == N * ldb and sC == N and bias is None and ldc == batch * N:
         # a batch of projections of ONE activation into interleaved column blocks (the fused
         # QKV): one GEMM against the stacked [batch * N][K] weights
         N, batch, sB, sC = N * batch, 1, 0, 0
@@ -307,7 +309,7 @@ def _gemm_pp(A, B, C, M, N, K, lda, ldb, ldc, a_kc, b_kc, batch, sA, sB, sC, bia
     rc = lib().ljs_gemm_pp(ctypes.c_void_p(A.data_ptr() + a_off * eA), b_arg,
                            ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb, ldc,
                            sA, sB, sC, sBias, batch, flags, alpha, splitk, cfg, _p(psum), ctypes.byref(cnt),
-                           _stream(C))
+                           _p(acopy), _stream(C))
     if rc == 0 and (_DEBUG_SYNC or os.environ.get("LJS_DEBUG_SYNC") == "1"):
         _ck(0, "ljs_gemm_pp")
     return rc, cnt.value
@@ -364,8 +366,16 @@ _GEMM_PP = os.environ.get("LJS_GEMM_PP", "1") == "1"
 def _pick_pp(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc, a_dtype, bias, sBias, relu, accumulate, zero_c,
              psum, res, acopy, slabs, sA, sB, sC, ldb) -> Optional[int]:
     """A ping-pong configuration for this GEMM, or None (csrc/kernels/gemm_pp.hip)."""
-    if not _GEMM_PP or a_dtype != torch.bfloat16 or accumulate or zero_c or res is not None \
-            or acopy is not None or K % 64:
+    if not _GEMM_PP or a_dtype not in (torch.bfloat16, torch.float32) or accumulate or zero_c or res is not None \
+            or K % 64 or (acopy is not None and a_dtype != torch.float32):
+        return None
+    if a_dtype == torch.float32:
+        # the activation cast fused in (cfg 21): the QKV projection shape, whole rounds of 128x384
+        Nf = N * batch
+        if (a_kc and b_kc and not out_f32 and splitk <= 1 and bias is None and not relu and psum is None
+                and (batch == 1 or (sA == 0 and sB == N * ldb and sC == N and ldc == Nf))
+                and Nf % 384 == 0 and (-(-M // 128) * (Nf // 384)) % _cus() == 0 and 4 * M * K < (1 << 31)):
+            return _PP_BASE + 21
         return None
     if a_kc and b_kc and not out_f32 and splitk <= 1 and N % 8 == 0 and ldc % 8 == 0:
         Nf = N

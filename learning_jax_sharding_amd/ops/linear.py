@@ -387,10 +387,16 @@ class _Linear(torch.autograd.Function):
         wmajor = nw > 1 and order[0] != 0
         # f32 activations (the reference's f32 input under a bf16 Dense): the GEMM rounds them as
         # it reads them and writes the bf16 copy the backward needs -- no separate cast pass
-        cast_on_load = (_CAST_ON_LOAD and not swap and not wmajor and x2.is_cuda and x2.dtype == torch.float32
+        cast_on_load = (not swap and not wmajor and x2.is_cuda and x2.dtype == torch.float32
                         and x2.is_contiguous() and res is None and b is None and not relu and K % 64 == 0
                         and N % 8 == 0 and out_dtype == torch.bfloat16 and x2.data_ptr() % 16 == 0
                         and M * nw * N >= (1 << 20))
+        # the ping-pong kernel's f32-A configuration (csrc/kernels/gemm_pp.hip AF32) converts the
+        # fragments in registers and writes the bf16 copy from them: on wherever it applies; the
+        # LDS-DMA kernel's f32 path stays opt-in (LJS_CAST_ON_LOAD=1, measured slower)
+        cast_on_load = cast_on_load and (_CAST_ON_LOAD or hip._pick_pp(
+            M, N, K, nw, True, True, False, 1, nw * N, torch.float32, None, 0, False, False, False, None, None,
+            x2, False, 0, N * K, N, K) is not None)
         if swap:   # batch-major x -> seq-major bf16 rows, rounded in the same pass
             xb = hip.swap01_bf16(x.contiguous()).view(M, K)
         else:

@@ -39,6 +39,18 @@ def cases():
                                 sC=512, tile=tile)
     out["qkv"] = (qkv_fn, [PP + 1, 2561], 2 * T * 640 * 1536)
 
+    x32 = torch.randn(T, 640, device=dev)
+    xb = torch.empty(T, 640, device=dev).bfloat16()
+
+    def qkv32_fn(tile):
+        if tile == "cast":   # the separate cast pass + the bf16 ping-pong GEMM
+            return lambda: (hip.cast_into(x32, xb) if hasattr(hip, "cast_into") else xb.copy_(x32),
+                            hip.gemm(xb, wqkv, qkv, T, 512, 640, 640, 640, 1536, True, True, batch=3, sA=0,
+                                     sB=512 * 640, sC=512, tile=PP + 1))
+        return lambda: hip.gemm(x32, wqkv, qkv, T, 512, 640, 640, 640, 1536, True, True, batch=3, sA=0,
+                                sB=512 * 640, sC=512, acopy=xb, tile=tile)
+    out["qkv32"] = (qkv32_fn, [PP + 21, "cast"], 2 * T * 640 * 1536)
+
     h = torch.randn(T, 512, device=dev).bfloat16()
     wo = torch.randn(640, 512, device=dev).bfloat16()
     bo = torch.randn(640, device=dev)
@@ -78,7 +90,7 @@ def cases():
 
 
 def main():
-    want = sys.argv[1:] or ["qkv", "out", "dh", "dwqkv", "dwo"]
+    want = sys.argv[1:] or ["qkv", "qkv32", "out", "dh", "dwqkv", "dwo"]
     cs = cases()
     for name in want:
         mk, tiles, flops = cs[name]

@@ -114,3 +114,21 @@ def test_pp_weight_grad_bptrs(hip):
     for i in range(3):
         ref = X.float().t() @ dys[i].float()
         torch.testing.assert_close(slabs[:, i].sum(0), ref, rtol=1e-3, atol=1e-3 * math.sqrt(T))
+
+
+@pytest.mark.parametrize("M", [1024, 296])
+def test_pp_f32_a_cast_fused_and_copy(hip, M):
+    """f32 A rounded to bf16 inside the GEMM (cfg 21): bit for bit the GEMM of the cast operand,
+    and the bf16 copy written for the backward equals the cast."""
+    N, K = 512, 640
+    x = _rand(M, K, seed=12, dtype=torch.float32)
+    wt = _rand(3, N, K, seed=13)
+    out = torch.full((M, 3 * N), float("nan"), dtype=torch.bfloat16, device=dev)
+    xb = torch.full((M, K), float("nan"), dtype=torch.bfloat16, device=dev)
+    hip.gemm(x, wt, out, M, N, K, K, K, 3 * N, True, True, batch=3, sA=0, sB=N * K, sC=N, acopy=xb,
+             tile=hip._PP_BASE + 21)
+    ref = torch.full((M, 3 * N), float("nan"), dtype=torch.bfloat16, device=dev)
+    hip.gemm(x.bfloat16(), wt, ref, M, N, K, K, K, 3 * N, True, True, batch=3, sA=0, sB=N * K, sC=N, tile=1282)
+    torch.cuda.synchronize()
+    assert torch.equal(xb, x.bfloat16())
+    assert torch.equal(out, ref)
