@@ -798,6 +798,32 @@ __global__ void rng_kernel(T* __restrict__ out, RngRegion reg, long n, unsigned 
   }
 }
 
+// Dropout with a counter-based mask (no mask stored): element i of the shard is kept iff the
+// Philox uniform of its GLOBAL index is < keep (the draw of random.uniform for that index, so the
+// mask is mesh-invariant and equal to the host path's), kept values divided by keep.  The
+// backward is the same kernel on dY (the mask is recomputed from the key).
+template <typename T>
+__global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, RngRegion reg, long n, unsigned k0,
+                               unsigned k1, float keep) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    long rem = i, gidx = 0;
+    for (int d = reg.ndim - 1; d >= 0; --d) {
+      const long li = rem % reg.size[d];
+      rem /= reg.size[d];
+      gidx += (reg.start[d] + li) * reg.gstride[d];
+    }
+    unsigned c0 = (unsigned)gidx, c1 = (unsigned)(gidx >> 32), c2 = 0, c3 = 0;
+    philox10(c0, c1, c2, c3, k0, k1);
+    const float u = (float)u01(c0);
+    if constexpr (sizeof(T) == 4) {
+      y[i] = u < keep ? x[i] / keep : 0.f;
+    } else {
+      y[i] = u < keep ? f2bf(bf2f(x[i]) / keep) : (bf16_t)0;
+    }
+  }
+}
 
 // out[s][b][k] = bf16(in[b][s][k]) for a [B][S][K] f32 or bf16 array (K % 8 == 0): the activations'
 // (batch, seq) storage order swapped to seq-major while they are rounded to bf16, so a sequence-
@@ -1233,6 +1259,30 @@ LJS_API int ljs_rng_fill(void* out, int is_bf16, int ndim, const long* start, co
   else
     hipLaunchKernelGGL(rng_kernel<float>, dim3(g), dim3(256), 0, s, (float*)out, reg, n, k0, k1, dist, lo, hi, erf_a,
                        erf_b);
+  return (int)hipGetLastError();
+}
+
+// y = dropout(x) of one shard (see dropout_kernel); x, y contiguous f32 (is_bf16 = 0) or bf16
+LJS_API int ljs_dropout(const void* x, void* y, int is_bf16, int ndim, const long* start, const long* size,
+                        const long* gstride, unsigned k0, unsigned k1, float keep, hipStream_t s) {
+  if (ndim < 1 || ndim > 8 || !(keep > 0.f)) return (int)hipErrorInvalidValue;
+  RngRegion reg;
+  long n = 1;
+  reg.ndim = ndim;
+  for (int d = 0; d < ndim; ++d) {
+    reg.start[d] = start[d];
+    reg.size[d] = size[d];
+    reg.gstride[d] = gstride[d];
+    n *= size[d];
+  }
+  if (n == 0) return 0;
+  const int g = grid_for(n, 256 * 4);
+  if (is_bf16)
+    hipLaunchKernelGGL(dropout_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, reg, n, k0,
+                       k1, keep);
+  else
+    hipLaunchKernelGGL(dropout_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)x, (float*)y, reg, n, k0, k1,
+                       keep);
   return (int)hipGetLastError();
 }
 

@@ -67,7 +67,9 @@ DenseGeneral = Dense
 
 
 class Dropout(Module):
-    """``nn.Dropout`` (``case6_attention.py:91,143``): identity when deterministic or rate 0."""
+    """``nn.Dropout`` (``case6_attention.py:91,143``): identity when deterministic or rate 0; else
+    keep-mask from the Philox uniform of each element's global index (mesh-invariant), kept values
+    divided by the keep probability - one fused HIP kernel per shard on GPU (``hip.dropout``)."""
 
     rate: float = 0.0
     deterministic: Optional[bool] = None
@@ -79,6 +81,14 @@ class Dropout(Module):
         from .. import random as _random
         k = rng if rng is not None else self.make_rng("dropout")
         keep = 1.0 - self.rate
+        if x.local and all(t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) for t in x.local.values()):
+            # one fused HIP pass per shard: the Philox uniform of each element's global index (the
+            # draw of random.uniform below, bit for bit), compare, scale; the backward recomputes
+            # the mask from the key instead of storing it
+            from ..ops import hip
+            loc = {d: hip.dropout(t, x.shape, x.tile.region(d, x.shape), k.k0, k.k1, keep)
+                   for d, t in x.local.items()}
+            return ShardedArray(x.shape, x.dtype, x.sharding, loc)
         u = _random.uniform(k, x.shape, torch.float32, sharding=x.sharding)
         scaled = core.binary("div", x, keep)
         return core.where(_lt(u, keep), scaled, 0.0)

@@ -72,6 +72,7 @@ _SIGS = {
                        c_void_p],
     "ljs_rng_fill": [c_void_p, c_int, c_int, _LP, _LP, _LP, c_uint, c_uint, c_int, c_float, c_float, c_float,
                      c_float, c_void_p],
+    "ljs_dropout": [c_void_p, c_void_p, c_int, c_int, _LP, _LP, _LP, c_uint, c_uint, c_float, c_void_p],
 }
 
 
@@ -1605,3 +1606,40 @@ def rng_fill(shape, region, k0, k1, dist, lo, hi, dtype, device) -> torch.Tensor
                                 eb, torch.cuda.current_stream(device).cuda_stream)
         _ck(rc, "ljs_rng_fill")
     return out if od == dtype else out.to(dtype)
+
+
+# ============================================================================ dropout
+def _dropout_raw(x: torch.Tensor, shape, region, k0: int, k1: int, keep: float) -> torch.Tensor:
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    nd = len(shape)
+    strides = [1] * nd
+    for i in range(nd - 2, -1, -1):
+        strides[i] = strides[i + 1] * shape[i + 1]
+    rc = lib().ljs_dropout(_p(x), _p(y), int(x.dtype == torch.bfloat16), nd, _longs([r[0] for r in region]),
+                           _longs([r1 - r0 for r0, r1 in region]), _longs(strides), k0, k1, keep, _stream(x))
+    _ck(rc, "ljs_dropout")
+    return y
+
+
+class _Dropout(torch.autograd.Function):
+    """Counter-based dropout of one shard (csrc/kernels/elementwise.hip dropout_kernel): the
+    backward recomputes the mask from the key, nothing is stored."""
+
+    @staticmethod
+    def forward(ctx, x, meta):
+        shape, region, k0, k1, keep = meta
+        ctx.meta = meta
+        return _dropout_raw(x, shape, region, k0, k1, keep)
+
+    @staticmethod
+    def backward(ctx, dy):
+        shape, region, k0, k1, keep = ctx.meta
+        return _dropout_raw(dy, shape, region, k0, k1, keep), None
+
+
+def dropout(x: torch.Tensor, shape, region, k0: int, k1: int, keep: float) -> torch.Tensor:
+    """Dropout of the shard ``x`` (region ``region`` of a global array of ``shape``), f32 / bf16."""
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        raise NotImplementedError(f"dropout kernel: f32 / bf16 only, got {x.dtype}")
+    return _Dropout.apply(x, (tuple(shape), tuple(region), int(k0), int(k1), float(keep)))

@@ -1058,3 +1058,27 @@ def test_slab_gemm_staged_epilogue_bit_exact(hip, T, K, N, tile, S):
     assert torch.equal(outs[0], outs[1])
     ref = (x.float().t() @ dy.float())
     torch.testing.assert_close(outs[0].sum(0), ref, rtol=2e-2, atol=2e-1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_dropout_kernel_matches_host_philox_mask(hip, dtype):
+    """The HIP dropout keeps element i iff the Philox uniform of its GLOBAL index is < keep (the
+    host path's random.uniform draw, bit for bit); a shard's region selects its indices; the
+    backward recomputes the same mask."""
+    from learning_jax_sharding_amd import random as R
+    shape = (4, 64, 96)
+    key = R.PRNGKey(3)
+    keep = 0.7
+    full = torch.randn(shape).to(dtype)
+    idx = np.arange(int(np.prod(shape)), dtype=np.uint64)
+    u = torch.from_numpy(R._dist_np(idx, key, "uniform", 0.0, 1.0).astype(np.float32)).view(shape)
+    ref = torch.where(u < keep, (full.float() / keep).to(dtype), torch.zeros((), dtype=dtype))
+    region = ((1, 3), (16, 48), (0, 96))
+    sl = tuple(slice(a, b) for a, b in region)
+    x = full[sl].contiguous().to(dev).requires_grad_()
+    y = hip.dropout(x, shape, region, key.k0, key.k1, keep)
+    y.backward(torch.ones_like(y))
+    torch.cuda.synchronize()
+    assert torch.equal(y.detach().cpu(), ref[sl])
+    gref = torch.where(u[sl] < keep, (torch.ones((), dtype=dtype).float() / keep).to(dtype), torch.zeros((), dtype=dtype))
+    assert torch.equal(x.grad.cpu(), gref)
