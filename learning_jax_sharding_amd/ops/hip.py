@@ -379,23 +379,22 @@ def _pick_pp(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc, a_dtype, bias, sB
             return _PP_BASE + 21
         return None
     if a_kc and b_kc and not out_f32 and splitk <= 1 and N % 8 == 0 and ldc % 8 == 0:
-        Nf = N
-        if batch > 1:
-            if not (sA == 0 and sB == N * ldb and sC == N and bias is None and ldc == batch * N):
-                return None
-            Nf = N * batch
+        Nf, nb = N, batch
+        if batch > 1 and sA == 0 and sB == N * ldb and sC == N and bias is None and ldc == batch * N:
+            Nf, nb = N * batch, 1          # interleaved column blocks: folded into one GEMM
         cus = _cus()
-        if bias is not None and (sBias != 0 or Nf > 4096):
+        if bias is not None and (sBias != 0 or Nf > 4096 or nb > 1):
             return None
+        rows = -(-M // 128) * nb
         # whole rounds of 256 blocks: [T][1536] at 128x384 (2 rounds at T = 16384), [T][640] at
-        # 128x320, [T][512] at 128x256
+        # 128x320, [T][512] at 128x256 (a weight-major batch of 3: 3 rounds)
         if bias is not None:
-            return _PP_BASE + 2 if Nf % 320 == 0 and (-(-M // 128) * (Nf // 320)) % cus == 0 else None
-        if Nf % 384 == 0 and (-(-M // 128) * (Nf // 384)) % cus == 0:
+            return _PP_BASE + 2 if Nf % 320 == 0 and (rows * (Nf // 320)) % cus == 0 else None
+        if Nf % 384 == 0 and (rows * (Nf // 384)) % cus == 0:
             return _PP_BASE + 1
-        if Nf % 320 == 0 and (-(-M // 128) * (Nf // 320)) % cus == 0:
+        if Nf % 320 == 0 and (rows * (Nf // 320)) % cus == 0:
             return _PP_BASE + 2
-        if Nf % 256 == 0 and (-(-M // 128) * (Nf // 256)) % cus == 0:
+        if Nf % 256 == 0 and (rows * (Nf // 256)) % cus == 0:
             return _PP_BASE + 3
         return None
     return None

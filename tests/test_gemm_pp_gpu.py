@@ -132,3 +132,17 @@ def test_pp_f32_a_cast_fused_and_copy(hip, M):
     torch.cuda.synchronize()
     assert torch.equal(xb, x.bfloat16())
     assert torch.equal(out, ref)
+
+
+def test_pp_weight_major_batch(hip):
+    """A batch of projections into separate [M][N] outputs (the seq-major fused QKV of the 2-D
+    layout): one launch over (batch, tiles)."""
+    M, N, K = 640, 512, 640
+    x = _rand(M, K, seed=14)
+    wt = _rand(3, N, K, seed=15)
+    out = torch.full((3, M, N), float("nan"), dtype=torch.bfloat16, device=dev)
+    hip.gemm(x, wt, out, M, N, K, K, K, N, True, True, batch=3, sA=0, sB=N * K, sC=M * N, tile=hip._PP_BASE + 3)
+    out0 = torch.full((3, M, N), float("nan"), dtype=torch.bfloat16, device=dev)
+    hip.gemm(x, wt, out0, M, N, K, K, K, N, True, True, batch=3, sA=0, sB=N * K, sC=M * N, tile=1282)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out0)
