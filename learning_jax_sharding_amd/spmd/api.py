@@ -106,6 +106,7 @@ class Jitted:
         self._calls: Dict[Any, int] = {}
         self._graphs: Dict[Any, _Captured] = {}
         self._fast = None   # (args of the last replay, its capture, its input copies)
+        self._md_failed = set()   # signatures whose multi-GPU capture failed (run eagerly)
         self.__wrapped__ = fun
 
     # ------------------------------------------------------------------ helpers
@@ -185,7 +186,8 @@ class Jitted:
             return cap.out_tree
         dyn, static = self._split(args)
         sig = self._signature(dyn, static)
-        if not self.capture or kwargs or not torch.cuda.is_available() or _spans_gpus():
+        if not self.capture or kwargs or not torch.cuda.is_available() or (
+                _spans_gpus() and (not _MULTI_GPU_CAPTURE or sig in self._md_failed)):
             # Python side effects (print) run once per signature, as at JAX trace time
             n = self._calls.get(sig, 0)
             self._calls[sig] = n + 1
@@ -226,12 +228,26 @@ class Jitted:
                     return y
                 return x
             full[i] = T.tree_map(cp, a, is_leaf=_leaf_is_array)
-        # one HIP graph per stretch between cross-process collectives (spmd/graphs.py)
-        from .graphs import SegmentedGraph
-        g = SegmentedGraph()
         # lazy outputs (an unread loss, uncombined weight gradients) are forced INSIDE the
         # capture: a thunk run after it would be eager, cached, and stale on every later replay
-        out = g.capture(lambda: _force_lazy(self._run(tuple(full), {})[0]))
+        if _spans_gpus():
+            # single controller over several GPUs: ONE graph with a branch per device
+            from .graphs import MultiDeviceGraph
+            g = MultiDeviceGraph(_gpu_indices())
+            try:
+                out = g.capture(lambda: _force_lazy(self._run(tuple(full), {})[0]))
+            except Exception as e:   # (e.g. a runtime without multi-device graphs) -> eager
+                import warnings
+                warnings.warn(f"multi-GPU graph capture failed ({e!r}); running this step eagerly")
+                g.release()
+                self._md_failed.add(sig)
+                torch.cuda.synchronize()
+                return self._run(args, {})[0]
+        else:
+            # one HIP graph per stretch between cross-process collectives (spmd/graphs.py)
+            from .graphs import SegmentedGraph
+            g = SegmentedGraph()
+            out = g.capture(lambda: _force_lazy(self._run(tuple(full), {})[0]))
         cap = _Captured(g, in_leaves, out, aliased)
         self._graphs[sig] = cap
         return self._replay(cap, args, sig)
@@ -343,12 +359,22 @@ def _multi_process() -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
-def _spans_gpus() -> bool:
-    """Single-controller run over several physical GPUs: one HIP graph captures one device's
-    stream only, so such a step runs eagerly (its collectives are grouped RCCL calls across the
-    GPUs, comm/native.py).  One process per GPU (torchrun) captures each rank's step."""
+def _gpu_indices() -> List[int]:
     from ..runtime.devices import local_devices
-    return len({d.torch_device.index for d in local_devices() if d.platform == "gpu"}) > 1
+    return sorted({d.torch_device.index for d in local_devices() if d.platform == "gpu"})
+
+
+def _spans_gpus() -> bool:
+    """Single-controller run over several physical GPUs: captured as ONE multi-device graph
+    (spmd/graphs.py MultiDeviceGraph; its collectives are the grouped single-controller RCCL
+    calls of comm/native.py, graph nodes on every device's branch).  One process per GPU
+    (torchrun) captures each rank's step as usual."""
+    return len(_gpu_indices()) > 1
+
+
+# LJS_MULTI_GPU_CAPTURE=0: single-controller multi-GPU steps run eagerly (the capture falls back
+# to eager by itself if the runtime refuses it)
+_MULTI_GPU_CAPTURE = os.environ.get("LJS_MULTI_GPU_CAPTURE", "1") == "1"
 
 
 _SEEDS: Dict[Tuple, torch.Tensor] = {}

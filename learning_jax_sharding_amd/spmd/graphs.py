@@ -30,7 +30,7 @@ from typing import Any, Callable, Dict, List, Optional
 
 import torch
 
-__all__ = ["SegmentedGraph", "current", "run_collective", "join"]
+__all__ = ["SegmentedGraph", "MultiDeviceGraph", "current", "run_collective", "join"]
 
 # process-wide (one capture at a time)
 _ACTIVE: List[Optional["SegmentedGraph"]] = [None]
@@ -221,3 +221,142 @@ def _side_stream() -> torch.cuda.Stream:
     if s is None:
         s = _SIDE[d] = torch.cuda.Stream()
     return s
+
+
+# ============================================================================ single controller, N GPUs
+class _TorchMD:
+    """The torch / HIP calls of a multi-device capture (a test double replaces them)."""
+
+    def synchronize(self, devs):
+        for d in devs:
+            torch.cuda.synchronize(d)
+
+    def new_stream(self, d):
+        return torch.cuda.Stream(device=d)
+
+    def current_stream(self, d):
+        return torch.cuda.current_stream(d)
+
+    def new_graph(self):
+        return torch.cuda.CUDAGraph()
+
+    def pool(self):
+        return torch.cuda.graph_pool_handle()
+
+    def device(self, d):
+        return torch.cuda.device(d)
+
+    def stream(self, s):
+        return torch.cuda.stream(s)
+
+    def event(self):
+        return torch.cuda.Event()
+
+    def begin_pool(self, d, pool):
+        # every allocation on device d until end_pool comes from the graph's private pool there
+        # (the capturing device's pool is routed by capture_begin itself)
+        torch._C._cuda_beginAllocateToPool(d, pool)
+
+    def end_pool(self, d, pool):
+        torch._C._cuda_endAllocateToPool(d, pool)
+
+    def release_pool(self, d, pool):
+        torch._C._cuda_releasePool(d, pool)
+
+
+class MultiDeviceGraph:
+    """ONE hipGraph of a single-controller step over several physical GPUs (the reference's own
+    execution model: one process, N devices, ``case6_attention.py:4-5,219-220``).
+
+    The capture begins on the first device's capture stream; every other device's capture stream
+    joins it through an event wait (a fork inside the capture), so the work the step issues on
+    each device's current stream - kernels, the grouped single-controller RCCL calls of
+    ``comm/native.py``, the peer-memory collectives' cross-device event waits - becomes nodes of
+    the same graph, with the cross-device orders as graph edges.  Each device's allocations go
+    to a private pool for the graph's lifetime (the capturing device's through ``capture_begin``,
+    the others' through the allocator's pool routing).  The other devices join back before the
+    capture ends.  Replay is one graph launch."""
+
+    def __init__(self, devices, backend=None):
+        self.devices = sorted(set(int(d) for d in devices))
+        self.be = backend or _TorchMD()
+        self.graph = None
+        self.pools: Dict[int, Any] = {}
+        self.items: List[tuple] = []
+        self.n_collectives = 0
+
+    def capture(self, fn: Callable[[], Any]):
+        import contextlib
+        be, devs = self.be, self.devices
+        d0, others = devs[0], devs[1:]
+        be.synchronize(devs)
+        streams = {d: be.new_stream(d) for d in devs}
+        for d in devs:
+            streams[d].wait_stream(be.current_stream(d))
+        g = be.new_graph()
+        prev = current()
+        began = []
+        with contextlib.ExitStack() as cx:
+            for d in devs:
+                cx.enter_context(be.stream(streams[d]))   # each device's current stream: its capture stream
+            with be.device(d0):
+                g.capture_begin(pool=be.pool(), capture_error_mode="relaxed")
+            try:
+                fork = be.event()
+                with be.device(d0):
+                    fork.record(streams[d0])
+                for d in others:
+                    with be.device(d):
+                        streams[d].wait_event(fork)       # joins the capture
+                        pool = be.pool()
+                        be.begin_pool(d, pool)
+                        self.pools[d] = pool
+                        began.append(d)
+                _ACTIVE[0] = self    # (single-threaded backward; collectives are graph nodes, no cuts)
+                out = fn()
+                for d in others:
+                    with be.device(d):
+                        ev = be.event()
+                        ev.record(streams[d])
+                    streams[d0].wait_event(ev)            # join back before the capture ends
+            finally:
+                _ACTIVE[0] = prev
+                for d in began:
+                    be.end_pool(d, self.pools[d])
+                with be.device(d0):
+                    g.capture_end()
+        for d in devs:
+            be.current_stream(d).wait_stream(streams[d])
+        be.synchronize(devs)
+        self.graph = g
+        self.items = [("graph", g)]
+        return out
+
+    # the SegmentedGraph interface of run_collective / join: nothing is cut here - a collective is
+    # issued on the current (capturing) streams and becomes part of the graph
+    def collective(self, fn: Callable[[], Any], async_: bool = False):
+        self.n_collectives += 1
+        return fn(), None
+
+    def side_stream(self):
+        return _side_stream()
+
+    def join(self, ev):
+        torch.cuda.current_stream().wait_event(ev)
+
+    def replay(self):
+        self.graph.replay()
+
+    def release(self):
+        """Return the other devices' pools (the graph keeps its own device's)."""
+        for d, pool in self.pools.items():
+            self.be.release_pool(d, pool)
+        self.pools = {}
+
+    def __del__(self):
+        try:
+            if self.pools and self.graph is not None:
+                self.graph = None
+                self.release()
+        except Exception:
+            pass
