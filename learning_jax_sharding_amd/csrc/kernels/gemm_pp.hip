@@ -156,6 +156,19 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// vmcnt with a wave-uniform runtime count (a jump over immediates; counts above 47 wait for 47)
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+#define LJS_W(k) case k: wait_vm<k>(); return;
+    LJS_W(0) LJS_W(1) LJS_W(2) LJS_W(3) LJS_W(4) LJS_W(5) LJS_W(6) LJS_W(7) LJS_W(8) LJS_W(9) LJS_W(10)
+    LJS_W(11) LJS_W(12) LJS_W(13) LJS_W(14) LJS_W(15) LJS_W(16) LJS_W(17) LJS_W(18) LJS_W(19) LJS_W(20)
+    LJS_W(21) LJS_W(22) LJS_W(23) LJS_W(24) LJS_W(25) LJS_W(26) LJS_W(27) LJS_W(28) LJS_W(29) LJS_W(30)
+    LJS_W(31) LJS_W(32) LJS_W(33) LJS_W(34) LJS_W(35) LJS_W(36) LJS_W(37) LJS_W(38) LJS_W(39) LJS_W(40)
+    LJS_W(41) LJS_W(42) LJS_W(43) LJS_W(44) LJS_W(45) LJS_W(46)
+#undef LJS_W
+    default: wait_vm<47>(); return;
+  }
+}
 
 // BM x BN block tile; GSN: the two wave groups split the tile's columns (else its rows); WVM:
 // waves of a group along M (4 / WVM along N); NST: LDS ring depth in K-tiles.
@@ -228,19 +241,25 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
     b_off = __builtin_amdgcn_readfirstlane(
         (int)((B_KC ? (long)w.tn * BN * p.ldb : (long)w.tn * BN) * 2 + (long)kt0 * b_step));
   };
-  auto issue_next = [&](int st) {
-    if (is_kt == 0) load_item(is_item);
+  // piece i (< L) of the current issue-side K-tile into stage st: A pieces first, then B
+  auto piece = [&](int st, int i) {
     const bf16_t* base = smem + st * STAGE;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) dma16(ra, va[i], a_off, base + (wave + 8 * i) * 512);
-#pragma unroll
-    for (int i = 0; i < LB; ++i) dma16(rb, vb[i], b_off, base + A_TILE + (wave + 8 * i) * 512);
+    if (i < LA) dma16(ra, va[i], a_off, base + (wave + 8 * i) * 512);
+    else dma16(rb, vb[i - LA], b_off, base + A_TILE + (wave + 8 * (i - LA)) * 512);
+  };
+  auto advance = [&]() {
     a_off += a_step;
     b_off += b_step;
     if (++is_kt == nk) {
       is_kt = 0;
       ++is_item;
     }
+  };
+  auto issue_next = [&](int st) {
+    if (is_kt == 0) load_item(is_item);
+#pragma unroll
+    for (int i = 0; i < L; ++i) piece(st, i);
+    advance();
   };
 
   f32x4 acc[TM][TN];
@@ -285,6 +304,35 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // C^T block
     __builtin_amdgcn_s_setprio(0);
   };
+  // NST >= 3: the K-tile two ahead is DMA'd from the M intervals, its pieces spread between the
+  // MFMAs (one LDS-DMA issue costs ~60 cycles among bare MFMAs but 100-185 inside a phase full of
+  // LDS reads and other pieces, MI355X_MICROARCH.md "LDS-DMA piece issue cost"): half the pieces
+  // in each of the tile's two M intervals, so the R intervals hold only the fragment reads
+  constexpr int H0 = L / 2, H1 = L - H0;
+  constexpr int NMF = TM * TN;
+  auto mfmas_dma = [&](int st, auto half_c) {
+    constexpr int HALF = decltype(half_c)::value;
+    constexpr int NP = HALF == 0 ? H0 : H1, P0 = HALF == 0 ? 0 : H0;
+    constexpr int STEP = NMF / (NP + 1) > 0 ? NMF / (NP + 1) : 1;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < NMF; ++m) {
+      const int i = m / TN, j = m % TN;
+      acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
+      if ((m + 1) % STEP == 0 && (m + 1) / STEP <= NP) {
+        __builtin_amdgcn_sched_barrier(0);
+        piece(st, P0 + (m + 1) / STEP - 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if constexpr (NMF / STEP < NP) {
+#pragma unroll
+      for (int q = NMF / STEP; q < NP; ++q) piece(st, P0 + q);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  using H0_ = std::integral_constant<int, 0>;
+  using H1_ = std::integral_constant<int, 1>;
 
   // ---- epilogue of item k (accumulators -> C), then zero the accumulators
   const bool psum_on = !OUT_F32 && p.psum != nullptr;
@@ -426,12 +474,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
   bar();
   if (grp == 1) bar();
 
+  constexpr bool DM = NST >= 3;   // DMA from the M intervals (else from R(f, 0))
   for (int it = 0, f = 0; it < my_items; ++it) {
     for (int kk = 0; kk < nk; ++kk, ++f) {
       const int st = f % NST;
-      // R(f, 0): refill the stage of tile f - 1 with tile f + NST - 1, the previous item's
+      // R(f, 0): refill the stage of tile f - 1 with tile f + NST - 1 (NST 2), the previous item's
       // epilogue (this group's partner is in its last MFMAs of it), k-step 0 fragments
-      if (f + NST - 1 < total) issue_next((f + NST - 1) % NST);
+      const bool dma = f + NST - 1 < total;
+      if constexpr (!DM) {
+        if (dma) issue_next((f + NST - 1) % NST);
+      }
       const bool epi = kk == 0 && it > 0;
       if (epi) epilogue(it - 1);
       bool ac = false;
@@ -449,7 +501,17 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       bar();
       // M(f, 0)
-      mfmas();
+      const int dst = (f + NST - 1) % NST;
+      if constexpr (DM) {
+        if (dma) {
+          if (is_kt == 0) load_item(is_item);
+          mfmas_dma(dst, H0_{});
+        } else {
+          mfmas();
+        }
+      } else {
+        mfmas();
+      }
       bar();
       // R(f, 1)
       read_frags(st, 1, ac);
@@ -458,16 +520,30 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(PPArgs p) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const bool more = f + 1 < total;
+      // vector-memory ops younger than tile f + 1's pieces at this wave's wait (they may stay in
+      // flight): the epilogue's stores (+ fused-sum store), the bf16 copy of A, and - DMA from the
+      // M intervals - tile f + 2's pieces issued so far (group 1 waits before its M(f, 1))
+      const int young_common = (epi ? S_EPI + (psum_on ? 1 : 0) : 0) + (ac ? S_AC : 0);
       if (grp == 1 && more) {
-        // the tail: fewer younger tiles in flight than NST - 2
-        if (f + NST - 1 >= total) wait_vm<0>();
+        if constexpr (DM) wait_vm_n(young_common + (dma ? H0 : 0));
+        else if (f + NST - 1 >= total) wait_vm<0>();
         else wait_next(epi, ac);
       }
       bar();
       // M(f, 1)
-      mfmas();
+      if constexpr (DM) {
+        if (dma) {
+          mfmas_dma(dst, H1_{});
+          advance();
+        } else {
+          mfmas();
+        }
+      } else {
+        mfmas();
+      }
       if (grp == 0 && more) {
-        if (f + NST - 1 >= total) wait_vm<0>();
+        if constexpr (DM) wait_vm_n(young_common + (dma ? L : 0));
+        else if (f + NST - 1 >= total) wait_vm<0>();
         else wait_next(epi, ac);
       }
       bar();

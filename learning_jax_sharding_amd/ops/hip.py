@@ -360,8 +360,10 @@ _SLAB_VST = os.environ.get("LJS_SLAB_VST", "1") == "1"
 _TILE_1602 = os.environ.get("LJS_GEMM_TILE1602", "1") == "1"
 
 
-# ping-pong kernel (gemm_pp.hip) for the large k-contiguous bf16 GEMMs: "1" on, "0" off
-_GEMM_PP = os.environ.get("LJS_GEMM_PP", "1") == "1"
+# ping-pong kernel (gemm_pp.hip) for the large k-contiguous bf16 GEMMs: "1" on, "0" off (the
+# default: in the B=64 step it ran QKV+cast 65.6 us vs 55.4, out-proj 21.7 vs 20.4, dh 19.6 vs
+# 18.0 - gpurun_out/r4c, profiles/r4c_b64_pp_kernels.md - and the step 0.2447 vs 0.2333 ms)
+_GEMM_PP = os.environ.get("LJS_GEMM_PP", "0") == "1"
 
 
 def _pick_pp(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc, a_dtype, bias, sBias, relu, accumulate, zero_c,

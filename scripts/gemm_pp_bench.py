@@ -37,7 +37,7 @@ def cases():
     def qkv_fn(tile):
         return lambda: hip.gemm(x, wqkv, qkv, T, 512, 640, 640, 640, 1536, True, True, batch=3, sA=0, sB=512 * 640,
                                 sC=512, tile=tile)
-    out["qkv"] = (qkv_fn, [PP + 1, 2561], 2 * T * 640 * 1536)
+    out["qkv"] = (qkv_fn, [PP + 1, PP + 3, 2561], 2 * T * 640 * 1536)
 
     x32 = torch.randn(T, 640, device=dev)
     xb = torch.empty(T, 640, device=dev).bfloat16()
