@@ -40,7 +40,14 @@ struct GemmArgs {
   bf16_t* acopy;    // f32-A kernels: the bf16 rounding of A ([M][K], dense), written by the items of
                     // batch 0 / tile column 0 (the operand the backward's weight gradient reads)
   const bf16_t* bptr[4];  // flags & kBPtrs (slab mode): batch b's B operand (instead of B + b * sB)
+  unsigned long long* trace;  // LJS_GEMM_TRACE builds only: per-wave timestamps (see gemm_trace)
 };
+
+// Timeline instrumentation of the LDS-DMA kernel (compiled in with -DLJS_GEMM_TRACE only, a
+// variant library for scripts/gemm_trace.py): per wave, kTraceSlots core-clock stamps (s_memtime)
+// written by lane 0 with vector stores -- kernel start, then per K-tile wait: before the counted
+// vmcnt, after it, after the barrier -- and the end.
+constexpr int kTraceSlots = 128;
 
 constexpr int kResAdd = 64, kResMask = 128, kResF32 = 256;
 // f32 output, m/n-contiguous operands, batch 1: split s writes its own slab C + s * sC (no
@@ -513,6 +520,27 @@ gemm_dma_kernel(
   const int my_items = slot < items ? (items - slot + G - 1) / G : 0;
   const int nk = p.kt_per_split;               // K-tiles per item (the split divides them)
   const int total = my_items * nk;
+#ifdef LJS_GEMM_TRACE
+  unsigned long long* trc = p.trace ? p.trace + ((long)blockIdx.x * NW + wave) * kTraceSlots : nullptr;
+  int trn = 0;
+  auto stamp = [&]() {
+    if (trc && trn < kTraceSlots - 1) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (lane == 0) trc[trn] = t;
+    }
+    ++trn;
+  };
+  auto stamp_end = [&]() {
+    if (trc) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (lane == 0) trc[kTraceSlots - 1] = t;
+    }
+  };
+#else
+  auto stamp = [&]() {};
+  auto stamp_end = [&]() {};
+#endif
+  stamp();
 
   constexpr int AES = AF32 ? 4 : 2;  // A element bytes
   const long a_bytes = AES * (A_KC ? (long)(p.M - 1) * p.lda + p.K : (long)(p.K - 1) * p.lda + p.M);
@@ -589,6 +617,7 @@ gemm_dma_kernel(
   // completed (so its stage may be refilled): this wave's pieces of g (the younger tiles' pieces
   // and, right after an epilogue, its S_EPI stores may stay in flight), then the barrier
   auto wait_landed = [&](int g) {
+    stamp();
     const bool tail = g + NST - 2 >= total;
     if constexpr (NST >= 3) {
       if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -602,8 +631,10 @@ gemm_dma_kernel(
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     after_epi = false;
+    stamp();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    stamp();
   };
   // Software-pipelined by half a K-tile: the fragments of k-step 0 of tile g + 1 are read (and
   // tile g + 1's barrier passed) while the k-step 1 MFMAs of tile g are still to issue, so the
@@ -885,6 +916,7 @@ gemm_dma_kernel(
       if (f + NST - 1 < total) issue_next((f + NST - 1) % NST);
     }
   }
+  stamp_end();
 }
 
 // explicit instantiations: hipcc (ROCm 7.2) otherwise leaves some of these kernels' host stubs
@@ -942,6 +974,7 @@ template __global__ void gemm_dma_kernel<128, 128, 2, 4, 3, true, true, false, 0
 #undef LJS_DMA_INST
 
 int g_cus = 0;
+unsigned long long* g_gemm_trace = nullptr;  // LJS_GEMM_TRACE builds: the next LDS-DMA launches' stamps
 
 template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF, int RES = 0, bool AF32 = false>
 hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
@@ -955,6 +988,7 @@ hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   const int items = ntm * ntn * a.batch * a.splitk;
   static const int order_env = getenv("LJS_GEMM_ORDER") ? atoi(getenv("LJS_GEMM_ORDER")) : 1;
   GemmArgs a2 = a;
+  a2.trace = g_gemm_trace;
   if (order_env && ntm < ntn) a2.flags |= kMFast;
   static const int bpc_env = getenv("LJS_DMA_BPC") ? atoi(getenv("LJS_DMA_BPC")) : 0;  // tuning override
   // blocks_per_cu 0 = one block per work item (measured best at the bench shapes: the
@@ -1009,6 +1043,19 @@ hipError_t dispatch_layout(const GemmArgs& a, int a_kc, int b_kc, int out_f32, h
 // and leading dimensions that are multiples of 8 elements.
 constexpr int kAF32 = 2048;  // A is f32 (k-contiguous): rounded to bf16 in the GEMM (acopy: its bf16 copy)
 
+// LJS_GEMM_TRACE builds: the LDS-DMA launches that follow write their per-wave timelines to
+// `buf` (blocks x waves x kTraceSlots u64, zeroed by the caller); null turns it off.  Returns
+// kTraceSlots, or 0 in a library built without the instrumentation.
+LJS_API int ljs_gemm_set_trace(void* buf) {
+#ifdef LJS_GEMM_TRACE
+  g_gemm_trace = (unsigned long long*)buf;
+  return kTraceSlots;
+#else
+  (void)buf;
+  return 0;
+#endif
+}
+
 LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
                           long lda, long ldb, long ldc, long sA, long sB, long sC, long sBias, int batch,
                           int a_kc, int b_kc, int out_f32, int flags, float alpha, int splitk, int tile,
@@ -1036,6 +1083,7 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   a.ldr = ldr;
   a.sR = sR;
   a.acopy = (bf16_t*)acopy;
+  a.trace = nullptr;
   if (flags & kBPtrs) {
     // B is a HOST array of `batch` (<= 4) device pointers, one B operand per batch
     if (batch < 1 || batch > 4 || !(flags & kSlabs)) return (int)hipErrorInvalidValue;

@@ -105,17 +105,16 @@ def _storage_key(g: torch.Tensor) -> Tuple[int, int]:
 
 
 def _covering_flat(grads: List[torch.Tensor]) -> Optional[torch.Tensor]:
-    """A flat view over the storage if ``grads`` are contiguous views that tile it exactly, in
-    order (a producer group); else None."""
-    st_ptr, st_bytes = _storage_key(grads[0])
-    off = 0
+    """A flat view over ``grads`` when they are contiguous views that follow each other in one
+    storage, in order (a producer group, or one gradient sharing its buffer with a tail that
+    belongs to another bucket, e.g. a dW with its bias gradient behind it); else None."""
+    st_ptr, _ = _storage_key(grads[0])
+    start = off = grads[0].storage_offset()
     for g in grads:
         if not g.is_contiguous() or _storage_key(g)[0] != st_ptr or g.storage_offset() != off:
             return None
         off += g.numel()
-    if off * grads[0].element_size() != st_bytes:
-        return None
-    return grads[0].new_empty(0).set_(grads[0].untyped_storage(), 0, (off,), (1,))
+    return grads[0].new_empty(0).set_(grads[0].untyped_storage(), start, (off - start,), (1,))
 
 
 class GradReducer:
