@@ -1155,6 +1155,60 @@ LJS_API int ljs_bcast_scalar(const void* g, int g_bf16, int C, float R, void* ro
   return (int)hipGetLastError();
 }
 
+// out (dense, row-major `full`) = src inside the box [lo, lo + size), zeros elsewhere: the
+// backward of a box slice (a sharded view of a replicated array) in one launch instead of a fill
+// plus a strided copy.  src element (c - lo) at sum_d (c_d - lo_d) * sstride_d.
+struct PadBox {
+  long full[6], lo[6], size[6], sstride[6];
+  int nd;
+};
+template <typename T>
+__global__ __launch_bounds__(256) void pad_box_kernel(const T* __restrict__ src, T* __restrict__ out, PadBox b,
+                                                      long total) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    long r = i, so = 0;
+    bool in = true;
+    for (int d = b.nd - 1; d >= 0; --d) {
+      const long c = r % b.full[d];
+      r /= b.full[d];
+      const long rel = c - b.lo[d];
+      in = in && rel >= 0 && rel < b.size[d];
+      so += rel * b.sstride[d];
+    }
+    out[i] = in ? src[so] : T(0);
+  }
+}
+
+LJS_API int ljs_pad_box(const void* src, void* out, int nd, const long* full, const long* lo, const long* size,
+                        const long* sstride, int esize, hipStream_t s) {
+  if (nd < 1 || nd > 6) return (int)hipErrorInvalidValue;
+  PadBox b;
+  long total = 1;
+  for (int d = 0; d < nd; ++d) {
+    b.full[d] = full[d];
+    b.lo[d] = lo[d];
+    b.size[d] = size[d];
+    b.sstride[d] = sstride[d];
+    total *= full[d];
+  }
+  b.nd = nd;
+  if (total == 0) return 0;
+  long grid = (total + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  if (esize == 2)
+    hipLaunchKernelGGL(pad_box_kernel<unsigned short>, dim3(grid), dim3(256), 0, s, (const unsigned short*)src,
+                       (unsigned short*)out, b, total);
+  else if (esize == 4)
+    hipLaunchKernelGGL(pad_box_kernel<unsigned>, dim3(grid), dim3(256), 0, s, (const unsigned*)src, (unsigned*)out, b,
+                       total);
+  else if (esize == 8)
+    hipLaunchKernelGGL(pad_box_kernel<unsigned long long>, dim3(grid), dim3(256), 0, s,
+                       (const unsigned long long*)src, (unsigned long long*)out, b, total);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
 LJS_API int ljs_sum_partials(const void* p, int n, void* out, int out_bf16, hipStream_t s) {
   hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, (const float*)p, n, out, out_bf16);
   return (int)hipGetLastError();

@@ -370,6 +370,25 @@ __device__ __forceinline__ int swz_mn16(int krow) {
 }
 
 
+// s_waitcnt vmcnt with a wave-uniform runtime count (a jump over immediates; counts above 47
+// wait for 47, which is only stricter)
+template <int N>
+__device__ __forceinline__ void wait_vm_imm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+#define LJS_W(k) case k: wait_vm_imm<k>(); return;
+    LJS_W(0) LJS_W(1) LJS_W(2) LJS_W(3) LJS_W(4) LJS_W(5) LJS_W(6) LJS_W(7) LJS_W(8) LJS_W(9) LJS_W(10)
+    LJS_W(11) LJS_W(12) LJS_W(13) LJS_W(14) LJS_W(15) LJS_W(16) LJS_W(17) LJS_W(18) LJS_W(19) LJS_W(20)
+    LJS_W(21) LJS_W(22) LJS_W(23) LJS_W(24) LJS_W(25) LJS_W(26) LJS_W(27) LJS_W(28) LJS_W(29) LJS_W(30)
+    LJS_W(31) LJS_W(32) LJS_W(33) LJS_W(34) LJS_W(35) LJS_W(36) LJS_W(37) LJS_W(38) LJS_W(39) LJS_W(40)
+    LJS_W(41) LJS_W(42) LJS_W(43) LJS_W(44) LJS_W(45) LJS_W(46)
+#undef LJS_W
+    default: wait_vm_imm<47>(); return;
+  }
+}
+
 // One operand tile (R rows x BK) of one K-tile: its 1 KiB DMA pieces, split over NW waves.
 // Per-lane offsets are relative to (row 0, k 0); the tile origin goes in the scalar offset.
 template <int R, bool KC, int NW>
@@ -484,21 +503,28 @@ constexpr int kSC1 = 16;  // buffer-instruction cache policy bit: sc1 (gfx940-fa
 // (a 4-wave kernel whose LDS ring lets two blocks share a CU is told so: the pipelined main loop's
 // second fragment set and the epilogue registers would otherwise push VGPR + AGPR past 256 and
 // halve the resident blocks)
-// AF32: A is f32 (k-contiguous), rounded to bf16 at the fragment read -- the activation cast
-// fused into the GEMM; the items of batch 0 / tile column 0 also write A's bf16 rounding
-// (p.acopy) for the backward.
-template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0, bool AF32 = false>
+// AF32: A is f32 (k-contiguous) -- the activation cast fused into the GEMM -- and the items of
+// batch 0 / tile column 0 also write A's bf16 rounding (p.acopy) for the backward.  1: an f32
+// LDS image (LDS-DMA), rounded at the fragment read; 2: register-staged -- each wave loads its
+// pieces of the next-but-two K-tile's A as f32 into VGPRs (global -> VGPR), and one K-tile later
+// rounds them and writes the bf16 image the LDS-DMA would have written (same swizzle), so the
+// ring, the fragment reads and the MFMA loop are the bf16 kernel's.
+template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0, int AF32 = 0>
 __global__ __launch_bounds__(WM * WN * 64,
-                            (WM * WN == 4 && NST * ((AF32 ? 2 : 1) * BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
+                            (WM * WN == 4 && NST * ((AF32 == 1 ? 2 : 1) * BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
 gemm_dma_kernel(
     GemmArgs p) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   static_assert(!AF32 || A_KC, "f32 A is k-contiguous");
-  constexpr int A_TILE = BM * BK * (AF32 ? 2 : 1), B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
-  using TA = typename std::conditional<AF32, DmaTileF32<BM, NW>, DmaTile<BM, A_KC, NW>>::type;
+  constexpr bool AIMG32 = AF32 == 1, AREG = AF32 == 2;
+  constexpr int A_TILE = BM * BK * (AIMG32 ? 2 : 1), B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
+  using TA = typename std::conditional<AIMG32, DmaTileF32<BM, NW>, DmaTile<BM, A_KC, NW>>::type;
   using TB = DmaTile<BN, B_KC, NW>;
-  constexpr int L = TA::PER_WAVE + TB::PER_WAVE;  // DMA instructions per wave per K-tile
+  // vector-memory instructions per wave per K-tile (register-staged A: two 16-byte f32 loads
+  // per bf16 DMA piece)
+  constexpr int LA = AREG ? 2 * TA::PER_WAVE : TA::PER_WAVE;
+  constexpr int L = LA + TB::PER_WAVE;
   // Operands swapped (C^T = B^T A^T per 16x16 block): each lane ends with 4 CONSECUTIVE
   // columns of one output row.  bf16 output: lanes pair up into 16-byte row chunks and leave
   // through exactly S_EPI buffer stores per lane (masked lanes get an out-of-range offset, so
@@ -559,6 +585,43 @@ gemm_dma_kernel(
   __amdgpu_buffer_rsrc_t ra, rb;
   int a_off = 0, b_off = 0;
   const int a_step = (int)a_kt, b_step = (int)b_kt;
+  // register-staged A (AREG): the loaded f32 pieces of one K-tile, the stage they go to, and the
+  // wave's vector-memory instructions issued after them (the counted wait before their rounding)
+  // The bf16 copy of A for the backward (p.acopy, [M][K]) leaves from the same registers: K-tile
+  // kt of a row block by its item j = b * ntn + n0 with kt % (batch * ntn) == j, so the copy is
+  // shared out over the row block's items (no f32 re-read).  Those stores are counted into the
+  // next K-tile wait (ac_x); masked rows get an out-of-range offset so the count is exact.
+  f32x4 areg[AREG ? 2 * TA::PER_WAVE : 1];
+  int a_pend = -1, a_young = 0, ac_x = 0;
+  int it_row0 = 0, it_kt0 = 0, it_j = 0;          // the issue-side item's row origin, K-tile, index
+  bool a_cp = false;
+  int a_cp_row0 = 0, a_cp_k0 = 0;
+  const int acJ = p.batch * ntn;
+  __amdgpu_buffer_rsrc_t rac;
+  if constexpr (AREG) rac = make_rsrc(p.acopy, p.acopy ? 2L * p.M * p.K : 0);
+  auto a_commit = [&]() {
+    if constexpr (AREG) {
+      if (a_pend < 0) return;
+      wait_vm_n(a_young);
+      bf16_t* base = smem + a_pend * STAGE;
+#pragma unroll
+      for (int i = 0; i < TA::PER_WAVE; ++i) {
+        const f32x4 lo = areg[2 * i], hi = areg[2 * i + 1];
+        const u32x4 v = u32x4{pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
+                              pack_bf16x2(hi[2], hi[3])};
+        *reinterpret_cast<u32x4*>(base + (wave + NW * i) * 512 + lane * 8) = v;
+        if (a_cp) {
+          const int row = 8 * (wave + NW * i) + (lane >> 3), slot = lane & 7;
+          const int grow = a_cp_row0 + row;
+          const int off = grow < p.M ? (int)(((long)grow * p.K + a_cp_k0 + 8 * (slot ^ ((row >> 1) & 7))) * 2)
+                                     : 0x7ffffff0;
+          __builtin_amdgcn_raw_buffer_store_b128(v, rac, off, 0, 0);
+        }
+      }
+      if (a_cp) ac_x += TA::PER_WAVE;
+      a_pend = -1;
+    }
+  };
   auto load_item = [&](int k) {
     const WorkItem w = decode_item(p, slot + G * k, ntm, ntn);
     ra = make_rsrc(reinterpret_cast<const unsigned char*>(p.A) + (long)w.b * p.sA * AES, a_bytes);
@@ -567,11 +630,40 @@ gemm_dma_kernel(
         (int)((A_KC ? (long)w.m0 * BM * p.lda : (long)w.m0 * BM) * AES + w.kt0 * a_kt));
     b_off = __builtin_amdgcn_readfirstlane(
         (int)((B_KC ? (long)w.n0 * BN * p.ldb : (long)w.n0 * BN) * 2 + w.kt0 * b_kt));
+    if constexpr (AREG) {
+      it_row0 = w.m0 * BM;
+      it_kt0 = w.kt0;
+      it_j = w.b * ntn + w.n0;
+    }
+  };
+  // A's pieces of the next K-tile: LDS-DMA, or (AREG) f32 loads into areg after rounding the
+  // pending ones into their stage
+  auto issue_a = [&](int st) {
+    if constexpr (AREG) {
+      a_commit();
+#pragma unroll
+      for (int i = 0; i < TA::PER_WAVE; ++i) {
+        areg[2 * i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, 2 * ta.voff[i], a_off, 0));
+        areg[2 * i + 1] =
+            __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, 2 * ta.voff[i] + 16, a_off, 0));
+      }
+      a_pend = st;
+      a_young = 0;
+      a_cp = p.acopy != nullptr && (it_kt0 + is_kt) % acJ == it_j;
+      a_cp_row0 = it_row0;
+      a_cp_k0 = (it_kt0 + is_kt) * BK;
+    } else {
+      ta.issue(ra, smem + st * STAGE, a_off, wave);
+    }
+  };
+  auto issue_b = [&](int st) {
+    tb.issue(rb, smem + st * STAGE + A_TILE, b_off, wave);
+    if constexpr (AREG) a_young += TB::PER_WAVE;
   };
   auto issue_next = [&](int st) {
     if (is_kt == 0) load_item(is_item);
-    ta.issue(ra, smem + st * STAGE, a_off, wave);
-    tb.issue(rb, smem + st * STAGE + A_TILE, b_off, wave);
+    issue_a(st);
+    issue_b(st);
     a_off += a_step;
     b_off += b_step;
     if (++is_kt == nk) { is_kt = 0; ++is_item; }
@@ -580,10 +672,10 @@ gemm_dma_kernel(
   auto issue_half = [&](int st, bool second) {
     if (!second) {
       if (is_kt == 0) load_item(is_item);
-      ta.issue(ra, smem + st * STAGE, a_off, wave);
+      issue_a(st);
       a_off += a_step;
     } else {
-      tb.issue(rb, smem + st * STAGE + A_TILE, b_off, wave);
+      issue_b(st);
       b_off += b_step;
       if (++is_kt == nk) { is_kt = 0; ++is_item; }
     }
@@ -619,7 +711,11 @@ gemm_dma_kernel(
   auto wait_landed = [&](int g) {
     stamp();
     const bool tail = g + NST - 2 >= total;
-    if constexpr (NST >= 3) {
+    if constexpr (AREG) {
+      // the register-staged A's bf16-copy stores (ac_x) are younger than this tile's B pieces too
+      wait_vm_n(tail ? 0 : L * (NST - 2) + (after_epi ? S_EPI + (psum_on ? 1 : 0) : 0) + ac_x);
+      ac_x = 0;
+    } else if constexpr (NST >= 3) {
       if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else if (SWAP && after_epi && psum_on)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2) + S_EPI + 1) : "memory");
@@ -646,7 +742,7 @@ gemm_dma_kernel(
     const bf16_t* Bs_ = As_ + A_TILE;
 #pragma unroll
     for (int ii = 0; ii < TM; ++ii) {
-      if constexpr (AF32) af[ii] = frag_f32(As_, wr * (BM / WM) + ii * 16, ks, lane);
+      if constexpr (AIMG32) af[ii] = frag_f32(As_, wr * (BM / WM) + ii * 16, ks, lane);
       else af[ii] = frag<BM, A_KC>(As_, wr * (BM / WM) + ii * 16, ks, lane);
     }
 #pragma unroll
@@ -667,10 +763,15 @@ gemm_dma_kernel(
   // transposed-read weight-gradient kernels, 1-2 % slower pipelined while the k-contiguous
   // forward / dX kernels gain 3-4 %: QKV 2561 45.3 -> 43.7 us, 1282 48.1 -> 46.1 us)
   constexpr bool PIPE = TM + TN <= 8 && A_KC && B_KC;
+  static_assert(!AREG || (PIPE && !OUT_F32 && RES == 0), "register-staged A: the pipelined bf16-output loop");
+  if constexpr (AREG) {
+    if (total == 1) a_commit();   // (tile 0 rounded into its stage before its barrier)
+  }
   if (PIPE && total > 0) {
     wait_landed(0);
     read_frags(0, 0, ka, kb);
     if (NST - 1 < total) issue_next((NST - 1) % NST);
+    else a_commit();
   }
 
   for (int it = 0, f = 0; it < my_items; ++it) {
@@ -700,6 +801,7 @@ gemm_dma_kernel(
       wait_landed(f + 1);
       read_frags(f + 1, 0, ka, kb);
       if (more) issue_half(f % NST, false);
+      else a_commit();   // (AREG: the last loaded K-tile still goes to its stage)
     }
     mfmas(la, lb);
     if (more) issue_half(f % NST, true);
@@ -709,7 +811,7 @@ gemm_dma_kernel(
     const WorkItem w = decode_item(p, slot + G * it, ntm, ntn);
     const int m0 = w.m0 * BM + wr * (BM / WM), n0 = w.n0 * BN + wc * (BN / WN);
     const int g = lane >> 4;
-    if constexpr (AF32) {
+    if constexpr (AIMG32) {
       // this row block's bf16 A for the backward (re-read from L2 where the DMA just streamed
       // it), shared out by K-tile over the row block's batch x column items (item j copies
       // K-tiles j, j + J, ...), so no item carries the whole row block's copy and the round's
@@ -823,6 +925,7 @@ gemm_dma_kernel(
         tsum = 0.f;
       }
       after_epi = true;
+      if constexpr (AREG) a_young += S_EPI + (psum_on ? 1 : 0);
     } else {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]
       const bool vec = (p.ldc & 3) == 0 && (p.sC & 3) == 0 && ((((uintptr_t)p.C) & 15) == 0);
@@ -914,6 +1017,7 @@ gemm_dma_kernel(
       wait_landed(f);
       read_frags(f, 0, ka, kb);
       if (f + NST - 1 < total) issue_next((f + NST - 1) % NST);
+      else a_commit();
     }
   }
   stamp_end();
@@ -969,14 +1073,15 @@ LJS_DMA_INST_RES(128, 128, 2, 4, 3)
 LJS_DMA_INST_RES(128, 128, 2, 4, 4)
 #undef LJS_DMA_INST_RES
 // f32-A (cast-on-load) forward GEMMs: 128x128, 8 waves, 3 stages (144 KiB with the f32 A image)
-template __global__ void gemm_dma_kernel<128, 128, 2, 4, 3, true, true, false, 0, true>(GemmArgs);
+template __global__ void gemm_dma_kernel<128, 128, 2, 4, 3, true, true, false, 0, 1>(GemmArgs);
+template __global__ void gemm_dma_kernel<256, 128, 4, 2, 3, true, true, false, 0, 2>(GemmArgs);
 #undef LJS_DMA_INST_LAYOUTS
 #undef LJS_DMA_INST
 
 int g_cus = 0;
 unsigned long long* g_gemm_trace = nullptr;  // LJS_GEMM_TRACE builds: the next LDS-DMA launches' stamps
 
-template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF, int RES = 0, bool AF32 = false>
+template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF, int RES = 0, int AF32 = 0>
 hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   if (!g_cus) {
     int dev = 0;
@@ -998,7 +1103,7 @@ hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   // walks `rounds` items with the next item's first K-tiles in flight during the current
   // item's epilogue (measured at T = 16384: QKV projection 43.8 -> 39.9 us on 128x128 x 2/CU).
   // Otherwise one block per item, which lets the dispatcher balance a ragged last round.
-  constexpr int kLdsBytes = NST * ((AF32 ? 2 : 1) * BM + BN) * BK * 2;
+  constexpr int kLdsBytes = NST * ((AF32 == 1 ? 2 : 1) * BM + BN) * BK * 2;
   constexpr int kNatural = (WM * WN == 4 && kLdsBytes <= 80 * 1024) ? 2 : 1;  // resident blocks / CU
   if (bpc == 0 && bpc_env == 0 && items > g_cus * kNatural && items % (g_cus * kNatural) == 0) bpc = kNatural;
   int grid = bpc > 0 ? g_cus * bpc : items;
@@ -1103,7 +1208,11 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     a.kt_per_split = K / 64;
     a.splitk = 1;
     a.flags = flags & ~kAF32;
-    return (int)launch_dma<128, 128, 2, 4, 3, true, true, false, 0, true>(a, stream, 0);
+    // 2561: the 256x128 8-wave kernel with A register-staged (global f32 -> VGPR -> bf16 LDS
+    // image); else the 8-wave 128x128 kernel over an f32 LDS image
+    if (tile == 2561 && (long)M * lda * 4 < (1L << 30))
+      return (int)launch_dma<256, 128, 4, 2, 3, true, true, false, 0, 2>(a, stream, 0);
+    return (int)launch_dma<128, 128, 2, 4, 3, true, true, false, 0, 1>(a, stream, 0);
   }
 
   if (psum_count) *psum_count = 0;

@@ -60,6 +60,8 @@ _SIGS = {
     "ljs_relu_bwd_colsum": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_relu_bwd": [c_void_p, c_void_p, c_int, c_int, c_long, c_long, c_void_p, c_void_p],
     "ljs_bcast_scalar": [c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    "ljs_pad_box": [c_void_p, c_void_p, c_int, _LP, _LP, _LP, _LP,
+                    c_int, c_void_p],
     "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p,
                         c_void_p, c_int, c_float, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
@@ -1275,6 +1277,43 @@ def concat_parts(parts, dim: int) -> torch.Tensor:
     out = torch.empty(cs[:pdim] + (n * cs[pdim],) + cs[pdim + 1:], dtype=p0.dtype, device=p0.device)
     _pack_launch(pparts, out, A, n, inner, 2, None)
     return out.permute(_inv(o))
+
+
+def pad_box(src: torch.Tensor, full, lo) -> torch.Tensor:
+    """A dense tensor of shape ``full`` holding ``src`` at offset ``lo`` and zeros elsewhere, in
+    one HIP launch (the backward of a box slice; ``src`` may be strided)."""
+    nd = len(full)
+    assert src.dim() == nd and src.is_cuda and nd <= 6
+    out = torch.empty(tuple(full), dtype=src.dtype, device=src.device)
+    arr = lambda v: (c_long * nd)(*[int(x) for x in v])  # noqa: E731
+    rc = lib().ljs_pad_box(_p(src), _p(out), nd, arr(full), arr(lo), arr(src.shape), arr(src.stride()),
+                           src.element_size(), _stream(out))
+    _ck(rc, "pad_box")
+    return out
+
+
+class _BoxSlice(torch.autograd.Function):
+    """``t[box]`` whose backward is one :func:`pad_box` launch (torch's slice_backward is a fill
+    plus a copy kernel)."""
+
+    @staticmethod
+    def forward(ctx, t, box):
+        ctx.full = tuple(t.shape)
+        ctx.lo = tuple(s.start for s in box)
+        return t[box]
+
+    @staticmethod
+    def backward(ctx, g):
+        return pad_box(g, ctx.full, ctx.lo), None
+
+
+def box_slice(t: torch.Tensor, box) -> torch.Tensor:
+    """``t[box]`` (a tuple of unit-step slices with explicit bounds): on a GPU tensor that needs a
+    gradient, the backward runs as one HIP launch."""
+    if t.is_cuda and t.requires_grad and torch.is_grad_enabled() and t.dtype.itemsize in (2, 4, 8) \
+            and t.dim() <= 6 and len(box) == t.dim():
+        return _BoxSlice.apply(t, tuple(box))
+    return t[box]
 
 
 def bcast_scalar(g: torch.Tensor, C: int, R: int, want_db: bool, db_out: Optional[torch.Tensor] = None,

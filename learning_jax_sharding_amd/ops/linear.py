@@ -391,12 +391,14 @@ class _Linear(torch.autograd.Function):
                         and x2.is_contiguous() and res is None and b is None and not relu and K % 64 == 0
                         and N % 8 == 0 and out_dtype == torch.bfloat16 and x2.data_ptr() % 16 == 0
                         and M * nw * N >= (1 << 20))
-        # the ping-pong kernel's f32-A configuration (csrc/kernels/gemm_pp.hip AF32) converts the
-        # fragments in registers and writes the bf16 copy from them: on wherever it applies; the
-        # LDS-DMA kernel's f32 path stays opt-in (LJS_CAST_ON_LOAD=1, measured slower)
-        cast_on_load = cast_on_load and (_CAST_ON_LOAD or hip._pick_pp(
-            M, N, K, nw, True, True, False, 1, nw * N, torch.float32, None, 0, False, False, False, None, None,
-            x2, False, 0, N * K, N, K) is not None)
+        # "auto": where the f32 A is register-staged (the 256x128 tile: global f32 -> VGPR -> bf16
+        # LDS image, the bf16 copy stored from the same registers) or the ping-pong kernel's f32-A
+        # configuration applies; the f32-LDS-image kernels stay opt-in ("1", measured slower)
+        if cast_on_load and _CAST_ON_LOAD != "1":
+            cast_on_load = _CAST_ON_LOAD == "auto" and (
+                hip.pick_tile(M, N, K, nw, True, True, False, 1, nw * N) == 2561 or hip._pick_pp(
+                    M, N, K, nw, True, True, False, 1, nw * N, torch.float32, None, 0, False, False, False, None,
+                    None, x2, False, 0, N * K, N, K) is not None)
         if swap:   # batch-major x -> seq-major bf16 rows, rounded in the same pass
             xb = hip.swap01_bf16(x.contiguous()).view(M, K)
         else:
@@ -780,7 +782,8 @@ class _FFBlock(torch.autograd.Function):
 # and LDS reads of the K-loop, which costs more than the cast pass it saves.  Re-measured inside the
 # step with the bf16 copy shared out over the items: B=8 even (0.0898-0.0904 vs 0.0896-0.0899 ms),
 # B=16 and B=64 slower (profiles/PERF_NOTES.md)
-_CAST_ON_LOAD = os.environ.get("LJS_CAST_ON_LOAD", "0") == "1"
+# "auto" (default): the register-staged form (see linear()); "1": every f32-A kernel; "0": off
+_CAST_ON_LOAD = os.environ.get("LJS_CAST_ON_LOAD", "auto")
 
 # order of the FF block's backward GEMMs after dA (dX, dW_out, dW_in): which operands are still
 # in the Infinity Cache when each runs.  dW_in right after dA (which it reads, 84 MB at the bench

@@ -165,7 +165,13 @@ def _local_slice(x: ShardedArray, src: TileAssignment, dst: TileAssignment, shap
         if d not in dst.coords:
             continue
         rel = _rel(dst.region(d, shape), src.region(d, shape))
-        out[d] = t[rel]
+        if all(r.start == 0 and r.stop == n for r, n in zip(rel, t.shape)):
+            out[d] = t
+        elif t.is_cuda:
+            from ..ops import hip as _hip
+            out[d] = _hip.box_slice(t, rel)
+        else:
+            out[d] = t[rel]
     return out
 
 

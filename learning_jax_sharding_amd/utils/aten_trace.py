@@ -57,7 +57,8 @@ def _desc(a) -> str:
 # framework (ops.hip) helpers whose launches are data movement or glue rather than the step's
 # math: traced by call site too (they are ctypes calls, invisible to the dispatcher)
 _HIP_GLUE = ("rank_major", "from_rank_major", "concat_parts", "slab_reduce", "cast_transpose_bf16", "swap01_bf16",
-             "transpose_bf16", "colsum_ld", "sum_n", "sum_ptrs", "cast", "cast_into", "bcast_scalar")
+             "transpose_bf16", "colsum_ld", "sum_n", "sum_ptrs", "cast", "cast_into", "bcast_scalar", "pad_box",
+             "_pack_launch")
 
 
 class AtenTrace(TorchDispatchMode):

@@ -46,10 +46,10 @@ def cases():
         if tile == "cast":   # the separate cast pass + the bf16 ping-pong GEMM
             return lambda: (hip.cast_into(x32, xb) if hasattr(hip, "cast_into") else xb.copy_(x32),
                             hip.gemm(xb, wqkv, qkv, T, 512, 640, 640, 640, 1536, True, True, batch=3, sA=0,
-                                     sB=512 * 640, sC=512, tile=PP + 1))
+                                     sB=512 * 640, sC=512, tile=2561))
         return lambda: hip.gemm(x32, wqkv, qkv, T, 512, 640, 640, 640, 1536, True, True, batch=3, sA=0,
                                 sB=512 * 640, sC=512, acopy=xb, tile=tile)
-    out["qkv32"] = (qkv32_fn, [PP + 21, "cast"], 2 * T * 640 * 1536)
+    out["qkv32"] = (qkv32_fn, [2561, PP + 21, "cast"], 2 * T * 640 * 1536)
 
     h = torch.randn(T, 512, device=dev).bfloat16()
     wo = torch.randn(640, 512, device=dev).bfloat16()

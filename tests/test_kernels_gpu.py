@@ -846,6 +846,28 @@ def test_gemm_f32_a_cast_on_load(hip, M, N, K, batch):
     assert torch.equal(xb, ref_x)
 
 
+@pytest.mark.parametrize("M,N,K,batch", [(16384, 512, 640, 3), (2048, 512, 640, 3), (300, 136, 128, 1),
+                                         (520, 256, 1024, 1), (4096 + 72, 128, 640, 2)])
+def test_gemm_f32_a_register_staged(hip, M, N, K, batch):
+    """The 256x128 kernel with A register-staged (global f32 -> VGPR -> bf16 LDS image; tile
+    2561 + f32 A) == cast pass + bf16 GEMM bit for bit; the bf16 copy it writes from the same
+    registers (shared out over each row block's items by K-tile) == the cast pass's output."""
+    x = _rand(M, K, dtype=torch.float32, seed=94)
+    w = _rand(batch, N, K, seed=95)
+    ref_x = x.bfloat16()
+    ref = torch.empty(M, batch * N, dtype=torch.bfloat16, device=dev)
+    hip.gemm(ref_x, w, ref, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N, tile=1282)
+    out = torch.full((M, batch * N), float("nan"), dtype=torch.bfloat16, device=dev)
+    xb = torch.full((M, K), float("nan"), dtype=torch.bfloat16, device=dev)
+    hip.gemm(x, w, out, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N, acopy=xb, tile=2561)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert torch.equal(xb, ref_x)
+    out2 = torch.full((M, batch * N), float("nan"), dtype=torch.bfloat16, device=dev)
+    hip.gemm(x, w, out2, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N, tile=2561)
+    assert torch.equal(out2, ref)
+
+
 def test_linear_f32_input_cast_on_load(hip, monkeypatch):
     """hip.linear on an f32 activation: the cast-on-load GEMM path gives the same outputs and
     weight gradients as the separate-cast path."""
@@ -853,12 +875,12 @@ def test_linear_f32_input_cast_on_load(hip, monkeypatch):
     x = _rand(4096, 640, dtype=torch.float32, seed=92)
     ws = [(_rand(640, 512, dtype=torch.float32, seed=93 + i) * 0.05).requires_grad_() for i in range(3)]
     res = {}
-    for flag in (False, True):
+    for flag in ("0", "1"):
         monkeypatch.setattr(L, "_CAST_ON_LOAD", flag)
         ys = hip.linear(x, ws, None, torch.bfloat16, False, torch.bfloat16)
         gs = torch.autograd.grad(ys, ws, [torch.ones_like(y) for y in ys])
         res[flag] = [y.clone() for y in ys] + [g.clone() for g in gs]
-    for a, b in zip(res[False], res[True]):
+    for a, b in zip(res["0"], res["1"]):
         assert torch.equal(a, b)
 
 
@@ -1082,3 +1104,22 @@ def test_dropout_kernel_matches_host_philox_mask(hip, dtype):
     assert torch.equal(y.detach().cpu(), ref[sl])
     gref = torch.where(u[sl] < keep, (torch.ones((), dtype=dtype).float() / keep).to(dtype), torch.zeros((), dtype=dtype))
     assert torch.equal(x.grad.cpu(), gref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_box_slice_backward_is_pad(hip, dtype):
+    """box_slice's backward (one pad_box launch) equals torch's slice_backward, for a strided
+    incoming gradient too."""
+    full = torch.randn(6, 40, 24, dtype=torch.float32).to(dtype).to(dev).requires_grad_()
+    box = (slice(2, 5), slice(8, 32), slice(0, 24))
+    y = hip.box_slice(full, box)
+    assert y.shape == (3, 24, 24)
+    g = torch.randn(24, 3, 24, dtype=torch.float32).to(dtype).to(dev).transpose(0, 1)   # non-contiguous
+    y.backward(g)
+    ref = torch.zeros(6, 40, 24, dtype=dtype, device=dev)
+    ref[box] = g
+    torch.cuda.synchronize()
+    assert torch.equal(full.grad, ref)
+    v = torch.randn(640, device=dev).requires_grad_()
+    hip.box_slice(v, (slice(320, 640),)).sum().backward()
+    assert torch.equal(v.grad, torch.cat([torch.zeros(320, device=dev), torch.ones(320, device=dev)]))
