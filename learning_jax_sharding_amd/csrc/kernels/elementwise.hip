@@ -315,7 +315,21 @@ __global__ void colsum_bcast_kernel(const void* __restrict__ in, int is_bf16, in
 // reading each slab as one streaming pass.  The output's columns may be split into column
 // blocks of width cb stored as separate [R][cb] matrices (out_bs apart): the fused dW[q|k|v]
 // GEMM produces [640][1536] slabs whose column blocks are dWq, dWk, dWv.
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slabs, int S, long slab_stride,
+// 4 consecutive slab elements as f32 from f32 or bf16 slabs (bf16 slabs: the weight-gradient
+// GEMM's split-K partials rounded once each, summed here in f32)
+template <typename ST>
+__device__ __forceinline__ f32x4 ld_slab4(const ST* __restrict__ p, long e) {
+  if constexpr (sizeof(ST) == 4) {
+    return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + e);
+  } else {
+    const u32x2 r = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(p) + e);
+    return f32x4{__uint_as_float(r[0] << 16), __uint_as_float(r[0] & 0xffff0000u), __uint_as_float(r[1] << 16),
+                 __uint_as_float(r[1] & 0xffff0000u)};
+  }
+}
+
+template <typename ST>
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const ST* __restrict__ slabs, int S, long slab_stride,
                                                           int R, int C, float* __restrict__ out, int cb,
                                                           long out_bs, int accumulate,
                                                           bf16_t* __restrict__ out_bf16, float* __restrict__ tail,
@@ -332,16 +346,16 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   const long n4 = (long)R * C / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const long e = 4 * i;
-    f32x4 acc = *reinterpret_cast<const f32x4*>(slabs + e);
+    f32x4 acc = ld_slab4(slabs, e);
     int s = 1;
     for (; s + 3 < S; s += 4) {  // 4 independent slab loads in flight
-      f32x4 v0 = *reinterpret_cast<const f32x4*>(slabs + s * slab_stride + e);
-      f32x4 v1 = *reinterpret_cast<const f32x4*>(slabs + (s + 1) * slab_stride + e);
-      f32x4 v2 = *reinterpret_cast<const f32x4*>(slabs + (s + 2) * slab_stride + e);
-      f32x4 v3 = *reinterpret_cast<const f32x4*>(slabs + (s + 3) * slab_stride + e);
+      f32x4 v0 = ld_slab4(slabs, s * slab_stride + e);
+      f32x4 v1 = ld_slab4(slabs, (s + 1) * slab_stride + e);
+      f32x4 v2 = ld_slab4(slabs, (s + 2) * slab_stride + e);
+      f32x4 v3 = ld_slab4(slabs, (s + 3) * slab_stride + e);
       acc += (v0 + v1) + (v2 + v3);
     }
-    for (; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(slabs + s * slab_stride + e);
+    for (; s < S; ++s) acc += ld_slab4(slabs, s * slab_stride + e);
     const int r = (int)(e / C), c = (int)(e % C);
     float* dst = out + (long)(c / cb) * out_bs + (long)r * cb + (c % cb);
     if (accumulate) acc += *reinterpret_cast<const f32x4*>(dst);
@@ -511,11 +525,16 @@ struct AdamTensor {
 };
 
 // the slab sum of slab_reduce_kernel, in its order (bit-identical results)
-__device__ __forceinline__ float slab_sum1(const float* __restrict__ g, long gS, long ss, long i) {
-  float acc = g[i];
+template <typename ST>
+__device__ __forceinline__ float slab_sum1(const ST* __restrict__ g, long gS, long ss, long i) {
+  auto ld = [&](long j) {
+    if constexpr (sizeof(ST) == 4) return reinterpret_cast<const float*>(g)[j];
+    else return bf2f(reinterpret_cast<const bf16_t*>(g)[j]);
+  };
+  float acc = ld(i);
   long s = 1;
-  for (; s + 3 < gS; s += 4) acc += (g[s * ss + i] + g[(s + 1) * ss + i]) + (g[(s + 2) * ss + i] + g[(s + 3) * ss + i]);
-  for (; s < gS; ++s) acc += g[s * ss + i];
+  for (; s + 3 < gS; s += 4) acc += (ld(s * ss + i) + ld((s + 1) * ss + i)) + (ld((s + 2) * ss + i) + ld((s + 3) * ss + i));
+  for (; s < gS; ++s) acc += ld(s * ss + i);
   return acc;
 }
 constexpr int kAdamMax = 32;
@@ -570,42 +589,47 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
     }
     if (T.gS > 0) {
       // the slab sum of slab_reduce_kernel (same order, bit-identical) with the loads of all NQ
-      // rows of a 4-slab group in flight together
-      const float* G = reinterpret_cast<const float*>(T.g);
+      // rows of a 4-slab group in flight together; f32 or bf16 slabs (T.g_bf16)
+      auto slab_sum = [&](auto tag) {
+        using ST = decltype(tag);
+        const ST* G = reinterpret_cast<const ST*>(T.g);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) gv[q] = *reinterpret_cast<const f32x4*>(G + gix[q]);
-      long s = 1;
-      for (; s + 3 < T.gS; s += 4) {
-        f32x4 v[NQ][4];
+        for (int q = 0; q < NQ; ++q) gv[q] = ld_slab4(G, gix[q]);
+        long s = 1;
+        for (; s + 3 < T.gS; s += 4) {
+          f32x4 v[NQ][4];
 #pragma unroll
-        for (int q = 0; q < NQ; ++q)
+          for (int q = 0; q < NQ; ++q)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[q][j] = *reinterpret_cast<const f32x4*>(G + (s + j) * T.g_ss + gix[q]);
+            for (int j = 0; j < 4; ++j) v[q][j] = ld_slab4(G, (s + j) * T.g_ss + gix[q]);
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) gv[q] += (v[q][0] + v[q][1]) + (v[q][2] + v[q][3]);
-      }
-      // the 1-3 remaining slabs: their loads issued together (one round trip, not one each),
-      // added one by one in slab_reduce's order
-      if (NQ <= 2 && s < T.gS) {   // (64-row tiles: registers would halve the occupancy)
-        f32x4 r[NQ][3];
+          for (int q = 0; q < NQ; ++q) gv[q] += (v[q][0] + v[q][1]) + (v[q][2] + v[q][3]);
+        }
+        // the 1-3 remaining slabs: their loads issued together (one round trip, not one each),
+        // added one by one in slab_reduce's order
+        if (NQ <= 2 && s < T.gS) {   // (64-row tiles: registers would halve the occupancy)
+          f32x4 r[NQ][3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          if (s + j < T.gS) {
+          for (int j = 0; j < 3; ++j)
+            if (s + j < T.gS) {
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) r[q][j] = *reinterpret_cast<const f32x4*>(G + (s + j) * T.g_ss + gix[q]);
-          }
+              for (int q = 0; q < NQ; ++q) r[q][j] = ld_slab4(G, (s + j) * T.g_ss + gix[q]);
+            }
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          if (s + j < T.gS) {
+          for (int j = 0; j < 3; ++j)
+            if (s + j < T.gS) {
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) gv[q] += r[q][j];
-          }
-        s = T.gS;
-      }
-      for (; s < T.gS; ++s) {
+              for (int q = 0; q < NQ; ++q) gv[q] += r[q][j];
+            }
+          s = T.gS;
+        }
+        for (; s < T.gS; ++s) {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) gv[q] += *reinterpret_cast<const f32x4*>(G + s * T.g_ss + gix[q]);
-      }
+          for (int q = 0; q < NQ; ++q) gv[q] += ld_slab4(G, s * T.g_ss + gix[q]);
+        }
+      };
+      if (T.g_bf16) slab_sum(bf16_t{});
+      else slab_sum(float{});
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -711,7 +735,8 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
     if (row < T.R && col < T.C) {
       const long i = (long)row * T.C + col;
       const long gi = (long)row * T.g_ld + col;
-      float g = T.gS > 0   ? slab_sum1(reinterpret_cast<const float*>(T.g), T.gS, T.g_ss, gi)
+      float g = T.gS > 0   ? (T.g_bf16 ? slab_sum1(reinterpret_cast<const bf16_t*>(T.g), T.gS, T.g_ss, gi)
+                                        : slab_sum1(reinterpret_cast<const float*>(T.g), T.gS, T.g_ss, gi))
                 : T.gS < 0 ? __int_as_float((int)T.g_ld)
                 : T.g_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(T.g)[gi])
                            : reinterpret_cast<const float*>(T.g)[gi];
@@ -1132,7 +1157,7 @@ LJS_API int ljs_colsum(const void* in, int is_bf16, int R, int C, long ld, void*
 // floats apart).  Requires C % 4 == 0, cb % 4 == 0, C % cb == 0 and 16-byte aligned buffers.
 LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, int C, void* out, int cb, long out_bs,
                             int accumulate, void* out_bf16, void* tail, void* tail_bf16, int tail_n, float tail_val,
-                            hipStream_t s) {
+                            int slabs_bf16, hipStream_t s) {
   if (tail_n < 0 || (tail_n > 0 && !tail)) return (int)hipErrorInvalidValue;
   if (C % 4 || cb % 4 || C % cb || slab_stride % 4 || out_bs % 4 || S < 1 || (((uintptr_t)slabs) & 15) ||
       (((uintptr_t)out) & 15))
@@ -1142,9 +1167,14 @@ LJS_API int ljs_slab_reduce(const void* slabs, int S, long slab_stride, int R, i
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
   if (out_bf16 && (((uintptr_t)out_bf16) & 7)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, s, (const float*)slabs, S, slab_stride, R, C,
-                     (float*)out, cb, out_bs, accumulate, (bf16_t*)out_bf16, (float*)tail, (bf16_t*)tail_bf16,
-                     tail_n, tail_val);
+  if (slabs_bf16)
+    hipLaunchKernelGGL(slab_reduce_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)slabs, S, slab_stride,
+                       R, C, (float*)out, cb, out_bs, accumulate, (bf16_t*)out_bf16, (float*)tail,
+                       (bf16_t*)tail_bf16, tail_n, tail_val);
+  else
+    hipLaunchKernelGGL(slab_reduce_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)slabs, S, slab_stride, R,
+                       C, (float*)out, cb, out_bs, accumulate, (bf16_t*)out_bf16, (float*)tail, (bf16_t*)tail_bf16,
+                       tail_n, tail_val);
   return (int)hipGetLastError();
 }
 
@@ -1357,7 +1387,7 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
     t.qn = r[10]; t.sn8 = r[11]; t.qt = r[12]; t.st8 = r[13];
     t.gS = r[9]; t.g_ld = r[14]; t.g_ss = r[15];
     if (t.gS == 0) t.g_ld = t.C;
-    if (t.gS > 0 && (t.g_bf16 || t.g_ld < t.C || t.g_ss < 1)) return (int)hipErrorInvalidValue;
+    if (t.gS > 0 && (t.g_ld < t.C || t.g_ss < 1)) return (int)hipErrorInvalidValue;   // (g_bf16: bf16 slabs)
     t.tiles_c = (t.C + 63) / 64;
     auto al = [](long ptr, long a) { return ptr % a == 0; };
     t.vec = t.C % 4 == 0 && al(t.p, 16) && al(t.m, 16) && al(t.v, 16) && al(t.sn, 8) && al(t.st, 8) &&

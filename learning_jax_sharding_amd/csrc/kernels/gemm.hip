@@ -63,6 +63,9 @@ constexpr int kBPtrs = 4096;
 // slab mode, the block's LAST item: its f32 tile leaves through the (then idle) LDS ring as whole
 // 256-byte rows (16-byte chunk XOR row), not as 64-byte pieces of 16 rows per store instruction
 constexpr int kSlabVst = 8192;
+// slab mode with bf16 slabs: each split's partial sum is rounded to bf16 once (summed in f32 by
+// slab_reduce / the fused Adam) -- half the bytes of f32 slabs written here and read there
+constexpr int kSlabBf16 = 16384;
 
 // Epilogue operand R applied to 8 consecutive output values (after bias / ReLU, f32):
 //   residual add: out = bf16(bf16(v) + bf16(R))   (the unfused "y = dense(x); y + R" in bf16:
@@ -701,8 +704,10 @@ gemm_dma_kernel(
   const bool psum_on = !OUT_F32 && p.psum != nullptr;
   float tsum = 0.f;
   const bool slabs = OUT_F32 && (p.flags & kSlabs);
+  const bool slab16 = slabs && (p.flags & kSlabBf16);
   const __amdgpu_buffer_rsrc_t rc = make_rsrc(
-      p.C, (OUT_F32 ? 4 : 2) * ((long)((slabs ? p.splitk * p.batch : p.batch) - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
+      p.C, (OUT_F32 && !slab16 ? 4 : 2) *
+               ((long)((slabs ? p.splitk * p.batch : p.batch) - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
   bool after_epi = false;
 
   // K-tile g landed in LDS for every wave, and every wave's fragment reads of tile g - 1
@@ -949,7 +954,18 @@ gemm_dma_kernel(
             const int r = 4 * q + (lane >> 4), c = lane & 15;
             const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + ((c ^ (r & 7)) << 4));
             const int row = m0 + r, col = n0 + 4 * c;
-            if (row < p.M && col + 4 <= p.N) {
+            if (slab16) {
+              const u32x2 h = u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+              if (row < p.M && col + 4 <= p.N) {
+                __builtin_amdgcn_raw_buffer_store_b64(h, rc, (int)((cb + (long)row * p.ldc + col) * 2), 0, 0);
+              } else if (row < p.M) {
+                bf16_t* C = reinterpret_cast<bf16_t*>(p.C) + cb + (long)row * p.ldc + col;
+                const float f[4] = {v[0], v[1], v[2], v[3]};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                  if (col + e < p.N) C[e] = f2bf(f[e]);
+              }
+            } else if (row < p.M && col + 4 <= p.N) {
               const u32x4 bits = __builtin_bit_cast(u32x4, v);
               __builtin_amdgcn_raw_buffer_store_b128(bits, rc, (int)((cb + (long)row * p.ldc + col) * 4), 0, 0);
             } else if (row < p.M) {
@@ -989,6 +1005,18 @@ gemm_dma_kernel(
           }
           acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           if (row >= p.M || col >= p.N) continue;
+          if (slab16) {
+            bf16_t* C16 = reinterpret_cast<bf16_t*>(p.C) + cb + (long)row * p.ldc + col;
+            if (vec && col + 4 <= p.N) {
+              const u32x2 h = u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+              __builtin_amdgcn_raw_buffer_store_b64(h, rc, (int)((cb + (long)row * p.ldc + col) * 2), 0, 0);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (col + e < p.N) C16[e] = f2bf(v[e]);
+            }
+            continue;
+          }
           float* C = reinterpret_cast<float*>(p.C) + cb + (long)row * p.ldc + col;
           if (p.splitk > 1 && !slabs) {
 #pragma unroll

@@ -63,7 +63,7 @@ _SIGS = {
     "ljs_pad_box": [c_void_p, c_void_p, c_int, _LP, _LP, _LP, _LP,
                     c_int, c_void_p],
     "ljs_slab_reduce": [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p,
-                        c_void_p, c_int, c_float, c_void_p],
+                        c_void_p, c_int, c_float, c_int, c_void_p],
     "ljs_softmax_rows_f32": [c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ljs_adam_f32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
@@ -246,11 +246,15 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     last split may run past K, where it reads zeros), so the split need not divide the K-tiles.
     """
     assert A.dtype in (torch.bfloat16, torch.float32) and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
-    out_f32 = C.dtype == torch.float32
+    # bf16 slabs (slab mode, C bf16): the f32-output slab kernels, each partial rounded once
+    slab16 = slabs and C.dtype == torch.bfloat16
+    out_f32 = C.dtype == torch.float32 or slab16
     if tile is None:
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc, A.dtype, bias, sBias, relu, accumulate,
                          zero_c, psum, res, acopy, slabs, sA, sB, sC, ldb)
-    if tile >= _PP_BASE:
+    if tile >= _PP_BASE and slab16:
+        tile = None
+    if tile is not None and tile >= _PP_BASE:
         rc, cnt = _gemm_pp(A, B, C, M, N, K, lda, ldb, ldc, a_kc, b_kc, batch, sA, sB, sC, bias, sBias, relu, alpha,
                            splitk, tile - _PP_BASE, a_off, b_off, c_off, slabs, b_list, psum, acopy)
         if rc == 0:
@@ -259,7 +263,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
         (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0) | (512 if slabs else 0) | \
-        (2048 if A.dtype == torch.float32 else 0) | (8192 if (slabs and _SLAB_VST) else 0)
+        (2048 if A.dtype == torch.float32 else 0) | (8192 if (slabs and _SLAB_VST) else 0) | (16384 if slab16 else 0)
     if res is not None:
         assert not out_f32 and res.dtype in (torch.bfloat16, torch.float32), (C.dtype, res.dtype)
         flags |= (64 if res_mode == "add" else 128) | (256 if res.dtype == torch.float32 else 0)
@@ -1125,7 +1129,7 @@ def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, ac
     ``out_bf16`` (same layout as ``out``) also receives the sums rounded to bf16.  ``tail`` (f32,
     and ``tail_bf16``) is filled with the constant ``tail_val`` by the same launch."""
     S, R, C = slabs.shape
-    assert slabs.dtype == torch.float32 and out.dtype == torch.float32 and slabs.is_contiguous()
+    assert slabs.dtype in (torch.float32, torch.bfloat16) and out.dtype == torch.float32 and slabs.is_contiguous()
     assert out_bf16 is None or (out_bf16.dtype == torch.bfloat16 and out_bf16.numel() == out.numel())
     tn = 0
     if tail is not None:
@@ -1134,7 +1138,8 @@ def slab_reduce(slabs: torch.Tensor, out: torch.Tensor, cb: int, out_bs: int, ac
                                      and tail_bf16.is_contiguous())
         tn = tail.numel()
     rc = lib().ljs_slab_reduce(_p(slabs), S, R * C, R, C, _p(out), cb, out_bs, int(accumulate), _p(out_bf16),
-                               _p(tail), _p(tail_bf16 if tn else None), tn, float(tail_val), _stream(out))
+                               _p(tail), _p(tail_bf16 if tn else None), tn, float(tail_val),
+                               int(slabs.dtype == torch.bfloat16), _stream(out))
     _ck(rc, "slab_reduce")
 
 
@@ -1539,8 +1544,10 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
         R, C = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
         if isinstance(g, SlabGrad):
             # the weight gradient is still its split-K slabs: the kernel sums them (no combine)
-            assert g.shape == tuple(p.shape) and g.slabs.dtype == torch.float32 and g.slabs.is_contiguous()
-            gsrc = (g.slabs.data_ptr() + 4 * g.offset, 0, g.S, g.ld, g.slab_stride)
+            assert g.shape == tuple(p.shape) and g.slabs.dtype in (torch.float32, torch.bfloat16) \
+                and g.slabs.is_contiguous()
+            es = g.slabs.element_size()
+            gsrc = (g.slabs.data_ptr() + es * g.offset, int(es == 2), g.S, g.ld, g.slab_stride)
         elif isinstance(g, ConstGrad):
             assert g.shape == tuple(p.shape)
             bits = int(np.asarray(g.value, dtype=np.float32).view(np.int32))

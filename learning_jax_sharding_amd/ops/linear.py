@@ -209,6 +209,14 @@ def _defer_ok(*ts) -> bool:
     return d is not None and all(t is not None and t.dtype == torch.float32 and _key(t) in d["safe"] for t in ts)
 
 
+# split-K weight-gradient slabs in bf16 (LJS_SLAB_BF16=1, default): each split's partial sum is
+# rounded once and the S partials are summed in f32 (slab_reduce / the fused Adam), so dW carries
+# at most the error of the reference's one bf16 rounding of the whole sum (bf16 dot output,
+# case6_attention.py's Dense(dtype=bf16) backward) spread over S smaller partials -- and the slab
+# stream the GEMM writes and Adam re-reads is halved (63 -> 31 MB per B=64 step)
+_SLAB_DT = torch.bfloat16 if os.environ.get("LJS_SLAB_BF16", "1") == "1" else torch.float32
+
+
 def _dw_slabs_wmajor(xb: torch.Tensor, dys, T: int, K: int, N: int, ws, pend):
     """The weight gradients xb^T @ dys[i] of weight-major cotangents dys [nw][T][N] (a seq-major
     fused projection, ops.linear.token_outer) as ONE slab-mode launch (batch i, split s -> slab
@@ -219,7 +227,7 @@ def _dw_slabs_wmajor(xb: torch.Tensor, dys, T: int, K: int, N: int, ws, pend):
     tile, S, slab_mode = hip.pick_dw_slabs(K, nw * N, T)
     if not slab_mode or (_DW_SPLIT and T % (64 * _DW_SPLIT) == 0):
         return None
-    slabs = torch.empty((S, nw, K, N), dtype=torch.float32, device=xb.device)
+    slabs = torch.empty((S, nw, K, N), dtype=_SLAB_DT, device=xb.device)
     out = torch.empty((nw, K, N), dtype=torch.float32, device=xb.device)
     # dys: the nw [T][N] cotangents (separate tensors: q's from the attention backward, k's and
     # v's from the sequence gather's reduce-scatter), read through per-batch B pointers
@@ -256,7 +264,7 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
     tile, S, slab_mode = hip.pick_dw_slabs(K, Nt, T)
     if _DW_SPLIT and T % (64 * _DW_SPLIT) == 0:
         S, slab_mode = _DW_SPLIT, False
-    slabs = torch.empty((S, K, Nt), dtype=torch.float32, device=xb.device)
+    slabs = torch.empty((S, K, Nt), dtype=_SLAB_DT if slab_mode else torch.float32, device=xb.device)
     if slab_mode:  # one launch, split s of the token range into slab s (uneven last split)
         hip.gemm(xb, dy, slabs, K, Nt, T, K, ld, Nt, False, False, sC=K * Nt, splitk=S, tile=tile, slabs=True)
     else:
