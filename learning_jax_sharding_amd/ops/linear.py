@@ -209,12 +209,12 @@ def _defer_ok(*ts) -> bool:
     return d is not None and all(t is not None and t.dtype == torch.float32 and _key(t) in d["safe"] for t in ts)
 
 
-# split-K weight-gradient slabs in bf16 (LJS_SLAB_BF16=1, default): each split's partial sum is
+# split-K weight-gradient slabs in bf16 (LJS_SLAB_BF16=1, opt-in): each split's partial sum is
 # rounded once and the S partials are summed in f32 (slab_reduce / the fused Adam), so dW carries
 # at most the error of the reference's one bf16 rounding of the whole sum (bf16 dot output,
 # case6_attention.py's Dense(dtype=bf16) backward) spread over S smaller partials -- and the slab
 # stream the GEMM writes and Adam re-reads is halved (63 -> 31 MB per B=64 step)
-_SLAB_DT = torch.bfloat16 if os.environ.get("LJS_SLAB_BF16", "1") == "1" else torch.float32
+_SLAB_DT = torch.bfloat16 if os.environ.get("LJS_SLAB_BF16", "0") == "1" else torch.float32
 
 
 def _dw_slabs_wmajor(xb: torch.Tensor, dys, T: int, K: int, N: int, ws, pend):

@@ -36,13 +36,23 @@ _ROOT = os.path.dirname(_PKG)
 
 
 def _site(depth: int = 4) -> Tuple[str, ...]:
+    """The innermost ``depth`` framework frames of the current stack; when the innermost Python
+    frame is outside the framework (torch's autograd / dispatch code), it leads as ``[torch] ...``
+    so an op launched from inside torch (e.g. an autograd Function's output handling) is told
+    apart from one the framework line issued itself."""
     out = []
+    first = True
     for fr in reversed(traceback.extract_stack()[:-3]):
         f = os.path.abspath(fr.filename)
-        if f.startswith(_ROOT) and "aten_trace" not in f:
+        if "aten_trace" in f or "_python_dispatch" in f:
+            continue
+        if f.startswith(_ROOT):
             out.append(f"{os.path.relpath(f, _ROOT)}:{fr.lineno} {fr.name}")
             if len(out) >= depth:
                 break
+        elif first:
+            out.append(f"[torch] {os.path.basename(f)}:{fr.lineno} {fr.name}")
+        first = False
     return tuple(out)
 
 
