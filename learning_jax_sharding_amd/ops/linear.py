@@ -790,8 +790,14 @@ class _FFBlock(torch.autograd.Function):
 # and LDS reads of the K-loop, which costs more than the cast pass it saves.  Re-measured inside the
 # step with the bf16 copy shared out over the items: B=8 even (0.0898-0.0904 vs 0.0896-0.0899 ms),
 # B=16 and B=64 slower (profiles/PERF_NOTES.md)
-# "auto" (default): the register-staged form (see linear()); "1": every f32-A kernel; "0": off
-_CAST_ON_LOAD = os.environ.get("LJS_CAST_ON_LOAD", "auto")
+# Round 4, the register-staged form (the 256x128 tile: global f32 -> VGPR -> bf16 LDS image, the
+# bf16 copy stored from the same registers; bit-exact, tests/test_kernels_gpu.py
+# test_gemm_f32_a_register_staged): QKV 64.8 us vs 49.3 for cast + bf16 GEMM isolated, 73.2 vs
+# 55.4 in the step, B=64 0.2551-0.2578 vs 0.2351-0.2399 ms (gpurun_out/r4j) -- the f32 loads are
+# waited on one K-tile after their issue, where the LDS-DMA ring hides two.
+# "0" (default): the cast pass; "auto": the register-staged / ping-pong forms where they apply;
+# "1": every f32-A kernel
+_CAST_ON_LOAD = os.environ.get("LJS_CAST_ON_LOAD", "0")
 
 # order of the FF block's backward GEMMs after dA (dX, dW_out, dW_in): which operands are still
 # in the Infinity Cache when each runs.  dW_in right after dA (which it reads, 84 MB at the bench
