@@ -639,8 +639,19 @@ def ff_block(x, w_in, w_out, residual=None, fp8: bool = True):
         x = reshard_tile(x, xt.unshard([x.ndim - 1]), note="ff.x")
         xt = x.tile
     devs = xt.device_ids
-    wi = reshard_tile(w_in, TileAssignment.replicated(devs, 2), note="ff.w_in")
-    wo = reshard_tile(w_out, TileAssignment.replicated(devs, 2), note="ff.w_out")
+    rep = TileAssignment.replicated(devs, 2)
+    if fp8 and all(t.is_cuda for t in x.local.values()):
+        # sharded weights gathered as their shards' MX-fp8 shadows (a quarter of the f32 bytes,
+        # no per-step quantization of the gathered copy; parallel/weight_gather.gather_mx)
+        from ..parallel import weight_gather as _wg
+        gi, go = _wg.mx_eligible(w_in, rep), _wg.mx_eligible(w_out, rep)
+        wi = _wg.gather_mx(w_in, rep, gi, note="ff.w_in") if gi is not None else \
+            reshard_tile(w_in, rep, note="ff.w_in")
+        wo = _wg.gather_mx(w_out, rep, go, note="ff.w_out") if go is not None else \
+            reshard_tile(w_out, rep, note="ff.w_out")
+    else:
+        wi = reshard_tile(w_in, rep, note="ff.w_in")
+        wo = reshard_tile(w_out, rep, note="ff.w_out")
     self_res = residual is x
     r_loc = None
     if residual is not None and not self_res:

@@ -21,11 +21,11 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 __all__ = ["get", "get_stacked", "get_mx", "mx_eligible", "entry", "adopt", "mark_fresh", "kinds_of", "register_proxy",
-           "is_proxy"]
+           "register_mx_proxy", "is_proxy"]
 
 
 class _Entry:
-    __slots__ = ("ref", "bufs", "versions", "proxy", "shared")
+    __slots__ = ("ref", "bufs", "versions", "proxy", "shared", "mx")
 
     def __init__(self, w: torch.Tensor):
         self.ref = weakref.ref(w)
@@ -33,6 +33,7 @@ class _Entry:
         self.versions: Dict[str, int] = {}
         self.proxy = False
         self.shared = None   # proxies of ONE gathered buffer (virtual devices of a GPU): derived shadows
+        self.mx = None       # MX-fp8 proxies: {"QT": (q, s), "QN": (q, s)} gathered from the shards
 
 
 _REG: Dict[Tuple, _Entry] = {}
@@ -160,6 +161,17 @@ def is_proxy(w: torch.Tensor) -> bool:
     return e is not None and e.proxy
 
 
+def register_mx_proxy(w: torch.Tensor, mx: Dict[str, Tuple[torch.Tensor, torch.Tensor]]) -> None:
+    """``w`` (an uninitialised f32 tensor of the full weight's shape) stands for a weight whose
+    MX-fp8 shadows ``mx`` ("QT" and "QN": (codes, scales)) were all-gathered from the shards' own
+    (``parallel/weight_gather.gather_mx``): the MX GEMMs read them; anything needing the f32
+    values or a bf16 shadow raises."""
+    e = entry(w)
+    e.proxy = True
+    e.mx = dict(mx)
+    weakref.finalize(w, _drop, _key(w), e)
+
+
 def mx_eligible(w: torch.Tensor) -> bool:
     """Weights whose MX-fp8 shadows the fused Adam can keep (64 x 64 tiles of its 4-wide path)."""
     import os
@@ -176,6 +188,8 @@ def get_mx(w: torch.Tensor, kind: str):
     from . import fp8
     e = entry(w)
     if e.proxy:
+        if e.mx is not None and kind in e.mx:
+            return e.mx[kind]
         raise RuntimeError("MX-fp8 shadows of a gathered-weight proxy are not available (bf16 gather)")
     K, N = w.shape
     if kind not in e.bufs:

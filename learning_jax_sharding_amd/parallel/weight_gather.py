@@ -32,7 +32,7 @@ from ..sharding.shardings import sharding_from_tile
 from ..sharding.tile import TileAssignment
 from ..spmd import plan as _plan
 
-__all__ = ["eligible", "gather_bf16"]
+__all__ = ["eligible", "gather_bf16", "mx_eligible", "gather_mx"]
 
 _ON = os.environ.get("LJS_GATHER_SHADOWS", "1") == "1"
 # how the backward reduce-scatters ran (tests / diagnostics): one-pass slab sums vs combined grads
@@ -248,3 +248,68 @@ def gather_bf16(kernels: Sequence[ShardedArray], dst: TileAssignment, dim: int, 
     outs = _GatherBf16.apply((tuple(tuple(g) for g in groups), dim, devs, nw, n), *flat)
     return [ShardedArray(k.shape, k.dtype, sh, {d: outs[j * nw + i] for j, d in enumerate(devs)})
             for i, k in enumerate(kernels)]
+
+
+# ----------------------------------------------------------------------------- MX-fp8 shadow gather
+def mx_eligible(w: ShardedArray, dst: TileAssignment) -> Optional[int]:
+    """Gather dim when the f32 weight ``w`` (2-D, GPU shards) is all-gathered to ``dst`` along one
+    dim and every shard keeps MX-fp8 shadows (``shadow.mx_eligible``: 64-aligned shard shape, so
+    no 32-element MX block straddles a shard boundary); else None."""
+    if not _ON or w.ndim != 2 or w.dtype != torch.float32 or w.tile == dst or not w.local:
+        return None
+    from ..ops import shadow
+    if not all(t.is_cuda and shadow.mx_eligible(t) for t in w.local.values()):
+        return None
+    return _gather_dim(w.tile, dst, w.shape)
+
+
+class _GatherMx(torch.autograd.Function):
+    """f32 shards -> f32 proxies of the gathered weight whose MX-fp8 shadows are the shards' own,
+    all-gathered: for W [R][C] gathered along dim g, "QN" (codes [R][C], scales [R][C/32]: blocks
+    along C) is gathered along g and "QT" (codes [C][R], scales [C][R/32]: blocks along R) along
+    1 - g -- both exactly the full weight's MX quantization, since the 64-aligned shards hold whole
+    blocks.  A quarter of the f32 gather's bytes, and no per-step quantization of the gathered
+    weight.  The backward is the bf16-shadow gather's: the f32 gradient reduce-scattered."""
+
+    @staticmethod
+    def forward(ctx, meta, *flat):
+        groups, dim, devs, nw, n = meta
+        from ..ops import hip, shadow
+        parts = {}
+        for kind, gd in (("QN", dim), ("QT", 1 - dim)):
+            for j in (0, 1):   # codes, scales
+                loc = {d: shadow.get_mx(flat[i], kind)[j] for i, d in enumerate(devs)}
+                if _loopback(groups, loc):
+                    out = {}
+                    for grp in groups:
+                        buf = hip.concat_parts([loc[d] for d in grp], gd)
+                        for d in grp:
+                            out[d] = buf
+                else:
+                    out = C._run(C._Spec("all_gather", groups, dim=gd), loc)
+                parts[(kind, j)] = {d: (t if t.is_contiguous() else t.contiguous()) for d, t in out.items()}
+        R_loc, C_loc = flat[0].shape
+        R, Cn = (R_loc * n, C_loc) if dim == 0 else (R_loc, C_loc * n)
+        outs = []
+        for d, t in zip(devs, flat):
+            p = torch.empty((R, Cn), dtype=torch.float32, device=t.device)
+            shadow.register_mx_proxy(p, {k: (parts[(k, 0)][d], parts[(k, 1)][d]) for k in ("QN", "QT")})
+            outs.append(p)
+        ctx.meta = meta
+        return tuple(outs)
+
+    backward = staticmethod(_GatherBf16.backward)
+
+
+def gather_mx(w: ShardedArray, dst: TileAssignment, dim: int, note: str = "") -> ShardedArray:
+    """``w`` all-gathered along ``dim`` to ``dst`` as an MX-fp8-shadow proxy (see _GatherMx)."""
+    src = w.tile
+    groups = src.groups_along([dim])
+    n = src.tile_shape[dim]
+    t0 = next(iter(w.local.values()))
+    _plan.record("all_gather", dim=dim, groups=tuple(tuple(g) for g in groups),
+                 bytes_in=2 * t0.numel() + 2 * (t0.numel() // 32), note=f"{note}.mx_shadows", dtype="float8_e4m3fn")
+    devs = tuple(sorted(w.local))
+    outs = _GatherMx.apply((tuple(tuple(g) for g in groups), dim, devs, 1, n), *[w.local[d] for d in devs])
+    return ShardedArray(w.shape, w.dtype, sharding_from_tile(dst, like=[w.sharding]),
+                        {d: outs[j] for j, d in enumerate(devs)})

@@ -393,3 +393,44 @@ def test_block_gpu_local_first_kv_gather(host_devices, gpu_devices, monkeypatch)
         for name in gh[k]:
             a, b = gh[k][name], gg[k][name]
             np.testing.assert_allclose(b, a, rtol=5e-2, atol=5e-2 * np.abs(a).max(), err_msg=f"{k}/{name}")
+
+
+def _ff_fp8_run(mesh_shape, B=4, S=128, M=640, F=1280):
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd import nn
+    from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
+    from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
+    from learning_jax_sharding_amd.spmd import plan as _plan
+    rules = (("batch", "data"), ("embed", "model"), ("hidden", "model"))   # case6_attention.py:183-187
+    mesh = Mesh(create_device_mesh(mesh_shape), ("data", "model"))
+    model = nn.FeedForward(F, fp8=True)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (B, S, M))
+    params = model.init(ljs.random.PRNGKey(1), x)["params"]
+    params = ljs.device_put(params, nn.logical_to_mesh_sharding(nn.get_partition_spec(params), mesh, rules))
+    x = ljs.device_put(x, NamedSharding(mesh, P("data", "model")))
+
+    def loss(p):
+        y = model.apply({"params": p}, x, residual=x)
+        return (y.astype(ljs.numpy.float32) * y.astype(ljs.numpy.float32)).sum()
+
+    with mesh, nn.axis_rules(rules), _plan.record_plan() as rec:
+        val, g = ljs.value_and_grad(loss)(params)
+    notes = [st.info.get("note", "") for st in rec.steps]
+    return float(np.asarray(val)), ljs.tree_map(lambda a: np.asarray(a), nn.unbox(g)), notes
+
+
+def test_fp8_ff_block_2d_gathers_mx_shadows(gpu_devices):
+    """Reference rules on a 2x2 virtual mesh shard both FF weights along M over 'model': the
+    fused MX-fp8 block gathers the shards' MX-fp8 shadows (64-aligned shards hold whole MX
+    blocks, so the gathered codes are the full weight's quantization) instead of the f32
+    weights; loss and gradients match the 1x1 run."""
+    gpu_devices(1)
+    v1, g1, _ = _ff_fp8_run((1, 1))
+    gpu_devices(4)
+    v4, g4, notes = _ff_fp8_run((2, 2))
+    assert sum("mx_shadows" in n for n in notes) == 2, notes
+    assert abs(v1 - v4) <= 2e-2 * max(1.0, abs(v1)), (v1, v4)
+    for k in g1:
+        a, b = np.asarray(g1[k], np.float64), np.asarray(g4[k], np.float64)
+        rel = np.linalg.norm(b - a) / max(np.linalg.norm(a), 1e-12)
+        assert rel < 3e-2, (k, rel)
