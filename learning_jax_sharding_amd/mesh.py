@@ -15,7 +15,7 @@ import numpy as np
 
 from .runtime.devices import Device, process_index
 
-__all__ = ["Mesh", "current_mesh", "create_device_mesh"]
+__all__ = ["Mesh", "current_mesh", "create_device_mesh", "create_hybrid_device_mesh", "node_of"]
 
 _TLS = threading.local()
 
@@ -119,3 +119,54 @@ def create_device_mesh(mesh_shape: Sequence[int], devices: Optional[Sequence[Dev
     for i, d in enumerate(devs[:n]):
         arr[i] = d
     return arr.reshape(mesh_shape)
+
+
+def node_of(d: Device) -> int:
+    """The node (host) a device sits on: ranks are grouped ``LOCAL_WORLD_SIZE`` per node (torchrun's
+    launch order, one process per GPU), a single-controller process owns one node's GPUs."""
+    import os
+    lws = int(os.environ.get("LJS_LOCAL_WORLD_SIZE", os.environ.get("LOCAL_WORLD_SIZE", "0")) or 0)
+    if lws <= 0:
+        return 0
+    return d.process_index // lws
+
+
+def create_hybrid_device_mesh(mesh_shape: Sequence[int], dcn_mesh_shape: Sequence[int],
+                              devices: Optional[Sequence[Device]] = None) -> np.ndarray:
+    """``mesh_utils.create_hybrid_device_mesh``: a mesh of shape ``mesh_shape * dcn_mesh_shape``
+    (elementwise) whose ``dcn_mesh_shape`` factor spans nodes and whose ``mesh_shape`` factor
+    spans the GPUs of one node.  On MI355X the in-node factor rides the point-to-point xGMI links
+    (7 per GPU, ~153 GB/s each) and the cross-node factor the network, so an axis that carries the
+    step's large or frequent collectives (tensor / sequence parallel) belongs in ``mesh_shape``
+    and data parallelism - one bucketed gradient all-reduce per step - in ``dcn_mesh_shape``.
+    Nodes are ordered by their lowest device id, and a node's GPUs fill its sub-mesh row-major."""
+    mesh_shape = tuple(int(s) for s in mesh_shape)
+    dcn_mesh_shape = tuple(int(s) for s in dcn_mesh_shape)
+    if len(mesh_shape) != len(dcn_mesh_shape):
+        raise ValueError(f"mesh_shape {mesh_shape} and dcn_mesh_shape {dcn_mesh_shape} need the same rank")
+    from .runtime.devices import devices as _all
+    devs = list(_all() if devices is None else devices)
+    per_node = int(np.prod(mesh_shape)) if mesh_shape else 1
+    n_nodes = int(np.prod(dcn_mesh_shape)) if dcn_mesh_shape else 1
+    groups: "OrderedDict[int, list]" = OrderedDict()
+    for d in sorted(devs, key=lambda d: d.id):
+        groups.setdefault(node_of(d), []).append(d)
+    nodes = [g for g in groups.values()]
+    if len(nodes) == 1 and n_nodes > 1 and len(nodes[0]) >= per_node * n_nodes:
+        # one node's devices standing in for several (host / virtual devices): consecutive blocks
+        flat = nodes[0]
+        nodes = [flat[i * per_node:(i + 1) * per_node] for i in range(n_nodes)]
+    if len(nodes) < n_nodes or any(len(g) < per_node for g in nodes[:n_nodes]):
+        raise ValueError(f"hybrid mesh {mesh_shape} x dcn {dcn_mesh_shape} needs {n_nodes} nodes of {per_node} "
+                         f"devices; have {[len(g) for g in nodes]}")
+    nd = len(mesh_shape)
+    # [dcn_0, .., dcn_{k-1}, ici_0, .., ici_{k-1}] -> interleave (dcn_i, ici_i) -> merge each pair
+    blocks = np.empty(dcn_mesh_shape + mesh_shape, dtype=object)
+    for ni, node in enumerate(nodes[:n_nodes]):
+        sub = np.empty(per_node, dtype=object)
+        for i, d in enumerate(node[:per_node]):
+            sub[i] = d
+        blocks[np.unravel_index(ni, dcn_mesh_shape)] = sub.reshape(mesh_shape)
+    order = [a for i in range(nd) for a in (i, nd + i)]
+    out = blocks.transpose(order).reshape(tuple(a * b for a, b in zip(dcn_mesh_shape, mesh_shape)))
+    return out

@@ -73,5 +73,11 @@ def ones(shape, dtype=None, device=None):
     return _device_put(_torch.ones(shape, dtype=_dt.canonicalize(dtype) or _torch.float32), device)
 
 
-def arange(n, dtype=None):
-    return _device_put(_torch.arange(n, dtype=_dt.canonicalize(dtype) or _torch.int32))
+def arange(start, stop=None, step=None, dtype=None):
+    """``jnp.arange``: int32 for integer arguments, float32 if any is a float (JAX's defaults)."""
+    args = [a for a in (start, stop, step) if a is not None]
+    if dtype is None:
+        dtype = _torch.float32 if any(isinstance(a, float) for a in args) else _torch.int32
+    if stop is None:
+        start, stop = 0, start
+    return _device_put(_torch.arange(start, stop, 1 if step is None else step, dtype=_dt.canonicalize(dtype) or dtype))

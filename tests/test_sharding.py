@@ -82,3 +82,41 @@ def test_tile_assignment_from_coords():
     ta = TileAssignment.from_coords({0: (0,), 1: (1,), 2: (0,), 3: (1,)}, (2,))
     assert ta.holders((0,)) == (0, 2)
     assert TileAssignment.from_coords({0: (0,), 1: (0,), 2: (0,), 3: (1,)}, (2,)) is None
+
+
+def test_hybrid_device_mesh(host_devices, monkeypatch):
+    """mesh_utils.create_hybrid_device_mesh: the dcn factor of each axis spans nodes (outer), the
+    per-node factor a node's devices; nodes from LOCAL_WORLD_SIZE process groups, or consecutive
+    blocks of one process's devices."""
+    from learning_jax_sharding_amd.experimental import mesh_utils
+    from learning_jax_sharding_amd import mesh as M
+    host_devices(8)
+    m = mesh_utils.create_hybrid_device_mesh((1, 4), (2, 1))
+    assert [[d.id for d in r] for r in m] == [[0, 1, 2, 3], [4, 5, 6, 7]]
+    m = mesh_utils.create_hybrid_device_mesh((2, 2), (1, 2))
+    assert [[d.id for d in r] for r in m] == [[0, 1, 4, 5], [2, 3, 6, 7]]
+    with pytest.raises(ValueError):
+        mesh_utils.create_hybrid_device_mesh((2, 4), (2, 1))
+    # nodes from process groups: 4 processes x 2 devices, 2 processes per node
+    class D:
+        def __init__(self, i):
+            self.id, self.process_index = i, i // 2
+    devs = [D(i) for i in range(8)]
+    monkeypatch.setenv("LJS_LOCAL_WORLD_SIZE", "2")
+    m = M.create_hybrid_device_mesh((2, 2), (2, 1), devices=devs)
+    assert [[d.id for d in r] for r in m] == [[0, 1], [2, 3], [4, 5], [6, 7]]
+    assert [M.node_of(d) for d in devs] == [0, 0, 0, 0, 1, 1, 1, 1]
+
+
+def test_debug_print_and_callback(host_devices, capsys):
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd import debug
+    host_devices(4)
+    mesh = Mesh(create_device_mesh((2, 2)), ("a", "b"))
+    x = ljs.device_put(ljs.numpy.arange(8.0).reshape(2, 4), NamedSharding(mesh, P("a", "b")))
+    debug.print("sum={s} first={}", x[0, 0], s=x.sum())
+    seen = []
+    debug.callback(lambda v, k=None: seen.append((v.shape, float(k))), x, k=x.sum())
+    assert capsys.readouterr().out.strip() == "sum=28.0 first=0.0"
+    assert seen == [((2, 4), 28.0)]
+    assert ljs.numpy.arange(8).dtype == ljs.numpy.int32 and ljs.numpy.arange(0, 2, 0.5).shape == (4,)
