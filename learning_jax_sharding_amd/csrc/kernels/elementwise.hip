@@ -1195,6 +1195,14 @@ struct PadBox {
 template <typename T>
 __global__ __launch_bounds__(256) void pad_box_kernel(const T* __restrict__ src, T* __restrict__ out, PadBox b,
                                                       long total) {
+  if (b.nd == 1 && total < (1L << 31)) {   // (a vector: 32-bit index math)
+    const int lo = (int)b.lo[0], n = (int)b.size[0], ss = (int)b.sstride[0];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)total; i += gridDim.x * 256) {
+      const int rel = i - lo;
+      out[i] = (rel >= 0 && rel < n) ? src[rel * ss] : T(0);
+    }
+    return;
+  }
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     long r = i, so = 0;
     bool in = true;

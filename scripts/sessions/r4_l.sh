@@ -19,4 +19,6 @@ done
 cd /tmp
 export WORLD_SIZE=4 RANK=0 LOCAL_RANK=0 LJS_DIST_BACKEND=fake MASTER_ADDR=127.0.0.1
 step $O/prof_2d_fp8.log env MASTER_PORT=29781 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_2d_fp8 -o run -- python3 $R/bench.py --gpus 4 --mesh 2d --model layer --fp8 --steps 16 --warmup 4
+cd $R
+step $O/mfma_rate.log timeout -k 10 120 ./scripts/mfma_rate
 echo done
