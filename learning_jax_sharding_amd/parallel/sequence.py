@@ -16,6 +16,14 @@ Two schedules are provided on (batch, seq, heads, head_dim) arrays whose seq dim
   locally, dK/dV accumulators travel with their blocks and arrive home after the last
   hop.  Causal blocks entirely above the diagonal are skipped.
 
+* ``mode="ulysses"`` - DeepSpeed-Ulysses: ONE all-to-all per tensor moves q, k and v from
+  sequence-sharded to head-sharded (every device then holds the full sequence of H/n heads),
+  the flash kernel runs locally with no K/V traffic of its own, and one all-to-all brings the
+  output back to sequence sharding.  Per device it moves 3 + 1 tensors of (n-1)/n of its shard
+  (the all-gather plan receives (n-1) shards of K and V), and the attention kernels see the
+  single-device shape (all keys, whole heads) instead of S/n-query blocks against S keys.
+  Needs the head count divisible by n; the backward is the transposed all-to-alls.
+
 Memory per device is O(S/n) for K/V instead of O(S), the stepping stone to long-context
 training on 288 GB parts; on xGMI the hop is a point-to-point neighbour transfer, one link.
 Each hop's K/V transfer is issued on a side HIP stream before the current block's flash
@@ -39,7 +47,7 @@ from ..ops import kernels as K
 from ..spmd import plan as _plan
 from ..spmd.reshard import reshard_tile
 
-__all__ = ["context_parallel_attention", "ring_attention"]
+__all__ = ["context_parallel_attention", "ring_attention", "ulysses_attention"]
 
 
 def context_parallel_attention(q: ShardedArray, k: ShardedArray, v: ShardedArray, scale: Optional[float] = None,
@@ -48,7 +56,43 @@ def context_parallel_attention(q: ShardedArray, k: ShardedArray, v: ShardedArray
         return core.dot_product_attention(q, k, v, scale=scale, causal=causal)
     if mode == "ring":
         return ring_attention(q, k, v, scale=scale, causal=causal)
+    if mode == "ulysses":
+        return ulysses_attention(q, k, v, scale=scale, causal=causal)
     raise ValueError(f"unknown context-parallel mode {mode!r}")
+
+
+# ----------------------------------------------------------------------------- ulysses
+def _seq_to_heads(t):
+    """The tile of ``t`` [batch, seq, heads, d] with its sequence split moved onto the heads: the
+    device holding sequence block i of a group holds head block i of the full sequence."""
+    from ..sharding.tile import TileAssignment
+    ts = t.tile_shape
+    coords = {d: (c[0], 0, c[1]) + tuple(c[3:]) for d, c in t.coords.items()}
+    return TileAssignment.from_coords(coords, (ts[0], 1, ts[1]) + tuple(ts[3:]))
+
+
+def ulysses_attention(q: ShardedArray, k: ShardedArray, v: ShardedArray, scale: Optional[float] = None,
+                      causal: bool = False) -> ShardedArray:
+    """All-to-all (sequence <-> heads) attention over q's sequence sharding (see module doc); the
+    all-gather plan when the heads are already split or do not divide over the group."""
+    if scale is None:
+        scale = q.shape[-1] ** -0.5
+    qt = q.tile
+    if qt.tile_shape[3] > 1:
+        q = reshard_tile(q, qt.unshard([3]), note="ulysses.q")
+        qt = q.tile
+    n = qt.tile_shape[1]
+    if n == 1 or qt.tile_shape[2] != 1 or q.shape[2] % n:
+        return core.dot_product_attention(q, k, v, scale=scale, causal=causal)
+    ht = _seq_to_heads(qt)
+    if ht is None:
+        return core.dot_product_attention(q, k, v, scale=scale, causal=causal)
+    _plan.record("ulysses_attention", group=n, q_tiles=qt.tile_shape, head_tiles=ht.tile_shape)
+    qh = reshard_tile(q, ht, note="ulysses.q")
+    kh = reshard_tile(k, ht, note="ulysses.k")
+    vh = reshard_tile(v, ht, note="ulysses.v")
+    oh = core.dot_product_attention(qh, kh, vh, scale=scale, causal=causal)
+    return reshard_tile(oh, qt, note="ulysses.out")
 
 
 # ----------------------------------------------------------------------------- ring

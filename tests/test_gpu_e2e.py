@@ -226,7 +226,7 @@ def test_ring_attention_gpu_matches_allgather(gpu_devices, causal):
     cot = torch.randn(2, 256, 4, 64, generator=g)
     sh = NamedSharding(mesh, P("data", "model"))
     res = {}
-    for mode in ("allgather", "ring"):
+    for mode in ("allgather", "ring", "ulysses"):
         leaves = [_fresh_leaf(ljs.device_put(a, sh)) for a in arrs]
         out = SQ.context_parallel_attention(*leaves, causal=causal, mode=mode)
         loss = (out.astype(jnp.float32) * ljs.device_put(cot, sh)).sum()
@@ -239,9 +239,10 @@ def test_ring_attention_gpu_matches_allgather(gpu_devices, causal):
             loc = {d: gs[ai * n_loc + i].float() for i, d in enumerate(leaf.local)}
             glob.append(np.asarray(ShardedArray(leaf.shape, torch.float32, leaf.sharding, loc)))
         res[mode] = (np.asarray(out.astype(jnp.float32)), glob)
-    np.testing.assert_allclose(res["ring"][0], res["allgather"][0], rtol=2e-2, atol=2e-2)
-    for a, b in zip(res["ring"][1], res["allgather"][1]):
-        np.testing.assert_allclose(a, b, rtol=3e-2, atol=3e-2 * max(1.0, np.abs(b).max()))
+    for mode in ("ring", "ulysses"):
+        np.testing.assert_allclose(res[mode][0], res["allgather"][0], rtol=2e-2, atol=2e-2)
+        for a, b in zip(res[mode][1], res["allgather"][1]):
+            np.testing.assert_allclose(a, b, rtol=3e-2, atol=3e-2 * max(1.0, np.abs(b).max()))
 
 
 def test_captured_value_and_grad_fresh_every_replay(gpu_devices):

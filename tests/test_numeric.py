@@ -231,21 +231,27 @@ def test_fp8_emulation_close_to_bf16(host_devices):
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("mesh_shape", [(1, 4), (2, 2)])
 def test_ring_attention_matches_allgather(host_devices, causal, mesh_shape):
-    """Ring attention (K/V blocks travel, LSE-merged) == the all-gather-KV plan, values and
-    gradients, on the seq-sharded layout of case6."""
+    """Ring attention (K/V blocks travel, LSE-merged) and Ulysses (sequence <-> heads
+    all-to-alls around a local attention) == the all-gather-KV plan, values and gradients, on the
+    seq-sharded layout of case6."""
     host_devices(4)
     from learning_jax_sharding_amd.parallel import sequence as SQ
+    from learning_jax_sharding_amd.spmd import plan as _plan
     mesh = Mesh(create_device_mesh(mesh_shape), ("data", "model"))
     g = torch.Generator().manual_seed(0)
-    B, S, H, D = 2, 32, 2, 16
+    B, S, H, D = 2, 32, 4, 16
     arrs = [torch.randn(B, S, H, D, generator=g).bfloat16() for _ in range(3)]
     cot = torch.randn(B, S, H, D, generator=g)
     sh = NamedSharding(mesh, P("data", "model"))
     res = {}
-    for mode in ("allgather", "ring"):
+    for mode in ("allgather", "ring", "ulysses"):
         q, k, v = (ljs.device_put(a, sh) for a in arrs)
         leaves = [ljs.spmd.api._fresh_leaf(a) for a in (q, k, v)]
-        out = SQ.context_parallel_attention(*leaves, causal=causal, mode=mode)
+        with _plan.record_plan() as rec:
+            out = SQ.context_parallel_attention(*leaves, causal=causal, mode=mode)
+        if mode == "ulysses":
+            kinds = [st.kind for st in rec.steps]
+            assert "ulysses_attention" in kinds and kinds.count("all_to_all") == 4, kinds
         loss = (out.astype(jnp.float32) * ljs.device_put(cot, sh)).sum()
         ins = [t for l in leaves for t in l.local.values()]
         outs = [t for t in loss.local.values()]
@@ -259,9 +265,10 @@ def test_ring_attention_matches_allgather(host_devices, causal, mesh_shape):
             ga = ShardedArray(leaf.shape, torch.float32, leaf.sharding, {d: t.float() for d, t in loc.items()})
             glob.append(np.asarray(ga))
         res[mode] = (np.asarray(out.astype(jnp.float32)), glob)
-    np.testing.assert_allclose(res["ring"][0], res["allgather"][0], rtol=2e-2, atol=2e-2)
-    for a, b in zip(res["ring"][1], res["allgather"][1]):
-        np.testing.assert_allclose(a, b, rtol=3e-2, atol=3e-2 * max(1.0, np.abs(b).max()))
+    for mode in ("ring", "ulysses"):
+        np.testing.assert_allclose(res[mode][0], res["allgather"][0], rtol=2e-2, atol=2e-2)
+        for a, b in zip(res[mode][1], res["allgather"][1]):
+            np.testing.assert_allclose(a, b, rtol=3e-2, atol=3e-2 * max(1.0, np.abs(b).max()))
 
 
 @pytest.mark.parametrize("preset", ["gspmd2d", "megatron", "fsdp"])
