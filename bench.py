@@ -50,9 +50,10 @@ def parse():
     p.add_argument("--steps", type=int, default=48)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--min-warmup", type=int, default=int(os.environ.get("LJS_BENCH_MIN_WARM", "64")),
-                   help="untimed steps in all before the timed region, at least (the GPU clock has not ramped "
-                        "after a few ms of work: --steps 20 --warmup 5 read 0.255-0.262 ms where --warmup 40 read "
-                        "0.233-0.237, gpurun_out/r3al); the JSON 'warmup' reports the total that ran")
+                   help="untimed steps in all before the timed region, at least (the first ~50 steps of a "
+                        "process run ~10 %% slower: --steps 20 --warmup 5 read 0.253-0.262 ms where 64 untimed "
+                        "steps read 0.227-0.238, gpurun_out/r3al, r4m; not the DVFS clock: 160 ms of scratch "
+                        "GEMMs before the warmup changed nothing); the JSON 'warmup' reports the total that ran")
     p.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("LJS_BENCH_BPG", "64")))
     p.add_argument("--seq", type=int, default=256)
     p.add_argument("--dim", type=int, default=640)

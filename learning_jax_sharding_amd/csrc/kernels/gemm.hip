@@ -763,6 +763,24 @@ gemm_dma_kernel(
       }
   };
   static_assert(BK == 64, "two k-steps per K-tile");
+  // LJS_GEMM_PIN: the k-step 1 fragments (la / lb) are redefined through an empty asm right after
+  // the k-step 0 MFMAs (a sched_barrier keeps it there).  The compiler then places its lgkmcnt
+  // wait for them at that point, where their reads are long done, instead of in front of the
+  // k-step 1 MFMAs -- where, with the next tile's fragment reads issued after the barrier still
+  // in flight (and an SMEM load on the item-change path), it could only emit lgkmcnt(0) and so
+  // exposed the new reads' LDS latency once per K-tile.
+#ifndef LJS_GEMM_PIN
+#define LJS_GEMM_PIN 1
+#endif
+  auto pin = [&](bf16x8* af, bf16x8* bfr) {
+#if LJS_GEMM_PIN
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii) asm volatile("" : "+v"(af[ii]));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bfr[j]));
+#endif
+  };
   // (wave tiles with more than 8 fragments per k-step -- 128x160's 32x160 -- keep the plain
   // loop: two fragment sets would not fit beside their epilogue registers; so do the
   // transposed-read weight-gradient kernels, 1-2 % slower pipelined while the k-contiguous
@@ -797,6 +815,7 @@ gemm_dma_kernel(
     }
     read_frags(f, 1, la, lb);
     mfmas(ka, kb);
+    pin(la, lb);
     // inside an item: DMA of tile f + NST into the stage of tile f (free once barrier f + 1 is
     // passed), issued in two halves around the k-step 1 MFMAs.  An item's last tile does this
     // after its epilogue instead (below), so no fragments are live across the epilogue.
