@@ -54,6 +54,34 @@ __device__ __forceinline__ float row4_sum(float v) {
   return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 
+// Pair exchange of the swapped-operand MFMA epilogues: lanes l and l ^ 16 hold the two 16-column
+// blocks (a0, a1) of one output row; afterwards every lane holds 8 consecutive columns: lo = a0 of
+// itself and of lane l + 16 (even 16-lane rows), or a1 of lane l - 16 and of itself (odd rows).
+// One v_permlane16_swap per element (odd rows of the first operand <-> even rows of the second):
+// no ds_bpermute round trip through the LDS crossbar and no selects.
+#ifndef LJS_EPI_PLSWAP
+#define LJS_EPI_PLSWAP 1
+#endif
+__device__ __forceinline__ void pair_rows16(const f32x4& a0, const f32x4& a1, bool even, float (&v)[8]) {
+#if LJS_EPI_PLSWAP
+  (void)even;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a0[e]), __float_as_uint(a1[e]), false, false);
+    v[e] = __uint_as_float(r[0]);
+    v[4 + e] = __uint_as_float(r[1]);
+  }
+#else
+  const f32x4 keep = even ? a0 : a1, send = even ? a1 : a0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float recv = __shfl_xor(send[e], 16, 64);
+    v[e] = even ? keep[e] : recv;
+    v[4 + e] = even ? recv : keep[e];
+  }
+#endif
+}
+
 __device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

@@ -442,15 +442,12 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const f32x4 a0 = acc[i][2 * q], a1 = acc[i][2 * q + 1];
-      const f32x4 keep = even ? a0 : a1, send = even ? a1 : a0;
-      f32x4 recv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) recv[e] = __shfl_xor(send[e], 16, 64);
       float v[8];
+      pair_rows16(a0, a1, even, v);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[e] = (even ? keep[e] : recv[e]) + bv[e];
-        v[4 + e] = (even ? recv[e] : keep[e]) + bv[4 + e];
+        v[e] += bv[e];
+        v[4 + e] += bv[4 + e];
         if (relu) {
           v[e] = fmaxf(v[e], 0.f);
           v[4 + e] = fmaxf(v[4 + e], 0.f);

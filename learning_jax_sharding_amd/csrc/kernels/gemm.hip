@@ -888,16 +888,38 @@ gemm_dma_kernel(
       };
       load_r(0);
       float bvs[TN / 2][8];
+      // bias: this lane's 8 consecutive columns as one or two 16-byte loads (aligned bias rows;
+      // N % 8 == 0 here) instead of 8 scalar loads of each width
+      const bool bias_vec = has_bias && ((((uintptr_t)p.bias) & 15) == 0) && (p.sBias % 8) == 0;
 #pragma unroll
       for (int q = 0; q < TN / 2; ++q) {
         const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
+        const long bo = (long)w.b * p.sBias + col;
+        if (bias_vec && col + 8 <= p.N) {
+          if (bias_f32) {
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.bias) + bo);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.bias) + bo + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              bvs[q][e] = lo[e];
+              bvs[q][4 + e] = hi[e];
+            }
+          } else {
+            const u32x4 u = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.bias) + bo);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              bvs[q][2 * e] = __uint_as_float(u[e] << 16);
+              bvs[q][2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+            }
+          }
+          continue;
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           bvs[q][e] = 0.f;
           if (has_bias && col + e < p.N) {
-            const long bo = (long)w.b * p.sBias + col + e;
-            bvs[q][e] = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo]
-                                 : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo]);
+            bvs[q][e] = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo + e]
+                                 : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo + e]);
           }
         }
       }
@@ -911,16 +933,8 @@ gemm_dma_kernel(
           const f32x4 a0 = acc[ii][2 * q] * p.alpha, a1 = acc[ii][2 * q + 1] * p.alpha;
           acc[ii][2 * q] = f32x4{0.f, 0.f, 0.f, 0.f};
           acc[ii][2 * q + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
-          const f32x4 keep = even ? a0 : a1, send = even ? a1 : a0;
-          f32x4 recv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) recv[e] = __shfl_xor(send[e], 16, 64);
           float v[8];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = even ? keep[e] : recv[e];
-            v[4 + e] = even ? recv[e] : keep[e];
-          }
+          pair_rows16(a0, a1, even, v);
           u32x4 pk;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {

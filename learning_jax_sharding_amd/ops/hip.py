@@ -1530,9 +1530,6 @@ class ConstGrad:
         self.value, self.shape = float(value), tuple(shape)
 
 
-_ADAM_HEAVY_FIRST = os.environ.get("LJS_ADAM_HEAVY_FIRST", "1") == "1"
-
-
 def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step: bool = False) -> None:
     """In-place fused Adam over many params (one launch per 32): entries = [(p, g, m, v)].
 
@@ -1571,11 +1568,6 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
     step_i = step if step.dtype == torch.int32 else step.to(torch.int32)
     ticket = _workspace(step_i.device, "adam_ticket", 64 << 10) if increment_step else None  # two-level tickets
     rows = _early_adam(rows, step_i, lr, b1, b2, eps, wd, increment_step)
-    if _ADAM_HEAVY_FIRST:
-        # tiles of many-slab gradients first: workgroups are dispatched in block order, so the
-        # slow ones (dWo's 12-24 slabs vs 4-8 for dWqkv) start in the first round and the short
-        # ones fill in behind them instead of leaving them as the launch's tail
-        rows.sort(key=lambda r: -max(0, int(r[0][9])))
     for i in range(0, len(rows), 32):
         chunk = rows[i:i + 32]
         tab = np.asarray([r[0] for r in chunk], dtype=np.int64).reshape(-1)
