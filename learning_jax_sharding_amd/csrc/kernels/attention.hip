@@ -59,6 +59,15 @@ struct AttnArgs {
                      // LDS image as full 128-byte rows (stage_rows16 / flush_rows), LJS_ATTN_VST
 };
 
+// A/B switches (compile-time): the resident forward's key loop fully unrolled at 256 keys, and
+// the fused backward's dQ slices without per-slice guards when all 256 keys are valid
+#ifndef LJS_ATTN_FWD_UNROLL
+#define LJS_ATTN_FWD_UNROLL 1
+#endif
+#ifndef LJS_ATTN_DQ_UNGUARD
+#define LJS_ATTN_DQ_UNGUARD 1
+#endif
+
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // f32 pair arithmetic of the softmax / dS: packed v_pk_* (LJS_ATTN_PK=1) or two scalar ops
@@ -447,8 +456,16 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if ((a.Sk % BLK) == 0 && !a.causal) {
-    for (int kt = 0; kt < nkt; ++kt)
-      fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kt * BLK, qrow, lane);
+    if (LJS_ATTN_FWD_UNROLL && nkt == FKR / BLK) {
+      // 256 keys: the key loop fully unrolled, so a tile's K / V fragment reads can issue during
+      // the previous tile's softmax
+#pragma unroll
+      for (int kt = 0; kt < FKR / BLK; ++kt)
+        fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kt * BLK, qrow, lane);
+    } else {
+      for (int kt = 0; kt < nkt; ++kt)
+        fwd_tile<false>(a, st, Ks + kt * BLK * D, Vs + kt * BLK * D, qf, kt * BLK, qrow, lane);
+    }
   } else {
     for (int kt = 0; kt < nkt; ++kt) {
       const int kbase = kt * BLK;
@@ -1623,14 +1640,28 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       f32x4 dq[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
       // unrolled over the at most FK / 32 key slices: every LDS address is a lane offset plus an
       // immediate (the rolled loop recomputed the swizzled addresses, 12 VALU per slice)
+      if (LJS_ATTN_DQ_UNGUARD && nk32 == FK / 32) {
+        // all key slices valid (Sk == 256): no per-slice guard, so the fragment reads of later
+        // slices can issue ahead of earlier slices' MFMAs
   #pragma unroll
-      for (int s2 = 0; s2 < FK / 32; ++s2) {
-        if (s2 < nk32) {
+        for (int s2 = 0; s2 < FK / 32; ++s2) {
           bf16x8 sb = frag_tr_o(dSt, 32 * s2, off_q);
   #pragma unroll
           for (int i = 0; i < 2; ++i) {
             bf16x8 ka = frag_tr_o(Ks, 32 * s2, off_k[i]);
             dq[i] = mfma16x16x32(ka, sb, dq[i]);
+          }
+        }
+      } else {
+  #pragma unroll
+        for (int s2 = 0; s2 < FK / 32; ++s2) {
+          if (s2 < nk32) {
+            bf16x8 sb = frag_tr_o(dSt, 32 * s2, off_q);
+  #pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              bf16x8 ka = frag_tr_o(Ks, 32 * s2, off_k[i]);
+              dq[i] = mfma16x16x32(ka, sb, dq[i]);
+            }
           }
         }
       }

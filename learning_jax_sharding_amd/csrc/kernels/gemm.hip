@@ -763,14 +763,15 @@ gemm_dma_kernel(
       }
   };
   static_assert(BK == 64, "two k-steps per K-tile");
-  // LJS_GEMM_PIN: the k-step 1 fragments (la / lb) are redefined through an empty asm right after
+  // LJS_GEMM_PIN (off: neutral at B=64, +0.7 us on the 8-wave 128x128 QKV at B=8, gpurun_out/r4p):
+  // the k-step 1 fragments (la / lb) are redefined through an empty asm right after
   // the k-step 0 MFMAs (a sched_barrier keeps it there).  The compiler then places its lgkmcnt
   // wait for them at that point, where their reads are long done, instead of in front of the
   // k-step 1 MFMAs -- where, with the next tile's fragment reads issued after the barrier still
   // in flight (and an SMEM load on the item-change path), it could only emit lgkmcnt(0) and so
   // exposed the new reads' LDS latency once per K-tile.
 #ifndef LJS_GEMM_PIN
-#define LJS_GEMM_PIN 1
+#define LJS_GEMM_PIN 0
 #endif
   auto pin = [&](bf16x8* af, bf16x8* bfr) {
 #if LJS_GEMM_PIN
@@ -785,7 +786,8 @@ gemm_dma_kernel(
   // loop: two fragment sets would not fit beside their epilogue registers; so do the
   // transposed-read weight-gradient kernels, 1-2 % slower pipelined while the k-contiguous
   // forward / dX kernels gain 3-4 %: QKV 2561 45.3 -> 43.7 us, 1282 48.1 -> 46.1 us)
-  constexpr bool PIPE = TM + TN <= 8 && A_KC && B_KC;
+  // (one 8-wave block per CU has 256 VGPRs per wave: 10 fragments fit twice beside 24 accumulators)
+  constexpr bool PIPE = (TM + TN <= 8 || (NW == 8 && TM + TN <= 10)) && A_KC && B_KC;
   static_assert(!AREG || (PIPE && !OUT_F32 && RES == 0), "register-staged A: the pipelined bf16-output loop");
   if constexpr (AREG) {
     if (total == 1) a_commit();   // (tile 0 rounded into its stage before its barrier)
@@ -923,6 +925,10 @@ gemm_dma_kernel(
           }
         }
       }
+      // PLAIN: alpha 1, no bias, no ReLU (the QKV projection, dX GEMMs): no per-element multiply,
+      // add or max in the store loop (a wave-uniform choice between two instances)
+      auto store_item = [&](auto plain_tag) {
+        constexpr bool PLAIN = decltype(plain_tag)::value && RES == 0;
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) {
         if (ii + 1 < TM) load_r(ii + 1);
@@ -930,16 +936,22 @@ gemm_dma_kernel(
         for (int q = 0; q < TN / 2; ++q) {  // both halves of a row's 128 B back to back
           const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
           const float* bv = bvs[q];
-          const f32x4 a0 = acc[ii][2 * q] * p.alpha, a1 = acc[ii][2 * q + 1] * p.alpha;
+          f32x4 a0 = acc[ii][2 * q], a1 = acc[ii][2 * q + 1];
+          if constexpr (!PLAIN) {
+            a0 *= p.alpha;
+            a1 *= p.alpha;
+          }
           acc[ii][2 * q] = f32x4{0.f, 0.f, 0.f, 0.f};
           acc[ii][2 * q + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
           float v[8];
           pair_rows16(a0, a1, even, v);
           u32x4 pk;
+          if constexpr (!PLAIN) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            v[e] += bv[e];
-            if (relu) v[e] = fmaxf(v[e], 0.f);
+            for (int e = 0; e < 8; ++e) {
+              v[e] += bv[e];
+              if (relu) v[e] = fmaxf(v[e], 0.f);
+            }
           }
           if constexpr (RES != 0) apply_res8(v, p.flags, rv[ii & 1][q][0], rv[ii & 1][q][0], rv[ii & 1][q][RES == 2 ? 1 : 0]);
 #pragma unroll
@@ -955,6 +967,12 @@ gemm_dma_kernel(
           }
         }
       }
+      };
+#ifndef LJS_GEMM_PLAIN_EPI
+#define LJS_GEMM_PLAIN_EPI 1
+#endif
+      if (LJS_GEMM_PLAIN_EPI && RES == 0 && p.alpha == 1.f && !has_bias && !relu) store_item(std::true_type{});
+      else store_item(std::false_type{});
       if (psum_on) {
         // fused loss reduction: this wave's share of sum(C) -- of the bf16 values just stored --
         // to its own slot (one store per wave, counted in the next K-step's vmcnt)
@@ -1107,6 +1125,9 @@ LJS_DMA_INST_64(4)
 #undef LJS_DMA_INST_64
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, false)
 LJS_DMA_INST(256, 128, 4, 2, 3, true, true, true)
+// 256x192, 8 waves of 64x96, 2 stages (112 KiB): 7 DMA pieces and 20 fragment reads per wave per
+// 48 MFMAs (256x128: 6 and 16 per 32); [T][1536] outputs are 2 items per block
+LJS_DMA_INST(256, 192, 4, 2, 2, true, true, false)
 // weight gradients (m/n-contiguous operands, f32 slabs): 256-wide tiles, 8 waves, 3 stages, one
 // block per CU -- 48 KiB of operands per 64-deep K-tile for twice the MFMA work of 128x128
 LJS_DMA_INST(256, 128, 4, 2, 3, false, false, true)
@@ -1313,12 +1334,26 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if ((tile == 643 || tile == 644) && !(dma_ok && dma_store_ok)) tile = 64;
   if ((tile == 2563 || tile == 12856) && !(!a_kc && !b_kc && out_f32)) tile = 1282;
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
+  if (tile == 2562 && !(a_kc && b_kc && !out_f32 && !(flags & (kResAdd | kResMask)))) tile = 1282;
+  if (tile == 2562 && batch > 1) {
+    // weight-major batches side by side in C over contiguous B (the fused Q/K/V projection):
+    // one GEMM over N * batch columns
+    if (sA == 0 && sB == (long)N * ldb && sC == N && ldc == (long)N * batch && !bias) {
+      a.N = N * batch;
+      a.batch = 1;
+      N = a.N;
+      batch = 1;
+    } else {
+      tile = 2561;
+    }
+  }
   if (tile == 1602 && !(a_kc && b_kc && !out_f32 && a.splitk == 1)) tile = 1282;
   if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;
   // fused output sum (psum): LDS-DMA kernels with bf16 output only; one float per (item, wave)
   if (psum && !out_f32 && tile > 1000) {
-    const int bm = tile == 2561 ? 256 : 128, nw = (tile == 2561 || tile == 12883 || tile == 12884) ? 8 : 4;
-    const int bn = tile == 1602 ? 160 : 128;
+    const int bm = (tile == 2561 || tile == 2562) ? 256 : 128;
+    const int nw = (tile == 2561 || tile == 2562 || tile == 12883 || tile == 12884) ? 8 : 4;
+    const int bn = tile == 1602 ? 160 : tile == 2562 ? 192 : 128;
     a.psum = (float*)psum;
     if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch * a.splitk * nw;
   }
@@ -1328,6 +1363,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     e = launch_dma<128, 256, 2, 4, 3, false, false, true>(a, stream, 0);
   } else if (tile == 1602) {
     e = launch_dma_kk<128, 160, 4, 1, 2>(a, stream);
+  } else if (tile == 2562) {
+    e = launch_dma<256, 192, 4, 2, 2, true, true, false, 0>(a, stream, 0);
   } else if (tile == 2561) {
     if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);
     else e = launch_dma_kk<256, 128, 4, 2, 3>(a, stream);

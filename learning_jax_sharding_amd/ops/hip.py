@@ -358,6 +358,9 @@ def _psum_for(t: torch.Tensor):
 # fragment reads it beats the 128x128 x 2/CU kernel at the QKV projection (37.9 vs 40.4 us) and
 # the FF up-projection (60.7 vs 65.2 us; scripts/gemm_tiles_out.py)
 _TILE_2561 = os.environ.get("LJS_GEMM_TILE2561", "1") == "1"
+# 256x192 tile (8 waves of 64x96, 2 stages; a weight-major batch folded into one GEMM): fewer DMA
+# pieces and fragment reads per MFMA than 256x128, one stage less in flight (A/B: LJS_GEMM_TILE2562)
+_TILE_2562 = os.environ.get("LJS_GEMM_TILE2562", "0") == "1"
 # slab-mode GEMMs: the last item's f32 tile leaves through LDS as whole rows (kSlabVst)
 _SLAB_VST = os.environ.get("LJS_SLAB_VST", "1") == "1"
 
@@ -426,6 +429,10 @@ def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f3
             and ldc % 8 == 0 and tiles128 % 512 and (-(-M // 128) * (N // 160) * batch) % 512 == 0):
         return 1602
     if K % 64 == 0 and tiles128 >= 96 and (out_f32 or (N % 8 == 0 and ldc % 8 == 0)):
+        if (_TILE_2562 and a_kc and b_kc and not out_f32 and res is None and M >= 4096 and splitk <= 1
+                and (N * batch) % 192 == 0 and (batch == 1 or (bias is None and sA == 0 and sB == N * ldb
+                                                                and sC == N and ldc == N * batch))):
+            return 2562
         if _TILE_2561 and a_kc and b_kc and not out_f32 and M >= 4096 and N * batch >= 1024 and N % 128 == 0:
             return 2561
         if a_kc and b_kc and not out_f32 and tiles128 < 256 and splitk <= 1:

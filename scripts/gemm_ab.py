@@ -2,7 +2,7 @@
 the default tile of each case from scripts/gemm_pp_bench.py, medians of 7 rounds x 20 launches.
 Run once per build (``LJS_KERNELS_LIB=<variant .so>``), interleaving the processes.
 
-    python scripts/gemm_ab.py [case ...]     cases: qkv out dh dwqkv dwo (default: all)
+    python scripts/gemm_ab.py [case ...]     cases: qkv out dh dwqkv dwo, or case:tile (default: all)
 """
 import os
 import sys
@@ -15,12 +15,14 @@ def main():
     want = sys.argv[1:] or ["qkv", "out", "dh", "dwqkv", "dwo"]
     cs = gb.cases()
     tag = os.path.basename(os.path.dirname(os.environ.get("LJS_KERNELS_LIB", "default/x")))
-    for name in want:
+    for spec in want:
+        name, _, t = spec.partition(":")       # "qkv:2562" times that tile instead of the default
         mk, tiles, flops = cs[name]
-        fn = mk(tiles[-1])
+        tile = int(t) if t else tiles[-1]
+        fn = mk(tile)
         v = sorted(gb.timeit(fn) for _ in range(7))
         med = v[len(v) // 2]
-        print(f"{tag:10s} {name:6s} tile {tiles[-1]}: {med:7.2f} us ({flops / med / 1e6:6.0f} TF, min {v[0]:.2f})",
+        print(f"{tag:10s} {name:6s} tile {tile}: {med:7.2f} us ({flops / med / 1e6:6.0f} TF, min {v[0]:.2f})",
               flush=True)
 
 

@@ -34,7 +34,7 @@ def _stored(mat, kc_rowmajor: bool):
 
 @pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (0, 0), (1, 0), (0, 1)])
 @pytest.mark.parametrize("out_f32", [0, 1])
-@pytest.mark.parametrize("tile", [64, 128, 2561, 1284, 1282, 12883, 12884, 1602, 643, 644, 2563, 12856])
+@pytest.mark.parametrize("tile", [64, 128, 2561, 2562, 1284, 1282, 12883, 12884, 1602, 643, 644, 2563, 12856])
 @pytest.mark.parametrize("M,N,K", [(256, 192, 320), (136, 72, 40), (512, 1536, 640), (304, 136, 128), (384, 640, 512)])
 def test_gemm_layouts(hip, a_kc, b_kc, out_f32, tile, M, N, K):
     A = _rand(M, K, seed=1)
@@ -66,6 +66,24 @@ def test_gemm_dma_splitk_batched_broadcast(hip, tile):
     out = torch.empty((500, 320), dtype=torch.bfloat16, device=dev)
     hip.gemm(row, W, out, 500, 320, 256, 0, 256, 320, True, True, tile=tile)
     torch.testing.assert_close(out.float(), (row.float() @ W.float().t()).expand(500, 320), rtol=2e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("M", [1024, 1000])
+def test_gemm_tile2562_folded_batch(hip, M):
+    """256x192 tile: a weight-major batch of 3 side by side in C (the fused Q/K/V projection) is
+    folded into one GEMM over 3N columns; ragged rows; bit-identical to the 256x128 kernel (same
+    k order per output element)."""
+    N, K, nb = 512, 640, 3
+    x = _rand(M, K, seed=21)
+    w = _rand(nb, N, K, seed=22)
+    out = torch.full((M, nb * N), float("nan"), dtype=torch.bfloat16, device=dev)
+    hip.gemm(x, w, out, M, N, K, K, K, nb * N, True, True, batch=nb, sA=0, sB=N * K, sC=N, tile=2562)
+    ref = torch.full_like(out, float("nan"))
+    hip.gemm(x, w, ref, M, N, K, K, K, nb * N, True, True, batch=nb, sA=0, sB=N * K, sC=N, tile=2561)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    f = torch.einsum("mk,bnk->mbn", x.float(), w.float()).reshape(M, nb * N)
+    torch.testing.assert_close(out.float(), f, rtol=2e-2, atol=2e-2 * math.sqrt(K))
 
 
 def test_gemm_identity_asymmetric(hip):
