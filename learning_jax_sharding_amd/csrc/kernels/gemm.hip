@@ -925,10 +925,6 @@ gemm_dma_kernel(
           }
         }
       }
-      // PLAIN: alpha 1, no bias, no ReLU (the QKV projection, dX GEMMs): no per-element multiply,
-      // add or max in the store loop (a wave-uniform choice between two instances)
-      auto store_item = [&](auto plain_tag) {
-        constexpr bool PLAIN = decltype(plain_tag)::value && RES == 0;
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) {
         if (ii + 1 < TM) load_r(ii + 1);
@@ -936,22 +932,16 @@ gemm_dma_kernel(
         for (int q = 0; q < TN / 2; ++q) {  // both halves of a row's 128 B back to back
           const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
           const float* bv = bvs[q];
-          f32x4 a0 = acc[ii][2 * q], a1 = acc[ii][2 * q + 1];
-          if constexpr (!PLAIN) {
-            a0 *= p.alpha;
-            a1 *= p.alpha;
-          }
+          const f32x4 a0 = acc[ii][2 * q] * p.alpha, a1 = acc[ii][2 * q + 1] * p.alpha;
           acc[ii][2 * q] = f32x4{0.f, 0.f, 0.f, 0.f};
           acc[ii][2 * q + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
           float v[8];
           pair_rows16(a0, a1, even, v);
           u32x4 pk;
-          if constexpr (!PLAIN) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              v[e] += bv[e];
-              if (relu) v[e] = fmaxf(v[e], 0.f);
-            }
+          for (int e = 0; e < 8; ++e) {
+            v[e] += bv[e];
+            if (relu) v[e] = fmaxf(v[e], 0.f);
           }
           if constexpr (RES != 0) apply_res8(v, p.flags, rv[ii & 1][q][0], rv[ii & 1][q][0], rv[ii & 1][q][RES == 2 ? 1 : 0]);
 #pragma unroll
@@ -967,12 +957,6 @@ gemm_dma_kernel(
           }
         }
       }
-      };
-#ifndef LJS_GEMM_PLAIN_EPI
-#define LJS_GEMM_PLAIN_EPI 1
-#endif
-      if (LJS_GEMM_PLAIN_EPI && RES == 0 && p.alpha == 1.f && !has_bias && !relu) store_item(std::true_type{});
-      else store_item(std::false_type{});
       if (psum_on) {
         // fused loss reduction: this wave's share of sum(C) -- of the bf16 values just stored --
         // to its own slot (one store per wave, counted in the next K-step's vmcnt)
