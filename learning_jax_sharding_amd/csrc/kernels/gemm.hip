@@ -694,14 +694,18 @@ gemm_dma_kernel(
   for (int s = 0; s < NST - 1; ++s)
     if (s < total) issue_next(s);
 
-  const bool relu = p.flags & 1;
-  const bool has_bias = (p.flags & 2) && p.splitk == 1;
+  // RES 3 (PLAIN): alpha 1, no bias / ReLU / fused sum -- a compile-time epilogue, so the kernel
+  // carries one store loop with nothing but the pair exchange, the bf16 packing and the stores
+  constexpr bool PLAIN = RES == 3;
+  constexpr bool HAS_R = RES == 1 || RES == 2;
+  const bool relu = !PLAIN && (p.flags & 1);
+  const bool has_bias = !PLAIN && (p.flags & 2) && p.splitk == 1;
   const bool bias_f32 = p.flags & 4;
   const bool accumulate = p.flags & 8;
   // flags & 32: output stores with sc1, which drop the written lines from the XCD's L2 (plain
   // stores keep them) so the output stream does not evict the operand panels other blocks reuse
   const bool st_sc1 = p.flags & 32;
-  const bool psum_on = !OUT_F32 && p.psum != nullptr;
+  const bool psum_on = !OUT_F32 && !PLAIN && p.psum != nullptr;
   float tsum = 0.f;
   const bool slabs = OUT_F32 && (p.flags & kSlabs);
   const bool slab16 = slabs && (p.flags & kSlabBf16);
@@ -872,10 +876,10 @@ gemm_dma_kernel(
       // processed, so only the first block's latency is exposed per item)
       u32x4 rv[2][TN / 2][RES == 2 ? 2 : 1];
       __amdgpu_buffer_rsrc_t rr;
-      if constexpr (RES != 0)
+      if constexpr (HAS_R)
         rr = make_rsrc(p.res, (RES == 2 ? 4 : 2) * ((long)(p.batch - 1) * p.sR + (long)(p.M - 1) * p.ldr + p.N));
       auto load_r = [&](int ii) {
-        if constexpr (RES != 0) {
+        if constexpr (HAS_R) {
 #pragma unroll
           for (int q = 0; q < TN / 2; ++q) {
             const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
@@ -932,18 +936,21 @@ gemm_dma_kernel(
         for (int q = 0; q < TN / 2; ++q) {  // both halves of a row's 128 B back to back
           const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
           const float* bv = bvs[q];
-          const f32x4 a0 = acc[ii][2 * q] * p.alpha, a1 = acc[ii][2 * q + 1] * p.alpha;
+          const f32x4 a0 = PLAIN ? acc[ii][2 * q] : acc[ii][2 * q] * p.alpha;
+          const f32x4 a1 = PLAIN ? acc[ii][2 * q + 1] : acc[ii][2 * q + 1] * p.alpha;
           acc[ii][2 * q] = f32x4{0.f, 0.f, 0.f, 0.f};
           acc[ii][2 * q + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
           float v[8];
           pair_rows16(a0, a1, even, v);
           u32x4 pk;
+          if constexpr (!PLAIN) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            v[e] += bv[e];
-            if (relu) v[e] = fmaxf(v[e], 0.f);
+            for (int e = 0; e < 8; ++e) {
+              v[e] += bv[e];
+              if (relu) v[e] = fmaxf(v[e], 0.f);
+            }
           }
-          if constexpr (RES != 0) apply_res8(v, p.flags, rv[ii & 1][q][0], rv[ii & 1][q][0], rv[ii & 1][q][RES == 2 ? 1 : 0]);
+          if constexpr (HAS_R) apply_res8(v, p.flags, rv[ii & 1][q][0], rv[ii & 1][q][0], rv[ii & 1][q][RES == 2 ? 1 : 0]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
           const int row = m0 + ii * 16 + (lane & 15);
@@ -1130,8 +1137,10 @@ LJS_DMA_INST_8W(4)
 // epilogue-operand variants (bf16 output, k-contiguous operands: forward and dX GEMMs)
 #define LJS_DMA_INST_RES(BM, BN, WM, WN, NST) \
   template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 1>(GemmArgs); \
-  template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 2>(GemmArgs);
+  template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 2>(GemmArgs); \
+  template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 3>(GemmArgs);
 LJS_DMA_INST_RES(128, 160, 4, 1, 2)
+LJS_DMA_INST_RES(256, 192, 4, 2, 2)
 LJS_DMA_INST_RES(256, 128, 4, 2, 3)
 LJS_DMA_INST_RES(128, 128, 2, 2, 2)
 LJS_DMA_INST_RES(128, 128, 2, 2, 4)
@@ -1186,6 +1195,10 @@ hipError_t launch_dma_kk(const GemmArgs& a, hipStream_t s) {
     if (a.flags & kResF32) return launch_dma<BM, BN, WM, WN, NST, true, true, false, 2>(a, s, 0);
     return launch_dma<BM, BN, WM, WN, NST, true, true, false, 1>(a, s, 0);
   }
+  // plain epilogue (RES 3): LJS_GEMM_PLAIN=0 keeps the general kernel
+  static const int plain_env = getenv("LJS_GEMM_PLAIN") ? atoi(getenv("LJS_GEMM_PLAIN")) : 1;
+  if (plain_env && a.alpha == 1.f && !(a.flags & 3) && !a.psum)
+    return launch_dma<BM, BN, WM, WN, NST, true, true, false, 3>(a, s, 0);
   return launch_dma<BM, BN, WM, WN, NST, true, true, false, 0>(a, s, 0);
 }
 
@@ -1348,7 +1361,7 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   } else if (tile == 1602) {
     e = launch_dma_kk<128, 160, 4, 1, 2>(a, stream);
   } else if (tile == 2562) {
-    e = launch_dma<256, 192, 4, 2, 2, true, true, false, 0>(a, stream, 0);
+    e = launch_dma_kk<256, 192, 4, 2, 2>(a, stream);
   } else if (tile == 2561) {
     if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);
     else e = launch_dma_kk<256, 128, 4, 2, 3>(a, stream);
