@@ -319,10 +319,12 @@ __global__ void colsum_bcast_kernel(const void* __restrict__ in, int is_bf16, in
 // GEMM's split-K partials rounded once each, summed here in f32)
 template <typename ST>
 __device__ __forceinline__ f32x4 ld_slab4(const ST* __restrict__ p, long e) {
+  // global (not flat) loads: they retire in order, so a loop can wait for an older group with a
+  // counted vmcnt while a younger one is in flight (a flat load forces vmcnt(0) + lgkmcnt(0))
   if constexpr (sizeof(ST) == 4) {
-    return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + e);
+    return *(const __attribute__((address_space(1))) f32x4*)(reinterpret_cast<const float*>(p) + e);
   } else {
-    const u32x2 r = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(p) + e);
+    const u32x2 r = *(const __attribute__((address_space(1))) u32x2*)(reinterpret_cast<const bf16_t*>(p) + e);
     return f32x4{__uint_as_float(r[0] << 16), __uint_as_float(r[0] & 0xffff0000u), __uint_as_float(r[1] << 16),
                  __uint_as_float(r[1] & 0xffff0000u)};
   }
@@ -537,6 +539,9 @@ __device__ __forceinline__ float slab_sum1(const ST* __restrict__ g, long gS, lo
   for (; s < gS; ++s) acc += ld(s * ss + i);
   return acc;
 }
+#ifndef LJS_ADAM_SLAB_DB
+#define LJS_ADAM_SLAB_DB 1
+#endif
 constexpr int kAdamMax = 32;
 // rows per Adam tile (x 64 columns): a template parameter (LJS_ADAM_ROWS = 16 / 32 / 64); smaller
 // tiles give more, shorter workgroups (a ragged last round of 64-row tiles idles most CUs)
@@ -583,9 +588,10 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
       ok[q] = row < T.R;
       gix[q] = ok[q] ? (long)row * T.g_ld + cbase : cbase;
       const long i = ok[q] ? (long)row * T.C + cbase : cbase;
-      mv[q] = *reinterpret_cast<const f32x4*>(Mm + i);
-      vv[q] = *reinterpret_cast<const f32x4*>(Vv + i);
-      pv[q] = *reinterpret_cast<const f32x4*>(P + i);
+      // (global, not flat, loads: see ld_slab4)
+      mv[q] = *(const __attribute__((address_space(1))) f32x4*)(Mm + i);
+      vv[q] = *(const __attribute__((address_space(1))) f32x4*)(Vv + i);
+      pv[q] = *(const __attribute__((address_space(1))) f32x4*)(P + i);
     }
     if (T.gS > 0) {
       // the slab sum of slab_reduce_kernel (same order, bit-identical) with the loads of all NQ
@@ -596,6 +602,37 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
 #pragma unroll
         for (int q = 0; q < NQ; ++q) gv[q] = ld_slab4(G, gix[q]);
         long s = 1;
+#if LJS_ADAM_SLAB_DB
+        // groups of 4 slabs double-buffered: group g + 1's loads are issued before group g is
+        // added, so a tile with S slabs pays ~S / 8 exposed round trips instead of S / 4 (dWo at
+        // B=64: 24 slabs).  Same additions in the same order as slab_reduce (bit-identical).
+        // (tiles of <= 32 rows: two 64-row buffers would spill)
+        const long full = NQ <= 2 ? 1 + ((T.gS - 1) / 4) * 4 : 1;   // slabs [1, full) in groups of 4
+        if (s < full) {
+          f32x4 va[NQ][4], vb[NQ][4];
+          auto load = [&](f32x4 (&v)[NQ][4], long s0) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[q][j] = ld_slab4(G, (s0 + j) * T.g_ss + gix[q]);
+          };
+          auto add = [&](f32x4 (&v)[NQ][4]) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) gv[q] += (v[q][0] + v[q][1]) + (v[q][2] + v[q][3]);
+          };
+          load(va, s);
+          for (;;) {
+            if (s + 4 < full) load(vb, s + 4);
+            add(va);
+            s += 4;
+            if (s >= full) break;
+            if (s + 4 < full) load(va, s + 4);
+            add(vb);
+            s += 4;
+            if (s >= full) break;
+          }
+        }
+#endif
         for (; s + 3 < T.gS; s += 4) {
           f32x4 v[NQ][4];
 #pragma unroll

@@ -695,20 +695,21 @@ gemm_dma_kernel(
     if (s < total) issue_next(s);
 
   // RES 3 (PLAIN): alpha 1, no bias / ReLU / fused sum -- a compile-time epilogue, so the kernel
-  // carries one store loop with nothing but the pair exchange, the bf16 packing and the stores
+  // carries one store loop with nothing but the pair exchange, the bf16 packing and the stores;
+  // for f32 output: f32 split-K slabs only (no atomics, accumulate, bias, bf16 slabs)
   constexpr bool PLAIN = RES == 3;
   constexpr bool HAS_R = RES == 1 || RES == 2;
   const bool relu = !PLAIN && (p.flags & 1);
   const bool has_bias = !PLAIN && (p.flags & 2) && p.splitk == 1;
   const bool bias_f32 = p.flags & 4;
-  const bool accumulate = p.flags & 8;
+  const bool accumulate = !PLAIN && (p.flags & 8);
   // flags & 32: output stores with sc1, which drop the written lines from the XCD's L2 (plain
   // stores keep them) so the output stream does not evict the operand panels other blocks reuse
   const bool st_sc1 = p.flags & 32;
   const bool psum_on = !OUT_F32 && !PLAIN && p.psum != nullptr;
   float tsum = 0.f;
-  const bool slabs = OUT_F32 && (p.flags & kSlabs);
-  const bool slab16 = slabs && (p.flags & kSlabBf16);
+  const bool slabs = OUT_F32 && (PLAIN || (p.flags & kSlabs));  // (f32 PLAIN: slab mode only)
+  const bool slab16 = !PLAIN && slabs && (p.flags & kSlabBf16);
   const __amdgpu_buffer_rsrc_t rc = make_rsrc(
       p.C, (OUT_F32 && !slab16 ? 4 : 2) *
                ((long)((slabs ? p.splitk * p.batch : p.batch) - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
@@ -987,7 +988,7 @@ gemm_dma_kernel(
             const int r = ii * 16 + (lane & 15);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-              *reinterpret_cast<f32x4*>(img + r * 256 + (((4 * j + g) ^ (r & 7)) << 4)) = acc[ii][j] * p.alpha;
+              *reinterpret_cast<f32x4*>(img + r * 256 + (((4 * j + g) ^ (r & 7)) << 4)) = PLAIN ? acc[ii][j] : acc[ii][j] * p.alpha;
           }
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           const long cb = (long)(w.split * p.batch + w.b) * p.sC;
@@ -1042,7 +1043,7 @@ gemm_dma_kernel(
           f32x4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            v[e] = acc[ii][j][e] * p.alpha + bv[e];
+            v[e] = PLAIN ? acc[ii][j][e] : acc[ii][j][e] * p.alpha + bv[e];
             if (relu) v[e] = fmaxf(v[e], 0.f);
           }
           acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1104,6 +1105,10 @@ gemm_dma_kernel(
   LJS_DMA_INST(128, 128, 2, 2, NST, false, true, false) LJS_DMA_INST(128, 128, 2, 2, NST, false, true, true)
 LJS_DMA_INST_LAYOUTS(2)
 LJS_DMA_INST_LAYOUTS(4)
+// f32 split-K slab kernels with the compile-time plain epilogue (weight gradients: m/n-contiguous)
+template __global__ void gemm_dma_kernel<128, 128, 2, 2, 2, false, false, true, 3>(GemmArgs);
+template __global__ void gemm_dma_kernel<128, 128, 2, 4, 4, false, false, true, 3>(GemmArgs);
+template __global__ void gemm_dma_kernel<128, 128, 2, 4, 3, false, false, true, 3>(GemmArgs);
 // 64x64 tiles (4 waves of 32x32, 3 or 4 stages): the small-M GEMMs of the reference shape
 // (2048 tokens), where 128x128 tiles leave most CUs idle
 #define LJS_DMA_INST_64(NST)                                                                               \
@@ -1200,6 +1205,16 @@ hipError_t launch_dma_kk(const GemmArgs& a, hipStream_t s) {
   if (plain_env && a.alpha == 1.f && !(a.flags & 3) && !a.psum)
     return launch_dma<BM, BN, WM, WN, NST, true, true, false, 3>(a, s, 0);
   return launch_dma<BM, BN, WM, WN, NST, true, true, false, 0>(a, s, 0);
+}
+
+// weight-gradient (m/n-contiguous, f32 output) launch: the plain split-K slab instance (RES 3)
+// when the slabs are f32 and nothing else is asked for (LJS_GEMM_PLAIN=0: the general kernel)
+template <int BM, int BN, int WM, int WN, int NST>
+hipError_t launch_slab(const GemmArgs& a, hipStream_t s) {
+  static const int plain_env = getenv("LJS_GEMM_PLAIN") ? atoi(getenv("LJS_GEMM_PLAIN")) : 1;
+  if (plain_env && (a.flags & kSlabs) && !(a.flags & (kSlabBf16 | 1 | 2 | 8 | 16)) && a.alpha == 1.f)
+    return launch_dma<BM, BN, WM, WN, NST, false, false, true, 3>(a, s, 0);
+  return launch_dma<BM, BN, WM, WN, NST, false, false, true, 0>(a, s, 0);
 }
 
 template <int BM, int BN, bool AK, bool BKc, bool OF>
@@ -1369,8 +1384,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     // 128x128, 8 waves, 3 / 4 stages (weight-grad MN x MN f32, or k-contiguous operands)
     const bool d4 = tile == 12884;
     if (!a_kc) {
-      if (d4) e = launch_dma<128, 128, 2, 4, 4, false, false, true>(a, stream, 0);
-      else e = launch_dma<128, 128, 2, 4, 3, false, false, true>(a, stream, 0);
+      if (d4) e = launch_slab<128, 128, 2, 4, 4>(a, stream);
+      else e = launch_slab<128, 128, 2, 4, 3>(a, stream);
     } else if (out_f32) {
       if (d4) e = launch_dma<128, 128, 2, 4, 4, true, true, true>(a, stream, 0);
       else e = launch_dma<128, 128, 2, 4, 3, true, true, true>(a, stream, 0);
@@ -1393,6 +1408,7 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
       e = hipErrorInvalidValue;
     }
   } else if (tile == 1284 || tile == 1282) {
+    if (tile == 1282 && !a_kc && !b_kc && out_f32) return (int)launch_slab<128, 128, 2, 2, 2>(a, stream);
     // (plain if/else, not ?: -- see the explicit-instantiation note above)
     if (a_kc && b_kc && !out_f32) {
       if (tile == 1284) return (int)launch_dma_kk<128, 128, 2, 2, 4>(a, stream);
