@@ -396,6 +396,30 @@ def test_adam_multi_and_shadows(hip):
     torch.testing.assert_close(shadow.entry(ws[1], create=False).bufs["N"], ws[1].bfloat16())
 
 
+@pytest.mark.parametrize("S", [3, 7, 11, 24])
+def test_adam_multi_slab_grads_bit_exact(hip, S):
+    """Adam reading split-K slabs directly (the kernel's slab sum, double-buffered in <= 32-row
+    tiles under LJS_ADAM_ROWS=32) equals slab_reduce + Adam on the combined gradient, bit for bit."""
+    shapes = [(640, 512), (512, 640)]
+    ws = [torch.randn(*sh, device=dev) for sh in shapes]
+    slabs = [torch.randn(S, *sh, device=dev) for sh in shapes]
+    ms = [torch.rand(*sh, device=dev) * 1e-2 for sh in shapes]
+    vs = [torch.rand(*sh, device=dev) * 1e-3 for sh in shapes]
+    w2, m2, v2 = [w.clone() for w in ws], [m.clone() for m in ms], [v.clone() for v in vs]
+    step = torch.full((), 3, dtype=torch.int32, device=dev)
+    gsl = [hip.SlabGrad(sl, S, 0, sh[1], sh[0] * sh[1], sh) for sl, sh in zip(slabs, shapes)]
+    hip.adam_multi(list(zip(ws, gsl, ms, vs)), step, 1e-3, 0.9, 0.999, 1e-8, 0.0)
+    gc = []
+    for sl, sh in zip(slabs, shapes):
+        g = torch.empty(*sh, device=dev)
+        hip.slab_reduce(sl, g, sh[1], sh[0] * sh[1])
+        gc.append(g)
+    hip.adam_multi(list(zip(w2, gc, m2, v2)), step, 1e-3, 0.9, 0.999, 1e-8, 0.0)
+    torch.cuda.synchronize()
+    for a, b in zip(ws + ms + vs, w2 + m2 + v2):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("with_bf16", [False, True])
 def test_adam_multi_mx_shadows(hip, with_bf16):
     """The fused Adam rewrites a weight's MX-fp8 shadows (blocks along rows and, transposed,
