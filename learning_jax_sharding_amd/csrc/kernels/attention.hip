@@ -1487,7 +1487,10 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
   }
 }
 
-template <bool KVDMA>
+// SW 1: the sweep instance of the common case alone (Sq % 64 == 0, Sk == 256, not causal, dQ
+// staged: a.vst == 1), so the kernel's register allocation is that one loop's, not the maximum
+// over the four sweep instances; SW 0: all four, chosen at run time
+template <bool KVDMA, int SW = 0>
 __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[FK * D];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[FK * D];
@@ -1699,7 +1702,10 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       }
     }
   };
-  if (a.vst == 1) {  // (LJS_ATTN_VST=2: dK / dV staged, dQ per lane -- A/B)
+  if constexpr (SW == 1) {
+    (void)wave_mask;
+    sweep(std::false_type{}, std::true_type{});
+  } else if (a.vst == 1) {  // (LJS_ATTN_VST=2: dK / dV staged, dQ per lane -- A/B)
     if (wave_mask) sweep(std::true_type{}, std::true_type{});
     else sweep(std::false_type{}, std::true_type{});
   } else {
@@ -1927,8 +1933,11 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
     f.out3 = (bf16_t*)dq; f.out3_sb = dqs[0]; f.out3_ss = dqs[1]; f.out3_sh = dqs[2];
     f.vst = vst_ok(dk, dks) && vst_ok(dv, dvs) && vst_ok(dq, dqs) ? attn_vst() : 0;
     static const int kv_dma = getenv("LJS_ATTN_BWD_KV_DMA") ? atoi(getenv("LJS_ATTN_BWD_KV_DMA")) : 0;
-    if (kv_dma) hipLaunchKernelGGL(attn_bwd_fused_kernel<true>, dim3(H, B), dim3(FT), 0, stream, f);
-    else hipLaunchKernelGGL(attn_bwd_fused_kernel<false>, dim3(H, B), dim3(FT), 0, stream, f);
+    static const int one_sweep = getenv("LJS_ATTN_BWD_SW") ? atoi(getenv("LJS_ATTN_BWD_SW")) : 1;
+    if (kv_dma) hipLaunchKernelGGL((attn_bwd_fused_kernel<true, 0>), dim3(H, B), dim3(FT), 0, stream, f);
+    else if (one_sweep && f.vst == 1 && Sq % BLK == 0 && Sk == FK && !causal)
+      hipLaunchKernelGGL((attn_bwd_fused_kernel<false, 1>), dim3(H, B), dim3(FT), 0, stream, f);
+    else hipLaunchKernelGGL((attn_bwd_fused_kernel<false, 0>), dim3(H, B), dim3(FT), 0, stream, f);
     return (int)hipGetLastError();
   }
   AttnArgs c = a;
