@@ -697,11 +697,12 @@ gemm_dma_kernel(
   // RES 3 (PLAIN): alpha 1, no bias / ReLU / fused sum -- a compile-time epilogue, so the kernel
   // carries one store loop with nothing but the pair exchange, the bf16 packing and the stores;
   // for f32 output: f32 split-K slabs only (no atomics, accumulate, bias, bf16 slabs)
-  constexpr bool PLAIN = RES == 3;
+  // RES 4 (BSUM): alpha 1, an f32 bias, no ReLU (the out-projection: bias + fused loss sum)
+  constexpr bool PLAIN = RES == 3, BSUM = RES == 4, NOALPHA = PLAIN || BSUM;
   constexpr bool HAS_R = RES == 1 || RES == 2;
-  const bool relu = !PLAIN && (p.flags & 1);
-  const bool has_bias = !PLAIN && (p.flags & 2) && p.splitk == 1;
-  const bool bias_f32 = p.flags & 4;
+  const bool relu = !PLAIN && !BSUM && (p.flags & 1);
+  const bool has_bias = BSUM || (!PLAIN && (p.flags & 2) && p.splitk == 1);
+  const bool bias_f32 = BSUM || (p.flags & 4);
   const bool accumulate = !PLAIN && (p.flags & 8);
   // flags & 32: output stores with sc1, which drop the written lines from the XCD's L2 (plain
   // stores keep them) so the output stream does not evict the operand panels other blocks reuse
@@ -937,8 +938,8 @@ gemm_dma_kernel(
         for (int q = 0; q < TN / 2; ++q) {  // both halves of a row's 128 B back to back
           const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
           const float* bv = bvs[q];
-          const f32x4 a0 = PLAIN ? acc[ii][2 * q] : acc[ii][2 * q] * p.alpha;
-          const f32x4 a1 = PLAIN ? acc[ii][2 * q + 1] : acc[ii][2 * q + 1] * p.alpha;
+          const f32x4 a0 = NOALPHA ? acc[ii][2 * q] : acc[ii][2 * q] * p.alpha;
+          const f32x4 a1 = NOALPHA ? acc[ii][2 * q + 1] : acc[ii][2 * q + 1] * p.alpha;
           acc[ii][2 * q] = f32x4{0.f, 0.f, 0.f, 0.f};
           acc[ii][2 * q + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
           float v[8];
@@ -1143,7 +1144,8 @@ LJS_DMA_INST_8W(4)
 #define LJS_DMA_INST_RES(BM, BN, WM, WN, NST) \
   template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 1>(GemmArgs); \
   template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 2>(GemmArgs); \
-  template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 3>(GemmArgs);
+  template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 3>(GemmArgs); \
+  template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 4>(GemmArgs);
 LJS_DMA_INST_RES(128, 160, 4, 1, 2)
 LJS_DMA_INST_RES(256, 192, 4, 2, 2)
 LJS_DMA_INST_RES(256, 128, 4, 2, 3)
@@ -1204,6 +1206,10 @@ hipError_t launch_dma_kk(const GemmArgs& a, hipStream_t s) {
   static const int plain_env = getenv("LJS_GEMM_PLAIN") ? atoi(getenv("LJS_GEMM_PLAIN")) : 1;
   if (plain_env && a.alpha == 1.f && !(a.flags & 3) && !a.psum)
     return launch_dma<BM, BN, WM, WN, NST, true, true, false, 3>(a, s, 0);
+  // bias (f32) + optional fused sum, alpha 1, no ReLU (RES 4)
+  static const int bsum_env = getenv("LJS_GEMM_BSUM") ? atoi(getenv("LJS_GEMM_BSUM")) : 1;
+  if (plain_env && bsum_env && a.alpha == 1.f && (a.flags & 7) == 6 && a.splitk == 1)
+    return launch_dma<BM, BN, WM, WN, NST, true, true, false, 4>(a, s, 0);
   return launch_dma<BM, BN, WM, WN, NST, true, true, false, 0>(a, s, 0);
 }
 
