@@ -1148,6 +1148,7 @@ LJS_DMA_INST_8W(4)
   template __global__ void gemm_dma_kernel<BM, BN, WM, WN, NST, true, true, false, 4>(GemmArgs);
 LJS_DMA_INST_RES(128, 160, 4, 1, 2)
 LJS_DMA_INST_RES(256, 192, 4, 2, 2)
+LJS_DMA_INST_RES(64, 64, 2, 2, 4)
 LJS_DMA_INST_RES(256, 128, 4, 2, 3)
 LJS_DMA_INST_RES(128, 128, 2, 2, 2)
 LJS_DMA_INST_RES(128, 128, 2, 2, 4)
@@ -1403,6 +1404,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     if (a_kc && b_kc && !out_f32 && (flags & (kResAdd | kResMask))) {
       e = hipErrorInvalidValue;  // no epilogue-operand variant at 64x64: use the register-staged tile
     } else {
+      // k-contiguous bf16 output: the compile-time epilogue instances (plain / bias + sum)
+      if (tile == 644 && a_kc && b_kc && !out_f32) return (int)launch_dma_kk<64, 64, 2, 2, 4>(a, stream);
 #define LJS_DMA(AK, BK_, OF)                                                                   \
   if (a_kc == AK && b_kc == BK_ && out_f32 == OF) {                                            \
     if (tile == 644) return (int)launch_dma<64, 64, 2, 2, 4, AK, BK_, OF>(a, stream, 0);       \
