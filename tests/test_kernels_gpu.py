@@ -573,7 +573,7 @@ def test_ticket_reductions_rearm(hip):
     torch.testing.assert_close(got, row.float() * 1000, rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("S,R,C,cb", [(8, 640, 1536, 512), (16, 512, 640, 640), (3, 40, 24, 8)])
+@pytest.mark.parametrize("S,R,C,cb", [(8, 640, 1536, 512), (16, 512, 640, 640), (3, 40, 24, 8), (24, 512, 640, 640), (11, 640, 512, 512), (30, 64, 64, 64)])
 def test_slab_reduce(hip, S, R, C, cb):
     slabs = _rand(S, R, C, dtype=torch.float32, seed=400 + S)
     nb = C // cb
