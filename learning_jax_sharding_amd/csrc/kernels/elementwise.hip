@@ -330,10 +330,6 @@ __device__ __forceinline__ f32x4 ld_slab4(const ST* __restrict__ p, long e) {
   }
 }
 
-#ifndef LJS_SLAB_BATCH
-#define LJS_SLAB_BATCH 1
-#endif
-constexpr int kSlabBatch = 25;  // slab_reduce: up to this many slabs loaded in one round trip
 template <typename ST>
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const ST* __restrict__ slabs, int S, long slab_stride,
                                                           int R, int C, float* __restrict__ out, int cb,
@@ -352,41 +348,16 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const ST* __restrict__
   const long n4 = (long)R * C / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const long e = 4 * i;
-    f32x4 acc;
-    if (LJS_SLAB_BATCH && S <= kSlabBatch) {
-      // every slab's load in flight at once (one round trip; the split counts are <= 24), then the
-      // additions in the order below (bit-identical)
-      f32x4 v[kSlabBatch];
-      const ST* sp = slabs + e;   // running pointer: no per-slab 64-bit offset registers
-#pragma unroll
-      for (int j = 0; j < kSlabBatch; ++j)
-        if (j < S) {
-          v[j] = ld_slab4(sp, 0);
-          sp += slab_stride;
-        }
-      acc = v[0];
-      int s = 1;
-#pragma unroll
-      for (int j = 1; j + 3 < kSlabBatch; j += 4)
-        if (j + 3 < S) {
-          acc += (v[j] + v[j + 1]) + (v[j + 2] + v[j + 3]);
-          s = j + 4;
-        }
-#pragma unroll
-      for (int j = 1; j < kSlabBatch; ++j)
-        if (j >= s && j < S) acc += v[j];
-    } else {
-      acc = ld_slab4(slabs, e);
-      int s = 1;
-      for (; s + 3 < S; s += 4) {  // 4 independent slab loads in flight
-        f32x4 v0 = ld_slab4(slabs, s * slab_stride + e);
-        f32x4 v1 = ld_slab4(slabs, (s + 1) * slab_stride + e);
-        f32x4 v2 = ld_slab4(slabs, (s + 2) * slab_stride + e);
-        f32x4 v3 = ld_slab4(slabs, (s + 3) * slab_stride + e);
-        acc += (v0 + v1) + (v2 + v3);
-      }
-      for (; s < S; ++s) acc += ld_slab4(slabs, s * slab_stride + e);
+    f32x4 acc = ld_slab4(slabs, e);
+    int s = 1;
+    for (; s + 3 < S; s += 4) {  // 4 independent slab loads in flight
+      f32x4 v0 = ld_slab4(slabs, s * slab_stride + e);
+      f32x4 v1 = ld_slab4(slabs, (s + 1) * slab_stride + e);
+      f32x4 v2 = ld_slab4(slabs, (s + 2) * slab_stride + e);
+      f32x4 v3 = ld_slab4(slabs, (s + 3) * slab_stride + e);
+      acc += (v0 + v1) + (v2 + v3);
     }
+    for (; s < S; ++s) acc += ld_slab4(slabs, s * slab_stride + e);
     const int r = (int)(e / C), c = (int)(e % C);
     float* dst = out + (long)(c / cb) * out_bs + (long)r * cb + (c % cb);
     if (accumulate) acc += *reinterpret_cast<const f32x4*>(dst);
@@ -571,9 +542,6 @@ __device__ __forceinline__ float slab_sum1(const ST* __restrict__ g, long gS, lo
 #ifndef LJS_ADAM_SLAB_DB
 #define LJS_ADAM_SLAB_DB 1
 #endif
-#ifndef LJS_ADAM_REM_BATCH
-#define LJS_ADAM_REM_BATCH 1
-#endif
 constexpr int kAdamMax = 32;
 // rows per Adam tile (x 64 columns): a template parameter (LJS_ADAM_ROWS = 16 / 32 / 64); smaller
 // tiles give more, shorter workgroups (a ragged last round of 64-row tiles idles most CUs)
@@ -665,35 +633,28 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
           }
         }
 #endif
-        // the 1-3 slabs past the whole groups: their loads ride along with the last group's (or,
-        // with no whole group left, with slab 0's) -- one round trip in all, not one more per
-        // remainder slab -- and are added one by one afterwards in slab_reduce's order
-        const long rem0 = T.gS - (T.gS - s) % 4;
-        const int nrem = LJS_ADAM_REM_BATCH ? (int)(T.gS - rem0) : 0;
-        f32x4 r[NQ][3];
-        auto load_rem = [&]() {
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-            if (j < nrem) {
-#pragma unroll
-              for (int q = 0; q < NQ; ++q) r[q][j] = ld_slab4(G, (rem0 + j) * T.g_ss + gix[q]);
-            }
-        };
-        if (nrem && s == rem0) load_rem();
         for (; s + 3 < T.gS; s += 4) {
           f32x4 v[NQ][4];
 #pragma unroll
           for (int q = 0; q < NQ; ++q)
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[q][j] = ld_slab4(G, (s + j) * T.g_ss + gix[q]);
-          if (nrem && s + 4 == rem0) load_rem();
 #pragma unroll
           for (int q = 0; q < NQ; ++q) gv[q] += (v[q][0] + v[q][1]) + (v[q][2] + v[q][3]);
         }
-        if (nrem) {
+        // the 1-3 remaining slabs: their loads issued together (one round trip, not one each),
+        // added one by one in slab_reduce's order
+        if (NQ <= 2 && s < T.gS) {   // (64-row tiles: registers would halve the occupancy)
+          f32x4 r[NQ][3];
 #pragma unroll
           for (int j = 0; j < 3; ++j)
-            if (j < nrem) {
+            if (s + j < T.gS) {
+#pragma unroll
+              for (int q = 0; q < NQ; ++q) r[q][j] = ld_slab4(G, (s + j) * T.g_ss + gix[q]);
+            }
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            if (s + j < T.gS) {
 #pragma unroll
               for (int q = 0; q < NQ; ++q) gv[q] += r[q][j];
             }

@@ -266,10 +266,11 @@ __device__ __forceinline__ f32x4 f8_mfma(const i32x8& a, const i32x8& b, const f
 // tiles + the per-row scale words), counted vmcnt, one raw barrier per K-tile.
 // FIX: the epilogue's flags as compile-time constants for the FF block's two epilogue-heavy
 // GEMMs (1: up projection = ReLU + both MX copies, no bf16 output; 2: dA = e4m3 ReLU mask +
-// both MX copies, no bf16 output); 0 reads p.flags at run time
+// both MX copies, no bf16 output; 3: plain f32 output, the weight gradients' split-K slabs); 0 reads
+// p.flags at run time
 template <int FIX>
 __device__ __forceinline__ int f8_flags(const F8Args& p) {
-  return FIX == 1 ? (1 | 256 | 512) : FIX == 2 ? (128 | 1024 | 256 | 512) : p.flags;
+  return FIX == 1 ? (1 | 256 | 512) : FIX == 2 ? (128 | 1024 | 256 | 512) : FIX == 3 ? 32 : p.flags;
 }
 
 template <int BM, int NST, int FIX = 0>
@@ -394,7 +395,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
   const bool relu = flags & 1, has_bias = flags & 2, bias_f32 = flags & 4, out_f32 = flags & 32;
   const bool res_add = flags & 64, res_mask = flags & 128, qout = flags & 256;
   const bool qtout = flags & 512, r_fp8 = flags & 1024;
-  void* const Cp = FIX ? nullptr : p.C;   // (the fixed epilogues write no bf16 output)
+  void* const Cp = (FIX == 1 || FIX == 2) ? nullptr : p.C;   // (those fixed epilogues write no bf16 output)
   const bool even = (g & 1) == 0;
   // the epilogue operand's 8 chunks per lane are all requested before the first is used (one
   // exposed latency per item instead of one per 16-row block); rows / columns outside the
@@ -640,6 +641,7 @@ template __global__ void gemm_mx_fp8_kernel<256, 2, 0>(F8Args);
 template __global__ void gemm_mx_fp8_kernel<256, 3, 0>(F8Args);
 template __global__ void gemm_mx_fp8_kernel<128, 2, 1>(F8Args);
 template __global__ void gemm_mx_fp8_kernel<128, 2, 2>(F8Args);
+template __global__ void gemm_mx_fp8_kernel<128, 2, 3>(F8Args);
 
 // ---------------------------------------------------------------------------- GEMM, 8 waves
 // Large-tile MX-fp8 GEMM: BM x BN output tile, 8 waves (WM x WN, each (BM/WM) x (BN/WN)), BK =
@@ -979,6 +981,13 @@ hipError_t launch_f8(const F8Args& a, int tiles, hipStream_t s) {
       hipLaunchKernelGGL((gemm_mx_fp8_kernel<128, 2, 2>), dim3(tiles), dim3(256), 0, s, a);
       return hipGetLastError();
     }
+  }
+  // plain f32 output (the FF weight gradients): its own instance -- the general kernel's 288
+  // registers (VGPR + AGPR) left one wave per SIMD (LJS_F8_FIX3=0 off)
+  static const int fix3 = getenv("LJS_F8_FIX3") ? atoi(getenv("LJS_F8_FIX3")) : 1;
+  if (fix3 && BM == 128 && NST == 2 && a.flags == 32 && a.bias == nullptr) {
+    hipLaunchKernelGGL((gemm_mx_fp8_kernel<128, 2, 3>), dim3(tiles), dim3(256), 0, s, a);
+    return hipGetLastError();
   }
   hipLaunchKernelGGL((gemm_mx_fp8_kernel<BM, NST, 0>), dim3(tiles), dim3(BM * 2), 0, s, a);
   return hipGetLastError();

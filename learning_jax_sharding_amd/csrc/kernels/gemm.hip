@@ -1357,7 +1357,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if (tile == 2562 && batch > 1) {
     // weight-major batches side by side in C over contiguous B (the fused Q/K/V projection):
     // one GEMM over N * batch columns
-    if (sA == 0 && sB == (long)N * ldb && sC == N && ldc == (long)N * batch && !bias) {
+    if (sA == 0 && sB == (long)N * ldb && sC == N && ldc == (long)N * batch && !bias &&
+        (long)N * batch * ldb < (1L << 30)) {   // (the folded B still addressable by 32-bit offsets)
       a.N = N * batch;
       a.batch = 1;
       N = a.N;
