@@ -1802,6 +1802,10 @@ static int g_fwd_nsub = -1;
 // K/V-resident forward (Sk <= 256): 0 off, 4 / 8 / 16 waves per block; -1 = read LJS_ATTN_FWD_RES
 static int g_fwd_res = -1;
 LJS_API void ljs_attn_set_fwd_res(int v) { g_fwd_res = v; }
+// fused backward's K / V staging: 1 = LDS-DMA in flight with the first query block, 0 = register
+// copy (default), -1 = read LJS_ATTN_BWD_KV_DMA
+static int g_bwd_kv_dma = -1;
+LJS_API void ljs_attn_set_bwd_kv_dma(int v) { g_bwd_kv_dma = v; }
 LJS_API void ljs_attn_set_fwd_nsub(int v) { g_fwd_nsub = v; }
 
 // strides are in elements, ordered (batch, seq, head); head_dim must be 64 and contiguous.
@@ -1932,11 +1936,13 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
     f.out2 = (bf16_t*)dv; f.out2_sb = dvs[0]; f.out2_ss = dvs[1]; f.out2_sh = dvs[2];
     f.out3 = (bf16_t*)dq; f.out3_sb = dqs[0]; f.out3_ss = dqs[1]; f.out3_sh = dqs[2];
     f.vst = vst_ok(dk, dks) && vst_ok(dv, dvs) && vst_ok(dq, dqs) ? attn_vst() : 0;
-    static const int kv_dma = getenv("LJS_ATTN_BWD_KV_DMA") ? atoi(getenv("LJS_ATTN_BWD_KV_DMA")) : 0;
+    if (g_bwd_kv_dma < 0) g_bwd_kv_dma = getenv("LJS_ATTN_BWD_KV_DMA") ? atoi(getenv("LJS_ATTN_BWD_KV_DMA")) : 0;
+    const int kv_dma = g_bwd_kv_dma;
     static const int one_sweep = getenv("LJS_ATTN_BWD_SW") ? atoi(getenv("LJS_ATTN_BWD_SW")) : 1;
-    if (kv_dma) hipLaunchKernelGGL((attn_bwd_fused_kernel<true, 0>), dim3(H, B), dim3(FT), 0, stream, f);
-    else if (one_sweep && f.vst == 1 && Sq % BLK == 0 && Sk == FK && !causal)
-      hipLaunchKernelGGL((attn_bwd_fused_kernel<false, 1>), dim3(H, B), dim3(FT), 0, stream, f);
+    const bool sw1 = one_sweep && f.vst == 1 && Sq % BLK == 0 && Sk == FK && !causal;
+    if (kv_dma && sw1) hipLaunchKernelGGL((attn_bwd_fused_kernel<true, 1>), dim3(H, B), dim3(FT), 0, stream, f);
+    else if (kv_dma) hipLaunchKernelGGL((attn_bwd_fused_kernel<true, 0>), dim3(H, B), dim3(FT), 0, stream, f);
+    else if (sw1) hipLaunchKernelGGL((attn_bwd_fused_kernel<false, 1>), dim3(H, B), dim3(FT), 0, stream, f);
     else hipLaunchKernelGGL((attn_bwd_fused_kernel<false, 0>), dim3(H, B), dim3(FT), 0, stream, f);
     return (int)hipGetLastError();
   }

@@ -106,6 +106,16 @@ def set_attention_fwd_resident(waves: int):
     fn(int(waves))
 
 
+def set_attention_bwd_kv_dma(enabled: Optional[bool]):
+    """Fused short-key backward: K / V land in LDS by LDS-DMA in flight with the first query block
+    (True) or through registers (False, the default); None re-reads ``LJS_ATTN_BWD_KV_DMA``.
+    Bit-identical either way."""
+    fn = lib().ljs_attn_set_bwd_kv_dma
+    fn.argtypes = [c_int]
+    fn.restype = None
+    fn(-1 if enabled is None else int(bool(enabled)))
+
+
 def set_attention_vst(enabled: Optional[bool]):
     """Attention output row tiles (forward O, backward dK / dV) stored through an LDS image as
     whole 128-byte rows with 16-byte stores (True), or per lane as 8-byte pieces (False); None

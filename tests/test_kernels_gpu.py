@@ -230,6 +230,28 @@ def test_attention_bwd_block_fused_matches_split(hip, attn_fwd_nsub, Sq, Sk, cau
         torch.testing.assert_close(a.float(), b_.float(), rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("B,Sq,Sk,H,causal,q_offset", [(4, 128, 256, 8, False, 0), (2, 256, 256, 4, False, 0),
+                                                     (2, 192, 128, 3, False, 0), (2, 130, 256, 3, True, 64)])
+def test_attention_bwd_fused_kv_dma_bit_exact(hip, B, Sq, Sk, H, causal, q_offset):
+    """Fused backward with K / V staged by LDS-DMA (both sweep instances: the one-sweep common
+    case at Sk == 256 and the general one) == the register-staged copy, bit for bit."""
+    D = 64
+    q, do = _rand(B, Sq, H, D, seed=1), _rand(B, Sq, H, D, seed=2)
+    k, v = _rand(B, Sk, H, D, seed=3), _rand(B, Sk, H, D, seed=4)
+    o, lse = hip.attn_fwd_lse(q, k, v, D ** -0.5, causal, q_offset)
+    hip.set_attention_bwd_fused(True)
+    outs = {}
+    try:
+        for kv in (True, False):
+            hip.set_attention_bwd_kv_dma(kv)
+            outs[kv] = hip.attn_bwd_block(q, k, v, o, do, lse, D ** -0.5, causal, q_offset)
+    finally:
+        hip.set_attention_bwd_kv_dma(None)
+        hip.set_attention_bwd_fused(None)
+    for a, b_, name in zip(outs[True], outs[False], ("dq", "dk", "dv")):
+        assert torch.equal(a, b_), name
+
+
 @pytest.mark.parametrize("B,Sq,Sk,H,causal,q_offset", [(8, 256, 256, 8, False, 0), (2, 192, 128, 3, False, 0),
                                                      (2, 130, 256, 3, True, 64), (1, 64, 100, 2, True, 0)])
 def test_attention_bwd_pair_matches_two_launches(hip, B, Sq, Sk, H, causal, q_offset):
