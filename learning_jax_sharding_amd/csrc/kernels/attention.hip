@@ -1524,8 +1524,8 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       dma_lds_x4(rv, ok ? (int)(((long)row * a.v_ss + c) * 2) : 0x7ffffff0, Vs + pc * 512);
     }
   } else {
-    // register-staged copy (the default: 45.98 vs 47.01 us for the LDS-DMA form at B=64,
-    // gpurun_out/r3aj; LJS_ATTN_BWD_KV_DMA=1 selects the DMA form)
+    // register-staged copy (the default from 3 query blocks up: 45.98 vs 47.01 us for the
+    // LDS-DMA form at B=64, gpurun_out/r3aj; the launch picks the DMA form for <= 128 queries)
 #pragma unroll
     for (int i = 0; i < FK * 8 / FT; ++i) {
       int c = tid + FT * i, row = c >> 3, c16 = c & 7;
@@ -1803,7 +1803,7 @@ static int g_fwd_nsub = -1;
 static int g_fwd_res = -1;
 LJS_API void ljs_attn_set_fwd_res(int v) { g_fwd_res = v; }
 // fused backward's K / V staging: 1 = LDS-DMA in flight with the first query block, 0 = register
-// copy (default), -1 = read LJS_ATTN_BWD_KV_DMA
+// copy, 2 = automatic (DMA for <= 128 queries, the default), -1 = read LJS_ATTN_BWD_KV_DMA
 static int g_bwd_kv_dma = -1;
 LJS_API void ljs_attn_set_bwd_kv_dma(int v) { g_bwd_kv_dma = v; }
 LJS_API void ljs_attn_set_fwd_nsub(int v) { g_fwd_nsub = v; }
@@ -1936,8 +1936,13 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
     f.out2 = (bf16_t*)dv; f.out2_sb = dvs[0]; f.out2_ss = dvs[1]; f.out2_sh = dvs[2];
     f.out3 = (bf16_t*)dq; f.out3_sb = dqs[0]; f.out3_ss = dqs[1]; f.out3_sh = dqs[2];
     f.vst = vst_ok(dk, dks) && vst_ok(dv, dvs) && vst_ok(dq, dqs) ? attn_vst() : 0;
-    if (g_bwd_kv_dma < 0) g_bwd_kv_dma = getenv("LJS_ATTN_BWD_KV_DMA") ? atoi(getenv("LJS_ATTN_BWD_KV_DMA")) : 0;
-    const int kv_dma = g_bwd_kv_dma;
+    if (g_bwd_kv_dma < 0) g_bwd_kv_dma = getenv("LJS_ATTN_BWD_KV_DMA") ? atoi(getenv("LJS_ATTN_BWD_KV_DMA")) : 2;
+    // 2 = automatic: the DMA form when a block sweeps at most two query blocks (the 2-D mesh's
+    // 128 local queries against 256 gathered keys: the K / V prologue is a third of the block's
+    // time there, and overlapping it with the first query block's loads measured 58.8 -> 57.1 us,
+    // 2-D rehearsal step 0.2963 -> 0.2937 ms median, gpurun_out/r4ab); at 256 queries it is
+    // neutral (0.2194 vs 0.2196 ms), so the register copy stays there
+    const bool kv_dma = g_bwd_kv_dma == 1 || (g_bwd_kv_dma == 2 && Sq <= 2 * BLK);
     static const int one_sweep = getenv("LJS_ATTN_BWD_SW") ? atoi(getenv("LJS_ATTN_BWD_SW")) : 1;
     const bool sw1 = one_sweep && f.vst == 1 && Sq % BLK == 0 && Sk == FK && !causal;
     if (kv_dma && sw1) hipLaunchKernelGGL((attn_bwd_fused_kernel<true, 1>), dim3(H, B), dim3(FT), 0, stream, f);

@@ -108,8 +108,8 @@ def set_attention_fwd_resident(waves: int):
 
 def set_attention_bwd_kv_dma(enabled: Optional[bool]):
     """Fused short-key backward: K / V land in LDS by LDS-DMA in flight with the first query block
-    (True) or through registers (False, the default); None re-reads ``LJS_ATTN_BWD_KV_DMA``.
-    Bit-identical either way."""
+    (True) or through registers (False); None re-reads ``LJS_ATTN_BWD_KV_DMA`` (default 2:
+    LDS-DMA when a block sweeps at most 128 queries).  Bit-identical either way."""
     fn = lib().ljs_attn_set_bwd_kv_dma
     fn.argtypes = [c_int]
     fn.restype = None
