@@ -26,7 +26,7 @@ import torch
 
 from . import hip
 from . import streams as _streams
-from .linear import _Linear, _bf16
+from .linear import _Linear, _bf16, _inv_perm
 
 __all__ = ["quantize_mx_ref", "dequantize_mx_ref", "mx_linear_ref", "quant_rows", "quant_cols", "gemm_mx",
            "linear_fp8", "fp8_dense", "E4M3_MAX", "BLOCK"]
@@ -429,10 +429,18 @@ class _FFBlockFp8(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_in, w_out, res):
-        lead = x.shape[:-1]
         M = x.shape[-1]
         F = w_in.shape[1]
-        x2 = _bf16(x.reshape(-1, M).contiguous())
+        # rows (tokens) in x's STORAGE order (every op of the block is per token except the weight
+        # gradients, which sum over all of them): a seq-major activation - the 2-D mesh's out
+        # projection output, stored [seq][batch][M] - is read without a transposing copy, and y
+        # (and dX) keep that order.  The residual, when it is x, is the same bf16 rows.
+        nd = x.dim()
+        o = hip.storage_order(x) if x.is_cuda else None
+        order = tuple(o) if o is not None and o[-1] == nd - 1 else tuple(range(nd))
+        xs = x.permute(order)
+        pshape = tuple(xs.shape[:-1])
+        x2 = _bf16(xs.reshape(-1, M).contiguous())
         T = x2.shape[0]
         dev = x.device
         # [T][M] blocked along M (the up projection's operand) and [M][T] blocked along T
@@ -448,19 +456,19 @@ class _FFBlockFp8(torch.autograd.Function):
         y = torch.empty((T, M), dtype=torch.bfloat16, device=dev)
         r2 = None
         if res is not None:
-            r2 = _bf16(res.reshape(T, M).contiguous())
+            r2 = x2 if res is x else _bf16(res.permute(order).reshape(T, M).contiguous())
         gemm_mx(qa, sa, qwo, swo, T, M, F, y, res=r2)
         ctx.save_for_backward(qa, qaT, saT, qxT, sxT, w_in, w_out)
-        ctx.meta = (lead, M, F, T, res is not None, res is x)
-        return y.view(tuple(lead) + (M,))
+        ctx.meta = (order, pshape, M, F, T, res is not None, res is x)
+        return y.view(pshape + (M,)).permute(_inv_perm(order))
 
     @staticmethod
     def backward(ctx, dy):
         from .linear import _row_view
         qa, qaT, saT, qxT, sxT, w_in, w_out = ctx.saved_tensors
-        lead, M, F, T, has_res, res_is_x = ctx.meta
+        order, pshape, M, F, T, has_res, res_is_x = ctx.meta
         dev = qa.device
-        dy2 = dy.reshape(T, M)
+        dy2 = dy.permute(order).reshape(T, M)       # the forward's row order (a view when dy shares it)
         bm = _bcast_grad_mx2(dy2, T) if ctx.needs_input_grad[2] else _bcast_grad_mx(dy2)
         if bm is not None:                          # scalar broadcast: its rows + MX rows, one launch
             t, qdy, sdy = bm[:3]
@@ -493,7 +501,7 @@ class _FFBlockFp8(torch.autograd.Function):
                     colsum=cs)
             if cs is not None:
                 hip.register_colsum(dx, _lazy_rows_sum(cs))
-            out["dx"] = dx.view(tuple(lead) + (M,))
+            out["dx"] = dx.view(pshape + (M,)).permute(_inv_perm(order))
         if ctx.needs_input_grad[2]:
             # dY blocked along tokens: one constant row for a broadcast scalar, else a column pass
             if bm is not None:

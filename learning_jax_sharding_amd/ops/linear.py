@@ -432,7 +432,15 @@ class _Linear(torch.autograd.Function):
         # residual fused into the epilogue (bf16 output, one kernel, 8-column-aligned operand)
         r2, r_ld = None, 0
         if res is not None:
-            r2 = res.permute(order).reshape(M, N)
+            if (order == (1, 0, 2) and res.dim() == 3 and res.is_cuda and res.is_contiguous() and N % 8 == 0
+                    and res.dtype in (torch.float32, torch.bfloat16) and res.data_ptr() % 16 == 0
+                    and res.shape[1] <= 65535):
+                # a batch-major residual under seq-major rows (the 2-D mesh's out projection with the
+                # layer's skip x): one transposing pass that also rounds to bf16 - the epilogue rounds
+                # the residual to bf16 before the add anyway - instead of an f32 transposing copy
+                r2 = hip.swap01_bf16(res).view(M, N)
+            else:
+                r2 = res.permute(order).reshape(M, N)
             if r2.dtype not in (torch.bfloat16, torch.float32):
                 r2 = r2.float()
             if not (r2.stride(1) == 1 and r2.stride(0) % 8 == 0 and r2.data_ptr() % 16 == 0):

@@ -811,6 +811,55 @@ def test_fp8_ff_block_matches_emulation(hip, T, M, Fd, bcast, self_res):
         assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("rdt", [torch.float32, torch.bfloat16])
+def test_linear_seq_major_rows_batch_major_residual(hip, rdt):
+    """Seq-major x with a batch-major residual (the 2-D mesh's out projection + the layer's skip):
+    the residual is transposed to the row order and rounded to bf16 in one pass - y bit-equal to
+    the batch-major run (the epilogue rounds the residual to bf16 before the add either way)."""
+    from learning_jax_sharding_amd.ops import linear as L
+    B, S, K, N = 8, 256, 512, 320
+    base = _rand(S, B, K, seed=80)
+    w = _rand(K, N, dtype=torch.float32, seed=81) * 0.05
+    r = _rand(B, S, N, dtype=rdt, seed=82)
+    ys = {}
+    for seq_major in (True, False):
+        x = base.permute(1, 0, 2) if seq_major else base.permute(1, 0, 2).contiguous()
+        ys[seq_major] = L.linear(x, [w], None, False, torch.bfloat16, residual=r)[0]
+    assert ys[True].stride() == base.permute(1, 0, 2).stride()
+    assert torch.equal(ys[True], ys[False])
+
+
+@pytest.mark.parametrize("bcast", [False, True])
+def test_fp8_ff_block_seq_major_rows(hip, bcast):
+    """A seq-major activation (batch, seq, M) stored [seq][batch][M] - the 2-D mesh's out
+    projection output - runs the fused MX-fp8 FF block in its storage row order without a copy:
+    y and dX (per-token rows, the residual x folded in) bit-equal to the batch-major run and laid
+    out like x; the weight gradients sum the tokens in another order AND block them differently
+    for their MX operands (32 consecutive storage rows share a scale), so they agree to the MX
+    quantization noise of two groupings (~3 % relative norm each), not bit for bit."""
+    from learning_jax_sharding_amd.ops import fp8 as F
+    B, S, M, Fd = 8, 128, 256, 512
+    base = _rand(S, B, M, seed=70)
+    wi0 = _rand(M, Fd, dtype=torch.float32, seed=71) * 0.05
+    wo0 = _rand(Fd, M, dtype=torch.float32, seed=72) * 0.03
+    cot = torch.full((), 0.5, dtype=torch.bfloat16, device=dev).expand(B, S, M) if bcast else \
+        _rand(S, B, M, seed=73).permute(1, 0, 2)
+    res = {}
+    for seq_major in (True, False):
+        x = (base.permute(1, 0, 2) if seq_major else base.permute(1, 0, 2).contiguous()).detach().requires_grad_()
+        wi, wo = wi0.clone().requires_grad_(), wo0.clone().requires_grad_()
+        y = F.ff_block_local(x, wi, wo, x)
+        if seq_major:
+            assert y.stride() == x.stride(), (y.stride(), x.stride())
+        y.backward(cot)
+        res[seq_major] = (y.detach(), x.grad, wi.grad, wo.grad)
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])
+    for a, b_ in zip(res[True][2:], res[False][2:]):
+        err = ((a.float() - b_.float()).norm() / b_.float().norm().clamp(min=1e-6)).item()
+        assert err < 6e-2, err
+
+
 def test_fp8_transformer_layer_trains(gpu_devices):
     """TransformerLayer(fp8=True) takes the fused fp8 FF block and its train step runs."""
     gpu_devices(1)
