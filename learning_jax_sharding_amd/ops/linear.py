@@ -737,25 +737,32 @@ class _FFBlock(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_in, w_out, res):
-        lead, M = x.shape[:-1], x.shape[-1]
+        M = x.shape[-1]
         F = w_in.shape[1]
-        x2 = _bf16(x.reshape(-1, M).contiguous())
+        # tokens in x's storage order (a seq-major activation is read without a transposing copy;
+        # y and dX keep its layout), as in _Linear
+        nd = x.dim()
+        o = hip.storage_order(x) if x.is_cuda else None
+        order = tuple(o) if o is not None and o[-1] == nd - 1 else tuple(range(nd))
+        xs = x.permute(order)
+        pshape = tuple(xs.shape[:-1])
+        x2 = _bf16(xs.reshape(-1, M).contiguous())
         T = x2.shape[0]
         a = torch.empty((T, F), dtype=torch.bfloat16, device=x.device)
         hip.gemm(x2, shadow.get(w_in, "T"), a, T, F, M, M, M, F, True, True, relu=True)
         y = torch.empty((T, M), dtype=torch.bfloat16, device=x.device)
         hip.gemm(a, shadow.get(w_out, "T"), y, T, M, F, F, F, M, True, True, res=x2 if res else None, res_ld=M)
         ctx.save_for_backward(x2, a, w_in, w_out)
-        ctx.meta = (lead, M, F, T, bool(res), x.dtype)
-        return y.view(tuple(lead) + (M,))
+        ctx.meta = (order, pshape, M, F, T, bool(res), x.dtype)
+        return y.view(pshape + (M,)).permute(_inv_perm(order))
 
     @staticmethod
     def backward(ctx, dy):
         from ..parallel import data as _dp
         x2, a, w_in, w_out = ctx.saved_tensors
-        lead, M, F, T, res, xdt = ctx.meta
+        order, pshape, M, F, T, res, xdt = ctx.meta
         dev = x2.device
-        t, ld = _row_view(dy, T, M)
+        t, ld = _row_view(dy.permute(order), T, M)
         wire = _dp.active_wire_dtype() == torch.bfloat16
         dA = torch.empty((T, F), dtype=torch.bfloat16, device=dev)
         hip.gemm(t, shadow.get(w_out, "N"), dA, T, F, M, ld, M, F, True, True, res=a, res_ld=F, res_mode="mask")
@@ -766,7 +773,7 @@ class _FFBlock(torch.autograd.Function):
                 dx = torch.empty((T, M), dtype=torch.bfloat16, device=dev)
                 hip.gemm(dA, shadow.get(w_in, "N"), dx, T, M, F, F, F, M, True, True, res=t if res else None,
                          res_ld=ld)
-                out["dx"] = dx.to(xdt).view(tuple(lead) + (M,))
+                out["dx"] = dx.to(xdt).view(pshape + (M,)).permute(_inv_perm(order))
 
         def wgrad(xb, g, g_ld, K, N, w):
             o = torch.empty((K, N), dtype=torch.float32, device=dev)

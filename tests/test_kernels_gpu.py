@@ -830,6 +830,33 @@ def test_linear_seq_major_rows_batch_major_residual(hip, rdt):
 
 
 @pytest.mark.parametrize("bcast", [False, True])
+def test_ff_block_bf16_seq_major_rows(hip, bcast):
+    """The bf16 fused FF block (residual x) on a seq-major activation runs in its storage row
+    order: y and dX bit-equal to the batch-major run and laid out like x; the weight gradients
+    (split-K token sums in another order) to f32 summation order."""
+    from learning_jax_sharding_amd.ops import linear as L
+    B, S, M, Fd = 8, 128, 256, 512
+    base = _rand(S, B, M, seed=90)
+    wi0 = _rand(M, Fd, dtype=torch.float32, seed=91) * 0.05
+    wo0 = _rand(Fd, M, dtype=torch.float32, seed=92) * 0.03
+    cot = torch.full((), 0.5, dtype=torch.bfloat16, device=dev).expand(B, S, M) if bcast else \
+        _rand(S, B, M, seed=93).permute(1, 0, 2)
+    res = {}
+    for seq_major in (True, False):
+        x = (base.permute(1, 0, 2) if seq_major else base.permute(1, 0, 2).contiguous()).detach().requires_grad_()
+        wi, wo = wi0.clone().requires_grad_(), wo0.clone().requires_grad_()
+        y = L.ff_block(x, wi, wo, True)
+        if seq_major:
+            assert y.stride() == x.stride(), (y.stride(), x.stride())
+        y.backward(cot)
+        res[seq_major] = (y.detach(), x.grad, wi.grad, wo.grad)
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])
+    for a, b_ in zip(res[True][2:], res[False][2:]):
+        torch.testing.assert_close(a, b_, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("bcast", [False, True])
 def test_fp8_ff_block_seq_major_rows(hip, bcast):
     """A seq-major activation (batch, seq, M) stored [seq][batch][M] - the 2-D mesh's out
     projection output - runs the fused MX-fp8 FF block in its storage row order without a copy:
