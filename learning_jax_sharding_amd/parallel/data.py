@@ -190,7 +190,14 @@ class GradReducer:
         me = next(iter(self.leaves[idxs[0]].local))
         flat32 = _covering_flat(grads)
         if flat32 is None:
-            flat32 = torch.cat([g.reshape(-1) for g in grads])
+            parts = [g.reshape(-1) for g in grads]
+            if parts[0].is_cuda and len(parts) > 1 and all(p.numel() == parts[0].numel() for p in parts):
+                # equal-size gradients from separate buffers (the 2-D mesh's head-sharded Q / K / V /
+                # out-projection weights): one HIP pack launch instead of torch's cat kernel
+                from ..ops.hip import concat_parts
+                flat32 = concat_parts(parts, 0)
+            else:
+                flat32 = torch.cat(parts)
         wire = None
         if self.wire_dtype is not None and flat32.dtype == torch.float32 and self.wire_dtype != flat32.dtype:
             wire = _take_twin(flat32, self.wire_dtype)
