@@ -820,6 +820,10 @@ def dense(x: ShardedArray, kernels: Sequence[ShardedArray], bias: Optional[Shard
     if residual is not None and not partial:
         if tuple(residual.shape) != out_shape:
             raise ValueError(f"residual shape {residual.shape} != output shape {out_shape}")
+        if residual.dtype == torch.float32 and compute_dtype == torch.bfloat16 and residual.tile != p.out_tile:
+            # the epilogue rounds the residual to bf16 before the add: round it before it moves
+            # (the 2-D mesh's skip x: half the bytes through the all-to-all and its pack kernels)
+            residual = convert(residual, torch.bfloat16)
         r_loc = reshard_tile(residual, p.out_tile, note="dense.residual").local
     loc_lists = {}
     # a (batch, seq, features) activation with its sequence sharded: outputs stored seq-major, so
