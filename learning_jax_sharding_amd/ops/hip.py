@@ -680,12 +680,19 @@ class _Cast(torch.autograd.Function):
         return _cast_raw(g.contiguous(), ctx.src) if supports_cast(g.dtype, ctx.src) else g.to(ctx.src), None
 
 
-def _cast_raw(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+def _cast_raw(t: torch.Tensor, dtype: torch.dtype, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``t`` in ``dtype`` by one HIP launch (into ``out``, a contiguous tensor of t's shape, when
+    given: a persistent buffer - e.g. a weight's bf16 shadow - is refreshed in place)."""
+    if out is not None and not (t.dtype != dtype and supports_cast(t.dtype, dtype) and t.is_contiguous()
+                                and out.is_contiguous() and out.dtype == dtype and out.shape == t.shape):
+        out.copy_(t)
+        return out
     if t.dtype == dtype:
         return t
     if not supports_cast(t.dtype, dtype) or not t.is_contiguous():
         return t.to(dtype)
-    out = torch.empty(t.shape, dtype=dtype, device=t.device)
+    if out is None:
+        out = torch.empty(t.shape, dtype=dtype, device=t.device)
     n = t.numel()
     if n == 0:
         return out

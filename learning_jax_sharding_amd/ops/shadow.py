@@ -109,7 +109,7 @@ def _refresh(w: torch.Tensor, e: _Entry, kind: str) -> torch.Tensor:
         if kind == "T":
             hip.cast_transpose_bf16(w, buf)
         else:
-            buf.copy_(hip._cast_raw(w.contiguous(), torch.bfloat16))
+            hip._cast_raw(w.contiguous(), torch.bfloat16, out=buf)   # cast straight into the shadow
         e.versions[kind] = w._version
     return buf
 
