@@ -375,12 +375,17 @@ def _quant_both(x2: torch.Tensor):
     return quant_rows(x2), _t_quant(x2)
 
 
+# upper bound on the split count (tuning / A/B: each split is one more f32 slab that the fused Adam
+# or the slab reduction reads back)
+_MX_SPLIT_MAX = int(os.environ.get("LJS_MX_WGRAD_SPLIT_MAX", "64"))
+
+
 def _pick_split(tiles: int, nkt: int) -> int:
     """Split-K count for an MX weight-gradient GEMM: the most splits keeping the work items within
     two 128x128 blocks per CU (2 x 256), each split at least 8 K-tiles, ceil-consistent."""
     best = 1
     for S in range(1, 65):
-        if tiles * S > 512 or nkt < 8 * S:
+        if tiles * S > 512 or nkt < 8 * S or S > _MX_SPLIT_MAX:
             break
         if hip.slab_count(nkt, S) == S:
             best = S
