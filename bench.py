@@ -79,10 +79,16 @@ def parse():
     p.add_argument("--rules", default="reference",
                    help="logical-axis rules preset (parallel/tensor.py PRESETS): reference (case6_attention.py:183-187), "
                         "case5 (embed->data: FSDP-sharded weights, case5_attention_dense.py:109-112), gspmd2d, megatron, dp")
+    p.add_argument("--secondary", default=os.environ.get("LJS_BENCH_SECONDARY", "auto"),
+                   choices=["auto", "on", "off", "0", "1"],
+                   help="also time the reference's 2-D DP x TP layout ((N/2, 2) mesh) in the same job and report it "
+                        "as the JSON line's 'secondary' object (auto: the headline block, --mesh dp, even N >= 2)")
     p.add_argument("--comm-timeout", type=float, default=None,
                    help="seconds a phase may run before the watchdog aborts the communicators and exits "
                         "(default LJS_COMM_TIMEOUT_S or 300)")
-    return p.parse_args()
+    a = p.parse_args()
+    a.secondary = {"0": "off", "1": "on"}.get(a.secondary, a.secondary)
+    return a
 
 
 def _free_port() -> int:
@@ -182,6 +188,119 @@ def main():
     on_gpu = os.environ.get("LJS_PLATFORM", "").lower() != "cpu" and torch.cuda.is_available()
     check_args(args, on_gpu)
     import learning_jax_sharding_amd as ljs
+
+    n = ljs.device_count()
+    if world > 1:
+        import torch.distributed as _dist
+        assert _dist.is_initialized() and _dist.get_world_size() == world, "process group not initialised"
+        assert n == world and ljs.local_device_count() == 1, (n, world)
+
+    import torch.distributed as dist
+    dist_on = dist.is_available() and dist.is_initialized()
+    cuda = torch.cuda.is_available()
+    rank = int(os.environ.get("RANK", "0"))
+    # physical GPUs doing the work: one per rank, or the one GPU under N virtual devices
+    n_gpus = world if world > 1 else (1 if cuda else 0)
+
+    def barrier_sync():
+        if cuda:
+            torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        if cuda:
+            torch.cuda.synchronize()
+
+    # failure detection: a daemon thread polls every RCCL communicator's async error and each
+    # phase's deadline; on an error or a hang it aborts the communicators, prints the phase and
+    # the partitions, and exits non-zero (comm/watchdog.py) instead of hanging in a synchronize
+    from learning_jax_sharding_amd.comm.backend import get_comm
+    wd = get_comm().watchdog(args.comm_timeout) if dist_on else None
+
+    def phase(name, timeout=None):
+        if wd is not None:
+            wd.phase(name, timeout)
+
+    env = dict(n=n, world=world, torch=torch, ljs=ljs, dist=dist, dist_on=dist_on, cuda=cuda,
+               barrier_sync=barrier_sync, phase=phase)
+    res = _measure(args, args.mesh, env)
+    comm = "none"
+    if dist_on:
+        c = get_comm()
+        comm = dist.get_backend() + ("+native-rccl" if getattr(c, "_native", None) is not None else "")
+    rec, printed = None, []
+    if rank == 0:
+        rec = _record(args, res, n, n_gpus, cuda, comm)
+    # the reference's own 2-D DP x TP layout (case6_attention.py:155-162,183-187; BASELINE config 4)
+    # timed in the same job as a secondary result: the headline stays the DP layout
+    if _want_secondary(args, n):
+        def on_fail(reason):
+            # a hang or RCCL error inside the secondary measurement must not cost the headline
+            if rec is not None and not printed:
+                printed.append(1)
+                rec["secondary"] = {"mesh": "2d", "error": reason[:300]}
+                print(json.dumps(rec), flush=True)
+            return 0
+        if wd is not None:
+            wd.on_fail = on_fail
+        try:
+            res2 = _measure(args, "2d", env, phase_timeout=float(os.environ.get("LJS_BENCH_SECONDARY_TIMEOUT_S", "240")))
+            if rec is not None:
+                rec["secondary"] = {
+                    "mesh": list(res2["mshape"]), "parallelism": _parallelism(args, res2["mshape"]),
+                    "ms_per_step": round(res2["ms"], 4),
+                    "tflops_per_gpu": round(res2["tflops_total"] / max(1, n_gpus if cuda else n), 3),
+                    "value": round(res2["tflops_total"], 3), "comm": comm,
+                    "graph_segments": res2["segs"], "steps_per_graph": res2["G"],
+                    "warmup_steps_run": res2["warm_run"], "rules": args.rules,
+                }
+        except Exception as e:   # (same on every rank: the measurement is SPMD)
+            if rec is not None:
+                rec["secondary"] = {"mesh": "2d", "error": f"{type(e).__name__}: {e}"[:300]}
+        if wd is not None:
+            wd.on_fail = None
+    if rec is not None and not printed:
+        printed.append(1)
+        print(json.dumps(rec), flush=True)
+    if dist_on:
+        phase("shutdown")
+        dist.barrier()
+        if wd is not None:
+            wd.stop()
+        get_comm().close()          # ncclCommDestroy of the native communicators
+        dist.destroy_process_group()
+
+
+def _want_secondary(args, n) -> bool:
+    """Time the reference's 2-D layout too: on by default for the headline block with an even
+    device count >= 2 under the DP mesh (``--secondary off`` / LJS_BENCH_SECONDARY=0 disables)."""
+    if args.secondary == "off":
+        return False
+    if args.secondary == "on":
+        return n >= 2 and n % 2 == 0
+    return args.model == "attention" and args.mesh == "dp" and n >= 2 and n % 2 == 0 and args.mode == "train"
+
+
+def _mesh_shape(mesh_arg, n):
+    if mesh_arg == "dp":
+        return (n, 1)
+    if mesh_arg == "2d":
+        return (max(1, n // 2), 2 if n >= 2 else 1)
+    return tuple(int(v) for v in mesh_arg.split("x"))
+
+
+def _parallelism(args, mshape) -> str:
+    par = f"dp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
+    if args.model == "fsdp" or (args.rules in ("case5", "fsdp", "gspmd2d") and mshape[0] > 1):
+        par = f"fsdp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
+    return par
+
+
+def _measure(args, mesh_arg, env, phase_timeout=None):
+    """Build the model on the mesh ``mesh_arg``, capture, warm up and time ``args.steps`` steps
+    (barrier + synchronize on both sides, max over ranks).  Returns the timing and its context."""
+    torch, ljs, dist = env["torch"], env["ljs"], env["dist"]
+    n, dist_on, cuda = env["n"], env["dist_on"], env["cuda"]
+    barrier_sync, phase = env["barrier_sync"], env["phase"]
     from learning_jax_sharding_amd import nn, optim
     from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
     from learning_jax_sharding_amd.models import (DenseStack, MultiHeadAttention, TransformerLayer,
@@ -191,17 +310,7 @@ def main():
     from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
     from learning_jax_sharding_amd.training import TrainState
 
-    n = ljs.device_count()
-    if world > 1:
-        import torch.distributed as _dist
-        assert _dist.is_initialized() and _dist.get_world_size() == world, "process group not initialised"
-        assert n == world and ljs.local_device_count() == 1, (n, world)
-    if args.mesh == "dp":
-        mshape = (n, 1)
-    elif args.mesh == "2d":
-        mshape = (max(1, n // 2), 2 if n >= 2 else 1)
-    else:
-        mshape = tuple(int(v) for v in args.mesh.split("x"))
+    mshape = _mesh_shape(mesh_arg, n)
     assert mshape[0] * mshape[1] == n, (mshape, n)
     mesh = Mesh(create_device_mesh(mshape), ("data", "model"))
     from learning_jax_sharding_amd.parallel.tensor import rules as _rules_preset
@@ -288,31 +397,8 @@ def main():
                 out = step(state, x)
         return out
 
-    import torch.distributed as dist
-    dist_on = dist.is_available() and dist.is_initialized()
-
-    cuda = torch.cuda.is_available()
-
-    def barrier_sync():
-        if cuda:
-            torch.cuda.synchronize()
-        if dist_on:
-            dist.barrier()
-        if cuda:
-            torch.cuda.synchronize()
-
-    # failure detection: a daemon thread polls every RCCL communicator's async error and each
-    # phase's deadline; on an error or a hang it aborts the communicators, prints the phase and
-    # the partitions, and exits non-zero (comm/watchdog.py) instead of hanging in a synchronize
-    from learning_jax_sharding_amd.comm.backend import get_comm
-    wd = get_comm().watchdog(args.comm_timeout) if dist_on else None
-
-    def phase(name):
-        if wd is not None:
-            wd.phase(name)
-
     with mesh, nn.axis_rules(rules):
-        phase("capture + warmup")
+        phase(f"capture + warmup ({mesh_arg})", phase_timeout)
         warm_run = 0   # every untimed step, capture steps included
         if multi is not None:
             # both graphs captured before the timed region, whatever W is
@@ -339,13 +425,13 @@ def main():
             if int(os.environ.get("RANK", "0")) == 0:
                 tr.write(aten_trace)
         barrier_sync()
-        phase("timed steps")
+        phase(f"timed steps ({mesh_arg})", phase_timeout)
         t0 = time.perf_counter()
         run(args.steps)
         th = time.perf_counter()  # host side done enqueuing (diagnostic: host- vs device-bound)
         barrier_sync()
         t1 = time.perf_counter()
-        phase("report")
+        phase(f"report ({mesh_arg})", phase_timeout)
     elapsed = t1 - t0
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if cuda else "cpu")
@@ -365,65 +451,54 @@ def main():
         flops = transformer_layer_flops(B, S, M, args.heads, args.dim_head, args.ff_dim, train=args.mode == "train")
     else:
         flops = attention_block_flops(B, S, M, args.heads, args.dim_head, train=args.mode == "train")
-    tflops_total = flops / (ms * 1e-3) / 1e12
-    tokens_per_s = B * S / (ms * 1e-3)
-    rank = int(os.environ.get("RANK", "0"))
-    # physical GPUs doing the work: one per rank, or the one GPU under N virtual devices
-    n_gpus = world if world > 1 else (1 if cuda else 0)
-    comm = "none"
-    if dist_on:
-        c = get_comm()
-        comm = dist.get_backend() + ("+native-rccl" if getattr(c, "_native", None) is not None else "")
-    if rank == 0:
-        par = f"dp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
-        if args.model == "fsdp" or (args.rules in ("case5", "fsdp", "gspmd2d") and mshape[0] > 1):
-            par = f"fsdp{mshape[0]}" + (f"xtp{mshape[1]}" if mshape[1] > 1 else "")
-        gemm = "MX-fp8" if args.fp8 else "bf16"
-        model_desc = {
-            "attention": f"case6 attention block (M={M}, heads={args.heads}x{args.dim_head}, bf16 compute, "
-                         f"f32 params, Adam)",
-            "layer": f"attention+FF transformer layer (M={M}, heads={args.heads}x{args.dim_head}, "
-                     f"ff={args.ff_dim}, FF GEMMs {gemm}, f32 params, Adam)",
-            "ff": f"case4 GSPMD feed-forward relu(x Win) Wout (M={M}, ff={args.ff_dim}, {gemm} GEMMs, "
-                  f"f32 params, Adam)",
-            "fsdp": f"case3 fully-sharded matmul chain ({args.layers} x Dense {M}x{M}, relu, bf16 compute, "
-                    f"f32 params FSDP-sharded over data, Adam)",
-        }[args.model]
-        rec = {
-            "metric": METRIC if args.model == "attention" else f"step-time ms + TFLOPS/GPU, {args.model} train step",
-            "value": round(tflops_total, 3),
-            "unit": "TFLOPS, whole job (matmul FLOPs of fwd+bwd summed over the n_gpus GPUs; the per-GPU rate "
-                    "the metric names is tflops_per_gpu = value / n_gpus)",
-            "n_gpus": n_gpus if cuda else n,
-            "n_devices": n,
-            "steps": args.steps,
-            # the untimed steps actually run before the timed region: --warmup plus the clock-ramp
-            # minimum (--min-warmup), so the field says what ran
-            "warmup": warm_run,
-            "warmup_requested": args.warmup,
-            "ms_per_step": round(ms, 4),
-            "tflops_per_gpu": round(tflops_total / max(1, n_gpus if cuda else n), 3),
-            "tokens_per_s": round(tokens_per_s, 1),
-            "host_ms_per_step": round((th - t0) / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": ("bf16+mx-fp8" if args.model == "layer" else "mx-fp8") if args.fp8 else "bf16",
-            "data": "synthetic (random normal x, random-init weights)",
-            "config": {"model": model_desc,
-                       "global_batch": B, "seq_len": S, "parallelism": par, "mode": args.mode,
-                       "hip_graph": capture, "graph_segments": segs, "steps_per_graph": G,
-                       "warmup_steps_run": warm_run, "mesh": list(mshape),
-                       "comm": comm, "grad_wire": os.environ.get("LJS_GRAD_COMM_DTYPE", "fp32"),
-                       "loss": "y.sum()" if args.loss == "sum" else "mean((y - target)^2)", "rules": args.rules},
-        }
-        print(json.dumps(rec), flush=True)
-    if dist_on:
-        dist.barrier()
-        if wd is not None:
-            wd.stop()
-        get_comm().close()          # ncclCommDestroy of the native communicators
-        dist.destroy_process_group()
+    # free this layout's graphs and state before another layout is built (the secondary run)
+    del state, step, multi
+    return dict(ms=ms, tflops_total=flops / (ms * 1e-3) / 1e12, tokens_per_s=B * S / (ms * 1e-3),
+                host_ms=(th - t0) / args.steps * 1e3, mshape=mshape, B=B, S=S, M=M, G=G, segs=segs,
+                warm_run=warm_run, capture=capture)
+
+
+def _record(args, res, n, n_gpus, cuda, comm):
+    M, mshape = res["M"], res["mshape"]
+    gemm = "MX-fp8" if args.fp8 else "bf16"
+    model_desc = {
+        "attention": f"case6 attention block (M={M}, heads={args.heads}x{args.dim_head}, bf16 compute, "
+                     f"f32 params, Adam)",
+        "layer": f"attention+FF transformer layer (M={M}, heads={args.heads}x{args.dim_head}, "
+                 f"ff={args.ff_dim}, FF GEMMs {gemm}, f32 params, Adam)",
+        "ff": f"case4 GSPMD feed-forward relu(x Win) Wout (M={M}, ff={args.ff_dim}, {gemm} GEMMs, "
+              f"f32 params, Adam)",
+        "fsdp": f"case3 fully-sharded matmul chain ({args.layers} x Dense {M}x{M}, relu, bf16 compute, "
+                f"f32 params FSDP-sharded over data, Adam)",
+    }[args.model]
+    return {
+        "metric": METRIC if args.model == "attention" else f"step-time ms + TFLOPS/GPU, {args.model} train step",
+        "value": round(res["tflops_total"], 3),
+        "unit": "TFLOPS, whole job (matmul FLOPs of fwd+bwd summed over the n_gpus GPUs; the per-GPU rate "
+                "the metric names is tflops_per_gpu = value / n_gpus)",
+        "n_gpus": n_gpus if cuda else n,
+        "n_devices": n,
+        "steps": args.steps,
+        # the untimed steps actually run before the timed region: --warmup plus the clock-ramp
+        # minimum (--min-warmup), so the field says what ran
+        "warmup": res["warm_run"],
+        "warmup_requested": args.warmup,
+        "ms_per_step": round(res["ms"], 4),
+        "tflops_per_gpu": round(res["tflops_total"] / max(1, n_gpus if cuda else n), 3),
+        "tokens_per_s": round(res["tokens_per_s"], 1),
+        "host_ms_per_step": round(res["host_ms"], 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": ("bf16+mx-fp8" if args.model == "layer" else "mx-fp8") if args.fp8 else "bf16",
+        "data": "synthetic (random normal x, random-init weights)",
+        "config": {"model": model_desc,
+                   "global_batch": res["B"], "seq_len": res["S"], "parallelism": _parallelism(args, mshape),
+                   "mode": args.mode, "hip_graph": res["capture"], "graph_segments": res["segs"],
+                   "steps_per_graph": res["G"], "warmup_steps_run": res["warm_run"], "mesh": list(mshape),
+                   "comm": comm, "grad_wire": os.environ.get("LJS_GRAD_COMM_DTYPE", "fp32"),
+                   "loss": "y.sum()" if args.loss == "sum" else "mean((y - target)^2)", "rules": args.rules},
+    }
 
 
 if __name__ == "__main__":

@@ -4,8 +4,9 @@ os.environ["XLA_FLAGS"] = '--xla_force_host_platform_device_count=4'
 os.environ.setdefault("LJS_NUM_DEVICES", "4")   # 4 virtual devices when run on one MI355X
 # On a node with >= 4 MI355X the same 4 devices are 4 physical GPUs driven by this one process
 # (the reference's single-controller model): mesh-axis collectives become grouped RCCL calls over
-# xGMI (comm/native.py, ncclCommInitAll + ncclCommSplit per group), and the steps run eagerly
-# (a HIP graph captures one device's stream; torchrun + bench.py is the captured multi-GPU path).
+# xGMI (comm/native.py, ncclCommInitAll + ncclCommSplit per group).  Such single-controller steps
+# run eagerly unless LJS_MULTI_GPU_CAPTURE=1 captures them as ONE multi-device HIP graph
+# (spmd/graphs.py MultiDeviceGraph); torchrun + bench.py is the captured one-process-per-GPU path.
 
 import functools
 import numpy as np

@@ -95,7 +95,17 @@ class LocalComm:
         key = tuple(t.device.index for t in ts)
         grp = self._p2p_groups.get(key)
         if grp is None:
-            grp = self._p2p_groups[key] = p2p.P2PGroup([t.device for t in ts], p2p.max_bytes())
+            try:
+                grp = p2p.P2PGroup([t.device for t in ts], p2p.max_bytes())
+            except (p2p.P2PUnavailable, RuntimeError) as e:
+                # no peer access / allocation failure on this node: the group stays on RCCL (or
+                # the copy path) for the process's lifetime, as DistComm does
+                import warnings
+                warnings.warn(f"peer-memory collectives unavailable for devices {key} ({e}); using RCCL")
+                grp = False
+            self._p2p_groups[key] = grp
+        if grp is False:
+            return None
         return grp if grp.fits(nbytes, chunked) else None
 
     def real_transfers(self, devices=None) -> bool:

@@ -213,15 +213,23 @@ class P2PGroup:
         return list(range(self.n)) if self.mode == "local" else [self.rank]
 
     def _enter(self):
-        """Order this collective after the group's previous one when that ran on another stream
-        (within the same capture, or both eager)."""
+        """Order this collective after the group's previous one when that ran on another stream:
+        within the same capture, or both eager, through the previous one's completion event; an
+        eager collective after one that was captured (and so runs inside graph replays) through
+        the latest replay's completion event (spmd/graphs.py last_replay)."""
+        from ..spmd.graphs import last_replay
         for m in self._members():
             s = torch.cuda.current_stream(self.devices[m])
             last = self._last.get(m)
             if last is None or last[0] == s.cuda_stream:
                 continue
-            if last[2] == _capture_id(s.cuda_stream):
+            cid = _capture_id(s.cuda_stream)
+            if last[2] == cid:
                 s.wait_event(last[1])
+            elif cid == 0:
+                ev = last_replay(self.devices[m].index)
+                if ev is not None:
+                    s.wait_event(ev)
 
     def _exit(self):
         for m in self._members():

@@ -49,6 +49,11 @@ class CommWatchdog:
         self._exit = exit_fn or os._exit
         self._phase = "startup"
         self._t0 = time.monotonic()
+        self._deadline = self.timeout_s
+        # called (reason) -> exit code, after the abort and before the exit: a caller that still has
+        # a result to report (bench.py's headline, measured before a secondary layout hung) prints
+        # it here and may choose the exit status
+        self.on_fail: Optional[Callable[[str], Optional[int]]] = None
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.failed: Optional[str] = None
@@ -60,8 +65,9 @@ class CommWatchdog:
             self._thread.start()
         return self
 
-    def phase(self, name: str) -> None:
-        """Enter a new phase: its deadline starts now."""
+    def phase(self, name: str, timeout_s: Optional[float] = None) -> None:
+        """Enter a new phase: its deadline (``timeout_s``, default the watchdog's) starts now."""
+        self._deadline = self.timeout_s if timeout_s is None else float(timeout_s)
         self._phase, self._t0 = name, time.monotonic()
 
     def stop(self) -> None:
@@ -90,8 +96,8 @@ class CommWatchdog:
                     nat.check()
                 except Exception as e:  # an asynchronous RCCL error on some communicator
                     reason = f"asynchronous RCCL error: {e}"
-            if reason is None and time.monotonic() - self._t0 > self.timeout_s:
-                reason = f"phase exceeded its {self.timeout_s:g} s deadline (hang: a peer rank lost or wedged)"
+            if reason is None and time.monotonic() - self._t0 > self._deadline:
+                reason = f"phase exceeded its {self._deadline:g} s deadline (hang: a peer rank lost or wedged)"
             if reason is not None:
                 self._fail(reason)
                 return
@@ -116,7 +122,15 @@ class CommWatchdog:
         else:
             lines.append("[ljs watchdog] no native RCCL communicators (torch process groups only)")
         print("\n".join(lines), file=sys.stderr, flush=True)
+        code = EXIT_CODE
+        if self.on_fail is not None:
+            try:
+                rc = self.on_fail(f"{reason} (phase {self._phase!r})")
+                if rc is not None:
+                    code = int(rc)
+            except Exception as e:  # pragma: no cover - defensive
+                print(f"[ljs watchdog] on_fail hook raised {e!r}", file=sys.stderr, flush=True)
         # give a main thread released by the abort a moment to unwind, then end the process:
         # it may still be blocked in a device synchronize that never returns
         time.sleep(self.grace_s)
-        self._exit(EXIT_CODE)
+        self._exit(code)

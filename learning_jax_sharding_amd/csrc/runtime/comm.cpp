@@ -105,7 +105,19 @@ LJS_RT_API int ljs_comm_get_unique_id(void* out) {
   return 0;
 }
 
+// Restores the caller's current device on scope exit: the helpers below select their device
+// with hipSetDevice, which must not leak into the single controller's later calls (torch's
+// current_stream() / synchronize() without a device argument act on the current device).
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() { (void)hipGetDevice(&prev); }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 LJS_RT_API int ljs_comm_init_rank(const void* unique_id, int nranks, int rank, int dev, void** handle) {
+  DeviceGuard guard;
   hipError_t e = hipSetDevice(dev);
   if (e != hipSuccess) return (int)e;
   ncclUniqueId id;
@@ -275,6 +287,7 @@ LJS_RT_API int ljs_comm_abort(void* handle) {
 // ---- peer-memory staging buffers for the direct P2P collectives (kernels/p2p.hip)
 // fine-grained uncached device memory, zero-filled, with an IPC handle for other processes
 LJS_RT_API int ljs_p2p_alloc(int dev, size_t bytes, void** ptr, void* ipc_handle /* 64 bytes or null */) {
+  DeviceGuard guard;
   hipError_t e = hipSetDevice(dev);
   if (e != hipSuccess) return (int)e;
   e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
@@ -294,6 +307,7 @@ LJS_RT_API int ljs_p2p_alloc(int dev, size_t bytes, void** ptr, void* ipc_handle
 LJS_RT_API int ljs_p2p_free(void* ptr) { return (int)hipFree(ptr); }
 
 LJS_RT_API int ljs_p2p_open(int dev, const void* ipc_handle, void** ptr) {
+  DeviceGuard guard;
   hipError_t e = hipSetDevice(dev);
   if (e != hipSuccess) return (int)e;
   hipIpcMemHandle_t h;
@@ -305,6 +319,7 @@ LJS_RT_API int ljs_p2p_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr);
 
 LJS_RT_API int ljs_p2p_enable_peer(int dev, int peer) {
   if (dev == peer) return 0;
+  DeviceGuard guard;
   hipError_t e = hipSetDevice(dev);
   if (e != hipSuccess) return (int)e;
   e = hipDeviceEnablePeerAccess(peer, 0);

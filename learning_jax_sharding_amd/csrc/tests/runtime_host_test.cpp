@@ -254,7 +254,15 @@ ncclResult_t ncclRecv(void* r, size_t count, ncclDataType_t dt, int peer, ncclCo
 namespace {
 std::map<void*, size_t> g_allocs;
 }
-hipError_t hipSetDevice(int) { return hipSuccess; }
+int g_cur_dev = 0;   // the host model's current device
+hipError_t hipSetDevice(int d) {
+  g_cur_dev = d;
+  return hipSuccess;
+}
+hipError_t hipGetDevice(int* d) {
+  *d = g_cur_dev;
+  return hipSuccess;
+}
 hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_t* p, int) {
   std::memset(p, 0, sizeof(*p));
   p->multiProcessorCount = 256;
@@ -424,12 +432,16 @@ void test_p2p_buffers() {
   void* p = nullptr;
   std::vector<char> ipc(64, 0);
   EXPECT(ljs_rt_ipc_handle_size() <= 64);
+  hipSetDevice(3);   // the controller's current device survives every helper below
   EXPECT(ljs_p2p_alloc(0, 4096, &p, ipc.data()) == 0);
+  EXPECT(g_cur_dev == 3);
   EXPECT(p != nullptr && static_cast<unsigned char*>(p)[4095] == 0);
   void* q = nullptr;
   EXPECT(ljs_p2p_open(1, ipc.data(), &q) == 0 && q == p);
+  EXPECT(g_cur_dev == 3);
   EXPECT(ljs_p2p_close(q) == 0);
   EXPECT(ljs_p2p_enable_peer(0, 1) == 0);  // "already enabled" is success
+  EXPECT(g_cur_dev == 3);
   {
     unsigned long long cid = 7;
     EXPECT(ljs_rt_capture_id(nullptr, &cid) == 0 && cid == 0);  // not capturing

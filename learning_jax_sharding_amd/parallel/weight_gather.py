@@ -292,7 +292,9 @@ class _GatherMx(torch.autograd.Function):
         R, Cn = (R_loc * n, C_loc) if dim == 0 else (R_loc, C_loc * n)
         outs = []
         for d, t in zip(devs, flat):
-            p = torch.empty((R, Cn), dtype=torch.float32, device=t.device)
+            # zero-stride stand-in: nothing reads the proxy's f32 values (the MX GEMMs read its
+            # registered shadows), so it holds one element, not a whole f32 weight per device
+            p = torch.empty((1,), dtype=torch.float32, device=t.device).expand(R, Cn)
             shadow.register_mx_proxy(p, {k: (parts[(k, 0)][d], parts[(k, 1)][d]) for k in ("QN", "QT")})
             outs.append(p)
         ctx.meta = meta

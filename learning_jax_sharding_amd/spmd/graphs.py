@@ -133,6 +133,12 @@ class SegmentedGraph:
     # ------------------------------------------------------------------ replay
     def replay(self):
         cur = torch.cuda.current_stream()
+        try:
+            self._replay(cur)
+        finally:
+            _note_replay({torch.cuda.current_device(): cur})
+
+    def _replay(self, cur):
         for it in self.items:
             kind = it[0]
             if kind == "graph":
@@ -210,6 +216,26 @@ def join(handle) -> None:
         seg.join(handle)
     else:
         torch.cuda.current_stream().wait_event(handle)
+
+
+# per device: an event recorded on the replay stream after the latest graph replay.  Work issued
+# eagerly on ANOTHER stream that shares state with the graph's collectives (the p2p groups' one
+# staging buffer and barrier sequence, comm/p2p.py _enter) waits on it: an event recorded inside
+# a capture cannot be waited on outside it.
+_LAST_REPLAY: Dict[int, Any] = {}
+
+
+def _note_replay(streams: Dict[int, Any]) -> None:
+    for d, s in streams.items():
+        with torch.cuda.device(d):
+            ev = torch.cuda.Event()
+            ev.record(s)
+        _LAST_REPLAY[d] = ev
+
+
+def last_replay(device: int):
+    """The completion event of the latest graph replay on ``device`` (or None)."""
+    return _LAST_REPLAY.get(device)
 
 
 _SIDE: Dict[int, torch.cuda.Stream] = {}
@@ -345,7 +371,27 @@ class MultiDeviceGraph:
         torch.cuda.current_stream().wait_event(ev)
 
     def replay(self):
-        self.graph.replay()
+        """One graph launch on d0's current stream, ordered against every device's current stream
+        on both sides: the graph's branches on device d read inputs that ``Jitted._replay`` copied
+        on d's own current stream (so d0's stream waits for each of them before the launch), and
+        later work on d - including the next replay's input copies into the buffers this one is
+        still reading - waits for the whole graph (each device's stream waits on d0's after it)."""
+        be, devs = self.be, self.devices
+        d0, others = devs[0], devs[1:]
+        s0 = be.current_stream(d0)
+        for d in others:
+            with be.device(d):
+                ev = be.event()
+                ev.record(be.current_stream(d))
+            s0.wait_event(ev)
+        with be.device(d0):
+            self.graph.replay()
+            done = be.event()
+            done.record(s0)
+        for d in others:
+            be.current_stream(d).wait_event(done)
+        if isinstance(be, _TorchMD):
+            _note_replay({d: be.current_stream(d) for d in devs})
 
     def release(self):
         """Return the other devices' pools (the graph keeps its own device's)."""

@@ -55,6 +55,51 @@ def test_bench_spawns_ranks(gpus, mesh, par):
     # value is the whole-job aggregate (the driver's contract); the per-GPU rate the metric names
     # is tflops_per_gpu = value / n_gpus
     assert abs(rec["value"] - rec["tflops_per_gpu"] * gpus) <= 1e-3 * gpus
+    # the reference's 2-D DP x TP layout is timed in the same job under the default DP mesh
+    if mesh == "dp":
+        sec = rec["secondary"]
+        assert "error" not in sec, sec
+        assert sec["mesh"] == [gpus // 2, 2] and sec["parallelism"] == f"dp{gpus // 2}xtp2"
+        assert sec["ms_per_step"] > 0 and sec["comm"].startswith("gloo")
+        for k in ("tflops_per_gpu", "graph_segments", "steps_per_graph", "warmup_steps_run"):
+            assert k in sec, k
+    else:
+        assert "secondary" not in rec
+
+
+@pytest.mark.parametrize("gpus", [2])
+def test_bench_secondary_2d_two_ranks(gpus):
+    """N=2: the secondary object is the (1, 2) mesh (the reference layout at two GPUs); the
+    headline fields are unchanged and the line is still ONE JSON line."""
+    env = dict(os.environ, LJS_PLATFORM="cpu")
+    env.pop("LJS_NUM_DEVICES", None)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), *TINY],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["config"]["parallelism"] == "dp2" and rec["config"]["mesh"] == [2, 1]
+    assert rec["secondary"]["mesh"] == [1, 2] and rec["secondary"]["parallelism"] == "dp1xtp2"
+    assert "error" not in rec["secondary"]
+
+
+def test_watchdog_on_fail_hook_reports_and_sets_exit():
+    """A hang in a later phase runs the on_fail hook (bench.py prints the headline it already
+    has) and exits with the hook's status; the per-phase deadline overrides the default."""
+    import time
+    from learning_jax_sharding_amd.comm.watchdog import CommWatchdog
+    codes, seen = [], []
+    wd = CommWatchdog(None, timeout_s=100.0, poll_s=0.01, exit_fn=codes.append, grace_s=0.0)
+    wd.on_fail = lambda reason: seen.append(reason) or 0
+    wd.start()
+    wd.phase("secondary", 0.05)
+    t0 = time.time()
+    while not codes and time.time() - t0 < 5:
+        time.sleep(0.01)
+    wd.stop()
+    assert codes == [0] and seen and "secondary" in seen[0]
 
 
 def test_bench_min_warmup_counts_every_untimed_step():

@@ -136,8 +136,15 @@ def test_multi_device_graph_capture_structure():
     joins = [x for x in log[b:e] if x[0] == "wait_event" and x[1] == 0]
     assert sorted(x[3] for x in joins) == [1, 2, 3]
     assert graphs.current() is None
+    n0 = len(log)
     g.replay()
-    assert log[-1] == ("replay",) and [x[0] for x in log].count("replay") == 1
+    rl = log[n0:]
+    assert [x[0] for x in rl].count("replay") == 1
+    r = [x[0] for x in rl].index("replay")
+    # device 0's stream waits for every other device's current stream before the launch ...
+    assert sorted(x[3] for x in rl[:r] if x[0] == "wait_event" and x[1] == 0) == [1, 2, 3]
+    # ... and every other device's current stream waits for the launch after it
+    assert sorted(x[1] for x in rl[r:] if x[0] == "wait_event" and x[3] == 0) == [1, 2, 3]
     g.release()
     assert sorted(x[1] for x in log if x[0] == "release_pool") == [1, 2, 3]
 
@@ -180,6 +187,7 @@ def test_jit_uses_multi_device_capture_when_steps_span_gpus(monkeypatch):
         def release(self):
             pass
 
+    monkeypatch.setattr(api, "_MULTI_GPU_CAPTURE", True)
     monkeypatch.setattr(api, "_spans_gpus", lambda: True)
     monkeypatch.setattr(api, "_gpu_indices", lambda: [0, 1])
     monkeypatch.setattr(graphs, "MultiDeviceGraph", _MD)

@@ -436,3 +436,29 @@ def test_all_to_all_node_keeps_no_activation(host_devices):
     meta = outs[0].grad_fn.perm_inputs
     assert meta is not None and not any(isinstance(v, torch.Tensor) for m in meta for v in m)
     assert meta[0][0] == (4, 6)
+
+
+def test_loss_seed_hoist_onto_leaf_inputs(host_devices, monkeypatch):
+    """The seed hoist when the all-to-all's inputs are themselves the differentiated leaves (their
+    edges are AccumulateGrad nodes): grad of sum(reshard(p)) is all ones, hoisted or not."""
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
+    from learning_jax_sharding_amd.sharding import NamedSharding, PartitionSpec as P
+    from learning_jax_sharding_amd.spmd import api
+    host_devices(4)
+    mesh = Mesh(create_device_mesh((4, 1)), ("data", "model"))
+    p = ljs.device_put(ljs.random.normal(ljs.random.PRNGKey(0), (16, 32)), NamedSharding(mesh, P("data", None)))
+
+    def loss(x):
+        return ljs.lax.with_sharding_constraint(x, NamedSharding(mesh, P(None, "data"))).sum()
+
+    res = {}
+    for hoist in (True, False):
+        monkeypatch.setattr(api, "_SEED_HOIST", hoist)
+        n0 = api.HOIST_STATS["hoisted"]
+        val, g = ljs.value_and_grad(loss)(p)
+        res[hoist] = (float(np.asarray(val)), np.asarray(g), api.HOIST_STATS["hoisted"] - n0)
+    assert res[True][2] > 0 and res[False][2] == 0
+    np.testing.assert_allclose(res[True][0], float(np.asarray(p).sum()), rtol=1e-5)
+    np.testing.assert_array_equal(res[True][1], np.ones((16, 32), np.float32))
+    np.testing.assert_array_equal(res[False][1], res[True][1])
