@@ -292,9 +292,12 @@ class _GatherMx(torch.autograd.Function):
         R, Cn = (R_loc * n, C_loc) if dim == 0 else (R_loc, C_loc * n)
         outs = []
         for d, t in zip(devs, flat):
-            # zero-stride stand-in: nothing reads the proxy's f32 values (the MX GEMMs read its
-            # registered shadows), so it holds one element, not a whole f32 weight per device
-            p = torch.empty((1,), dtype=torch.float32, device=t.device).expand(R, Cn)
+            # (a dense, uninitialised stand-in: the allocation moves no bytes.  A zero-stride proxy
+            # - one element expanded - was tried and failed the 2x2 MX-gather parity test
+            # (tests/test_gpu_e2e.py::test_fp8_ff_block_2d_gathers_mx_shadows, gpurun_out/r5a):
+            # the FF block's layout checks treat a non-contiguous weight as one to copy, and the
+            # copy is not a registered proxy)
+            p = torch.empty((R, Cn), dtype=torch.float32, device=t.device)
             shadow.register_mx_proxy(p, {k: (parts[(k, 0)][d], parts[(k, 1)][d]) for k in ("QN", "QT")})
             outs.append(p)
         ctx.meta = meta
