@@ -1099,6 +1099,280 @@ gemm_dma_kernel(
   stamp_end();
 }
 
+// ============================================================================ lean K-loop GEMM
+// The persistent LDS-DMA GEMM's k-contiguous, bf16-output path (forward projections and dX GEMMs)
+// with the per-K-tile bookkeeping out of the K-loop.  A DMA / MFMA / barrier probe
+// (scripts/probe_dma_mfma.hip, profiles/r5_probe_dma_mfma.txt) measured what a K-tile of this
+// structure costs per SIMD: 32 MFMAs per wave alone 1180 cycles; + 6 DMA pieces and 16 fragment
+// reads + one barrier 1440; + ~90 scalar instructions and 6 branches per K-tile 1850 -- and the
+// general kernel above carries about that much (stage index = tile mod NST through mul_hi, the
+// tail / after-epilogue / next-item tests and their vmcnt selection, all inside the loop).  Here:
+//  * the stage is a rotating offset (the DMA of tile f + NST goes to tile f's stage);
+//  * the K-loop of an item runs nk - 1 identical steps (one counted vmcnt, one barrier, half
+//    the next tile's pieces after its k-step-0 fragment reads, half after the k-step-1 MFMAs); the
+//    item's last K-tile, its epilogue and the next item's first barrier are peeled;
+//  * the issue cursor never tests for the end: past the block's last item it re-issues item 0's
+//    first K-tiles into stages nothing reads again (in range, so every step's count is the same).
+// Operands, images, fragment reads, MFMA orientation and the epilogue are gemm_dma_kernel's
+// (bit-identical results: tests/test_kernels_gpu.py::test_gemm_lean_bit_exact).
+// LJS_LEAN_PIN (variant builds, A/B): scheduling barriers between the K-loop's phases, so the
+// compiler keeps reads / MFMAs / barrier / DMA in the written order
+#ifndef LJS_LEAN_PIN
+#define LJS_LEAN_PIN 0
+#endif
+#if LJS_LEAN_PIN
+#define LJS_LEAN_SCHED() __builtin_amdgcn_sched_barrier(0)
+#else
+#define LJS_LEAN_SCHED() ((void)0)
+#endif
+template <int BM, int BN, int WM, int WN, int NST, int RES>
+__global__ __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
+gemm_lean_kernel(GemmArgs p) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int A_TILE = BM * BK, B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
+  using TA = DmaTile<BM, true, NW>;
+  using TB = DmaTile<BN, true, NW>;
+  constexpr int L = TA::PER_WAVE + TB::PER_WAVE;
+  static_assert(TN % 2 == 0, "column blocks pair up for 16-byte stores");
+  static_assert(NST >= 2, "at least one K-tile in flight");
+  constexpr int S_EPI = TM * TN / 2;
+  static_assert(L * (NST - 1) + S_EPI + 1 <= 63, "vmcnt immediate range");
+  constexpr bool PLAIN = RES == 3, BSUM = RES == 4, NOALPHA = PLAIN || BSUM;
+  constexpr bool HAS_R = RES == 1 || RES == 2;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int items = p.batch * ntm * ntn;
+  const int G = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, G);
+  const int my_items = slot < items ? (items - slot + G - 1) / G : 0;
+  if (my_items == 0) return;
+  const int nk = p.kt_per_split;   // K / 64 (no split-K on this path)
+
+  const long a_bytes = 2 * ((long)(p.M - 1) * p.lda + p.K);
+  const long b_bytes = 2 * ((long)(p.N - 1) * p.ldb + p.K);
+  TA ta;
+  TB tb;
+  ta.init(p.lda, wave, lane);
+  tb.init(p.ldb, wave, lane);
+
+  // ---- issue cursor: the item whose K-tiles are being fetched (NST K-tiles ahead of the MFMAs)
+  int is_item = 0, is_kt = 0;
+  __amdgpu_buffer_rsrc_t ra, rb;
+  int a_off = 0, b_off = 0;
+  auto load_item = [&](int k) {
+    const WorkItem w = decode_item(p, slot + G * (k < my_items ? k : 0), ntm, ntn);
+    ra = make_rsrc(p.A + (long)w.b * p.sA, a_bytes);
+    rb = make_rsrc(p.B + (long)w.b * p.sB, b_bytes);
+    a_off = __builtin_amdgcn_readfirstlane((int)((long)w.m0 * BM * p.lda * 2));
+    b_off = __builtin_amdgcn_readfirstlane((int)((long)w.n0 * BN * p.ldb * 2));
+  };
+  auto issue_a = [&](int so) { ta.issue(ra, smem + so, a_off, wave); };
+  auto issue_b = [&](int so) { tb.issue(rb, smem + so + A_TILE, b_off, wave); };
+  auto advance = [&]() {
+    a_off += BK * 2;
+    b_off += BK * 2;
+    if (++is_kt == nk) {
+      is_kt = 0;
+      load_item(++is_item);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_item(0);
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) {
+    issue_a(s * STAGE);
+    issue_b(s * STAGE);
+    advance();
+  }
+
+  const bool relu = !PLAIN && !BSUM && (p.flags & 1);
+  const bool has_bias = BSUM || (!PLAIN && (p.flags & 2));
+  const bool bias_f32 = BSUM || (p.flags & 4);
+  const bool st_sc1 = p.flags & 32;
+  const bool psum_on = !PLAIN && p.psum != nullptr;
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(p.C, 2 * ((long)(p.batch - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
+
+  bf16x8 ka[TM], kb[TN], la[TM], lb[TN];
+  auto read_frags = [&](int so, int ks, bf16x8* af, bf16x8* bfr) {
+    const bf16_t* As_ = smem + so;
+    const bf16_t* Bs_ = As_ + A_TILE;
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii) af[ii] = frag<BM, true>(As_, wr * (BM / WM) + ii * 16, ks, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, true>(Bs_, wc * (BN / WN) + j * 16, ks, lane);
+  };
+  auto mfmas = [&](const bf16x8* af, const bf16x8* bfr) {
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[ii][j] = mfma16x16x32(bfr[j], af[ii], acc[ii][j]);  // C^T block
+  };
+  auto next_so = [](int so) { return so + STAGE == NST * STAGE ? 0 : so + STAGE; };
+  auto barrier = []() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  // the stage of the (virtual) tile before the block's first: the first item start issues the
+  // DMA of tile NST - 1 into it
+  int so = (NST - 1) * STAGE;
+  // item start: tile f = the item's first (stage nso) landed -- this wave's pieces of the younger
+  // tiles and, after an epilogue, its S_EPI (+1 fused-sum) stores may stay in flight -- then the
+  // barrier, k-step 0 fragments, and the DMA of tile f + NST - 1 into the stage of tile f - 1
+  auto item_start = [&](bool after_epi) {
+    if (!after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");
+    else if (psum_on) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2) + S_EPI + 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2) + S_EPI) : "memory");
+    barrier();
+    const int nso = next_so(so);
+    read_frags(nso, 0, ka, kb);
+    issue_a(so);
+    issue_b(so);
+    advance();
+    so = nso;
+  };
+  item_start(false);
+
+  float tsum = 0.f;
+  for (int it = 0; it < my_items; ++it) {
+    for (int kk = 0; kk + 1 < nk; ++kk) {
+      read_frags(so, 1, la, lb);
+      LJS_LEAN_SCHED();
+      mfmas(ka, kb);
+      LJS_LEAN_SCHED();
+      const int nso = next_so(so);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");  // tile f + 1 landed
+      barrier();                                   // ... for every wave; every read of tile f done
+      read_frags(nso, 0, ka, kb);
+      issue_a(so);                                 // tile f + NST into tile f's stage
+      LJS_LEAN_SCHED();
+      mfmas(la, lb);
+      LJS_LEAN_SCHED();
+      issue_b(so);
+      advance();
+      so = nso;
+    }
+    // the item's last K-tile
+    read_frags(so, 1, la, lb);
+    mfmas(ka, kb);
+    mfmas(la, lb);
+
+    // ------------------------------------------------------------ epilogue of this item
+    const WorkItem w = decode_item(p, slot + G * it, ntm, ntn);
+    const int m0 = w.m0 * BM + wr * (BM / WM), n0 = w.n0 * BN + wc * (BN / WN);
+    const int g = lane >> 4;
+    const bool even = (g & 1) == 0;
+    u32x4 rv[2][TN / 2][RES == 2 ? 2 : 1];
+    __amdgpu_buffer_rsrc_t rr;
+    if constexpr (HAS_R)
+      rr = make_rsrc(p.res, (RES == 2 ? 4 : 2) * ((long)(p.batch - 1) * p.sR + (long)(p.M - 1) * p.ldr + p.N));
+    auto load_r = [&](int ii) {
+      if constexpr (HAS_R) {
+#pragma unroll
+        for (int q = 0; q < TN / 2; ++q) {
+          const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
+          const int row = m0 + ii * 16 + (lane & 15);
+          const bool ok = row < p.M && col < p.N;
+          const int off = ok ? (int)(((long)w.b * p.sR + (long)row * p.ldr + col) * (RES == 2 ? 4 : 2)) : 0x7ffffff0;
+          rv[ii & 1][q][0] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+          if constexpr (RES == 2)
+            rv[ii & 1][q][RES == 2 ? 1 : 0] = __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? off + 16 : off, 0, 0);
+        }
+      }
+    };
+    load_r(0);
+    float bvs[TN / 2][8];
+    const bool bias_vec = has_bias && ((((uintptr_t)p.bias) & 15) == 0) && (p.sBias % 8) == 0;
+#pragma unroll
+    for (int q = 0; q < TN / 2; ++q) {
+      const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
+      const long bo = (long)w.b * p.sBias + col;
+      if (bias_vec && col + 8 <= p.N) {
+        if (bias_f32) {
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.bias) + bo);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.bias) + bo + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bvs[q][e] = lo[e];
+            bvs[q][4 + e] = hi[e];
+          }
+        } else {
+          const u32x4 u = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(p.bias) + bo);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bvs[q][2 * e] = __uint_as_float(u[e] << 16);
+            bvs[q][2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+          }
+        }
+        continue;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bvs[q][e] = 0.f;
+        if (has_bias && col + e < p.N) {
+          bvs[q][e] = bias_f32 ? reinterpret_cast<const float*>(p.bias)[bo + e]
+                               : bf2f(reinterpret_cast<const bf16_t*>(p.bias)[bo + e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii) {
+      if (ii + 1 < TM) load_r(ii + 1);
+#pragma unroll
+      for (int q = 0; q < TN / 2; ++q) {
+        const int col = n0 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);
+        const float* bv = bvs[q];
+        const f32x4 a0 = NOALPHA ? acc[ii][2 * q] : acc[ii][2 * q] * p.alpha;
+        const f32x4 a1 = NOALPHA ? acc[ii][2 * q + 1] : acc[ii][2 * q + 1] * p.alpha;
+        acc[ii][2 * q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[ii][2 * q + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float v[8];
+        pair_rows16(a0, a1, even, v);
+        u32x4 pk;
+        if constexpr (!PLAIN) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            v[e] += bv[e];
+            if (relu) v[e] = fmaxf(v[e], 0.f);
+          }
+        }
+        if constexpr (HAS_R) apply_res8(v, p.flags, rv[ii & 1][q][0], rv[ii & 1][q][0], rv[ii & 1][q][RES == 2 ? 1 : 0]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+        const int row = m0 + ii * 16 + (lane & 15);
+        const bool ok = row < p.M && col < p.N;  // N % 8 == 0 (launcher): chunks are whole
+        const int off = ok ? (int)(((long)w.b * p.sC + (long)row * p.ldc + col) * 2) : 0x7ffffff0;
+        if (st_sc1) __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, kSC1);
+        else __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, 0);
+        if (psum_on && ok) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) tsum += __uint_as_float(pk[e] << 16) + __uint_as_float(pk[e] & 0xffff0000u);
+        }
+      }
+    }
+    if (psum_on) {
+      tsum = warp_sum64(tsum);
+      if (lane == 0) p.psum[(long)(slot + G * it) * NW + wave] = tsum;
+      tsum = 0.f;
+    }
+    if (it + 1 < my_items) item_start(true);
+  }
+  // the DMA pieces still in flight (the cursor's re-issues past the last item) land in this
+  // block's LDS: let them finish before the block's LDS can be handed to another
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // explicit instantiations: hipcc (ROCm 7.2) otherwise leaves some of these kernels' host stubs
 // undefined when they are only named inside launch_dma's instantiations
 #define LJS_DMA_INST(BM, BN, WM, WN, NST, AK, BKc, OF) \
@@ -1168,6 +1442,22 @@ LJS_DMA_INST_RES(256, 128, 2, 2, 3)
 LJS_DMA_INST_RES(256, 192, 2, 2, 2)
 LJS_DMA_INST_RES(256, 256, 2, 2, 2)
 #undef LJS_DMA_INST_RES
+// lean K-loop kernels (k-contiguous, bf16 output; every epilogue instance)
+#define LJS_LEAN_INST(BM, BN, WM, WN, NST)                                  \
+  template __global__ void gemm_lean_kernel<BM, BN, WM, WN, NST, 0>(GemmArgs); \
+  template __global__ void gemm_lean_kernel<BM, BN, WM, WN, NST, 1>(GemmArgs); \
+  template __global__ void gemm_lean_kernel<BM, BN, WM, WN, NST, 2>(GemmArgs); \
+  template __global__ void gemm_lean_kernel<BM, BN, WM, WN, NST, 3>(GemmArgs); \
+  template __global__ void gemm_lean_kernel<BM, BN, WM, WN, NST, 4>(GemmArgs);
+LJS_LEAN_INST(256, 128, 4, 2, 3)
+LJS_LEAN_INST(256, 192, 4, 2, 2)
+LJS_LEAN_INST(128, 160, 4, 1, 2)
+LJS_LEAN_INST(128, 128, 2, 2, 2)
+LJS_LEAN_INST(128, 128, 2, 2, 4)
+LJS_LEAN_INST(128, 128, 2, 4, 3)
+LJS_LEAN_INST(128, 128, 2, 4, 4)
+LJS_LEAN_INST(64, 64, 2, 2, 4)
+#undef LJS_LEAN_INST
 // f32-A (cast-on-load) forward GEMMs: 128x128, 8 waves, 3 stages (144 KiB with the f32 A image)
 template __global__ void gemm_dma_kernel<128, 128, 2, 4, 3, true, true, false, 0, 1>(GemmArgs);
 template __global__ void gemm_dma_kernel<256, 128, 4, 2, 3, true, true, false, 0, 2>(GemmArgs);
@@ -1235,6 +1525,39 @@ hipError_t launch_slab(const GemmArgs& a, hipStream_t s) {
   if (plain_env && (a.flags & kSlabs) && !(a.flags & (kSlabBf16 | 1 | 2 | 8 | 16)) && a.alpha == 1.f)
     return launch_dma<BM, BN, WM, WN, NST, false, false, true, 3>(a, s, 0);
   return launch_dma<BM, BN, WM, WN, NST, false, false, true, 0>(a, s, 0);
+}
+
+// the lean K-loop kernel (k-contiguous, bf16 output, no split): same grid choice as launch_dma
+template <int BM, int BN, int WM, int WN, int NST, int RES>
+hipError_t launch_lean(const GemmArgs& a, hipStream_t s) {
+  if (!g_cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_cus <= 0) g_cus = 256;
+  }
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  const int items = ntm * ntn * a.batch;
+  static const int order_env = getenv("LJS_GEMM_ORDER") ? atoi(getenv("LJS_GEMM_ORDER")) : 1;
+  GemmArgs a2 = a;
+  if (order_env && ntm < ntn) a2.flags |= kMFast;
+  constexpr int kLdsBytes = NST * (BM + BN) * BK * 2;
+  constexpr int kNatural = (WM * WN == 4 && kLdsBytes <= 80 * 1024) ? 2 : 1;
+  int grid = items;
+  if (items > g_cus * kNatural && items % (g_cus * kNatural) == 0) grid = g_cus * kNatural;
+  hipLaunchKernelGGL((gemm_lean_kernel<BM, BN, WM, WN, NST, RES>), dim3(grid), dim3(WM * WN * 64), 0, s, a2);
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN, int NST>
+hipError_t launch_lean_kk(const GemmArgs& a, hipStream_t s) {
+  if (a.flags & (kResAdd | kResMask)) {
+    if (a.flags & kResF32) return launch_lean<BM, BN, WM, WN, NST, 2>(a, s);
+    return launch_lean<BM, BN, WM, WN, NST, 1>(a, s);
+  }
+  if (a.alpha == 1.f && !(a.flags & 3) && !a.psum) return launch_lean<BM, BN, WM, WN, NST, 3>(a, s);
+  if (a.alpha == 1.f && (a.flags & 7) == 6) return launch_lean<BM, BN, WM, WN, NST, 4>(a, s);
+  return launch_lean<BM, BN, WM, WN, NST, 0>(a, s);
 }
 
 template <int BM, int BN, bool AK, bool BKc, bool OF>
@@ -1330,6 +1653,11 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   }
 
   if (psum_count) *psum_count = 0;
+  // A/B: tile code + 100000 forces the lean K-loop kernel where it applies, + 200000 the general one
+  const bool gen_req = tile >= 200000;
+  if (gen_req) tile -= 200000;
+  const bool lean_req = tile >= 100000;
+  if (lean_req) tile -= 100000;
   int nkt = (K + BK - 1) / BK;
   if (splitk < 1) splitk = 1;
   if (splitk > nkt) splitk = nkt;
@@ -1391,6 +1719,20 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     const int bn = tile == 1602 ? 160 : (tile == 2562 || tile == 2592) ? 192 : tile == 2552 ? 256 : 128;
     a.psum = (float*)psum;
     if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch * a.splitk * nw;
+  }
+  // the lean K-loop kernel for the k-contiguous bf16-output LDS-DMA tiles without split-K
+  // (LJS_GEMM_LEAN=0: the general kernel; tile code + 100000 forces the lean one for A/B)
+  static const int lean_env = getenv("LJS_GEMM_LEAN") ? atoi(getenv("LJS_GEMM_LEAN")) : 1;
+  if ((lean_env || lean_req) && !gen_req && a_kc && b_kc && !out_f32 && a.splitk == 1 && !(flags & kBPtrs) && dma_ok &&
+      dma_store_ok) {
+    if (tile == 2561) return (int)launch_lean_kk<256, 128, 4, 2, 3>(a, stream);
+    if (tile == 2562) return (int)launch_lean_kk<256, 192, 4, 2, 2>(a, stream);
+    if (tile == 1602) return (int)launch_lean_kk<128, 160, 4, 1, 2>(a, stream);
+    if (tile == 1282) return (int)launch_lean_kk<128, 128, 2, 2, 2>(a, stream);
+    if (tile == 1284) return (int)launch_lean_kk<128, 128, 2, 2, 4>(a, stream);
+    if (tile == 12883) return (int)launch_lean_kk<128, 128, 2, 4, 3>(a, stream);
+    if (tile == 12884) return (int)launch_lean_kk<128, 128, 2, 4, 4>(a, stream);
+    if (tile == 644 && !(flags & (kResAdd | kResMask))) return (int)launch_lean_kk<64, 64, 2, 2, 4>(a, stream);
   }
   if (tile == 2563) {
     e = launch_dma<256, 128, 4, 2, 3, false, false, true>(a, stream, 0);

@@ -262,9 +262,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     if tile is None:
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc, A.dtype, bias, sBias, relu, accumulate,
                          zero_c, psum, res, acopy, slabs, sA, sB, sC, ldb)
-    if tile >= _PP_BASE and slab16:
+    if _PP_BASE <= tile < _LEAN_REQ and slab16:
         tile = None
-    if tile is not None and tile >= _PP_BASE:
+    if tile is not None and _PP_BASE <= tile < _LEAN_REQ:
         rc, cnt = _gemm_pp(A, B, C, M, N, K, lda, ldb, ldc, a_kc, b_kc, batch, sA, sB, sC, bias, sBias, relu, alpha,
                            splitk, tile - _PP_BASE, a_off, b_off, c_off, slabs, b_list, psum, acopy)
         if rc == 0:
@@ -297,6 +297,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
 
 
 _PP_BASE = 30000   # tile codes >= _PP_BASE: the ping-pong kernel (csrc/kernels/gemm_pp.hip), cfg = code - base
+_LEAN_REQ = 100000  # tile code + _LEAN_REQ: force the lean K-loop kernel (gemm.hip gemm_lean_kernel; A/B),
+                    # + 2 * _LEAN_REQ: force the general LDS-DMA kernel
 
 
 def _gemm_pp(A, B, C, M, N, K, lda, ldb, ldc, a_kc, b_kc, batch, sA, sB, sC, bias, sBias, relu, alpha, splitk,

@@ -1263,3 +1263,43 @@ def test_box_slice_backward_is_pad(hip, dtype):
     v = torch.randn(640, device=dev).requires_grad_()
     hip.box_slice(v, (slice(320, 640),)).sum().backward()
     assert torch.equal(v.grad, torch.cat([torch.zeros(320, device=dev), torch.ones(320, device=dev)]))
+
+
+@pytest.mark.parametrize("tile,M,N,K,batch,mode", [
+    (2561, 4096, 512, 640, 3, "plain"), (2561, 1000, 384, 512, 1, "bias_relu"), (2562, 4096, 512, 640, 3, "plain"),
+    (1602, 4096, 640, 512, 1, "bias_sum"), (1602, 777, 640, 512, 1, "res_add"), (1282, 4096, 512, 640, 1, "mask"),
+    (1282, 300, 200, 128, 2, "alpha"), (1284, 2048, 512, 640, 1, "plain"), (12883, 2048, 1536, 640, 1, "plain"),
+    (12884, 1024, 256, 192, 1, "res_f32"), (644, 2048, 640, 512, 1, "bias_sum"), (644, 96, 72, 64, 1, "plain")])
+def test_gemm_lean_bit_exact(hip, tile, M, N, K, batch, mode):
+    """The lean K-loop kernel (gemm.hip gemm_lean_kernel, tile code + 100000) is bit-identical to
+    the general LDS-DMA kernel (code + 200000) for every epilogue instance: plain, bias(+ReLU),
+    bias + fused sum, alpha, residual add / ReLU mask (bf16 and f32 operand), ragged M / N,
+    weight-major batches folded or not, persistent and one-block-per-item grids."""
+    A = _rand(M, K, seed=1)
+    B = _rand(batch, N, K, seed=2)
+    ldc = N * batch if batch > 1 else N
+    kw = dict(batch=batch, sA=0, sB=N * K, sC=N) if batch > 1 else {}
+    if mode in ("bias_relu", "bias_sum"):
+        kw["bias"] = _rand(N, dtype=torch.float32, seed=3)
+        kw["relu"] = mode == "bias_relu"
+    if mode == "alpha":
+        kw["alpha"] = 0.37
+    if mode in ("res_add", "mask", "res_f32"):
+        kw["res"] = _rand(M, N, dtype=torch.float32 if mode == "res_f32" else torch.bfloat16, seed=4)
+        kw["res_ld"] = N
+        kw["res_mode"] = "mask" if mode == "mask" else "add"
+    outs = {}
+    for base in (200000, 100000):
+        C = torch.full((M, ldc), float("nan"), device=dev).bfloat16()
+        ps = torch.zeros(hip.psum_slots(M, ldc) * 2, device=dev) if mode == "bias_sum" else None
+        cnt = hip.gemm(A, B, C, M, N, K, K, K, ldc, True, True, tile=base + tile, psum=ps, **kw)
+        torch.cuda.synchronize()
+        outs[base] = (C, ps, cnt)
+    (c0, p0, n0), (c1, p1, n1) = outs[200000], outs[100000]
+    assert torch.equal(c0.view(torch.int16), c1.view(torch.int16))
+    assert n0 == n1
+    if p0 is not None:
+        assert torch.equal(p0[:n0], p1[:n1])
+    ref = (A.float() @ B.float().reshape(batch * N, K).t()) if batch > 1 else A.float() @ B[0].float().t()
+    if mode == "plain":
+        assert ((c1.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
