@@ -1111,20 +1111,13 @@ gemm_dma_kernel(
 //  * the K-loop of an item runs nk - 1 identical steps (one counted vmcnt, one barrier, half
 //    the next tile's pieces after its k-step-0 fragment reads, half after the k-step-1 MFMAs); the
 //    item's last K-tile, its epilogue and the next item's first barrier are peeled;
-//  * the issue cursor never tests for the end: past the block's last item it re-issues item 0's
-//    first K-tiles into stages nothing reads again (in range, so every step's count is the same).
+//  * the issue cursor never tests for the end: past the block's last item it issues K-tiles that
+//    read zeros (an empty-range descriptor) into stages nothing reads again, so every step's count is the same.
 // Operands, images, fragment reads, MFMA orientation and the epilogue are gemm_dma_kernel's
 // (bit-identical results: tests/test_kernels_gpu.py::test_gemm_lean_bit_exact).
-// LJS_LEAN_PIN (variant builds, A/B): scheduling barriers between the K-loop's phases, so the
-// compiler keeps reads / MFMAs / barrier / DMA in the written order
-#ifndef LJS_LEAN_PIN
-#define LJS_LEAN_PIN 0
-#endif
-#if LJS_LEAN_PIN
-#define LJS_LEAN_SCHED() __builtin_amdgcn_sched_barrier(0)
-#else
-#define LJS_LEAN_SCHED() ((void)0)
-#endif
+// The issue cursor's K-tiles past the block's last item go through a buffer descriptor with an
+// empty range: every lane is out of range whatever its offsets, so the pieces read zeros without a
+// memory access and retire at once (the block's final vmcnt(0) does not wait for an L2 round trip).
 template <int BM, int BN, int WM, int WN, int NST, int RES>
 __global__ __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
 gemm_lean_kernel(GemmArgs p) {
@@ -1170,6 +1163,10 @@ gemm_lean_kernel(GemmArgs p) {
     rb = make_rsrc(p.B + (long)w.b * p.sB, b_bytes);
     a_off = __builtin_amdgcn_readfirstlane((int)((long)w.m0 * BM * p.lda * 2));
     b_off = __builtin_amdgcn_readfirstlane((int)((long)w.n0 * BN * p.ldb * 2));
+    if (k >= my_items) {   // past the block's last item: an empty range (every piece reads zeros)
+      ra = make_rsrc(p.A, 0);
+      rb = make_rsrc(p.B, 0);
+    }
   };
   auto issue_a = [&](int so) { ta.issue(ra, smem + so, a_off, wave); };
   auto issue_b = [&](int so) { tb.issue(rb, smem + so + A_TILE, b_off, wave); };
@@ -1248,17 +1245,13 @@ gemm_lean_kernel(GemmArgs p) {
   for (int it = 0; it < my_items; ++it) {
     for (int kk = 0; kk + 1 < nk; ++kk) {
       read_frags(so, 1, la, lb);
-      LJS_LEAN_SCHED();
       mfmas(ka, kb);
-      LJS_LEAN_SCHED();
       const int nso = next_so(so);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");  // tile f + 1 landed
       barrier();                                   // ... for every wave; every read of tile f done
       read_frags(nso, 0, ka, kb);
       issue_a(so);                                 // tile f + NST into tile f's stage
-      LJS_LEAN_SCHED();
       mfmas(la, lb);
-      LJS_LEAN_SCHED();
       issue_b(so);
       advance();
       so = nso;
@@ -1368,8 +1361,8 @@ gemm_lean_kernel(GemmArgs p) {
     }
     if (it + 1 < my_items) item_start(true);
   }
-  // the DMA pieces still in flight (the cursor's re-issues past the last item) land in this
-  // block's LDS: let them finish before the block's LDS can be handed to another
+  // the DMA pieces still in flight (the cursor's past-the-end tiles) write this block's LDS: let
+  // them finish before the block's LDS can be handed to another
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -1727,7 +1720,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
       dma_store_ok) {
     if (tile == 2561) return (int)launch_lean_kk<256, 128, 4, 2, 3>(a, stream);
     if (tile == 2562) return (int)launch_lean_kk<256, 192, 4, 2, 2>(a, stream);
-    if (tile == 1602) return (int)launch_lean_kk<128, 160, 4, 1, 2>(a, stream);
+    // (128x160, one item per block: the general kernel measured 14.4 vs 14.8 us, gpurun_out/r5i)
+    if (tile == 1602 && lean_req) return (int)launch_lean_kk<128, 160, 4, 1, 2>(a, stream);
     if (tile == 1282) return (int)launch_lean_kk<128, 128, 2, 2, 2>(a, stream);
     if (tile == 1284) return (int)launch_lean_kk<128, 128, 2, 2, 4>(a, stream);
     if (tile == 12883) return (int)launch_lean_kk<128, 128, 2, 4, 3>(a, stream);

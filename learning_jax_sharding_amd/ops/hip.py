@@ -371,8 +371,10 @@ def _psum_for(t: torch.Tensor):
 # the FF up-projection (60.7 vs 65.2 us; scripts/gemm_tiles_out.py)
 _TILE_2561 = os.environ.get("LJS_GEMM_TILE2561", "1") == "1"
 # 256x192 tile (8 waves of 64x96, 2 stages; a weight-major batch folded into one GEMM): fewer DMA
-# pieces and fragment reads per MFMA than 256x128, one stage less in flight (A/B: LJS_GEMM_TILE2562)
-_TILE_2562 = os.environ.get("LJS_GEMM_TILE2562", "0") == "1"
+# pieces and fragment reads per MFMA than 256x128, one stage less in flight.  On by default with the
+# lean K-loop kernel (round 5: QKV 33.5 vs 39.2 us isolated, B=64 step 0.2124 / 0.2159 vs 0.2250 /
+# 0.2189 ms, gpurun_out/r5g); LJS_GEMM_TILE2562=0 for the 256x128 tile
+_TILE_2562 = os.environ.get("LJS_GEMM_TILE2562", "1") == "1"
 # slab-mode GEMMs: the last item's f32 tile leaves through LDS as whole rows (kSlabVst)
 _SLAB_VST = os.environ.get("LJS_SLAB_VST", "1") == "1"
 

@@ -1,8 +1,8 @@
 """Lean K-loop GEMM (gemm.hip gemm_lean_kernel) against the general LDS-DMA kernel at the step's
 k-contiguous shapes: outputs must be bit-identical, then interleaved timing rounds in one process.
-Run with LJS_GEMM_LEAN=0 so the plain tile code selects the general kernel (code + 100000 = lean).
+Tile code + 100000 forces the lean kernel, + 200000 the general one.
 
-    LJS_GEMM_LEAN=0 python scripts/gemm_lean_ab.py            (T = 16384 and T = 2048 cases)
+    python scripts/gemm_lean_ab.py            (T = 16384 and T = 2048 cases)
 """
 import os
 import sys
@@ -71,19 +71,20 @@ def main():
             fns = {}
             for t in tiles:
                 outp.zero_()
-                mk(t)()
+                mk(t + 2 * LEAN)()
                 torch.cuda.synchronize()
                 ref = outp.clone()
                 outp.fill_(float("nan"))
                 mk(t + LEAN)()
                 torch.cuda.synchronize()
-                same = torch.equal(outp.view(torch.int16), ref.view(torch.int16))
+                iv = torch.int16
+                same = torch.equal(outp.view(iv), ref.view(iv))
                 print(f"T={T} {name:8s} tile {t}: lean bit-exact {'ok' if same else 'FAIL'}", flush=True)
                 if not same:
-                    bad = (outp.view(torch.int16) != ref.view(torch.int16)).nonzero()
+                    bad = (outp.view(iv) != ref.view(iv)).nonzero()
                     print("   first mismatches", bad[:5].tolist(), flush=True)
                     continue
-                fns[t] = mk(t)
+                fns[t + 2 * LEAN] = mk(t + 2 * LEAN)
                 fns[t + LEAN] = mk(t + LEAN)
             res = {t: [] for t in fns}
             for _ in range(ROUNDS):
@@ -92,7 +93,7 @@ def main():
             for t, v in res.items():
                 v = sorted(v)
                 med = v[len(v) // 2]
-                kind = "lean" if t >= LEAN else "general"
+                kind = "general" if t >= 2 * LEAN else "lean"
                 print(f"T={T} {name:8s} tile {t % LEAN} {kind:7s}: {med:7.2f} us ({flops / med / 1e6:6.0f} TF, "
                       f"min {v[0]:.2f})", flush=True)
 

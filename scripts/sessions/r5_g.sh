@@ -19,7 +19,12 @@ for cfg in "lean LJS_GEMM_LEAN=1" "gen LJS_GEMM_LEAN=0" "lean2562 LJS_GEMM_TILE2
   env $2 timeout -k 10 200 python bench.py --batch-per-gpu 8 --steps 20 --warmup 5 > $O/b8_$1_$i.log 2>&1 || exit 3
 done
 done
-for f in $O/b*_*.log; do grep -h '^{' $f | python -c "
+for i in 1 2; do
+  timeout -k 10 120 python scripts/attn_time.py > $O/attn8_$i.log 2>&1 || exit 3
+  LJS_ATTN_FWD_RES=16 timeout -k 10 120 python scripts/attn_time.py > $O/attn16_$i.log 2>&1 || exit 3
+done
+LJS_ATTN_FWD_RES=16 timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/b64_fwd16.log 2>&1 || exit 3
+for f in $O/b*_*.log $O/b64_fwd16.log; do grep -h '^{' $f | python -c "
 import sys,json
 r=json.loads(sys.stdin.readline()); print('$(basename $f)', r['ms_per_step'])" >> $O/summary.txt; done
 echo done
