@@ -33,9 +33,6 @@ _SIGS = {
     "ljs_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
                       c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
                       ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p, c_void_p],
-    "ljs_gemm_pp": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
-                    c_long, c_long, c_long, c_int, c_int, c_float, c_int, c_int, c_void_p, ctypes.POINTER(c_int),
-                    c_void_p, c_void_p],
     "ljs_sum_partials": [c_void_p, c_int, c_void_p, c_int, c_void_p],
     "ljs_mse_colsum_ws_bytes": [c_int, c_int],
     "ljs_gemm_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long,
@@ -262,14 +259,6 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     if tile is None:
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc, A.dtype, bias, sBias, relu, accumulate,
                          zero_c, psum, res, acopy, slabs, sA, sB, sC, ldb)
-    if _PP_BASE <= tile < _LEAN_REQ and slab16:
-        tile = None
-    if tile is not None and _PP_BASE <= tile < _LEAN_REQ:
-        rc, cnt = _gemm_pp(A, B, C, M, N, K, lda, ldb, ldc, a_kc, b_kc, batch, sA, sB, sC, bias, sBias, relu, alpha,
-                           splitk, tile - _PP_BASE, a_off, b_off, c_off, slabs, b_list, psum, acopy)
-        if rc == 0:
-            return cnt
-        tile = None   # a shape / option the ping-pong kernel does not take: the LDS-DMA kernels
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
         (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0) | (512 if slabs else 0) | \
@@ -296,42 +285,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     return cnt.value
 
 
-_PP_BASE = 30000   # tile codes >= _PP_BASE: the ping-pong kernel (csrc/kernels/gemm_pp.hip), cfg = code - base
 _LEAN_REQ = 100000  # tile code + _LEAN_REQ: force the lean K-loop kernel (gemm.hip gemm_lean_kernel; A/B),
                     # + 2 * _LEAN_REQ: force the general LDS-DMA kernel
-
-
-def _gemm_pp(A, B, C, M, N, K, lda, ldb, ldc, a_kc, b_kc, batch, sA, sB, sC, bias, sBias, relu, alpha, splitk,
-             cfg, a_off, b_off, c_off, slabs, b_list, psum=None, acopy=None):
-    """Launch the ping-pong GEMM; returns (HIP status, fused-sum partials written); a non-zero
-    status means the configuration was not taken (nothing launched).  cfg 21: f32 A (rounded in
-    the GEMM; ``acopy`` receives its bf16 copy)."""
-    kc_cfg = cfg < 10 or cfg == 21
-    if (A.dtype == torch.float32) != (cfg == 21) or kc_cfg != (a_kc and b_kc and C.dtype == torch.bfloat16) or \
-            (not kc_cfg and (a_kc or b_kc or C.dtype != torch.float32)) or (acopy is not None and cfg != 21):
-        return -1, 0
-    if batch > 1 and kc_cfg and sA == 0 and sB == N * ldb and sC == N and bias is None and ldc == batch * N:
-        # a batch of projections of ONE activation into interleaved column blocks (the fused
-        # QKV): one GEMM against the stacked [batch * N][K] weights
-        N, batch, sB, sC = N * batch, 1, 0, 0
-    flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
-        (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (32 if _GEMM_SC1 else 0) | \
-        (512 if slabs else 0)
-    eA = A.element_size()
-    b_arg = ctypes.c_void_p(B.data_ptr() + b_off * eA)
-    b_keep = None
-    if b_list is not None:
-        flags |= 4096
-        b_keep = (c_void_p * len(b_list))(*[t.data_ptr() + b_off * eA for t in b_list])
-        b_arg = ctypes.cast(b_keep, c_void_p)
-    cnt = c_int(0)
-    rc = lib().ljs_gemm_pp(ctypes.c_void_p(A.data_ptr() + a_off * eA), b_arg,
-                           ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb, ldc,
-                           sA, sB, sC, sBias, batch, flags, alpha, splitk, cfg, _p(psum), ctypes.byref(cnt),
-                           _p(acopy), _stream(C))
-    if rc == 0 and (_DEBUG_SYNC or os.environ.get("LJS_DEBUG_SYNC") == "1"):
-        _ck(0, "ljs_gemm_pp")
-    return rc, cnt.value
 
 
 def psum_slots(M: int, N: int, batch: int = 1) -> int:
@@ -383,61 +338,14 @@ _SLAB_VST = os.environ.get("LJS_SLAB_VST", "1") == "1"
 _TILE_1602 = os.environ.get("LJS_GEMM_TILE1602", "1") == "1"
 
 
-# ping-pong kernel (gemm_pp.hip) for the large k-contiguous bf16 GEMMs: "1" on, "0" off (the
-# default: in the B=64 step it ran QKV+cast 65.6 us vs 55.4, out-proj 21.7 vs 20.4, dh 19.6 vs
-# 18.0 - gpurun_out/r4c, profiles/r4c_b64_pp_kernels.md - and the step 0.2447 vs 0.2333 ms)
-_GEMM_PP = os.environ.get("LJS_GEMM_PP", "0") == "1"
-
-
-def _pick_pp(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc, a_dtype, bias, sBias, relu, accumulate, zero_c,
-             psum, res, acopy, slabs, sA, sB, sC, ldb) -> Optional[int]:
-    """A ping-pong configuration for this GEMM, or None (csrc/kernels/gemm_pp.hip)."""
-    if not _GEMM_PP or a_dtype not in (torch.bfloat16, torch.float32) or accumulate or zero_c or res is not None \
-            or K % 64 or (acopy is not None and a_dtype != torch.float32):
-        return None
-    if a_dtype == torch.float32:
-        # the activation cast fused in (cfg 21): the QKV projection shape, whole rounds of 128x384
-        Nf = N * batch
-        if (a_kc and b_kc and not out_f32 and splitk <= 1 and bias is None and not relu and psum is None
-                and (batch == 1 or (sA == 0 and sB == N * ldb and sC == N and ldc == Nf))
-                and Nf % 384 == 0 and (-(-M // 128) * (Nf // 384)) % _cus() == 0 and 4 * M * K < (1 << 31)):
-            return _PP_BASE + 21
-        return None
-    if a_kc and b_kc and not out_f32 and splitk <= 1 and N % 8 == 0 and ldc % 8 == 0:
-        Nf, nb = N, batch
-        if batch > 1 and sA == 0 and sB == N * ldb and sC == N and bias is None and ldc == batch * N:
-            Nf, nb = N * batch, 1          # interleaved column blocks: folded into one GEMM
-        cus = _cus()
-        if bias is not None and (sBias != 0 or Nf > 4096 or nb > 1):
-            return None
-        rows = -(-M // 128) * nb
-        # whole rounds of 256 blocks: [T][1536] at 128x384 (2 rounds at T = 16384), [T][640] at
-        # 128x320, [T][512] at 128x256 (a weight-major batch of 3: 3 rounds)
-        if bias is not None:
-            return _PP_BASE + 2 if Nf % 320 == 0 and (rows * (Nf // 320)) % cus == 0 else None
-        if Nf % 384 == 0 and (rows * (Nf // 384)) % cus == 0:
-            return _PP_BASE + 1
-        if Nf % 320 == 0 and (rows * (Nf // 320)) % cus == 0:
-            return _PP_BASE + 2
-        if Nf % 256 == 0 and (rows * (Nf // 256)) % cus == 0:
-            return _PP_BASE + 3
-        return None
-    return None
-
-
 def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f32: bool, splitk: int = 1,
               ldc: int = 0, a_dtype=None, bias=None, sBias: int = 0, relu: bool = False, accumulate: bool = False,
               zero_c: bool = False, psum=None, res=None, acopy=None, slabs: bool = False, sA: int = 0, sB: int = 0,
               sC: int = 0, ldb: int = 0) -> int:
-    """Kernel/tile choice (measured on MI355X at the bench shapes, ``scripts/gemm_one.py``):
-    the ping-pong kernel (codes >= 30000) where a configuration fills whole rounds of the chip, the
-    LDS-DMA kernels (codes 2561 = 256x128 8 waves, 1282 = 128x128 4 waves x 2 blocks/CU)
+    """Kernel/tile choice (measured on MI355X at the bench shapes, ``scripts/gemm_one.py``): the
+    LDS-DMA kernels (codes 2562 = 256x192 8 waves, 2561 = 256x128 8 waves, 1602 = 128x160 4 waves,
+    1282 = 128x128 4 waves x 2 blocks/CU, ...; the k-contiguous ones run the lean K-loop kernel)
     whenever K is a multiple of 64, else the register-staged 128/64 tiles."""
-    if a_dtype is not None:
-        pp = _pick_pp(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc, a_dtype, bias, sBias, relu, accumulate,
-                      zero_c, psum, res, acopy, slabs, sA, sB, sC, ldb)
-        if pp is not None:
-            return pp
     tiles128 = -(-M // 128) * -(-N // 128) * batch * max(1, splitk)
     if (_TILE_1602 and K % 64 == 0 and a_kc and b_kc and not out_f32 and splitk <= 1 and N % 160 == 0
             and ldc % 8 == 0 and tiles128 % 512 and (-(-M // 128) * (N // 160) * batch) % 512 == 0):

@@ -400,13 +400,11 @@ class _Linear(torch.autograd.Function):
                         and N % 8 == 0 and out_dtype == torch.bfloat16 and x2.data_ptr() % 16 == 0
                         and M * nw * N >= (1 << 20))
         # "auto": where the f32 A is register-staged (the 256x128 tile: global f32 -> VGPR -> bf16
-        # LDS image, the bf16 copy stored from the same registers) or the ping-pong kernel's f32-A
-        # configuration applies; the f32-LDS-image kernels stay opt-in ("1", measured slower)
+        # LDS image, the bf16 copy stored from the same registers); the f32-LDS-image kernels stay
+        # opt-in ("1", measured slower)
         if cast_on_load and _CAST_ON_LOAD != "1":
-            cast_on_load = _CAST_ON_LOAD == "auto" and (
-                hip.pick_tile(M, N, K, nw, True, True, False, 1, nw * N) == 2561 or hip._pick_pp(
-                    M, N, K, nw, True, True, False, 1, nw * N, torch.float32, None, 0, False, False, False, None,
-                    None, x2, False, 0, N * K, N, K) is not None)
+            cast_on_load = _CAST_ON_LOAD == "auto" and hip.pick_tile(M, N, K, nw, True, True, False, 1,
+                                                                     nw * N) == 2561
         if swap:   # batch-major x -> seq-major bf16 rows, rounded in the same pass
             xb = hip.swap01_bf16(x.contiguous()).view(M, K)
         else:

@@ -1,5 +1,5 @@
 """A/B timing of kernel-library builds at the headline step's GEMM shapes (T = 16384 tokens):
-the default tile of each case from scripts/gemm_pp_bench.py, medians of 7 rounds x 20 launches.
+the default tile of each case from scripts/gemm_cases.py, medians of 7 rounds x 20 launches.
 Run once per build (``LJS_KERNELS_LIB=<variant .so>``), interleaving the processes.
 
     python scripts/gemm_ab.py [case ...]     cases: qkv out dh dwqkv dwo, or case:tile (default: all)
@@ -8,7 +8,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-import gemm_pp_bench as gb  # noqa: E402
+import gemm_cases as gb  # noqa: E402
 
 
 def main():

@@ -1,7 +1,7 @@
-"""A/B timing of the ping-pong GEMM (gemm_pp.hip, tile codes >= 30000) against the LDS-DMA
-kernels at the headline step's shapes (T = 16384 tokens), interleaved rounds in one process.
+"""The headline step's GEMM shapes (T = 16384 tokens) with their candidate tiles, timed in
+interleaved rounds in one process (the case table scripts/gemm_ab.py times per library build).
 
-    python scripts/gemm_pp_bench.py [case ...]     cases: qkv out dh dwqkv dwo (default: all)
+    python scripts/gemm_cases.py [case ...]     cases: qkv qkv32 out dh dwqkv dwo (default: all)
 """
 import os
 import sys
@@ -13,7 +13,6 @@ from learning_jax_sharding_amd.ops import hip  # noqa: E402
 
 dev = torch.device("cuda")
 T = int(os.environ.get("T", "16384"))
-PP = hip._PP_BASE
 
 
 def timeit(fn, iters=20):
@@ -37,7 +36,7 @@ def cases():
     def qkv_fn(tile):
         return lambda: hip.gemm(x, wqkv, qkv, T, 512, 640, 640, 640, 1536, True, True, batch=3, sA=0, sB=512 * 640,
                                 sC=512, tile=tile)
-    out["qkv"] = (qkv_fn, [PP + 1, PP + 3, 2561], 2 * T * 640 * 1536)
+    out["qkv"] = (qkv_fn, [2561, 2562], 2 * T * 640 * 1536)
 
     x32 = torch.randn(T, 640, device=dev)
     xb = torch.empty(T, 640, device=dev).bfloat16()
@@ -49,7 +48,7 @@ def cases():
                                      sB=512 * 640, sC=512, tile=2561))
         return lambda: hip.gemm(x32, wqkv, qkv, T, 512, 640, 640, 640, 1536, True, True, batch=3, sA=0,
                                 sB=512 * 640, sC=512, acopy=xb, tile=tile)
-    out["qkv32"] = (qkv32_fn, [2561, PP + 21, "cast"], 2 * T * 640 * 1536)
+    out["qkv32"] = (qkv32_fn, [2561, "cast"], 2 * T * 640 * 1536)
 
     h = torch.randn(T, 512, device=dev).bfloat16()
     wo = torch.randn(640, 512, device=dev).bfloat16()
@@ -59,7 +58,7 @@ def cases():
 
     def out_fn(tile):
         return lambda: hip.gemm(h, wo, y, T, 640, 512, 512, 512, 640, True, True, bias=bo, psum=ps, tile=tile)
-    out["out"] = (out_fn, [PP + 2, 1602], 2 * T * 512 * 640)
+    out["out"] = (out_fn, [1602], 2 * T * 512 * 640)
 
     dy = torch.randn(T, 640, device=dev).bfloat16()
     won = torch.randn(512, 640, device=dev).bfloat16()
@@ -67,7 +66,7 @@ def cases():
 
     def dh_fn(tile):
         return lambda: hip.gemm(dy, won, dh, T, 512, 640, 640, 640, 512, True, True, tile=tile)
-    out["dh"] = (dh_fn, [PP + 3, PP + 4, 1282], 2 * T * 512 * 640)
+    out["dh"] = (dh_fn, [2561, 1282], 2 * T * 512 * 640)
 
     dq = [torch.randn(T, 512, device=dev).bfloat16() for _ in range(3)]
 
@@ -77,7 +76,7 @@ def cases():
         sl = torch.empty(Se, 3, 640, 512, device=dev)
         return lambda: hip.gemm(x, dq[0], sl, 640, 512, T, 640, 512, 512, False, False, batch=3, sA=0,
                                 sC=640 * 512, splitk=Se, tile=tile, slabs=True, b_list=dq)
-    out["dwqkv"] = (dwqkv_fn, [PP + 11, PP + 12, 1282], 2 * T * 640 * 1536)
+    out["dwqkv"] = (dwqkv_fn, [1282], 2 * T * 640 * 1536)
 
     def dwo_fn(tile, S=24):
         nkt = T // 64
@@ -85,7 +84,7 @@ def cases():
         sl = torch.empty(Se, 512, 640, device=dev)
         return lambda: hip.gemm(h, dy, sl, 512, 640, T, 512, 640, 640, False, False, sC=512 * 640, splitk=Se,
                                 tile=tile, slabs=True)
-    out["dwo"] = (dwo_fn, [PP + 12, PP + 11, 1282], 2 * T * 512 * 640)
+    out["dwo"] = (dwo_fn, [1282], 2 * T * 512 * 640)
     return out
 
 
