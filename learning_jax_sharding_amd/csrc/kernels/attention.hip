@@ -168,6 +168,20 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16_t* lds, int base0, int base
   return join_bf16x8(lo, hi);
 }
 
+// dS^T image of the fused backward ([keys][64 queries] bf16): 8-byte piece c8 of row r sits at
+// c8 ^ fs(r & 15), fs a permutation of 0..15.  Its ds_write_b64 (16 contiguous lanes = 16 keys at
+// one c8 per bank group, bank = dword mod 32) hit only 4 distinct piece positions under img8's
+// 16-byte swizzle: 4-way conflicts, 24.5 % of the kernel's LDS cycles (profiles/r5j_step_pmc.md).
+// With fs the 16 keys cover all 16 positions, and the transposed reads (rows 0..7 / 8..15 per
+// half-wave, 4 consecutive pieces per row) still see distinct fs >> 2 per row parity: both
+// conflict-free.  Row offsets that are multiples of 16 do not change the swizzle.
+__device__ __forceinline__ int fs_swz(int row) { return (((row >> 1) & 3) << 2) | ((row & 1) << 1) | ((row >> 3) & 1); }
+__device__ __forceinline__ int imgS(int row, int c8) { return row * D + ((c8 ^ fs_swz(row & 15)) << 2); }
+__device__ __forceinline__ int trS_off(int db, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  return imgS(4 * g + (i >> 2), (db >> 2) + (i & 3));
+}
+
 // frag_tr with the row base split off: rows R0 + (4g + q) and R0 + 16 + (4g + q) for R0 a multiple
 // of 8 (the swizzle depends on (row >> 1) & 3 only, which R0 does not change), so the lane part
 // `off` = tr_off(db, lane) is computed once per kernel and R0 becomes an immediate LDS offset.
@@ -1464,7 +1478,7 @@ __device__ __forceinline__ void fused_tile(const AttnArgs& a, const bf16_t* Qt, 
         sbu[j][2 * tt] = pack_bf16x2(dsv[0], dsv[1]);
         sbu[j][2 * tt + 1] = pack_bf16x2(dsv[2], dsv[3]);
         // dS^T row (this lane's key), queries 16t + 4g .. +3
-        *reinterpret_cast<u32x2*>(dSt + img8(key0 + 16 * j + (lane & 15), 4 * t + g)) =
+        *reinterpret_cast<u32x2*>(dSt + imgS(key0 + 16 * j + (lane & 15), 4 * t + g)) =
             u32x2{sbu[j][2 * tt], sbu[j][2 * tt + 1]};
       }
     }
@@ -1604,7 +1618,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   int offtr[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) offtr[dt] = tr_off(16 * dt, lane);
-  const int off_q = tr_off(16 * qt, lane);
+  const int off_q = trS_off(16 * qt, lane);   // (dS^T image)
   const int off_k[2] = {tr_off(16 * dt0, lane), tr_off(16 * (dt0 + 1), lane)};
   // static priority for the second-dispatched half (MI355X_MICROARCH "Two waves per SIMD" item
   // 4): waves 4-7 lose VALU arbitration to their SIMD partners on every segment otherwise

@@ -3,6 +3,7 @@
 // capped at 2048 workgroups so one launch fills the 256 CUs without oversubscription.
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace {
 
@@ -524,6 +525,7 @@ struct AdamTensor {
   // their sum, added in slab_reduce's order: bit-identical, and no combine launch); gS = -1 a
   // constant gradient whose f32 bits are g_ld (the bias gradient of a loss-sum cotangent)
   long gS, g_ld, g_ss;
+  long trows;   // tile height: the launch's kAdamRows, or 16 / 32 (4-wide path, C % 64 == 0)
 };
 
 // the slab sum of slab_reduce_kernel, in its order (bit-identical results)
@@ -553,14 +555,68 @@ struct AdamBatch {
 
 // `step_offset`/`ticket`: with a ticket the kernel uses t = *step + step_offset and its last
 // arriving block stores *step + 1 (the optimizer's count increment, folded in: no extra launch).
-template <int kAdamRows>
-__global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* __restrict__ step, int step_offset,
-                                                         unsigned* __restrict__ ticket, float lr, float b1, float b2,
-                                                         float eps, float wd) {
+// kThreads: 256 (4 rows x 64 columns per pass) or 1024 (16 x 64 per pass, one row per thread on
+// 64-row tiles: 4x the waves per tile, so the slab streams have 4x the loads in flight per CU --
+// the kernel reads data the weight-gradient GEMMs just left in L2 / Infinity Cache, where the
+// fill rate scales with the number of waves issuing; profiles/r5c_probe_lds_fill.txt)
+//
+// The count increment's ticket (two-level, ticket_last_2lvl's words).  With `early` each block
+// draws its group word as soon as every wave holds its step value and its first loads are issued,
+// and reads the result once its loads have landed (before the Adam math, so the wait costs
+// nothing); each group's last arriver then draws the top word, and the overall last stores
+// step + 1 when it ends.  Drawn at the end after a full barrier (`early` 0) the increment cost the
+// store drain plus two serial atomic round trips per block: 13.1 vs 8.7 us for the step's parameter
+// set without it (scripts/adam_probe.py, gpurun_out/r5n).  The draw is a vector atomic from
+// inline asm: through the builtin, the compiler's wave-level atomic rewrite broadcast the result
+// (v_readfirstlane) and so waited for the atomic -- and every load before it -- at the draw.
+// (`early` 2: one word for all blocks, no second level)
+__device__ __forceinline__ unsigned draw_ticket(unsigned* ticket, int s0, int early) {
+  asm volatile("" ::"s"(__builtin_amdgcn_readfirstlane(s0)));   // this wave has its step value
+  __builtin_amdgcn_s_barrier();                                  // ... and so has every wave
+  unsigned tk = 0;
+  if (threadIdx.x == 0) {
+    unsigned* w = early == 2 ? ticket : ticket + 1 + (blockIdx.x >> 5);
+    asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(tk) : "v"(w), "v"(1u) : "memory");
+  }
+  return tk;
+}
+// thread 0 of the block drawing the overall last ticket gets true
+__device__ __forceinline__ bool settle_ticket(unsigned* ticket, unsigned tk, int early) {
+  if (threadIdx.x != 0) return false;
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(tk)::"memory");   // the draw's result
+  if (early == 2) {
+    if (tk != gridDim.x - 1) return false;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  const unsigned grp = blockIdx.x >> 5, n = gridDim.x;
+  const unsigned in_grp = n - (grp << 5) < 32u ? n - (grp << 5) : 32u;
+  if (tk != in_grp - 1) return false;
+  __hip_atomic_store(ticket + 1 + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ticket_last(ticket, (n + 31) >> 5);
+}
+__device__ __forceinline__ void finish_ticket(unsigned* ticket, int* step, int s0, int early, bool last) {
+  if (early) {
+    if (last) __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // every thread of this block has consumed its read of *step before the ticket is drawn
+  __syncthreads();
+  if (threadIdx.x == 0 && ticket_last_2lvl(ticket, blockIdx.x, gridDim.x))
+    __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int kAdamRows, int kThreads>
+__global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, int* __restrict__ step, int step_offset,
+                                                         unsigned* __restrict__ ticket, int early, float lr, float b1,
+                                                         float b2, float eps, float wd) {
   __shared__ float tr[kAdamRows][65];
   const int id = blockIdx.x;
+  // tensor of this tile: every tile_start compared at once (the loop form chained one kernel-
+  // argument load per tensor before the tile's first data load could issue)
   int ti = 0;
-  while (ti + 1 < batch.n && id >= batch.tile_start[ti + 1]) ++ti;
+#pragma unroll
+  for (int i = 1; i < kAdamMax; ++i) ti += (i < batch.n && id >= batch.tile_start[i]) ? 1 : 0;
   const AdamTensor T = batch.t[ti];
   const int local = id - batch.tile_start[ti];
   const int tr_i = local / (int)T.tiles_c, tc_i = local % (int)T.tiles_c;
@@ -572,19 +628,23 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
   float* Vv = reinterpret_cast<float*>(T.v);
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int col = tc_i * 64 + tx;
-  if (T.vec && (tc_i + 1) * 64 <= T.C) {
+  constexpr int RPP = kThreads / 16;   // rows per pass of the 4-wide path
+  // the 4-wide path of one tile of TR = RPP x NQ rows (the tensor's tile height T.trows)
+  auto vec_tile = [&](auto nq_tag) {
+    constexpr int NQ = decltype(nq_tag)::value;
+    constexpr int TR = RPP * NQ;
+    static_assert(NQ >= 1 && TR <= kAdamRows, "tile height");
     // full-width column block, 16-byte aligned rows: each thread owns 4 consecutive columns of
-    // 4 rows (all 16 loads issued up front), vector p/m/v/g loads and stores, 8-byte bf16
+    // NQ rows (all loads issued up front), vector p/m/v/g loads and stores, 8-byte bf16
     // shadow stores; the transposed shadow leaves as 8-byte stores from the LDS transpose
     const int c4 = (threadIdx.x & 15) * 4, r0 = threadIdx.x >> 4;
     const long cbase = (long)tc_i * 64 + c4;
-    constexpr int NQ = kAdamRows / 16;
     f32x4 gv[NQ], mv[NQ], vv[NQ], pv[NQ];
     bool ok[NQ];
     long gix[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const int row = tr_i * kAdamRows + r0 + 16 * q;
+      const int row = tr_i * TR + r0 + RPP * q;
       ok[q] = row < T.R;
       gix[q] = ok[q] ? (long)row * T.g_ld + cbase : cbase;
       const long i = ok[q] ? (long)row * T.C + cbase : cbase;
@@ -593,6 +653,8 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
       vv[q] = *(const __attribute__((address_space(1))) f32x4*)(Vv + i);
       pv[q] = *(const __attribute__((address_space(1))) f32x4*)(P + i);
     }
+    unsigned tk = 0;
+  if (ticket && early) tk = draw_ticket(ticket, s0, early);
     if (T.gS > 0) {
       // the slab sum of slab_reduce_kernel (same order, bit-identical) with the loads of all NQ
       // rows of a 4-slab group in flight together; f32 or bf16 slabs (T.g_bf16)
@@ -683,9 +745,10 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
         gv[q] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(T.g) + gi);
       }
     }
+    const bool last = ticket && early && settle_ticket(ticket, tk, early);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const int rl = r0 + 16 * q;
+      const int rl = r0 + RPP * q;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float g = gv[q][e];
@@ -698,7 +761,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
         tr[rl][c4 + e] = pv[q][e];
       }
       if (ok[q]) {
-        const long i = (long)(tr_i * kAdamRows + rl) * T.C + cbase;
+        const long i = (long)(tr_i * TR + rl) * T.C + cbase;
         *reinterpret_cast<f32x4*>(P + i) = pv[q];
         *reinterpret_cast<f32x4*>(Mm + i) = mv[q];
         *reinterpret_cast<f32x4*>(Vv + i) = vv[q];
@@ -715,7 +778,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
         const int x = mx_exponent(amax);
         const float inv = ldexpf(1.f, -x);
         if (ok[q]) {
-          const long i = (long)(tr_i * kAdamRows + rl) * T.C + cbase;
+          const long i = (long)(tr_i * TR + rl) * T.C + cbase;
           *reinterpret_cast<unsigned*>(reinterpret_cast<unsigned char*>(T.qn) + i) =
               pack4_e4m3(pv[q][0] * inv, pv[q][1] * inv, pv[q][2] * inv, pv[q][3] * inv);
           if ((threadIdx.x & 7) == 0) reinterpret_cast<unsigned char*>(T.sn8)[i / 32] = (unsigned char)(x + 127);
@@ -726,13 +789,14 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
       __syncthreads();
       // shadow_t[c][r]: thread -> 4 consecutive rows r4..r4+3 of output row c (bank-conflict
       // free: tr's row stride is 65 words)
-      constexpr int RL = kAdamRows / 4;            // lanes across the tile's rows
+      constexpr int RL = TR / 4;            // lanes across the tile's rows
       const int r4 = (threadIdx.x % RL) * 4, cl0 = threadIdx.x / RL;
-      const int orow0 = tc_i * 64, ocol = tr_i * kAdamRows + r4;
+      const int orow0 = tc_i * 64, ocol = tr_i * TR + r4;
       const bool rows_vec = (T.R & 3) == 0 && ocol + 4 <= T.R;
+      static_assert(kThreads / RL <= 64, "transpose pass wider than the tile");
 #pragma unroll
-      for (int q = 0; q < 64 / (256 / RL); ++q) {
-        const int cl = cl0 + (256 / RL) * q, c = orow0 + cl;
+      for (int q = 0; q < 64 / (kThreads / RL); ++q) {
+        const int cl = cl0 + (kThreads / RL) * q, c = orow0 + cl;
         if (T.st) {
           bf16_t* dst = reinterpret_cast<bf16_t*>(T.st) + (long)c * T.R + ocol;
           if (rows_vec) {
@@ -758,16 +822,26 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
         }
       }
     }
-    if (ticket) {
-      __syncthreads();
-      if (threadIdx.x == 0 && ticket_last_2lvl(ticket, blockIdx.x, gridDim.x))
-        __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ticket) finish_ticket(ticket, step, s0, early, last);
+  };
+  if (T.vec && (tc_i + 1) * 64 <= T.C) {
+    // per-tensor tile height (the launch's choice): shorter tiles for tensors with many gradient
+    // slabs, so their blocks' slab streams are no longer the kernel's tail
+    if constexpr (RPP == 16) {
+      if (T.trows == 16) vec_tile(std::integral_constant<int, 1>{});
+      else if (kAdamRows >= 32 && T.trows == 32) vec_tile(std::integral_constant<int, (kAdamRows >= 32 ? 2 : 1)>{});
+      else vec_tile(std::integral_constant<int, kAdamRows / RPP>{});
+    } else {
+      vec_tile(std::integral_constant<int, kAdamRows / RPP>{});
     }
     return;
   }
+  unsigned tk = 0;
+  if (ticket && early) tk = draw_ticket(ticket, s0, early);
+  const bool last = ticket && early && settle_ticket(ticket, tk, early);
 #pragma unroll 4
-  for (int rr = 0; rr < kAdamRows / 4; ++rr) {
-    const int rl = ty + 4 * rr, row = tr_i * kAdamRows + rl;
+  for (int rr = 0; rr < kAdamRows / (kThreads / 64); ++rr) {
+    const int rl = ty + (kThreads / 64) * rr, row = tr_i * kAdamRows + rl;
     float newp = 0.f;
     if (row < T.R && col < T.C) {
       const long i = (long)row * T.C + col;
@@ -791,17 +865,12 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamBatch batch, int* _
   if (T.st) {
     __syncthreads();
     const int orow0 = tc_i * 64;  // shadow_t[c][r]
-    for (int idx = threadIdx.x; idx < kAdamRows * 64; idx += 256) {
+    for (int idx = threadIdx.x; idx < kAdamRows * 64; idx += kThreads) {
       const int r = idx % kAdamRows, cl = idx / kAdamRows, c = orow0 + cl, ocol = tr_i * kAdamRows + r;
       if (c < T.C && ocol < T.R) reinterpret_cast<bf16_t*>(T.st)[(long)c * T.R + ocol] = f2bf(tr[r][cl]);
     }
   }
-  if (ticket) {
-    // every thread of this block has consumed its read of *step before the ticket is drawn
-    __syncthreads();
-    if (threadIdx.x == 0 && ticket_last_2lvl(ticket, blockIdx.x, gridDim.x))
-      __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (ticket) finish_ticket(ticket, step, s0, early, last);
 }
 
 // ------------------------------------------------------------------ Philox RNG
@@ -1415,6 +1484,16 @@ LJS_API int ljs_dropout(const void* x, void* y, int is_bf16, int ndim, const lon
   return (int)hipGetLastError();
 }
 
+// the optimizer count's increment as its own one-lane launch (ops/hip.py adam_multi: the ticket
+// form's cost in the Adam kernel exceeds a launch, scripts/adam_probe.py)
+__global__ void step_add_kernel(int* step) {
+  if (threadIdx.x == 0) *step += 1;
+}
+LJS_API int ljs_step_add(void* step, hipStream_t s) {
+  hipLaunchKernelGGL(step_add_kernel, dim3(1), dim3(64), 0, s, (int*)step);
+  return (int)hipGetLastError();
+}
+
 // table: n x 16 int64 {p, g, m, v, shadow_t, shadow_n, R, C, g_bf16, gS, qn, sn8, qt, st8, g_ld, g_ss}
 // (see AdamTensor); up to 32 per call
 LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset, void* ticket, float lr, float b1,
@@ -1423,6 +1502,11 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   AdamBatch b;
   static const int rows = getenv("LJS_ADAM_ROWS") ? atoi(getenv("LJS_ADAM_ROWS")) : 64;
   const int kAdamRows = rows == 16 || rows == 32 ? rows : 64;
+  static const int threads = getenv("LJS_ADAM_THREADS") ? atoi(getenv("LJS_ADAM_THREADS")) : 256;
+  // tensors whose gradient is >= split_s slabs get 32-row tiles (>= 3 split_s: 16-row): their
+  // blocks read split_s x more than a plain gradient's, and at 64 rows they were the kernel's tail
+  // (W_o's 24 slabs at B=64 against the QKV weights' 8).  LJS_ADAM_SPLIT_S=0: off.
+  static const int split_s = getenv("LJS_ADAM_SPLIT_S") ? atoi(getenv("LJS_ADAM_SPLIT_S")) : 16;
   int tiles = 0;
   for (int i = 0; i < n; ++i) {
     const long* r = table + 16 * i;
@@ -1442,21 +1526,32 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
     if ((t.qn || t.qt) && (!t.vec || kAdamRows != 64 || t.R % 64 || t.C % 64 || !al(t.qn, 4) || !al(t.qt, 4) ||
                            (t.qn && !t.sn8) || (t.qt && !t.st8)))
       return (int)hipErrorInvalidValue;
+    t.trows = kAdamRows;
+    if (kAdamRows == 64 && threads == 256 && split_s > 0 && t.vec && t.C % 64 == 0 && !t.qn && !t.qt &&
+        t.gS >= split_s)
+      t.trows = t.gS >= 3 * split_s ? 16 : 32;
     b.tile_start[i] = tiles;
-    tiles += (int)(((t.R + kAdamRows - 1) / kAdamRows) * t.tiles_c);
+    tiles += (int)(((t.R + t.trows - 1) / t.trows) * t.tiles_c);
   }
   b.tile_start[n] = tiles;
   b.n = n;
   if (ticket && 1 + (tiles + 31) / 32 > (64 << 10) / 4) return (int)hipErrorInvalidValue;  // ticket words
+  static const int early = getenv("LJS_ADAM_EARLY_TICKET") ? atoi(getenv("LJS_ADAM_EARLY_TICKET")) : 1;
   if (kAdamRows == 16)
-    hipLaunchKernelGGL(adam_multi_kernel<16>, dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, lr, b1, b2, eps, wd);
+    hipLaunchKernelGGL((adam_multi_kernel<16, 256>), dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
   else if (kAdamRows == 32)
-    hipLaunchKernelGGL(adam_multi_kernel<32>, dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, lr, b1, b2, eps, wd);
+    hipLaunchKernelGGL((adam_multi_kernel<32, 256>), dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
+  else if (threads == 1024)
+    hipLaunchKernelGGL((adam_multi_kernel<64, 1024>), dim3(tiles), dim3(1024), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
+  else if (threads == 512)
+    hipLaunchKernelGGL((adam_multi_kernel<64, 512>), dim3(tiles), dim3(512), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
   else
-    hipLaunchKernelGGL(adam_multi_kernel<64>, dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, lr, b1, b2, eps, wd);
+    hipLaunchKernelGGL((adam_multi_kernel<64, 256>), dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
   return (int)hipGetLastError();
 }
 

@@ -66,6 +66,7 @@ _SIGS = {
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
     "ljs_adam_multi": [_LP, c_int, c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float,
                        c_void_p],
+    "ljs_step_add": [c_void_p, c_void_p],
     "ljs_mse_loss": [c_void_p, c_void_p, c_int, c_long, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_mse_colsum": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p],
@@ -1466,6 +1467,13 @@ class ConstGrad:
         self.value, self.shape = float(value), tuple(shape)
 
 
+# How adam_multi's ``increment_step`` advances the count: "kernel" (default) a one-lane launch after
+# the Adam launches; "ticket" the last-arriving block of the last Adam launch (a two-level arrival
+# ticket in the kernel, LJS_ADAM_EARLY_TICKET picks its form).  The step's parameter set in a
+# graph (scripts/adam_probe.py, gpurun_out/r5n): no increment 9.1 us, + launch 10.7, ticket 13.0-13.5.
+_STEP_INC = os.environ.get("LJS_ADAM_STEP_INC", "kernel")
+
+
 def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step: bool = False) -> None:
     """In-place fused Adam over many params (one launch per 32): entries = [(p, g, m, v)].
 
@@ -1502,7 +1510,8 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
     if increment_step:
         assert step.dtype == torch.int32 and step.is_contiguous()
     step_i = step if step.dtype == torch.int32 else step.to(torch.int32)
-    ticket = _workspace(step_i.device, "adam_ticket", 64 << 10) if increment_step else None  # two-level tickets
+    use_ticket = increment_step and _STEP_INC == "ticket"
+    ticket = _workspace(step_i.device, "adam_ticket", 64 << 10) if use_ticket else None  # two-level tickets
     rows = _early_adam(rows, step_i, lr, b1, b2, eps, wd, increment_step)
     for i in range(0, len(rows), 32):
         chunk = rows[i:i + 32]
@@ -1510,9 +1519,11 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
         arr = (ctypes.c_long * tab.size)(*tab.tolist())
         last = i + 32 >= len(rows)
         rc = lib().ljs_adam_multi(arr, len(chunk), _p(step_i), int(increment_step),
-                                  _p(ticket) if (increment_step and last) else None, lr, b1, b2, eps, wd,
+                                  _p(ticket) if (use_ticket and last) else None, lr, b1, b2, eps, wd,
                                   _stream(step_i))
         _ck(rc, "ljs_adam_multi")
+    if increment_step and not use_ticket:
+        _ck(lib().ljs_step_add(_p(step_i), _stream(step_i)), "ljs_step_add")
     for p, _, _, _ in entries:
         shadow.mark_fresh(p)
 

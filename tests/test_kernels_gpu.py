@@ -442,6 +442,41 @@ def test_adam_multi_slab_grads_bit_exact(hip, S):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("S", [16, 24, 48])
+def test_adam_multi_short_tiles_with_shadows(hip, S):
+    """Tensors with >= 16 gradient slabs run in 32-row tiles (>= 48: 16-row) chosen per tensor in
+    the same launch as 64-row ones: p/m/v and both bf16 shadows equal slab_reduce + Adam on the
+    combined gradient (64-row tiles), bit for bit."""
+    from learning_jax_sharding_amd.ops import shadow
+    shapes = [(640, 512), (512, 640), (200, 128)]
+    Ss = [4, S, S]
+    ws = [torch.randn(*sh, device=dev) for sh in shapes]
+    slabs = [torch.randn(k, *sh, device=dev) for k, sh in zip(Ss, shapes)]
+    ms = [torch.rand(*sh, device=dev) * 1e-2 for sh in shapes]
+    vs = [torch.rand(*sh, device=dev) * 1e-3 for sh in shapes]
+    w2, m2, v2 = [w.clone() for w in ws], [m.clone() for m in ms], [v.clone() for v in vs]
+    for w in ws + w2:
+        shadow.get(w, "T")
+        shadow.get(w, "N")
+    step = torch.full((), 5, dtype=torch.int32, device=dev)
+    gsl = [hip.SlabGrad(sl, k, 0, sh[1], sh[0] * sh[1], sh) for sl, k, sh in zip(slabs, Ss, shapes)]
+    hip.adam_multi(list(zip(ws, gsl, ms, vs)), step, 1e-3, 0.9, 0.999, 1e-8, 0.01)
+    gc = []
+    for sl, sh in zip(slabs, shapes):
+        g = torch.empty(*sh, device=dev)
+        hip.slab_reduce(sl, g, sh[1], sh[0] * sh[1])
+        gc.append(g)
+    hip.adam_multi(list(zip(w2, gc, m2, v2)), step, 1e-3, 0.9, 0.999, 1e-8, 0.01)
+    torch.cuda.synchronize()
+    for a, b in zip(ws + ms + vs, w2 + m2 + v2):
+        assert torch.equal(a, b)
+    for a, b in zip(ws, w2):
+        ea, eb = shadow.entry(a, create=False), shadow.entry(b, create=False)
+        for kind in ("T", "N"):
+            assert torch.equal(ea.bufs[kind].view(torch.int16), eb.bufs[kind].view(torch.int16)), kind
+        assert torch.equal(ea.bufs["T"], a.t().bfloat16())
+
+
 @pytest.mark.parametrize("with_bf16", [False, True])
 def test_adam_multi_mx_shadows(hip, with_bf16):
     """The fused Adam rewrites a weight's MX-fp8 shadows (blocks along rows and, transposed,
