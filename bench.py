@@ -300,6 +300,8 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
     (barrier + synchronize on both sides, max over ranks).  Returns the timing and its context."""
     torch, ljs, dist = env["torch"], env["ljs"], env["dist"]
     n, dist_on, cuda = env["n"], env["dist_on"], env["cuda"]
+    if cuda:
+        torch.cuda.reset_peak_memory_stats()
     barrier_sync, phase = env["barrier_sync"], env["phase"]
     from learning_jax_sharding_amd import nn, optim
     from learning_jax_sharding_amd.mesh import Mesh, create_device_mesh
@@ -451,11 +453,14 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
         flops = transformer_layer_flops(B, S, M, args.heads, args.dim_head, args.ff_dim, train=args.mode == "train")
     else:
         flops = attention_block_flops(B, S, M, args.heads, args.dim_head, train=args.mode == "train")
+    # device memory held by this layout's graphs, state and caches (the G-step graph's private
+    # pool grows with G: PERF_NOTES round 5, multi-step graphs)
+    peak_gb = torch.cuda.max_memory_reserved() / 1e9 if cuda else None
     # free this layout's graphs and state before another layout is built (the secondary run)
     del state, step, multi
     return dict(ms=ms, tflops_total=flops / (ms * 1e-3) / 1e12, tokens_per_s=B * S / (ms * 1e-3),
                 host_ms=(th - t0) / args.steps * 1e3, mshape=mshape, B=B, S=S, M=M, G=G, segs=segs,
-                warm_run=warm_run, capture=capture)
+                warm_run=warm_run, capture=capture, peak_gb=peak_gb)
 
 
 def _record(args, res, n, n_gpus, cuda, comm):
@@ -487,6 +492,7 @@ def _record(args, res, n, n_gpus, cuda, comm):
         "tflops_per_gpu": round(res["tflops_total"] / max(1, n_gpus if cuda else n), 3),
         "tokens_per_s": round(res["tokens_per_s"], 1),
         "host_ms_per_step": round(res["host_ms"], 4),
+        "peak_mem_reserved_gb": None if res["peak_gb"] is None else round(res["peak_gb"], 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

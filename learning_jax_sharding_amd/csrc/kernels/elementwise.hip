@@ -555,60 +555,48 @@ struct AdamBatch {
 
 // `step_offset`/`ticket`: with a ticket the kernel uses t = *step + step_offset and its last
 // arriving block stores *step + 1 (the optimizer's count increment, folded in: no extra launch).
-// kThreads: 256 (4 rows x 64 columns per pass) or 1024 (16 x 64 per pass, one row per thread on
-// 64-row tiles: 4x the waves per tile, so the slab streams have 4x the loads in flight per CU --
-// the kernel reads data the weight-gradient GEMMs just left in L2 / Infinity Cache, where the
-// fill rate scales with the number of waves issuing; profiles/r5c_probe_lds_fill.txt)
+// kThreads: 256 (16 rows x 64 columns per pass).  512 / 1024 (more waves per tile, fewer loads per
+// thread) measured the same, 20.9 / 21.7 / 21.5 us in the B=64 step (gpurun_out/r5m): the loads in
+// flight per tile do not change with the thread count.
 //
-// The count increment's ticket (two-level, ticket_last_2lvl's words).  With `early` each block
-// draws its group word as soon as every wave holds its step value and its first loads are issued,
-// and reads the result once its loads have landed (before the Adam math, so the wait costs
-// nothing); each group's last arriver then draws the top word, and the overall last stores
-// step + 1 when it ends.  Drawn at the end after a full barrier (`early` 0) the increment cost the
-// store drain plus two serial atomic round trips per block: 13.1 vs 8.7 us for the step's parameter
-// set without it (scripts/adam_probe.py, gpurun_out/r5n).  The draw is a vector atomic from
-// inline asm: through the builtin, the compiler's wave-level atomic rewrite broadcast the result
-// (v_readfirstlane) and so waited for the atomic -- and every load before it -- at the draw.
-// (`early` 2: one word for all blocks, no second level)
-__device__ __forceinline__ unsigned draw_ticket(unsigned* ticket, int s0, int early) {
+// The count increment's ticket (opt-in, ops/hip.py LJS_ADAM_STEP_INC=ticket; two-level,
+// ticket_last_2lvl's words).  Each block draws its group word as soon as every wave holds its step
+// value and its first loads are issued, and reads the result once its loads have landed (before
+// the Adam math, so the wait costs nothing); each group's last arriver then draws the top word, and
+// the overall last stores step + 1 when it ends.  Drawn at the end after a full barrier (the round-4
+// form) the increment cost the store drain plus two serial atomic round trips per block: 13.8 vs
+// 9.1 us for the step's parameter set with plain gradients and no increment; drawn early, 13.2; one
+// word for all blocks, 12.8; a separate one-lane launch, 10.8 (scripts/adam_probe.py,
+// profiles/r5n_adam_probe_*.txt) -- hence the launch is the default.  The draw is a vector atomic
+// from inline asm: through the builtin, the compiler's wave-level atomic rewrite broadcast the
+// result (v_readfirstlane) and so waited for the atomic -- and every load before it -- at the draw.
+__device__ __forceinline__ unsigned draw_ticket(unsigned* ticket, int s0) {
   asm volatile("" ::"s"(__builtin_amdgcn_readfirstlane(s0)));   // this wave has its step value
   __builtin_amdgcn_s_barrier();                                  // ... and so has every wave
   unsigned tk = 0;
   if (threadIdx.x == 0) {
-    unsigned* w = early == 2 ? ticket : ticket + 1 + (blockIdx.x >> 5);
+    unsigned* w = ticket + 1 + (blockIdx.x >> 5);
     asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(tk) : "v"(w), "v"(1u) : "memory");
   }
   return tk;
 }
 // thread 0 of the block drawing the overall last ticket gets true
-__device__ __forceinline__ bool settle_ticket(unsigned* ticket, unsigned tk, int early) {
+__device__ __forceinline__ bool settle_ticket(unsigned* ticket, unsigned tk) {
   if (threadIdx.x != 0) return false;
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(tk)::"memory");   // the draw's result
-  if (early == 2) {
-    if (tk != gridDim.x - 1) return false;
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
-  }
   const unsigned grp = blockIdx.x >> 5, n = gridDim.x;
   const unsigned in_grp = n - (grp << 5) < 32u ? n - (grp << 5) : 32u;
   if (tk != in_grp - 1) return false;
   __hip_atomic_store(ticket + 1 + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return ticket_last(ticket, (n + 31) >> 5);
 }
-__device__ __forceinline__ void finish_ticket(unsigned* ticket, int* step, int s0, int early, bool last) {
-  if (early) {
-    if (last) __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  // every thread of this block has consumed its read of *step before the ticket is drawn
-  __syncthreads();
-  if (threadIdx.x == 0 && ticket_last_2lvl(ticket, blockIdx.x, gridDim.x))
-    __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void finish_ticket(int* step, int s0, bool last) {
+  if (last) __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int kAdamRows, int kThreads>
 __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, int* __restrict__ step, int step_offset,
-                                                         unsigned* __restrict__ ticket, int early, float lr, float b1,
+                                                         unsigned* __restrict__ ticket, float lr, float b1,
                                                          float b2, float eps, float wd) {
   __shared__ float tr[kAdamRows][65];
   const int id = blockIdx.x;
@@ -654,7 +642,7 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
       pv[q] = *(const __attribute__((address_space(1))) f32x4*)(P + i);
     }
     unsigned tk = 0;
-  if (ticket && early) tk = draw_ticket(ticket, s0, early);
+  if (ticket) tk = draw_ticket(ticket, s0);
     if (T.gS > 0) {
       // the slab sum of slab_reduce_kernel (same order, bit-identical) with the loads of all NQ
       // rows of a 4-slab group in flight together; f32 or bf16 slabs (T.g_bf16)
@@ -745,7 +733,7 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
         gv[q] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(T.g) + gi);
       }
     }
-    const bool last = ticket && early && settle_ticket(ticket, tk, early);
+    const bool last = ticket && settle_ticket(ticket, tk);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int rl = r0 + RPP * q;
@@ -822,7 +810,7 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
         }
       }
     }
-    if (ticket) finish_ticket(ticket, step, s0, early, last);
+    if (ticket) finish_ticket(step, s0, last);
   };
   if (T.vec && (tc_i + 1) * 64 <= T.C) {
     // per-tensor tile height (the launch's choice): shorter tiles for tensors with many gradient
@@ -837,8 +825,8 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
     return;
   }
   unsigned tk = 0;
-  if (ticket && early) tk = draw_ticket(ticket, s0, early);
-  const bool last = ticket && early && settle_ticket(ticket, tk, early);
+  if (ticket) tk = draw_ticket(ticket, s0);
+  const bool last = ticket && settle_ticket(ticket, tk);
 #pragma unroll 4
   for (int rr = 0; rr < kAdamRows / (kThreads / 64); ++rr) {
     const int rl = ty + (kThreads / 64) * rr, row = tr_i * kAdamRows + rl;
@@ -870,7 +858,7 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
       if (c < T.C && ocol < T.R) reinterpret_cast<bf16_t*>(T.st)[(long)c * T.R + ocol] = f2bf(tr[r][cl]);
     }
   }
-  if (ticket) finish_ticket(ticket, step, s0, early, last);
+  if (ticket) finish_ticket(step, s0, last);
 }
 
 // ------------------------------------------------------------------ Philox RNG
@@ -1502,7 +1490,6 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   AdamBatch b;
   static const int rows = getenv("LJS_ADAM_ROWS") ? atoi(getenv("LJS_ADAM_ROWS")) : 64;
   const int kAdamRows = rows == 16 || rows == 32 ? rows : 64;
-  static const int threads = getenv("LJS_ADAM_THREADS") ? atoi(getenv("LJS_ADAM_THREADS")) : 256;
   // tensors whose gradient is >= split_s slabs get 32-row tiles (>= 3 split_s: 16-row): their
   // blocks read split_s x more than a plain gradient's, and at 64 rows they were the kernel's tail
   // (W_o's 24 slabs at B=64 against the QKV weights' 8).  LJS_ADAM_SPLIT_S=0: off.
@@ -1527,7 +1514,7 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
                            (t.qn && !t.sn8) || (t.qt && !t.st8)))
       return (int)hipErrorInvalidValue;
     t.trows = kAdamRows;
-    if (kAdamRows == 64 && threads == 256 && split_s > 0 && t.vec && t.C % 64 == 0 && !t.qn && !t.qt &&
+    if (kAdamRows == 64 && split_s > 0 && t.vec && t.C % 64 == 0 && !t.qn && !t.qt &&
         t.gS >= split_s)
       t.trows = t.gS >= 3 * split_s ? 16 : 32;
     b.tile_start[i] = tiles;
@@ -1536,22 +1523,15 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   b.tile_start[n] = tiles;
   b.n = n;
   if (ticket && 1 + (tiles + 31) / 32 > (64 << 10) / 4) return (int)hipErrorInvalidValue;  // ticket words
-  static const int early = getenv("LJS_ADAM_EARLY_TICKET") ? atoi(getenv("LJS_ADAM_EARLY_TICKET")) : 1;
   if (kAdamRows == 16)
     hipLaunchKernelGGL((adam_multi_kernel<16, 256>), dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
+                       (unsigned*)ticket, lr, b1, b2, eps, wd);
   else if (kAdamRows == 32)
     hipLaunchKernelGGL((adam_multi_kernel<32, 256>), dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
-  else if (threads == 1024)
-    hipLaunchKernelGGL((adam_multi_kernel<64, 1024>), dim3(tiles), dim3(1024), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
-  else if (threads == 512)
-    hipLaunchKernelGGL((adam_multi_kernel<64, 512>), dim3(tiles), dim3(512), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
+                       (unsigned*)ticket, lr, b1, b2, eps, wd);
   else
     hipLaunchKernelGGL((adam_multi_kernel<64, 256>), dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, early, lr, b1, b2, eps, wd);
+                       (unsigned*)ticket, lr, b1, b2, eps, wd);
   return (int)hipGetLastError();
 }
 

@@ -797,7 +797,7 @@ gemm_dma_kernel(
   // wave: both fragment sets fit beside up to 256 accumulators)
   constexpr bool ONE_PER_CU = !(NW == 4 && NST * ((AIMG32 ? 2 : 1) * BM + BN) * 64 * 2 <= 80 * 1024);
   constexpr bool PIPE = (TM + TN <= 8 || (NW == 8 && TM + TN <= 10) || (NW == 4 && ONE_PER_CU && TM + TN <= 16)) &&
-                        A_KC && B_KC;
+                        A_KC && B_KC;   // (the last clause: 4-wave wide wave tiles, none instantiated since r5b)
   static_assert(!AREG || (PIPE && !OUT_F32 && RES == 0), "register-staged A: the pipelined bf16-output loop");
   if constexpr (AREG) {
     if (total == 1) a_commit();   // (tile 0 rounded into its stage before its barrier)
@@ -1396,9 +1396,6 @@ LJS_DMA_INST(256, 128, 4, 2, 3, true, true, true)
 // 256x192, 8 waves of 64x96, 2 stages (112 KiB): 7 DMA pieces and 20 fragment reads per wave per
 // 48 MFMAs (256x128: 6 and 16 per 32); [T][1536] outputs are 2 items per block
 LJS_DMA_INST(256, 192, 4, 2, 2, true, true, false)
-LJS_DMA_INST(256, 128, 2, 2, 3, true, true, false)
-LJS_DMA_INST(256, 192, 2, 2, 2, true, true, false)
-LJS_DMA_INST(256, 256, 2, 2, 2, true, true, false)
 // weight gradients (m/n-contiguous operands, f32 slabs): 256-wide tiles, 8 waves, 3 stages, one
 // block per CU -- 48 KiB of operands per 64-deep K-tile for twice the MFMA work of 128x128
 LJS_DMA_INST(256, 128, 4, 2, 3, false, false, true)
@@ -1428,12 +1425,6 @@ LJS_DMA_INST_RES(128, 128, 2, 2, 2)
 LJS_DMA_INST_RES(128, 128, 2, 2, 4)
 LJS_DMA_INST_RES(128, 128, 2, 4, 3)
 LJS_DMA_INST_RES(128, 128, 2, 4, 4)
-// wide wave tiles, 4 waves (2 x 2) and one block per CU (512 registers per wave): 128x64 / 128x96 /
-// 128x128 per wave -- 0.375 / 0.29 / 0.25 KiB of LDS fragment reads per MFMA against 0.5 for the
-// 64x64 wave tiles of 2561 / 1282 (verdict r4 item 1)
-LJS_DMA_INST_RES(256, 128, 2, 2, 3)
-LJS_DMA_INST_RES(256, 192, 2, 2, 2)
-LJS_DMA_INST_RES(256, 256, 2, 2, 2)
 #undef LJS_DMA_INST_RES
 // lean K-loop kernels (k-contiguous, bf16 output; every epilogue instance)
 #define LJS_LEAN_INST(BM, BN, WM, WN, NST)                                  \
@@ -1687,10 +1678,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if ((tile == 643 || tile == 644) && !(dma_ok && dma_store_ok)) tile = 64;
   if ((tile == 2563 || tile == 12856) && !(!a_kc && !b_kc && out_f32)) tile = 1282;
   if (tile == 2561 && !(a_kc && b_kc)) tile = 1284;
-  const bool wide4 = tile == 2522 || tile == 2592 || tile == 2552;   // 4-wave wide-wave-tile kernels
-  if (wide4 && !(a_kc && b_kc && !out_f32)) tile = 1282;
   if (tile == 2562 && !(a_kc && b_kc && !out_f32 && !(flags & (kResAdd | kResMask)))) tile = 1282;
-  if ((tile == 2562 || tile == 2592 || tile == 2552) && batch > 1) {
+  if (tile == 2562 && batch > 1) {
     // weight-major batches side by side in C over contiguous B (the fused Q/K/V projection):
     // one GEMM over N * batch columns
     if (sA == 0 && sB == (long)N * ldb && sC == N && ldc == (long)N * batch && !bias &&
@@ -1707,9 +1696,9 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   if ((tile == 12883 || tile == 12884) && !((!a_kc && !b_kc && out_f32) || (a_kc && b_kc))) tile = 1282;
   // fused output sum (psum): LDS-DMA kernels with bf16 output only; one float per (item, wave)
   if (psum && !out_f32 && tile > 1000) {
-    const int bm = (tile == 2561 || tile == 2562 || tile == 2522 || tile == 2592 || tile == 2552) ? 256 : 128;
+    const int bm = (tile == 2561 || tile == 2562) ? 256 : 128;
     const int nw = (tile == 2561 || tile == 2562 || tile == 12883 || tile == 12884) ? 8 : 4;
-    const int bn = tile == 1602 ? 160 : (tile == 2562 || tile == 2592) ? 192 : tile == 2552 ? 256 : 128;
+    const int bn = tile == 1602 ? 160 : tile == 2562 ? 192 : 128;
     a.psum = (float*)psum;
     if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch * a.splitk * nw;
   }
@@ -1736,12 +1725,6 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     e = launch_dma_kk<128, 160, 4, 1, 2>(a, stream);
   } else if (tile == 2562) {
     e = launch_dma_kk<256, 192, 4, 2, 2>(a, stream);
-  } else if (tile == 2522) {
-    e = launch_dma_kk<256, 128, 2, 2, 3>(a, stream);
-  } else if (tile == 2592) {
-    e = launch_dma_kk<256, 192, 2, 2, 2>(a, stream);
-  } else if (tile == 2552) {
-    e = launch_dma_kk<256, 256, 2, 2, 2>(a, stream);
   } else if (tile == 2561) {
     if (out_f32) e = launch_dma<256, 128, 4, 2, 3, true, true, true>(a, stream, 0);
     else e = launch_dma_kk<256, 128, 4, 2, 3>(a, stream);

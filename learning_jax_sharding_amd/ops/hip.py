@@ -1469,8 +1469,10 @@ class ConstGrad:
 
 # How adam_multi's ``increment_step`` advances the count: "kernel" (default) a one-lane launch after
 # the Adam launches; "ticket" the last-arriving block of the last Adam launch (a two-level arrival
-# ticket in the kernel, LJS_ADAM_EARLY_TICKET picks its form).  The step's parameter set in a
-# graph (scripts/adam_probe.py, gpurun_out/r5n): no increment 9.1 us, + launch 10.7, ticket 13.0-13.5.
+# ticket drawn early in the kernel).  The step's parameter set with plain gradients, in a graph
+# (scripts/adam_probe.py, profiles/r5n_adam_probe_*.txt): no increment 9.1 us, + launch 10.8,
+# ticket 13.2; steps B=64 0.2095 / 0.2132 vs 0.2113 / 0.2128 ms, B=8 0.0824 / 0.0825 vs
+# 0.0829 / 0.0828 (profiles/r5o_adam_ab_lines.txt).
 _STEP_INC = os.environ.get("LJS_ADAM_STEP_INC", "kernel")
 
 

@@ -690,7 +690,11 @@ def test_sum_backward_broadcast_row(hip):
     torch.testing.assert_close(g.float(), torch.full(x.shape, 0.25, device=dev))
 
 
-def test_adam_multi_folded_step_increment(hip):
+@pytest.mark.parametrize("mode", ["kernel", "ticket"])
+def test_adam_multi_folded_step_increment(hip, mode, monkeypatch):
+    """increment_step advances the device count by one per call -- by the one-lane launch (default)
+    or the in-kernel arrival ticket -- and the bias corrections use the new count."""
+    monkeypatch.setattr(hip, "_STEP_INC", mode)
     ws = [torch.randn(64 * 7, 130, device=dev) for _ in range(40)]  # > 32 tensors: two launches
     gs = [torch.randn_like(w) for w in ws]
     ms = [torch.zeros_like(w) for w in ws]
