@@ -374,9 +374,17 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
         step = ljs.jit(train_step, in_shardings=(state_sharding, x_sharding), out_shardings=state_sharding,
                        donate_argnums=0, capture=capture)
 
+        from learning_jax_sharding_amd.ops import linear as _lin
+
         def train_steps(state, x):  # G complete training steps, each on the previous one's state
-            for _ in range(G):
+            for i in range(G):
+                # the next step's input is known: its bf16 cast may run beside this step's
+                # backward on a side stream (ops/linear.prefetch_next_input); each step still
+                # casts its own input once
+                if i + 1 < G:
+                    _lin.prefetch_next_input(x)
                 state = train_step(state, x)
+            _lin.join_precasts()
             return state
         multi = ljs.jit(train_steps, in_shardings=(state_sharding, x_sharding), out_shardings=state_sharding,
                         donate_argnums=0, capture=capture) if G > 1 else None

@@ -372,8 +372,119 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
     if t.dtype == torch.bfloat16:
         return t
     if t.is_contiguous():
+        pre = _take_precast(t)
+        if pre is not None:
+            return pre
         return hip._cast_raw(t, torch.bfloat16)
     return t.to(torch.bfloat16)
+
+
+# ---------------------------------------------------------------------------- input-cast prefetch
+# The reference's f32 activation is rounded to bf16 inside its first Dense (case6_attention.py:
+# 96-99); here that is a streaming cast pass in front of the QKV GEMM (12 us at 64 x 256 tokens,
+# nothing to overlap it with inside its own step).  A multi-step runner that knows the NEXT
+# step's input registers it (`prefetch_next_input`) before running a step; that step's first
+# dense backward then forks the next input's cast onto a side stream, where it runs beside the
+# backward's GEMMs / attention, and the next step's dense takes the result after an event wait
+# (`_take_precast`) instead of casting.  Every step still casts its own input exactly once: only
+# WHEN changes.  Runners join what was not taken (`join_precasts`) before their capture ends.
+# Measured (bench.py G-step graphs, gpurun_out/r5t, profiles/r5t_precast_lines.txt): B=64 0.2472 /
+# 0.2476 ms with it vs 0.2180 / 0.2202 without, B=8 0.1013 / 0.1006 vs 0.0809 / 0.0806 -- the
+# side-stream branch in the replayed graph costs far more than the 12 us cast it hides (as the
+# side-stream weight gradients did, ops/streams.py).  Opt-in: LJS_PRECAST=1.
+_PRECAST_ON = os.environ.get("LJS_PRECAST", "0") == "1"
+_NEXT_INPUTS: List[torch.Tensor] = []
+_PRECAST = {}            # key -> (bf16 copy, event, source)
+_PRECAST_SIDE = {}       # device index -> side stream
+
+
+def _pc_key(t: torch.Tensor):
+    return (t.data_ptr(), t.numel(), t._version, t.device.index)
+
+
+def prefetch_next_input(*xs) -> None:
+    """Register the next step's input(s) (tensors or sharded arrays; f32 CUDA shards only) for
+    an early bf16 cast on a side stream during the coming step's backward."""
+    if not _PRECAST_ON:
+        return
+    _register_cut_hook()
+    for x in xs:
+        loc = getattr(x, "local", None)
+        ts = list(loc.values()) if isinstance(loc, dict) else [x]
+        for t in ts:
+            if (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+                    and t.numel() >= (1 << 20)):
+                _NEXT_INPUTS.append(t)
+
+
+def _launch_precasts(dev: torch.device) -> None:
+    from ..spmd import graphs as _graphs
+    if isinstance(_graphs.current(), _graphs.MultiDeviceGraph):
+        _NEXT_INPUTS.clear()      # (a single-controller multi-device capture: not forked there)
+        return
+    todo = [t for t in _NEXT_INPUTS if t.device == dev]
+    if not todo:
+        return
+    _NEXT_INPUTS[:] = [t for t in _NEXT_INPUTS if t.device != dev]
+    main = torch.cuda.current_stream(dev)
+    side = _PRECAST_SIDE.get(dev.index)
+    if side is None:
+        side = _PRECAST_SIDE[dev.index] = torch.cuda.Stream(dev)
+    ev0 = torch.cuda.Event()
+    ev0.record(main)
+    side.wait_event(ev0)
+    with torch.cuda.stream(side):
+        for t in todo:
+            t.record_stream(side)
+            xb = hip._cast_raw(t.reshape(-1), torch.bfloat16)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            _PRECAST[_pc_key(t)] = (xb, ev, t)
+
+
+def _take_precast(t: torch.Tensor):
+    if not _PRECAST or not t.is_cuda:
+        return None
+    ent = _PRECAST.pop(_pc_key(t), None)
+    if ent is None:
+        return None
+    xb, ev, _ = ent
+    if ev is not None:
+        main = torch.cuda.current_stream(t.device)
+        main.wait_event(ev)
+        xb.record_stream(main)
+    return xb.view(t.shape)
+
+
+def join_precasts() -> None:
+    """The current streams wait for every early cast nobody took (and forget them), and pending
+    registrations are dropped -- call before a capture or a step sequence ends (a capture
+    segment's end does it too: spmd/graphs.BEFORE_CUT)."""
+    _NEXT_INPUTS.clear()
+    while _PRECAST:
+        _, (xb, ev, src) = _PRECAST.popitem()
+        if ev is not None:
+            main = torch.cuda.current_stream(xb.device)
+            main.wait_event(ev)
+            xb.record_stream(main)
+
+
+def _join_forks() -> None:
+    # before a capture segment ends: the main streams wait for the forked casts (whose copies
+    # stay registered for the next step's dense: the next segment finds them already joined)
+    for k, (xb, ev, src) in list(_PRECAST.items()):
+        if ev is not None:
+            main = torch.cuda.current_stream(xb.device)
+            main.wait_event(ev)
+            xb.record_stream(main)
+            _PRECAST[k] = (xb, None, src)
+
+
+def _register_cut_hook() -> None:
+    from ..spmd import graphs as _graphs
+    if _join_forks not in _graphs.BEFORE_CUT:
+        _graphs.BEFORE_CUT.append(_join_forks)
+        _graphs.AFTER_CAPTURE.append(join_precasts)
 
 
 class _Linear(torch.autograd.Function):
@@ -480,6 +591,8 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *dys):
+        if _NEXT_INPUTS and dys and isinstance(dys[0], torch.Tensor) and dys[0].is_cuda:
+            _launch_precasts(dys[0].device)   # the next step's input cast, beside this backward
         lead, K, M, N, nw, relu, xdtype, has_b = ctx.meta
         order = getattr(ctx, "order", None)          # (the fp8 dense reuses this backward in row order)
         pshape = ctx.pshape if order is not None else tuple(lead)

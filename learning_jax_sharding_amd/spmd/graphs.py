@@ -36,6 +36,20 @@ __all__ = ["SegmentedGraph", "MultiDeviceGraph", "current", "run_collective", "j
 _ACTIVE: List[Optional["SegmentedGraph"]] = [None]
 
 
+# callables run before a capture segment ends: side-stream work forked inside the segment (an
+# input-cast prefetch, ops/linear.py) is joined back so the segment's capture closes cleanly
+BEFORE_CUT: List[Callable[[], None]] = []
+
+
+def _before_cut() -> None:
+    for fn in BEFORE_CUT:
+        fn()
+
+
+# callables run when a whole capture ends (state that must not leak into later calls)
+AFTER_CAPTURE: List[Callable[[], None]] = []
+
+
 def current() -> Optional["SegmentedGraph"]:
     return _ACTIVE[0]
 
@@ -67,6 +81,7 @@ class SegmentedGraph:
         self._g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
 
     def _cut(self):
+        _before_cut()
         with warnings.catch_warnings():
             # two adjacent cut points leave an empty segment: harmless, replays as a no-op
             warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
@@ -90,6 +105,8 @@ class SegmentedGraph:
                 finally:
                     if self._g is not None:
                         self._cut()
+                    for f in AFTER_CAPTURE:
+                        f()
         finally:
             _ACTIVE[0] = prev
         torch.cuda.current_stream().wait_stream(stream)

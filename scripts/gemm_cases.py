@@ -71,20 +71,29 @@ def cases():
     dq = [torch.randn(T, 512, device=dev).bfloat16() for _ in range(3)]
 
     def dwqkv_fn(tile, S=8):
+        if isinstance(tile, str):   # "tile:splits"
+            tile, S = (int(v) for v in tile.split(":"))
         nkt = T // 64
         Se = hip.slab_count(nkt, S)
         sl = torch.empty(Se, 3, 640, 512, device=dev)
         return lambda: hip.gemm(x, dq[0], sl, 640, 512, T, 640, 512, 512, False, False, batch=3, sA=0,
                                 sC=640 * 512, splitk=Se, tile=tile, slabs=True, b_list=dq)
     out["dwqkv"] = (dwqkv_fn, [1282], 2 * T * 640 * 1536)
+    # ring depth / waves per CU at the weight-gradient shape ("tile:splits")
+    out["dwqkv_ring"] = (dwqkv_fn, ["1282:8", "1284:8", "1284:4", "12883:8", "12883:4", "12884:8", "12884:4"],
+                         2 * T * 640 * 1536)
 
     def dwo_fn(tile, S=24):
+        if isinstance(tile, str):
+            tile, S = (int(v) for v in tile.split(":"))
         nkt = T // 64
         Se = hip.slab_count(nkt, S)
         sl = torch.empty(Se, 512, 640, device=dev)
         return lambda: hip.gemm(h, dy, sl, 512, 640, T, 512, 640, 640, False, False, sC=512 * 640, splitk=Se,
                                 tile=tile, slabs=True)
     out["dwo"] = (dwo_fn, [1282], 2 * T * 512 * 640)
+    out["dwo_ring"] = (dwo_fn, ["1282:24", "1284:24", "1284:12", "12883:24", "12883:12", "12884:24", "12884:12"],
+                       2 * T * 512 * 640)
     return out
 
 

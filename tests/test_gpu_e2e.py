@@ -160,6 +160,63 @@ def test_jit_graph_multi_step_capture_matches_single_steps(gpu_devices):
         np.testing.assert_array_equal(np.asarray(b), np.asarray(a))
 
 
+def test_jit_graph_multi_step_input_cast_prefetch_bit_exact(gpu_devices, monkeypatch):
+    """A multi-step graph whose steps register the next step's input (ops/linear.
+    prefetch_next_input): the next cast runs on a side stream during the backward and the next
+    step's dense takes it -- the state equals single-step replays bit for bit, each step's cast
+    ran (a kernel per step), and nothing stays registered after the capture."""
+    gpu_devices(1)
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd import optim
+    from learning_jax_sharding_amd.models import MultiHeadAttention
+    from learning_jax_sharding_amd.ops import linear as lin
+    from learning_jax_sharding_amd.training import TrainState
+    model = MultiHeadAttention(640, heads=8, dim_head=64)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (8, 256, 640))   # 1.3 M f32: prefetched
+
+    def make():
+        params = model.init(ljs.random.PRNGKey(1), x)["params"]
+        return TrainState.create(apply_fn=model.apply, params=params, tx=optim.adam(1e-3))
+
+    def step(state, x):
+        g = ljs.grad(lambda p: model.apply({"params": p}, x).sum())(state.params)
+        return state.apply_gradients(grads=g)
+
+    monkeypatch.setattr(lin, "_PRECAST_ON", True)   # (opt-in: LJS_PRECAST=1)
+    taken = []
+    orig = lin._take_precast
+
+    def spy(t):
+        r = orig(t)
+        taken.append(r is not None)
+        return r
+    lin._take_precast = spy
+    try:
+        def steps3(state, x):
+            for i in range(3):
+                if i + 1 < 3:
+                    lin.prefetch_next_input(x)
+                state = step(state, x)
+            lin.join_precasts()
+            return state
+
+        one = ljs.jit(step, donate_argnums=0, capture=True)
+        three = ljs.jit(steps3, donate_argnums=0, capture=True)
+        s1, s3 = make(), make()
+        for _ in range(3):
+            for _ in range(3):
+                s1 = one(s1, x)
+            s3 = three(s3, x)
+        torch.cuda.synchronize()
+    finally:
+        lin._take_precast = orig
+    assert any(taken), "no dense took a prefetched cast"
+    assert not lin._PRECAST and not lin._NEXT_INPUTS
+    assert int(np.asarray(s1.step)) == 9 and int(np.asarray(s3.step)) == 9
+    for a, b in zip(ljs.tree_util.tree_leaves(s1), ljs.tree_util.tree_leaves(s3)):
+        np.testing.assert_array_equal(np.asarray(b), np.asarray(a))
+
+
 def _run_layer(mesh_shape, fp8, B=2, S=128, M=640, ff=2560):
     import learning_jax_sharding_amd as ljs
     import learning_jax_sharding_amd.numpy as jnp
