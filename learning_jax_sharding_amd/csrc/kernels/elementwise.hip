@@ -1490,10 +1490,17 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   AdamBatch b;
   static const int rows = getenv("LJS_ADAM_ROWS") ? atoi(getenv("LJS_ADAM_ROWS")) : 64;
   const int kAdamRows = rows == 16 || rows == 32 ? rows : 64;
-  // tensors whose gradient is >= split_s slabs get 32-row tiles (>= 3 split_s: 16-row): their
-  // blocks read split_s x more than a plain gradient's, and at 64 rows they were the kernel's tail
-  // (W_o's 24 slabs at B=64 against the QKV weights' 8).  LJS_ADAM_SPLIT_S=0: off.
-  static const int split_s = getenv("LJS_ADAM_SPLIT_S") ? atoi(getenv("LJS_ADAM_SPLIT_S")) : 16;
+  // Tile heights balance the blocks' slab streams: a tensor whose gradient has r x the slabs of
+  // the launch's lightest slab gradient gets 32-row tiles at r >= 2 (16-row at r >= 4), so its
+  // blocks are not the kernel's tail -- W_o's 24 slabs against the QKV weights' 8 at B=64, 12
+  // against 4 at B=8 (B=8 step 0.0805-0.0813 vs 0.0824-0.0827 ms, profiles/r5x_b8_lines.txt).
+  // LJS_ADAM_BALANCE=0: every tile 64 rows.
+  static const int balance = getenv("LJS_ADAM_BALANCE") ? atoi(getenv("LJS_ADAM_BALANCE")) : 1;
+  long gs_min = 0;
+  for (int i = 0; i < n; ++i) {
+    const long g = table[16 * i + 9];
+    if (g > 0 && (gs_min == 0 || g < gs_min)) gs_min = g;
+  }
   int tiles = 0;
   for (int i = 0; i < n; ++i) {
     const long* r = table + 16 * i;
@@ -1514,9 +1521,9 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
                            (t.qn && !t.sn8) || (t.qt && !t.st8)))
       return (int)hipErrorInvalidValue;
     t.trows = kAdamRows;
-    if (kAdamRows == 64 && split_s > 0 && t.vec && t.C % 64 == 0 && !t.qn && !t.qt &&
-        t.gS >= split_s)
-      t.trows = t.gS >= 3 * split_s ? 16 : 32;
+    if (kAdamRows == 64 && balance && gs_min > 0 && t.vec && t.C % 64 == 0 && !t.qn && !t.qt &&
+        t.gS >= 2 * gs_min)
+      t.trows = t.gS >= 4 * gs_min ? 16 : 32;
     b.tile_start[i] = tiles;
     tiles += (int)(((t.R + t.trows - 1) / t.trows) * t.tiles_c);
   }

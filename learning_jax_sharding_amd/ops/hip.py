@@ -423,7 +423,7 @@ def pick_dw_slabs(K: int, N: int, T: int):
         while S > 1 and slab_count(nkt, S) != S:
             S -= 1
         return _DW_BIG_TILE, S, True
-    if T > 4096:
+    if T > 4096 or _DW_SMALL_TILE == 1282:
         nkt, tiles, slots = T // 64, -(-K // 128) * -(-N // 128), 2 * _cus()
         best, best_cost = 1, None
         for S in range(1, min(64, nkt) + 1):
