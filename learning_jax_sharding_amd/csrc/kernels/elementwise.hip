@@ -1474,11 +1474,11 @@ LJS_API int ljs_dropout(const void* x, void* y, int is_bf16, int ndim, const lon
 
 // the optimizer count's increment as its own one-lane launch (ops/hip.py adam_multi: the ticket
 // form's cost in the Adam kernel exceeds a launch, scripts/adam_probe.py)
-__global__ void step_add_kernel(int* step) {
-  if (threadIdx.x == 0) *step += 1;
+__global__ void step_add_kernel(int* step, int n) {
+  if (threadIdx.x == 0) *step += n;
 }
-LJS_API int ljs_step_add(void* step, hipStream_t s) {
-  hipLaunchKernelGGL(step_add_kernel, dim3(1), dim3(64), 0, s, (int*)step);
+LJS_API int ljs_step_add(void* step, int n, hipStream_t s) {
+  hipLaunchKernelGGL(step_add_kernel, dim3(1), dim3(64), 0, s, (int*)step, n);
   return (int)hipGetLastError();
 }
 

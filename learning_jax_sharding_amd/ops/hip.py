@@ -66,7 +66,7 @@ _SIGS = {
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
     "ljs_adam_multi": [_LP, c_int, c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float,
                        c_void_p],
-    "ljs_step_add": [c_void_p, c_void_p],
+    "ljs_step_add": [c_void_p, c_int, c_void_p],
     "ljs_mse_loss": [c_void_p, c_void_p, c_int, c_long, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_mse_colsum": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p],
@@ -1467,6 +1467,39 @@ class ConstGrad:
         self.value, self.shape = float(value), tuple(shape)
 
 
+# Count increments deferred inside a HIP-graph capture (a G-step graph): each Adam launch reads the
+# count as it was at the last flush plus the increments still pending, and the pending increments
+# become ONE launch when the capture segment ends (spmd/graphs.BEFORE_CUT) -- one count launch per
+# graph instead of one per step.  Eager calls and single-controller multi-device captures
+# increment at once.  LJS_ADAM_DEFER_INC=0: off.
+_DEFER_INC = os.environ.get("LJS_ADAM_DEFER_INC", "1") == "1"
+_PENDING_INC: Dict[int, list] = {}     # step data_ptr -> [step tensor, pending increments]
+
+
+def _flush_step_incs() -> None:
+    while _PENDING_INC:
+        _, (st, n) = _PENDING_INC.popitem()
+        if n:
+            _ck(lib().ljs_step_add(_p(st), n, _stream(st)), "ljs_step_add")
+
+
+def _defer_step_inc(step: torch.Tensor):
+    """Pending increments of ``step`` before this one (and one more recorded), or None when the
+    increment must be launched now."""
+    if not _DEFER_INC or _EARLY_ADAM:
+        return None
+    from ..spmd import graphs as _graphs
+    g = _graphs.current()
+    if g is None or isinstance(g, _graphs.MultiDeviceGraph):
+        return None
+    if _flush_step_incs not in _graphs.BEFORE_CUT:
+        _graphs.BEFORE_CUT.append(_flush_step_incs)
+    ent = _PENDING_INC.setdefault(step.data_ptr(), [step, 0])
+    pend = ent[1]
+    ent[1] += 1
+    return pend
+
+
 # How adam_multi's ``increment_step`` advances the count: "kernel" (default) a one-lane launch after
 # the Adam launches; "ticket" the last-arriving block of the last Adam launch (a two-level arrival
 # ticket drawn early in the kernel).  The step's parameter set with plain gradients, in a graph
@@ -1514,18 +1547,22 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
     step_i = step if step.dtype == torch.int32 else step.to(torch.int32)
     use_ticket = increment_step and _STEP_INC == "ticket"
     ticket = _workspace(step_i.device, "adam_ticket", 64 << 10) if use_ticket else None  # two-level tickets
+    # inside a capture the increments are deferred (one launch per capture segment, see
+    # _defer_step_inc): this launch reads the not-yet-incremented count, offset by what is pending
+    pend = _defer_step_inc(step_i) if (increment_step and not use_ticket) else None
+    offset = int(increment_step) + (pend or 0)
     rows = _early_adam(rows, step_i, lr, b1, b2, eps, wd, increment_step)
     for i in range(0, len(rows), 32):
         chunk = rows[i:i + 32]
         tab = np.asarray([r[0] for r in chunk], dtype=np.int64).reshape(-1)
         arr = (ctypes.c_long * tab.size)(*tab.tolist())
         last = i + 32 >= len(rows)
-        rc = lib().ljs_adam_multi(arr, len(chunk), _p(step_i), int(increment_step),
+        rc = lib().ljs_adam_multi(arr, len(chunk), _p(step_i), offset,
                                   _p(ticket) if (use_ticket and last) else None, lr, b1, b2, eps, wd,
                                   _stream(step_i))
         _ck(rc, "ljs_adam_multi")
-    if increment_step and not use_ticket:
-        _ck(lib().ljs_step_add(_p(step_i), _stream(step_i)), "ljs_step_add")
+    if increment_step and not use_ticket and pend is None:
+        _ck(lib().ljs_step_add(_p(step_i), 1, _stream(step_i)), "ljs_step_add")
     for p, _, _, _ in entries:
         shadow.mark_fresh(p)
 
