@@ -512,11 +512,10 @@ constexpr int kSC1 = 16;  // buffer-instruction cache policy bit: sc1 (gfx940-fa
 // pieces of the next-but-two K-tile's A as f32 into VGPRs (global -> VGPR), and one K-tile later
 // rounds them and writes the bf16 image the LDS-DMA would have written (same swizzle), so the
 // ring, the fragment reads and the MFMA loop are the bf16 kernel's.
+// (the body of gemm_dma_kernel; `bid` / `G` are the block's index and the grid as far as this
+// GEMM is concerned -- a grouped launch, gemm_dma_group2_kernel, runs two GEMMs' items in one grid)
 template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0, int AF32 = 0>
-__global__ __launch_bounds__(WM * WN * 64,
-                            (WM * WN == 4 && NST * ((AF32 == 1 ? 2 : 1) * BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
-gemm_dma_kernel(
-    GemmArgs p) {
+__device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, const int G) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   static_assert(!AF32 || A_KC, "f32 A is k-contiguous");
@@ -544,13 +543,12 @@ gemm_dma_kernel(
   const int wr = wave / WN, wc = wave % WN;
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
   const int items = p.batch * p.splitk * ntm * ntn;
-  const int G = gridDim.x;
-  const int slot = xcd_remap(blockIdx.x, G);   // same-XCD blocks take neighbouring items
+  const int slot = xcd_remap(bid, G);   // same-XCD blocks take neighbouring items
   const int my_items = slot < items ? (items - slot + G - 1) / G : 0;
   const int nk = p.kt_per_split;               // K-tiles per item (the split divides them)
   const int total = my_items * nk;
 #ifdef LJS_GEMM_TRACE
-  unsigned long long* trc = p.trace ? p.trace + ((long)blockIdx.x * NW + wave) * kTraceSlots : nullptr;
+  unsigned long long* trc = p.trace ? p.trace + ((long)bid * NW + wave) * kTraceSlots : nullptr;
   int trn = 0;
   auto stamp = [&]() {
     if (trc && trn < kTraceSlots - 1) {
@@ -1099,6 +1097,26 @@ gemm_dma_kernel(
   stamp_end();
 }
 
+template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0, int AF32 = 0>
+__global__ __launch_bounds__(WM * WN * 64,
+                            (WM * WN == 4 && NST * ((AF32 == 1 ? 2 : 1) * BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
+gemm_dma_kernel(GemmArgs p) {
+  gemm_dma_body<BM, BN, WM, WN, NST, A_KC, B_KC, OUT_F32, RES, AF32>(p, blockIdx.x, gridDim.x);
+}
+
+// Two GEMMs of the same kernel instance in ONE grid, one block per work item: blocks [0, g0) take
+// p0's items, the rest p1's.  The weight-gradient GEMMs of a layer at the reference shape (dW_qkv
+// and dW_o, 240 short items each) are latency-bound launches; grouped they share one round of
+// resident blocks instead of running back to back (ops/linear.py dW grouping).
+template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0>
+__global__ __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
+gemm_dma_group2_kernel(GemmArgs p0, GemmArgs p1, int g0) {
+  if ((int)blockIdx.x < g0)
+    gemm_dma_body<BM, BN, WM, WN, NST, A_KC, B_KC, OUT_F32, RES, 0>(p0, blockIdx.x, g0);
+  else
+    gemm_dma_body<BM, BN, WM, WN, NST, A_KC, B_KC, OUT_F32, RES, 0>(p1, blockIdx.x - g0, gridDim.x - g0);
+}
+
 // ============================================================================ lean K-loop GEMM
 // The persistent LDS-DMA GEMM's k-contiguous, bf16-output path (forward projections and dX GEMMs)
 // with the per-K-tile bookkeeping out of the K-loop.  A DMA / MFMA / barrier probe
@@ -1379,6 +1397,9 @@ LJS_DMA_INST_LAYOUTS(2)
 LJS_DMA_INST_LAYOUTS(4)
 // f32 split-K slab kernels with the compile-time plain epilogue (weight gradients: m/n-contiguous)
 template __global__ void gemm_dma_kernel<128, 128, 2, 2, 2, false, false, true, 3>(GemmArgs);
+template __global__ void gemm_dma_group2_kernel<128, 128, 2, 2, 2, false, false, true, 3>(GemmArgs, GemmArgs, int);
+template __global__ void gemm_dma_group2_kernel<128, 128, 2, 4, 4, false, false, true, 3>(GemmArgs, GemmArgs, int);
+template __global__ void gemm_dma_group2_kernel<128, 128, 2, 4, 3, false, false, true, 3>(GemmArgs, GemmArgs, int);
 template __global__ void gemm_dma_kernel<128, 128, 2, 4, 4, false, false, true, 3>(GemmArgs);
 template __global__ void gemm_dma_kernel<128, 128, 2, 4, 3, false, false, true, 3>(GemmArgs);
 // 64x64 tiles (4 waves of 32x32, 3 or 4 stages): the small-M GEMMs of the reference shape
@@ -1501,14 +1522,66 @@ hipError_t launch_dma_kk(const GemmArgs& a, hipStream_t s) {
   return launch_dma<BM, BN, WM, WN, NST, true, true, false, 0>(a, s, 0);
 }
 
+// Grouped weight-gradient launches (ljs_gemm_group_begin / _end): while a group is open, plain f32
+// slab GEMMs are recorded instead of launched; closing it launches two recorded GEMMs of the same
+// kernel instance as ONE grid (gemm_dma_group2_kernel, one block per work item) and anything else
+// one by one.  Same kernel body per item: bit-identical to separate launches.
+struct GroupRec {
+  GemmArgs a;
+  int kind;   // 1: 128x128 2x2 waves 2 stages, 2: 128x128 2x4 4 stages, 3: 128x128 2x4 3 stages
+};
+static bool g_group_on = false;
+static GroupRec g_group[2];
+static int g_group_n = 0;
+
+template <int BM, int BN>
+GemmArgs group_prep(const GemmArgs& a, int* items) {
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  *items = ntm * ntn * a.batch * a.splitk;
+  static const int order_env = getenv("LJS_GEMM_ORDER") ? atoi(getenv("LJS_GEMM_ORDER")) : 1;
+  GemmArgs a2 = a;
+  a2.trace = nullptr;
+  if (order_env && ntm < ntn) a2.flags |= kMFast;
+  return a2;
+}
+
 // weight-gradient (m/n-contiguous, f32 output) launch: the plain split-K slab instance (RES 3)
 // when the slabs are f32 and nothing else is asked for (LJS_GEMM_PLAIN=0: the general kernel)
 template <int BM, int BN, int WM, int WN, int NST>
 hipError_t launch_slab(const GemmArgs& a, hipStream_t s) {
   static const int plain_env = getenv("LJS_GEMM_PLAIN") ? atoi(getenv("LJS_GEMM_PLAIN")) : 1;
-  if (plain_env && (a.flags & kSlabs) && !(a.flags & (kSlabBf16 | 1 | 2 | 8 | 16)) && a.alpha == 1.f)
+  if (plain_env && (a.flags & kSlabs) && !(a.flags & (kSlabBf16 | 1 | 2 | 8 | 16)) && a.alpha == 1.f) {
+    constexpr int kind = (BM == 128 && BN == 128 && WM == 2 && WN == 2 && NST == 2)   ? 1
+                         : (BM == 128 && BN == 128 && WM == 2 && WN == 4 && NST == 4) ? 2
+                         : (BM == 128 && BN == 128 && WM == 2 && WN == 4 && NST == 3) ? 3
+                                                                                      : 0;
+    if (kind && g_group_on && g_group_n < 2) {
+      g_group[g_group_n].a = a;
+      g_group[g_group_n].kind = kind;
+      ++g_group_n;
+      return hipSuccess;
+    }
     return launch_dma<BM, BN, WM, WN, NST, false, false, true, 3>(a, s, 0);
+  }
   return launch_dma<BM, BN, WM, WN, NST, false, false, true, 0>(a, s, 0);
+}
+
+template <int WN, int NST>
+hipError_t launch_group_kind(const GroupRec* r, int n, hipStream_t s) {
+  if (n == 2) {
+    int i0 = 0, i1 = 0;
+    const GemmArgs a0 = group_prep<128, 128>(r[0].a, &i0), a1 = group_prep<128, 128>(r[1].a, &i1);
+    hipLaunchKernelGGL((gemm_dma_group2_kernel<128, 128, 2, WN, NST, false, false, true, 3>), dim3(i0 + i1),
+                       dim3(2 * WN * 64), 0, s, a0, a1, i0);
+    return hipGetLastError();
+  }
+  return launch_dma<128, 128, 2, WN, NST, false, false, true, 3>(r[0].a, s, 0);
+}
+
+hipError_t launch_rec(const GroupRec* r, int n, hipStream_t s) {
+  if (r[0].kind == 1) return launch_group_kind<2, 2>(r, n, s);
+  if (r[0].kind == 2) return launch_group_kind<4, 4>(r, n, s);
+  return launch_group_kind<4, 3>(r, n, s);
 }
 
 // the lean K-loop kernel (k-contiguous, bf16 output, no split): same grid choice as launch_dma
@@ -1572,6 +1645,25 @@ constexpr int kAF32 = 2048;  // A is f32 (k-contiguous): rounded to bf16 in the 
 // LJS_GEMM_TRACE builds: the LDS-DMA launches that follow write their per-wave timelines to
 // `buf` (blocks x waves x kTraceSlots u64, zeroed by the caller); null turns it off.  Returns
 // kTraceSlots, or 0 in a library built without the instrumentation.
+LJS_API void ljs_gemm_group_begin() {
+  g_group_on = true;
+  g_group_n = 0;
+}
+
+// launches what the open group recorded (grouped when it is two GEMMs of one kernel instance)
+LJS_API int ljs_gemm_group_end(hipStream_t stream) {
+  g_group_on = false;
+  const int n = g_group_n;
+  g_group_n = 0;
+  if (n == 0) return 0;
+  if (n == 2 && g_group[0].kind == g_group[1].kind) return (int)launch_rec(g_group, 2, stream);
+  for (int i = 0; i < n; ++i) {
+    const hipError_t e = launch_rec(&g_group[i], 1, stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
+}
+
 LJS_API int ljs_gemm_set_trace(void* buf) {
 #ifdef LJS_GEMM_TRACE
   g_gemm_trace = (unsigned long long*)buf;

@@ -30,6 +30,7 @@ _LP = ctypes.POINTER(ctypes.c_long)
 
 _SIGS = {
     "ljs_pack_rows": [c_void_p, c_int, c_void_p, c_long, c_long, c_long, c_int, c_void_p, c_void_p],
+    "ljs_gemm_group_end": [c_void_p],
     "ljs_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
                       c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
                       ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p, c_void_p],
@@ -286,6 +287,23 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     return cnt.value
 
 
+def gemm_group_begin():
+    """Open a grouped launch: the plain f32 slab GEMMs (weight gradients) that :func:`gemm` is
+    asked for until :func:`gemm_group_end` are recorded instead of launched."""
+    fn = lib().ljs_gemm_group_begin
+    fn.argtypes = []
+    fn.restype = None
+    fn()
+
+
+def gemm_group_end(dev_tensor: torch.Tensor):
+    """Launch what the open group recorded on ``dev_tensor``'s current stream: two GEMMs of one
+    kernel instance as ONE grid (one block per work item of either; the same kernel body per
+    item, so bit-identical to separate launches), anything else one by one."""
+    rc = lib().ljs_gemm_group_end(_stream(dev_tensor))
+    _ck(rc, "ljs_gemm_group_end")
+
+
 _LEAN_REQ = 100000  # tile code + _LEAN_REQ: force the lean K-loop kernel (gemm.hip gemm_lean_kernel; A/B),
                     # + 2 * _LEAN_REQ: force the general LDS-DMA kernel
 
@@ -398,7 +416,7 @@ def _cus() -> int:
         return 256
 
 
-def pick_dw_slabs(K: int, N: int, T: int):
+def pick_dw_slabs(K: int, N: int, T: int, grouped: bool = False):
     """(tile, K-chunks, slab mode) of a weight-gradient slab GEMM [K, N] = X^T dY over T tokens.
 
     T > 4096: 128x128 tiles (2 blocks per CU) in slab mode, the split count chosen by a cost
@@ -407,7 +425,11 @@ def pick_dw_slabs(K: int, N: int, T: int):
     tiles) ran 400 items on 512 block slots (78 %), now 5 x 52 K-tiles = 500 items; dW_o (20
     tiles) 16 x 16 -> 24 x 11.  At T <= 4096 the 8-wave 128x128 tile (one block per CU) in slab
     mode; ``LJS_DW_SMALL_TILE=644``: the 64x64 tile with the largest power-of-two batched split
-    keeping <= 512 items and >= 512 tokens per chunk (the round-2 default before)."""
+    keeping <= 512 items and >= 512 tokens per chunk (the round-2 default before).
+    ``grouped`` (T <= 4096; the GEMM will share one grid with another weight gradient,
+    ops.linear._launch_dw): the 128x128 2-blocks-per-CU tile sized for HALF the resident slots, so
+    the pair fills one round (B = 8: dW_qkv 4 splits + dW_o 11 = 480 items, 14.4 us vs 15.3 for
+    the 8-wave tile grouped and 16.1 separate; profiles/r5ae_dw_group_probe.txt)."""
     if K % 64 or N % 64 or T % 64:
         return 1282, pick_splitk_dma(K, N, T, 1), False
     if T > 4096 and not _DW_SLAB_MODE:
@@ -423,8 +445,10 @@ def pick_dw_slabs(K: int, N: int, T: int):
         while S > 1 and slab_count(nkt, S) != S:
             S -= 1
         return _DW_BIG_TILE, S, True
-    if T > 4096 or _DW_SMALL_TILE == 1282:
+    if T > 4096 or _DW_SMALL_TILE == 1282 or grouped:
         nkt, tiles, slots = T // 64, -(-K // 128) * -(-N // 128), 2 * _cus()
+        if grouped and T <= 4096:
+            slots //= 2
         best, best_cost = 1, None
         for S in range(1, min(64, nkt) + 1):
             if slab_count(nkt, S) != S:

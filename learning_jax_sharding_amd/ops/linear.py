@@ -181,6 +181,7 @@ class defer_wgrads:
 
     def __exit__(self, *exc):
         global _DEFER
+        flush_held_dw()
         _DEFER = self.prev
         return False
 
@@ -217,6 +218,50 @@ def _defer_ok(*ts) -> bool:
 _SLAB_DT = torch.bfloat16 if os.environ.get("LJS_SLAB_BF16", "0") == "1" else torch.float32
 
 
+# Grouped weight-gradient launches (LJS_DW_GROUP=1, the default): inside a deferring backward
+# (one device; the fused Adam reads the slabs after it) a slab-mode weight-gradient GEMM is held
+# back and launched together with the NEXT one as one grid (hip.gemm_group_*: one block per work
+# item of either, same kernel per item -> bit-identical).  At B = 8 the out-projection's and the
+# QKV projection's dW GEMMs are 240 items each: one 480-item grid fills the 512 resident slots
+# instead of two half-empty waves.  Anything that reads a held GEMM's slabs launches it first.
+_DW_GROUP = os.environ.get("LJS_DW_GROUP", "1") == "1"
+_HELD: List = []
+
+
+def _group_ok(ref: torch.Tensor) -> bool:
+    """Whether a slab-mode weight-gradient GEMM launched now may be grouped (see _DW_GROUP)."""
+    return _DW_GROUP and _DEFER is not None and ref.is_cuda and not hip._EARLY_ADAM
+
+
+def flush_held_dw():
+    """Launch the held weight-gradient GEMM (if any) on its own."""
+    while _HELD:
+        _HELD.pop()[0]()
+
+
+def _launch_dw(launch, ref: torch.Tensor) -> None:
+    """Run ``launch`` (one slab-mode weight-gradient hip.gemm) now, or hold it to be grouped with
+    the next one (see _DW_GROUP)."""
+    if not _group_ok(ref):
+        launch()
+        return
+    stream = torch.cuda.current_stream(ref.device)
+    if not _HELD:
+        _HELD.append((launch, stream))
+        return
+    prev, pst = _HELD.pop()
+    if pst != stream:
+        prev()
+        launch()
+        return
+    hip.gemm_group_begin()
+    try:
+        prev()
+        launch()
+    finally:
+        hip.gemm_group_end(ref)
+
+
 def _dw_slabs_wmajor(xb: torch.Tensor, dys, T: int, K: int, N: int, ws, pend):
     """The weight gradients xb^T @ dys[i] of weight-major cotangents dys [nw][T][N] (a seq-major
     fused projection, ops.linear.token_outer) as ONE slab-mode launch (batch i, split s -> slab
@@ -224,20 +269,21 @@ def _dw_slabs_wmajor(xb: torch.Tensor, dys, T: int, K: int, N: int, ws, pend):
     buffer (so a reduce-scatter / bucket takes them without a concatenation).  Each gradient is
     deferred as slabs when allowed (``pend``).  None when the slab-mode kernel does not apply."""
     nw = len(ws)
-    tile, S, slab_mode = hip.pick_dw_slabs(K, nw * N, T)
+    tile, S, slab_mode = hip.pick_dw_slabs(K, nw * N, T, grouped=_group_ok(xb))
     if not slab_mode or (_DW_SPLIT and T % (64 * _DW_SPLIT) == 0):
         return None
     slabs = torch.empty((S, nw, K, N), dtype=_SLAB_DT, device=xb.device)
     out = torch.empty((nw, K, N), dtype=torch.float32, device=xb.device)
     # dys: the nw [T][N] cotangents (separate tensors: q's from the attention backward, k's and
     # v's from the sequence gather's reduce-scatter), read through per-batch B pointers
-    hip.gemm(xb, dys[0], slabs, K, N, T, K, N, N, False, False, batch=nw, sA=0, sC=K * N, splitk=S,
-             tile=tile, slabs=True, b_list=dys)
+    _launch_dw(lambda: hip.gemm(xb, dys[0], slabs, K, N, T, K, N, N, False, False, batch=nw, sA=0, sC=K * N,
+                                splitk=S, tile=tile, slabs=True, b_list=dys), slabs)
     done = []
 
     def materialize():
         if not done:
             done.append(True)
+            flush_held_dw()
             hip.slab_reduce(slabs.view(S, nw * K, N), out.view(nw * K, N), N, 0)
     ev = None
     for i, w in enumerate(ws):
@@ -261,12 +307,13 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
     into f32 slabs [S][K][Nt], combined by one streaming reduction (which also fills ``tail`` =
     (f32 tensor, bf16 twin or None, constant)).  ``defer(slabs, S, materialize)``: the
     reduction is not launched; ``materialize()`` runs it (once) if the sums are ever read."""
-    tile, S, slab_mode = hip.pick_dw_slabs(K, Nt, T)
+    tile, S, slab_mode = hip.pick_dw_slabs(K, Nt, T, grouped=_group_ok(xb))
     if _DW_SPLIT and T % (64 * _DW_SPLIT) == 0:
         S, slab_mode = _DW_SPLIT, False
     slabs = torch.empty((S, K, Nt), dtype=_SLAB_DT if slab_mode else torch.float32, device=xb.device)
     if slab_mode:  # one launch, split s of the token range into slab s (uneven last split)
-        hip.gemm(xb, dy, slabs, K, Nt, T, K, ld, Nt, False, False, sC=K * Nt, splitk=S, tile=tile, slabs=True)
+        _launch_dw(lambda: hip.gemm(xb, dy, slabs, K, Nt, T, K, ld, Nt, False, False, sC=K * Nt, splitk=S,
+                                    tile=tile, slabs=True), slabs)
     else:
         kc = T // S
         hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
@@ -277,6 +324,7 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
         if done:
             return
         done.append(True)
+        flush_held_dw()
         if tail is not None:
             hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin, tail=tail[0], tail_bf16=tail[1],
                             tail_val=tail[2])

@@ -27,6 +27,25 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters * 1e3
 
 
+def timeit_graph(fn, iters=20):
+    """Launch-bound cases: ``iters`` calls captured in one HIP graph, timed over replays."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(3):
+        g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / (3 * iters) * 1e3
+
+
 def cases():
     out = {}
     x = torch.randn(T, 640, device=dev).bfloat16()
@@ -94,7 +113,34 @@ def cases():
     out["dwo"] = (dwo_fn, [1282], 2 * T * 512 * 640)
     out["dwo_ring"] = (dwo_fn, ["1282:24", "1284:24", "1284:12", "12883:24", "12883:12", "12884:24", "12884:12", "644:6", "644:8", "1282:12"],
                        2 * T * 512 * 640)
+
+    def dwgroup_fn(spec):
+        # "tile0:S0/tile1:S1[:sep]": the dW_qkv batch and dW_o as one grouped grid (or separate)
+        parts = spec.split("/")
+        sep = parts[-1].endswith(":sep")
+        (t0, S0), (t1, S1) = [(int(a), int(b)) for a, b, *_ in (q.split(":") for q in parts)]
+        nkt = T // 64
+        s0, s1 = hip.slab_count(nkt, S0), hip.slab_count(nkt, S1)
+        sl0 = torch.empty(s0, 3, 640, 512, device=dev)
+        sl1 = torch.empty(s1, 512, 640, device=dev)
+
+        def run():
+            if not sep:
+                hip.gemm_group_begin()
+            hip.gemm(x, dq[0], sl0, 640, 512, T, 640, 512, 512, False, False, batch=3, sA=0, sC=640 * 512,
+                     splitk=s0, tile=t0, slabs=True, b_list=dq)
+            hip.gemm(h, dy, sl1, 512, 640, T, 512, 640, 640, False, False, sC=512 * 640, splitk=s1, tile=t1,
+                     slabs=True)
+            if not sep:
+                hip.gemm_group_end(sl0)
+        return run
+    out["dwgroup"] = (dwgroup_fn, ["12884:4/12884:12:sep", "12884:4/12884:12", "1282:4/1282:12", "12884:2/12884:6",
+                                   "12884:3/12884:8", "1282:2/1282:6", "1282:8/1282:24", "12883:4/12883:12"],
+                      2 * T * 640 * 1536 + 2 * T * 512 * 640)
     return out
+
+
+_GRAPH_CASES = {"dwgroup"}
 
 
 def main():
@@ -106,7 +152,7 @@ def main():
         res = {t: [] for t in tiles}
         for _ in range(5):
             for t in tiles:
-                res[t].append(timeit(fns[t]))
+                res[t].append(timeit_graph(fns[t]) if name in _GRAPH_CASES else timeit(fns[t]))
         line = [f"{name:6s}"]
         for t in tiles:
             v = sorted(res[t])

@@ -691,6 +691,48 @@ def test_sum_backward_broadcast_row(hip):
     torch.testing.assert_close(g.float(), torch.full(x.shape, 0.25, device=dev))
 
 
+@pytest.mark.parametrize("S0,S1", [(4, 12), (8, 24), (4, 5)])
+def test_gemm_group_two_slab_gemms_bit_exact(hip, S0, S1):
+    """Two weight-gradient slab GEMMs (the bench's dW_qkv batch of 3 and dW_o) launched as one
+    grouped grid write exactly what two separate launches write; a group of one GEMM, and two of
+    different tiles, launch one by one."""
+    dev = "cuda"
+    torch.manual_seed(0)
+    T = 2048
+    x = torch.randn(T, 640, device=dev).bfloat16()
+    dq = [torch.randn(T, 512, device=dev).bfloat16() for _ in range(3)]
+    h = torch.randn(T, 512, device=dev).bfloat16()
+    dy = torch.randn(T, 640, device=dev).bfloat16()
+    nkt = T // 64
+    s0, s1 = hip.slab_count(nkt, S0), hip.slab_count(nkt, S1)
+
+    def run(group, tile1=1282):
+        sl0 = torch.full((s0, 3, 640, 512), float("nan"), device=dev)
+        sl1 = torch.full((s1, 512, 640), float("nan"), device=dev)
+        if group:
+            hip.gemm_group_begin()
+        hip.gemm(x, dq[0], sl0, 640, 512, T, 640, 512, 512, False, False, batch=3, sA=0, sC=640 * 512,
+                 splitk=s0, tile=1282, slabs=True, b_list=dq)
+        hip.gemm(h, dy, sl1, 512, 640, T, 512, 640, 640, False, False, sC=512 * 640, splitk=s1, tile=tile1,
+                 slabs=True)
+        if group:
+            hip.gemm_group_end(sl0)
+        torch.cuda.synchronize()
+        return sl0, sl1
+
+    r0, r1 = run(False)
+    g0, g1 = run(True)
+    assert torch.equal(r0, g0) and torch.equal(r1, g1)
+    # against an fp32 reference of the slab sums
+    ref1 = h.float().t() @ dy.float()
+    torch.testing.assert_close(g1.sum(0), ref1, rtol=2e-3, atol=2e-2)
+    m0, m1 = run(True, tile1=1284)   # different instances: launched one by one
+    assert torch.equal(r0, m0)
+    torch.testing.assert_close(m1.sum(0), ref1, rtol=2e-3, atol=2e-2)
+    hip.gemm_group_begin()
+    hip.gemm_group_end(x)             # empty group: nothing launched
+
+
 @pytest.mark.parametrize("mode", ["kernel", "ticket"])
 def test_adam_multi_folded_step_increment(hip, mode, monkeypatch):
     """increment_step advances the device count by one per call -- by the one-lane launch (default)
