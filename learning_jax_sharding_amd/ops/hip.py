@@ -416,7 +416,7 @@ def _cus() -> int:
         return 256
 
 
-def pick_dw_slabs(K: int, N: int, T: int, grouped: bool = False):
+def pick_dw_slabs(K: int, N: int, T: int):
     """(tile, K-chunks, slab mode) of a weight-gradient slab GEMM [K, N] = X^T dY over T tokens.
 
     T > 4096: 128x128 tiles (2 blocks per CU) in slab mode, the split count chosen by a cost
@@ -425,11 +425,7 @@ def pick_dw_slabs(K: int, N: int, T: int, grouped: bool = False):
     tiles) ran 400 items on 512 block slots (78 %), now 5 x 52 K-tiles = 500 items; dW_o (20
     tiles) 16 x 16 -> 24 x 11.  At T <= 4096 the 8-wave 128x128 tile (one block per CU) in slab
     mode; ``LJS_DW_SMALL_TILE=644``: the 64x64 tile with the largest power-of-two batched split
-    keeping <= 512 items and >= 512 tokens per chunk (the round-2 default before).
-    ``grouped`` (T <= 4096; the GEMM will share one grid with another weight gradient,
-    ops.linear._launch_dw): the 128x128 2-blocks-per-CU tile sized for HALF the resident slots, so
-    the pair fills one round (B = 8: dW_qkv 4 splits + dW_o 11 = 480 items, 14.4 us vs 15.3 for
-    the 8-wave tile grouped and 16.1 separate; profiles/r5ae_dw_group_probe.txt)."""
+    keeping <= 512 items and >= 512 tokens per chunk (the round-2 default before)."""
     if K % 64 or N % 64 or T % 64:
         return 1282, pick_splitk_dma(K, N, T, 1), False
     if T > 4096 and not _DW_SLAB_MODE:
@@ -445,10 +441,8 @@ def pick_dw_slabs(K: int, N: int, T: int, grouped: bool = False):
         while S > 1 and slab_count(nkt, S) != S:
             S -= 1
         return _DW_BIG_TILE, S, True
-    if T > 4096 or _DW_SMALL_TILE == 1282 or grouped:
+    if T > 4096 or _DW_SMALL_TILE == 1282:
         nkt, tiles, slots = T // 64, -(-K // 128) * -(-N // 128), 2 * _cus()
-        if grouped and T <= 4096:
-            slots //= 2
         best, best_cost = 1, None
         for S in range(1, min(64, nkt) + 1):
             if slab_count(nkt, S) != S:
@@ -477,6 +471,50 @@ def pick_dw_slabs(K: int, N: int, T: int, grouped: bool = False):
     while tiles * s * 2 <= 512 and T % (64 * s * 2) == 0 and T // (s * 2) >= 512:
         s *= 2
     return 644, s, False
+
+
+_PAIR_PICKS: Dict[tuple, Optional[tuple]] = {}
+# "S0,S1": force the pair's split counts (A/B)
+_DW_PAIR = os.environ.get("LJS_DW_PAIR", "")
+
+
+def pick_dw_pair(tiles0: int, size0: int, tiles1: int, size1: int, T: int):
+    """(tile, S0, S1) for two weight-gradient slab GEMMs over the same T tokens launched as ONE
+    grid (ops.linear._hold_dw; ``tiles`` = 128x128 output tiles, ``size`` = elements of one slab),
+    or None when no pair of split counts fits one round of resident blocks.
+
+    The 128x128 tile at 2 blocks per CU; the pair's items all start together, so the grid takes
+    about its LONGEST item (~1.2 us per K-tile + ~1 us prologue / epilogue) plus the slab traffic
+    (written here, read back by the combine or the fused Adam, ~5 TB/s) -- minimised over split
+    pairs with tiles0 * S0 + tiles1 * S1 <= resident slots.  At the step shapes (dW_o 20 tiles,
+    dW_qkv 60): 6 + 6 splits, 480 items of 43 K-tiles at T = 16384: 52.1 us for the pair vs 59.7
+    for the 24 + 8-split launches back to back, and half the slab bytes
+    (profiles/r5ah_dw_pair_probe.txt)."""
+    key = (tiles0, size0, tiles1, size1, T, _cus())
+    if key in _PAIR_PICKS:
+        return _PAIR_PICKS[key]
+    nkt, slots = T // 64, 2 * _cus()
+    best, best_cost = None, None
+    if _DW_PAIR:
+        s0, s1 = (int(v) for v in _DW_PAIR.split(","))
+        best = (1282, slab_count(nkt, s0), slab_count(nkt, s1))
+    else:
+        for s0 in range(1, min(64, nkt) + 1):
+            if tiles0 * s0 > slots:
+                break
+            if slab_count(nkt, s0) != s0:
+                continue
+            for s1 in range(1, min(64, nkt) + 1):
+                if tiles0 * s0 + tiles1 * s1 > slots:
+                    break
+                if slab_count(nkt, s1) != s1:
+                    continue
+                kps = max(-(-nkt // s0), -(-nkt // s1))
+                cost = kps * 1.2 + 1.0 + _DW_TRAFFIC_W * (s0 * size0 + s1 * size1) * 4 / 5e6
+                if best_cost is None or cost < best_cost - 1e-9:
+                    best, best_cost = (1282, s0, s1), cost
+    _PAIR_PICKS[key] = best
+    return best
 
 
 def pick_splitk_dma(M: int, N: int, K: int, batch: int) -> int:

@@ -219,45 +219,68 @@ _SLAB_DT = torch.bfloat16 if os.environ.get("LJS_SLAB_BF16", "0") == "1" else to
 
 
 # Grouped weight-gradient launches (LJS_DW_GROUP=1, the default): inside a deferring backward
-# (one device; the fused Adam reads the slabs after it) a slab-mode weight-gradient GEMM is held
-# back and launched together with the NEXT one as one grid (hip.gemm_group_*: one block per work
-# item of either, same kernel per item -> bit-identical).  At B = 8 the out-projection's and the
-# QKV projection's dW GEMMs are 240 items each: one 480-item grid fills the 512 resident slots
-# instead of two half-empty waves.  Anything that reads a held GEMM's slabs launches it first.
+# (one device; the fused Adam reads the slabs after it) a slab-mode weight-gradient GEMM whose sums
+# are deferred is held back as a job (its split count still open) and launched together with the
+# NEXT one as one grid (hip.gemm_group_*: one block per work item of either, same kernel per item
+# -> bit-identical), the pair's split counts chosen together (hip.pick_dw_pair: one round of
+# resident blocks, equal-length items, fewer slabs).  At B = 64 the out-projection's and the QKV
+# projection's dW GEMMs ran as 480 + 480 items (8 and 24 splits, 63 MB of slabs); paired they are
+# 360 + 120 items of 6 splits each (31 MB).  Anything that reads a held GEMM's slabs launches it first.
 _DW_GROUP = os.environ.get("LJS_DW_GROUP", "1") == "1"
 _HELD: List = []
 
 
+class _DwJob:
+    """A held slab-mode weight-gradient GEMM: ``run(tile, S)`` allocates its S slabs, launches it
+    and registers its deferred sums."""
+    __slots__ = ("K", "N", "T", "tiles", "run")
+
+    def __init__(self, K: int, N: int, T: int, tiles: int, run):
+        self.K, self.N, self.T, self.tiles, self.run = K, N, T, tiles, run
+
+    def run_alone(self):
+        tile, S, _ = hip.pick_dw_slabs(self.K, self.N, self.T)
+        self.run(tile, S)
+
+
 def _group_ok(ref: torch.Tensor) -> bool:
     """Whether a slab-mode weight-gradient GEMM launched now may be grouped (see _DW_GROUP)."""
-    return _DW_GROUP and _DEFER is not None and ref.is_cuda and not hip._EARLY_ADAM
+    return _DW_GROUP and _DEFER is not None and ref.is_cuda and not hip._EARLY_ADAM and not _DW_SPLIT
+
+
+def deferred_pending():
+    """The active deferral's pending map (gradient data_ptr -> (descriptor, materialize)), with any
+    held weight-gradient GEMM launched first so its entries are in it; None outside a deferral."""
+    if _DEFER is None:
+        return None
+    flush_held_dw()
+    return _DEFER["pending"]
 
 
 def flush_held_dw():
     """Launch the held weight-gradient GEMM (if any) on its own."""
     while _HELD:
-        _HELD.pop()[0]()
+        _HELD.pop()[0].run_alone()
 
 
-def _launch_dw(launch, ref: torch.Tensor) -> None:
-    """Run ``launch`` (one slab-mode weight-gradient hip.gemm) now, or hold it to be grouped with
-    the next one (see _DW_GROUP)."""
-    if not _group_ok(ref):
-        launch()
-        return
+def _hold_dw(job: _DwJob, ref: torch.Tensor) -> None:
+    """Hold ``job`` to be grouped with the next one, or launch it with the held one as a pair."""
     stream = torch.cuda.current_stream(ref.device)
     if not _HELD:
-        _HELD.append((launch, stream))
+        _HELD.append((job, stream))
         return
     prev, pst = _HELD.pop()
-    if pst != stream:
-        prev()
-        launch()
+    pick = hip.pick_dw_pair(prev.tiles, prev.K * prev.N, job.tiles, job.K * job.N, job.T) \
+        if pst == stream and prev.T == job.T else None
+    if pick is None:
+        prev.run_alone()
+        job.run_alone()
         return
+    tile, s0, s1 = pick
     hip.gemm_group_begin()
     try:
-        prev()
-        launch()
+        prev.run(tile, s0)
+        job.run(tile, s1)
     finally:
         hip.gemm_group_end(ref)
 
@@ -269,34 +292,41 @@ def _dw_slabs_wmajor(xb: torch.Tensor, dys, T: int, K: int, N: int, ws, pend):
     buffer (so a reduce-scatter / bucket takes them without a concatenation).  Each gradient is
     deferred as slabs when allowed (``pend``).  None when the slab-mode kernel does not apply."""
     nw = len(ws)
-    tile, S, slab_mode = hip.pick_dw_slabs(K, nw * N, T, grouped=_group_ok(xb))
+    tile, S, slab_mode = hip.pick_dw_slabs(K, nw * N, T)
     if not slab_mode or (_DW_SPLIT and T % (64 * _DW_SPLIT) == 0):
         return None
-    slabs = torch.empty((S, nw, K, N), dtype=_SLAB_DT, device=xb.device)
     out = torch.empty((nw, K, N), dtype=torch.float32, device=xb.device)
-    # dys: the nw [T][N] cotangents (separate tensors: q's from the attention backward, k's and
-    # v's from the sequence gather's reduce-scatter), read through per-batch B pointers
-    _launch_dw(lambda: hip.gemm(xb, dys[0], slabs, K, N, T, K, N, N, False, False, batch=nw, sA=0, sC=K * N,
-                                splitk=S, tile=tile, slabs=True, b_list=dys), slabs)
-    done = []
+    deferred = [pend is not None and _defer_ok(w) for w in ws]
 
-    def materialize():
-        if not done:
-            done.append(True)
-            flush_held_dw()
-            hip.slab_reduce(slabs.view(S, nw * K, N), out.view(nw * K, N), N, 0)
-    ev = None
-    for i, w in enumerate(ws):
-        if pend is not None and _defer_ok(w):
-            sg = hip.SlabGrad(slabs, S, i * K * N, N, nw * K * N, (K, N))
-            if hip._EARLY_ADAM:
-                if ev is None:
-                    ev = torch.cuda.Event()
-                    ev.record()
-                sg.ready = ev
-            pend[out[i].data_ptr()] = (sg, materialize)
-        else:
-            materialize()
+    def run(tile, S):
+        slabs = torch.empty((S, nw, K, N), dtype=_SLAB_DT, device=xb.device)
+        # dys: the nw [T][N] cotangents (separate tensors: q's from the attention backward, k's and
+        # v's from the sequence gather's reduce-scatter), read through per-batch B pointers
+        hip.gemm(xb, dys[0], slabs, K, N, T, K, N, N, False, False, batch=nw, sA=0, sC=K * N, splitk=S,
+                 tile=tile, slabs=True, b_list=dys)
+        done = []
+
+        def materialize():
+            if not done:
+                done.append(True)
+                flush_held_dw()
+                hip.slab_reduce(slabs.view(S, nw * K, N), out.view(nw * K, N), N, 0)
+        ev = None
+        for i in range(nw):
+            if deferred[i]:
+                sg = hip.SlabGrad(slabs, S, i * K * N, N, nw * K * N, (K, N))
+                if hip._EARLY_ADAM:
+                    if ev is None:
+                        ev = torch.cuda.Event()
+                        ev.record()
+                    sg.ready = ev
+                pend[out[i].data_ptr()] = (sg, materialize)
+            else:
+                materialize()
+    if all(deferred) and _group_ok(xb):
+        _hold_dw(_DwJob(K, nw * N, T, nw * -(-K // 128) * -(-N // 128), run), xb)
+    else:
+        run(tile, S)
     return [out[i] for i in range(nw)]
 
 
@@ -307,40 +337,45 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
     into f32 slabs [S][K][Nt], combined by one streaming reduction (which also fills ``tail`` =
     (f32 tensor, bf16 twin or None, constant)).  ``defer(slabs, S, materialize)``: the
     reduction is not launched; ``materialize()`` runs it (once) if the sums are ever read."""
-    tile, S, slab_mode = hip.pick_dw_slabs(K, Nt, T, grouped=_group_ok(xb))
+    tile, S, slab_mode = hip.pick_dw_slabs(K, Nt, T)
     if _DW_SPLIT and T % (64 * _DW_SPLIT) == 0:
         S, slab_mode = _DW_SPLIT, False
-    slabs = torch.empty((S, K, Nt), dtype=_SLAB_DT if slab_mode else torch.float32, device=xb.device)
-    if slab_mode:  # one launch, split s of the token range into slab s (uneven last split)
-        _launch_dw(lambda: hip.gemm(xb, dy, slabs, K, Nt, T, K, ld, Nt, False, False, sC=K * Nt, splitk=S,
-                                    tile=tile, slabs=True), slabs)
-    else:
-        kc = T // S
-        hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld, sC=K * Nt,
-                 tile=tile)
-    done = []
 
-    def materialize():
-        if done:
-            return
-        done.append(True)
-        flush_held_dw()
-        if tail is not None:
-            hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin, tail=tail[0], tail_bf16=tail[1],
-                            tail_val=tail[2])
+    def run(tile, S):
+        slabs = torch.empty((S, K, Nt), dtype=_SLAB_DT if slab_mode else torch.float32, device=xb.device)
+        if slab_mode:  # one launch, split s of the token range into slab s (uneven last split)
+            hip.gemm(xb, dy, slabs, K, Nt, T, K, ld, Nt, False, False, sC=K * Nt, splitk=S, tile=tile, slabs=True)
         else:
-            hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
-    if defer is not None:
-        defer(slabs, S, materialize)
-        if _DEFER is not None and slabs.is_cuda and hip._EARLY_ADAM:
-            # the optimizer may update this weight as soon as its slabs exist (hip._early_adam)
-            ev = torch.cuda.Event()
-            ev.record()
-            for desc, _ in _DEFER["pending"].values():
-                if isinstance(desc, hip.SlabGrad) and desc.slabs is slabs:
-                    desc.ready = ev
+            kc = T // S
+            hip.gemm(xb, dy, slabs, K, Nt, kc, K, ld, Nt, False, False, batch=S, sA=kc * K, sB=kc * ld,
+                     sC=K * Nt, tile=tile)
+        done = []
+
+        def materialize():
+            if done:
+                return
+            done.append(True)
+            flush_held_dw()
+            if tail is not None:
+                hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin, tail=tail[0], tail_bf16=tail[1],
+                                tail_val=tail[2])
+            else:
+                hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
+        if defer is not None:
+            defer(slabs, S, materialize)
+            if _DEFER is not None and slabs.is_cuda and hip._EARLY_ADAM:
+                # the optimizer may update this weight as soon as its slabs exist (hip._early_adam)
+                ev = torch.cuda.Event()
+                ev.record()
+                for desc, _ in _DEFER["pending"].values():
+                    if isinstance(desc, hip.SlabGrad) and desc.slabs is slabs:
+                        desc.ready = ev
+        else:
+            materialize()
+    if slab_mode and defer is not None and _group_ok(xb):
+        _hold_dw(_DwJob(K, Nt, T, -(-K // 128) * -(-Nt // 128), run), xb)
     else:
-        materialize()
+        run(tile, S)
 
 
 def _row_view(dy: torch.Tensor, M: int, N: int) -> Tuple[torch.Tensor, int]:

@@ -193,7 +193,7 @@ class _GatherBf16(torch.autograd.Function):
         _plan.record("reduce_scatter", groups=groups, note="backward.bf16_shadow_gather")
         from ..ops import linear as _lin
         res = [None] * len(gs)
-        pend = _lin._DEFER["pending"] if _lin._DEFER is not None else None
+        pend = _lin.deferred_pending()
         stacked = _stacked_grads(gs, devs, nw, pend)
         if stacked is not None and not _loopback(groups, stacked):
             # the nw gradients are slices of one [nw][K][N] buffer on every device (a batched

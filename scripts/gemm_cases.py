@@ -99,7 +99,7 @@ def cases():
                                 sC=640 * 512, splitk=Se, tile=tile, slabs=True, b_list=dq)
     out["dwqkv"] = (dwqkv_fn, [1282], 2 * T * 640 * 1536)
     # ring depth / waves per CU at the weight-gradient shape ("tile:splits")
-    out["dwqkv_ring"] = (dwqkv_fn, ["1282:8", "1284:8", "1284:4", "12883:8", "12883:4", "12884:8", "12884:4", "644:2", "644:4", "1282:4"],
+    out["dwqkv_ring"] = (dwqkv_fn, ["1282:8", "1284:8", "1284:4", "12883:8", "12883:4", "12884:8", "12884:4", "644:1", "644:2", "644:4", "1282:4"],
                          2 * T * 640 * 1536)
 
     def dwo_fn(tile, S=24):
@@ -111,7 +111,7 @@ def cases():
         return lambda: hip.gemm(h, dy, sl, 512, 640, T, 512, 640, 640, False, False, sC=512 * 640, splitk=Se,
                                 tile=tile, slabs=True)
     out["dwo"] = (dwo_fn, [1282], 2 * T * 512 * 640)
-    out["dwo_ring"] = (dwo_fn, ["1282:24", "1284:24", "1284:12", "12883:24", "12883:12", "12884:24", "12884:12", "644:6", "644:8", "1282:12"],
+    out["dwo_ring"] = (dwo_fn, ["1282:24", "1284:24", "1284:12", "12883:24", "12883:12", "12884:24", "12884:12", "644:1", "644:2", "644:6", "644:8", "1282:12"],
                        2 * T * 512 * 640)
 
     def dwgroup_fn(spec):
@@ -134,13 +134,18 @@ def cases():
             if not sep:
                 hip.gemm_group_end(sl0)
         return run
+    out["dwgroup_big"] = (dwgroup_fn, ["1282:8/1282:24:sep", "1282:8/1282:24", "1282:6/1282:6", "1282:5/1282:7",
+                                       "1282:6/1282:8", "1282:7/1282:5", "1282:8/1282:8", "1282:4/1282:4",
+                                       "1282:6/1282:12", "1282:4/1282:12"],
+                          2 * T * 640 * 1536 + 2 * T * 512 * 640)
     out["dwgroup"] = (dwgroup_fn, ["12884:4/12884:12:sep", "12884:4/12884:12", "1282:4/1282:12", "12884:2/12884:6",
-                                   "12884:3/12884:8", "1282:2/1282:6", "1282:8/1282:24", "12883:4/12883:12"],
+                                   "12884:3/12884:8", "1282:2/1282:6", "1282:8/1282:24", "12883:4/12883:12", "644:1/644:1:sep",
+                                   "644:2/644:2:sep"],
                       2 * T * 640 * 1536 + 2 * T * 512 * 640)
     return out
 
 
-_GRAPH_CASES = {"dwgroup"}
+_GRAPH_CASES = {"dwgroup", "dwgroup_big", "dwqkv_ring", "dwo_ring"}
 
 
 def main():

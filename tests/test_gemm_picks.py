@@ -1,0 +1,37 @@
+"""Host-side GEMM dispatch decisions (ops/hip.py cost models), pinned on the CPU."""
+import pytest
+
+from learning_jax_sharding_amd.ops import hip
+
+
+@pytest.fixture
+def chip(monkeypatch):
+    monkeypatch.setattr(hip, "_cus", lambda: 256)
+    monkeypatch.setattr(hip, "_PAIR_PICKS", {})
+    monkeypatch.setattr(hip, "_DW_PAIR", "")
+
+
+def test_dw_pair_one_round_equal_splits(chip):
+    # the step's dW_o (20 tiles of [512 x 640]) and dW_qkv (60 tiles of [640 x 1536])
+    for T in (2048, 16384):
+        tile, s0, s1 = hip.pick_dw_pair(20, 512 * 640, 60, 640 * 1536, T)
+        assert tile == 1282
+        assert 20 * s0 + 60 * s1 <= 512            # one round of 2 blocks x 256 CUs
+        assert hip.slab_count(T // 64, s0) == s0 and hip.slab_count(T // 64, s1) == s1
+    assert hip.pick_dw_pair(20, 512 * 640, 60, 640 * 1536, 16384)[1:] == (6, 6)
+
+
+def test_dw_pair_none_when_no_round_fits(chip):
+    assert hip.pick_dw_pair(400, 128 * 128, 200, 128 * 128, 16384) is None
+
+
+def test_dw_pair_forced(chip, monkeypatch):
+    monkeypatch.setattr(hip, "_DW_PAIR", "11,4")
+    assert hip.pick_dw_pair(20, 512 * 640, 60, 640 * 1536, 2048) == (1282, 11, 4)
+
+
+def test_dw_single_picks_unchanged(chip):
+    # the separate launches (a lone held GEMM, or grouping off)
+    assert hip.pick_dw_slabs(640, 1536, 16384) == (1282, 8, True)
+    assert hip.pick_dw_slabs(512, 640, 16384) == (1282, 24, True)
+    assert hip.pick_dw_slabs(640, 1536, 2048) == (12884, 4, True)
