@@ -1488,13 +1488,21 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
                            float b2, float eps, float wd, hipStream_t s) {
   if (n < 1 || n > kAdamMax) return (int)hipErrorInvalidValue;
   AdamBatch b;
-  static const int rows = getenv("LJS_ADAM_ROWS") ? atoi(getenv("LJS_ADAM_ROWS")) : 64;
-  const int kAdamRows = rows == 16 || rows == 32 ? rows : 64;
+  // Tile height (x 64 columns): 32 rows by default -- 660 workgroups for the step's 1.3 M
+  // parameters instead of 330 of 64 rows, which left a ragged second round on 256 CUs (B=8 step
+  // 0.0752-0.0753 vs 0.0775-0.0778 ms, B=64 0.1987-0.2007 vs 0.2005-0.2036, x3 interleaved,
+  // profiles/r5aj_adam_rows_lines.txt); 64 when a tensor carries MX-fp8 shadows (written by 64-row
+  // tiles only).  LJS_ADAM_ROWS = 16 / 32 / 64 forces the launch's height.
+  static const int rows = getenv("LJS_ADAM_ROWS") ? atoi(getenv("LJS_ADAM_ROWS")) : 0;
+  bool any_mx = false;
+  for (int i = 0; i < n; ++i) any_mx = any_mx || table[16 * i + 10] || table[16 * i + 12];
+  const int kAdamRows = rows == 16 || rows == 32 || rows == 64 ? rows : (any_mx ? 64 : 32);
   // Tile heights balance the blocks' slab streams: a tensor whose gradient has r x the slabs of
-  // the launch's lightest slab gradient gets 32-row tiles at r >= 2 (16-row at r >= 4), so its
-  // blocks are not the kernel's tail -- W_o's 24 slabs against the QKV weights' 8 at B=64, 12
-  // against 4 at B=8 (B=8 step 0.0805-0.0813 vs 0.0824-0.0827 ms, profiles/r5x_b8_lines.txt).
-  // LJS_ADAM_BALANCE=0: every tile 64 rows.
+  // the launch's lightest slab gradient gets half-height tiles at r >= 2 (16-row at r >= 4), so
+  // its blocks are not the kernel's tail -- W_o's 24 slabs against the QKV weights' 8 at B=64, 12
+  // against 4 at B=8 before the weight-gradient pair's joint split counts (B=8 step 0.0805-0.0813
+  // vs 0.0824-0.0827 ms, profiles/r5x_b8_lines.txt).  LJS_ADAM_BALANCE=0: every tile the
+  // launch's height.
   static const int balance = getenv("LJS_ADAM_BALANCE") ? atoi(getenv("LJS_ADAM_BALANCE")) : 1;
   long gs_min = 0;
   for (int i = 0; i < n; ++i) {
@@ -1521,9 +1529,9 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
                            (t.qn && !t.sn8) || (t.qt && !t.st8)))
       return (int)hipErrorInvalidValue;
     t.trows = kAdamRows;
-    if (kAdamRows == 64 && balance && gs_min > 0 && t.vec && t.C % 64 == 0 && !t.qn && !t.qt &&
+    if (kAdamRows >= 32 && balance && gs_min > 0 && t.vec && t.C % 64 == 0 && !t.qn && !t.qt &&
         t.gS >= 2 * gs_min)
-      t.trows = t.gS >= 4 * gs_min ? 16 : 32;
+      t.trows = t.gS >= 4 * gs_min || kAdamRows == 32 ? 16 : 32;
     b.tile_start[i] = tiles;
     tiles += (int)(((t.R + t.trows - 1) / t.trows) * t.tiles_c);
   }

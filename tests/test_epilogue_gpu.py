@@ -239,6 +239,9 @@ def test_deferred_wgrad_combine_bit_exact(gpu_devices, monkeypatch, model_kind):
             deferred.append(1)
         return r
     monkeypatch.setattr(linear, "_defer_ok", counting_ok)
+    # (the grouped weight-gradient pair picks its own split counts, so its sums round differently:
+    # compared separately, test_grouped_wgrad_pair_matches_separate)
+    monkeypatch.setattr(linear, "_DW_GROUP", False)
     res = {}
     for flag in (False, True):
         monkeypatch.setattr(linear, "_DEFER_ON", flag)
@@ -264,3 +267,64 @@ def test_deferred_wgrad_combine_bit_exact(gpu_devices, monkeypatch, model_kind):
             assert torch.equal(a, b), (a.float() - b.float()).abs().max()
         else:
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("model_kind", ["attention", "layer"])
+def test_grouped_wgrad_pair_matches_separate(gpu_devices, monkeypatch, model_kind):
+    """The grouped weight-gradient pair (ops/linear._hold_dw: one grid, jointly chosen split
+    counts) trains like the separate launches: same gradients up to the f32 re-association of
+    different split counts, under eager and captured steps."""
+    gpu_devices(1)
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd import optim
+    from learning_jax_sharding_amd.models import MultiHeadAttention, TransformerLayer
+    from learning_jax_sharding_amd.ops import hip, linear
+    from learning_jax_sharding_amd.training import TrainState
+    if model_kind == "attention":
+        model = MultiHeadAttention(640, 8, 64)
+    else:
+        model = TransformerLayer(640, heads=8, dim_head=64, ff_dim=2560)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (8, 256, 640))
+
+    def make():
+        params = model.init(ljs.random.PRNGKey(1), x)["params"]
+        return TrainState.create(apply_fn=model.apply, params=params, tx=optim.adam(1e-3))
+
+    def step(state, x):
+        g = ljs.grad(lambda p: model.apply({"params": p}, x).sum())(state.params)
+        return state.apply_gradients(grads=g)
+
+    pairs = []
+    orig = hip.pick_dw_pair
+
+    def counting(*a):
+        r = orig(*a)
+        pairs.append(r)
+        return r
+    monkeypatch.setattr(hip, "pick_dw_pair", counting)
+    res = {}
+    for flag in (False, True):
+        monkeypatch.setattr(linear, "_DW_GROUP", flag)
+        n0 = len(pairs)
+        sj = make()
+        jstep = ljs.jit(step, donate_argnums=0, capture=True)
+        for _ in range(3):
+            sj = jstep(sj, x)
+        se = step(make(), x)
+        torch.cuda.synchronize()
+        _, g = ljs.value_and_grad(lambda p: model.apply({"params": p}, x).sum())(make().params)
+        torch.cuda.synchronize()
+        assert (len(pairs) > n0) == flag and all(p is not None for p in pairs[n0:])
+        res[flag] = ([np.asarray(l).copy() for l in ljs.tree_util.tree_leaves(ljs.nn.unbox(g))],
+                     [np.asarray(l).copy() for l in ljs.tree_util.tree_leaves(sj)] +
+                     [np.asarray(l).copy() for l in ljs.tree_util.tree_leaves(se)])
+    # gradients: f32 re-association only
+    for a, b in zip(res[False][0], res[True][0]):
+        np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(a).max())))
+    # trained states: Adam normalises each update to ~lr, so a near-zero gradient element whose
+    # sign the re-association flips moves by ~lr, and the next steps' gradients are taken at those
+    # slightly different weights -- the trajectories agree in norm, not bit for bit
+    for a, b in zip(res[False][1], res[True][1]):
+        a64, b64 = np.asarray(a, np.float64), np.asarray(b, np.float64)
+        assert np.linalg.norm(b64 - a64) <= 5e-2 * max(np.linalg.norm(a64), 1e-12), \
+            (np.linalg.norm(b64 - a64), np.linalg.norm(a64))
