@@ -416,7 +416,7 @@ def _cus() -> int:
         return 256
 
 
-def pick_dw_slabs(K: int, N: int, T: int):
+def _dw_single(K: int, N: int, T: int):
     """(tile, K-chunks, slab mode) of a weight-gradient slab GEMM [K, N] = X^T dY over T tokens.
 
     T > 4096: 128x128 tiles (2 blocks per CU) in slab mode, the split count chosen by a cost
@@ -427,9 +427,9 @@ def pick_dw_slabs(K: int, N: int, T: int):
     mode; ``LJS_DW_SMALL_TILE=644``: the 64x64 tile with the largest power-of-two batched split
     keeping <= 512 items and >= 512 tokens per chunk (the round-2 default before)."""
     if K % 64 or N % 64 or T % 64:
-        return 1282, pick_splitk_dma(K, N, T, 1), False
+        return 1282, pick_splitk_dma(K, N, T, 1), False, None
     if T > 4096 and not _DW_SLAB_MODE:
-        return 1282, pick_splitk_dma(K, N, T, 1), False
+        return 1282, pick_splitk_dma(K, N, T, 1), False, None
     if T > 4096 and _DW_BIG_TILE in (644, 12884):
         # (A/B: fewer, longer slabs -- 64x64 tiles at 2 blocks/CU or 8-wave 128x128 at 1 block/CU,
         # split count filling one round of resident blocks)
@@ -440,7 +440,7 @@ def pick_dw_slabs(K: int, N: int, T: int):
         S = max(1, min(nkt, slots // max(1, tiles)))
         while S > 1 and slab_count(nkt, S) != S:
             S -= 1
-        return _DW_BIG_TILE, S, True
+        return _DW_BIG_TILE, S, True, None
     if T > 4096 or _DW_SMALL_TILE == 1282:
         nkt, tiles, slots = T // 64, -(-K // 128) * -(-N // 128), 2 * _cus()
         best, best_cost = 1, None
@@ -454,7 +454,7 @@ def pick_dw_slabs(K: int, N: int, T: int):
             cost = rounds * (kps * 1.2 + 1.0) + _DW_TRAFFIC_W * S * K * N * 4 / 5e6
             if best_cost is None or cost < best_cost - 1e-9:
                 best, best_cost = S, cost
-        return 1282, best, True
+        return 1282, best, True, best_cost
     if _DW_SMALL_TILE == 12884:
         # (A/B: 8-wave 128x128, 4 stages, one block per CU, uneven slab splits)
         nkt, tiles = T // 64, -(-K // 128) * -(-N // 128)
@@ -465,12 +465,18 @@ def pick_dw_slabs(K: int, N: int, T: int):
             cost = -(-tiles * S // _cus()) * (-(-nkt // S) * 1.2 + 1.0) + _DW_TRAFFIC_W * S * K * N * 4 / 5e6
             if best_cost is None or cost < best_cost - 1e-9:
                 best, best_cost = S, cost
-        return 12884, best, True
+        return 12884, best, True, best_cost
     tiles = (K // 64) * (N // 64)
     s = 1
     while tiles * s * 2 <= 512 and T % (64 * s * 2) == 0 and T // (s * 2) >= 512:
         s *= 2
-    return 644, s, False
+    return 644, s, False, None
+
+
+def pick_dw_slabs(K: int, N: int, T: int):
+    """(tile, K-chunks, slab mode) of a weight-gradient slab GEMM (see :func:`_dw_single`, which
+    also returns the cost model's estimate in us, or None where no model applies)."""
+    return _dw_single(K, N, T)[:3]
 
 
 _PAIR_PICKS: Dict[tuple, Optional[tuple]] = {}
@@ -478,10 +484,10 @@ _PAIR_PICKS: Dict[tuple, Optional[tuple]] = {}
 _DW_PAIR = os.environ.get("LJS_DW_PAIR", "")
 
 
-def pick_dw_pair(tiles0: int, size0: int, tiles1: int, size1: int, T: int):
-    """(tile, S0, S1) for two weight-gradient slab GEMMs over the same T tokens launched as ONE
-    grid (ops.linear._hold_dw; ``tiles`` = 128x128 output tiles, ``size`` = elements of one slab),
-    or None when no pair of split counts fits one round of resident blocks.
+def pick_dw_pair(K0: int, N0: int, K1: int, N1: int, T: int):
+    """(tile, S0, S1) for two weight-gradient slab GEMMs [K, N] over the same T tokens launched
+    as ONE grid (ops.linear._hold_dw), or None when no pair of split counts fits one round of
+    resident blocks or the two separate launches' estimate (:func:`_dw_single`) is lower.
 
     The 128x128 tile at 2 blocks per CU; the pair's items all start together, so the grid takes
     about its LONGEST item (~1.2 us per K-tile + ~1 us prologue / epilogue) plus the slab traffic
@@ -489,8 +495,12 @@ def pick_dw_pair(tiles0: int, size0: int, tiles1: int, size1: int, T: int):
     pairs with tiles0 * S0 + tiles1 * S1 <= resident slots.  At the step shapes (dW_o 20 tiles,
     dW_qkv 60): 6 + 6 splits, 480 items of 43 K-tiles at T = 16384: 52.1 us for the pair vs 59.7
     for the 24 + 8-split launches back to back, and half the slab bytes
-    (profiles/r5ah_dw_pair_probe.txt)."""
-    key = (tiles0, size0, tiles1, size1, T, _cus())
+    (profiles/r5ah_dw_pair_probe.txt).  The FF block's pair (two 100-tile GEMMs) would need
+    items of 128 K-tiles for one round and stays separate (bf16 layer 0.6475 / 0.6503 ms paired vs
+    0.6314 / 0.6333, profiles/r5an_layer_pair_lines.txt)."""
+    tiles0, size0 = -(-K0 // 128) * -(-N0 // 128), K0 * N0
+    tiles1, size1 = -(-K1 // 128) * -(-N1 // 128), K1 * N1
+    key = (K0, N0, K1, N1, T, _cus())
     if key in _PAIR_PICKS:
         return _PAIR_PICKS[key]
     nkt, slots = T // 64, 2 * _cus()
@@ -513,6 +523,9 @@ def pick_dw_pair(tiles0: int, size0: int, tiles1: int, size1: int, T: int):
                 cost = kps * 1.2 + 1.0 + _DW_TRAFFIC_W * (s0 * size0 + s1 * size1) * 4 / 5e6
                 if best_cost is None or cost < best_cost - 1e-9:
                     best, best_cost = (1282, s0, s1), cost
+        c0, c1 = _dw_single(K0, N0, T)[3], _dw_single(K1, N1, T)[3]
+        if best is not None and c0 is not None and c1 is not None and c0 + c1 <= best_cost:
+            best = None
     _PAIR_PICKS[key] = best
     return best
 

@@ -270,7 +270,7 @@ def _hold_dw(job: _DwJob, ref: torch.Tensor) -> None:
         _HELD.append((job, stream))
         return
     prev, pst = _HELD.pop()
-    pick = hip.pick_dw_pair(prev.tiles, prev.K * prev.N, job.tiles, job.K * job.N, job.T) \
+    pick = hip.pick_dw_pair(prev.K, prev.N, job.K, job.N, job.T) \
         if pst == stream and prev.T == job.T else None
     if pick is None:
         prev.run_alone()

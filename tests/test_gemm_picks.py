@@ -14,20 +14,26 @@ def chip(monkeypatch):
 def test_dw_pair_one_round_equal_splits(chip):
     # the step's dW_o (20 tiles of [512 x 640]) and dW_qkv (60 tiles of [640 x 1536])
     for T in (2048, 16384):
-        tile, s0, s1 = hip.pick_dw_pair(20, 512 * 640, 60, 640 * 1536, T)
+        tile, s0, s1 = hip.pick_dw_pair(512, 640, 640, 1536, T)
         assert tile == 1282
         assert 20 * s0 + 60 * s1 <= 512            # one round of 2 blocks x 256 CUs
         assert hip.slab_count(T // 64, s0) == s0 and hip.slab_count(T // 64, s1) == s1
-    assert hip.pick_dw_pair(20, 512 * 640, 60, 640 * 1536, 16384)[1:] == (6, 6)
+    assert hip.pick_dw_pair(512, 640, 640, 1536, 16384)[1:] == (6, 6)
 
 
 def test_dw_pair_none_when_no_round_fits(chip):
-    assert hip.pick_dw_pair(400, 128 * 128, 200, 128 * 128, 16384) is None
+    assert hip.pick_dw_pair(2560, 2560, 2560, 1280, 16384) is None
 
 
 def test_dw_pair_forced(chip, monkeypatch):
     monkeypatch.setattr(hip, "_DW_PAIR", "11,4")
-    assert hip.pick_dw_pair(20, 512 * 640, 60, 640 * 1536, 2048) == (1282, 11, 4)
+    assert hip.pick_dw_pair(512, 640, 640, 1536, 2048) == (1282, 11, 4)
+
+
+def test_dw_pair_ff_block_stays_separate(chip):
+    # two 100-tile GEMMs (the FF block's [2560 x 640] / [640 x 2560]) would need 2-3 splits for one
+    # round: the separate launches' estimate is lower
+    assert hip.pick_dw_pair(2560, 640, 640, 2560, 16384) is None
 
 
 def test_dw_single_picks_unchanged(chip):
