@@ -240,19 +240,36 @@ def join(handle) -> None:
 # staging buffer and barrier sequence, comm/p2p.py _enter) waits on it: an event recorded inside
 # a capture cannot be waited on outside it.
 _LAST_REPLAY: Dict[int, Any] = {}
+# LJS_REPLAY_EVENT=1: record the completion event after every replay (A/B)
+_EAGER_REPLAY_EVENT = os.environ.get("LJS_REPLAY_EVENT", "0") == "1"
 
 
 def _note_replay(streams: Dict[int, Any]) -> None:
+    """Remember the stream each device's latest replay ran on.  The completion event is recorded
+    only when someone asks for it (:func:`last_replay`, the P2P collectives' ordering): an event
+    recorded on that stream later still follows the replay.  Recorded after every replay (the
+    round-4 form) it put a marker packet between consecutive graph launches."""
+    if _EAGER_REPLAY_EVENT:
+        for d, s in streams.items():
+            with torch.cuda.device(d):
+                ev = torch.cuda.Event()
+                ev.record(s)
+            _LAST_REPLAY[d] = ev
+        return
     for d, s in streams.items():
-        with torch.cuda.device(d):
-            ev = torch.cuda.Event()
-            ev.record(s)
-        _LAST_REPLAY[d] = ev
+        _LAST_REPLAY[d] = s
 
 
 def last_replay(device: int):
-    """The completion event of the latest graph replay on ``device`` (or None)."""
-    return _LAST_REPLAY.get(device)
+    """An event that completes after the latest graph replay on ``device`` (or None)."""
+    e = _LAST_REPLAY.get(device)
+    if e is None or isinstance(e, torch.cuda.Event):
+        return e
+    with torch.cuda.device(device):
+        ev = torch.cuda.Event()
+        ev.record(e)
+    _LAST_REPLAY[device] = ev
+    return ev
 
 
 _SIDE: Dict[int, torch.cuda.Stream] = {}
