@@ -1529,9 +1529,11 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
                            (t.qn && !t.sn8) || (t.qt && !t.st8)))
       return (int)hipErrorInvalidValue;
     t.trows = kAdamRows;
-    if (kAdamRows >= 32 && balance && gs_min > 0 && t.vec && t.C % 64 == 0 && !t.qn && !t.qt &&
-        t.gS >= 2 * gs_min)
-      t.trows = t.gS >= 4 * gs_min || kAdamRows == 32 ? 16 : 32;
+    const bool short_ok = t.vec && t.C % 64 == 0 && !t.qn && !t.qt;
+    // a 64-row launch chosen for another tensor's MX shadows: the rest keep the 32-row default
+    if (short_ok && rows == 0 && kAdamRows == 64) t.trows = 32;
+    if (t.trows >= 32 && balance && gs_min > 0 && short_ok && t.gS >= 2 * gs_min)
+      t.trows = t.gS >= 4 * gs_min || t.trows == 32 ? 16 : 32;
     b.tile_start[i] = tiles;
     tiles += (int)(((t.R + t.trows - 1) / t.trows) * t.tiles_c);
   }
