@@ -503,11 +503,15 @@ def pick_dw_pair(K0: int, N0: int, K1: int, N1: int, T: int):
     key = (K0, N0, K1, N1, T, _cus())
     if key in _PAIR_PICKS:
         return _PAIR_PICKS[key]
-    nkt, slots = T // 64, 2 * _cus()
+    nkt = T // 64
+    # T <= 4096: the 8-wave 128x128 tile at one block per CU, as for a single weight gradient there
+    # (B = 8 pair at 3 + 3 splits: 12.66 us vs 14.49 for the 1282 pair at 6 + 6, and half the slabs;
+    # at T = 16384 72.0 vs 53.8, profiles/r5au_dw_pair_8w_probe.txt)
+    tile, slots = (12884, _cus()) if (T <= 4096 and _DW_SMALL_TILE == 12884) else (1282, 2 * _cus())
     best, best_cost = None, None
     if _DW_PAIR:
-        s0, s1 = (int(v) for v in _DW_PAIR.split(","))
-        best = (1282, slab_count(nkt, s0), slab_count(nkt, s1))
+        v = [int(t) for t in _DW_PAIR.split(",")]
+        best = (v[2] if len(v) > 2 else tile, slab_count(nkt, v[0]), slab_count(nkt, v[1]))
     else:
         for s0 in range(1, min(64, nkt) + 1):
             if tiles0 * s0 > slots:
@@ -522,7 +526,7 @@ def pick_dw_pair(K0: int, N0: int, K1: int, N1: int, T: int):
                 kps = max(-(-nkt // s0), -(-nkt // s1))
                 cost = kps * 1.2 + 1.0 + _DW_TRAFFIC_W * (s0 * size0 + s1 * size1) * 4 / 5e6
                 if best_cost is None or cost < best_cost - 1e-9:
-                    best, best_cost = (1282, s0, s1), cost
+                    best, best_cost = (tile, s0, s1), cost
         c0, c1 = _dw_single(K0, N0, T)[3], _dw_single(K1, N1, T)[3]
         if best is not None and c0 is not None and c1 is not None and c0 + c1 <= best_cost:
             best = None

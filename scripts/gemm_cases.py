@@ -138,6 +138,10 @@ def cases():
                                        "1282:6/1282:8", "1282:7/1282:5", "1282:8/1282:8", "1282:4/1282:4",
                                        "1282:6/1282:12", "1282:4/1282:12"],
                           2 * T * 640 * 1536 + 2 * T * 512 * 640)
+    # one round of the 8-wave tiles at one block per CU (256 slots)
+    out["dwgroup_8w"] = (dwgroup_fn, ["1282:6/1282:6", "12884:3/12884:3", "12883:3/12883:3", "12884:3/12884:3:sep",
+                                      "12884:2/12884:6", "12883:2/12883:6"],
+                          2 * T * 640 * 1536 + 2 * T * 512 * 640)
     out["dwgroup"] = (dwgroup_fn, ["12884:4/12884:12:sep", "12884:4/12884:12", "1282:4/1282:12", "12884:2/12884:6",
                                    "12884:3/12884:8", "1282:2/1282:6", "1282:8/1282:24", "12883:4/12883:12", "644:1/644:1:sep",
                                    "644:2/644:2:sep"],
@@ -145,7 +149,7 @@ def cases():
     return out
 
 
-_GRAPH_CASES = {"dwgroup", "dwgroup_big", "dwqkv_ring", "dwo_ring"}
+_GRAPH_CASES = {"dwgroup", "dwgroup_big", "dwgroup_8w", "dwqkv_ring", "dwo_ring"}
 
 
 def main():

@@ -13,12 +13,13 @@ def chip(monkeypatch):
 
 def test_dw_pair_one_round_equal_splits(chip):
     # the step's dW_o (20 tiles of [512 x 640]) and dW_qkv (60 tiles of [640 x 1536])
-    for T in (2048, 16384):
+    for T, want_tile, slots in ((2048, 12884, 256), (16384, 1282, 512)):
         tile, s0, s1 = hip.pick_dw_pair(512, 640, 640, 1536, T)
-        assert tile == 1282
-        assert 20 * s0 + 60 * s1 <= 512            # one round of 2 blocks x 256 CUs
+        assert tile == want_tile
+        assert 20 * s0 + 60 * s1 <= slots           # one round of resident blocks
         assert hip.slab_count(T // 64, s0) == s0 and hip.slab_count(T // 64, s1) == s1
     assert hip.pick_dw_pair(512, 640, 640, 1536, 16384)[1:] == (6, 6)
+    assert hip.pick_dw_pair(512, 640, 640, 1536, 2048)[1:] == (3, 3)
 
 
 def test_dw_pair_none_when_no_round_fits(chip):
@@ -27,7 +28,10 @@ def test_dw_pair_none_when_no_round_fits(chip):
 
 def test_dw_pair_forced(chip, monkeypatch):
     monkeypatch.setattr(hip, "_DW_PAIR", "11,4")
-    assert hip.pick_dw_pair(512, 640, 640, 1536, 2048) == (1282, 11, 4)
+    assert hip.pick_dw_pair(512, 640, 640, 1536, 2048) == (12884, 11, 4)
+    monkeypatch.setattr(hip, "_DW_PAIR", "6,6,1282")
+    monkeypatch.setattr(hip, "_PAIR_PICKS", {})
+    assert hip.pick_dw_pair(512, 640, 640, 1536, 2048) == (1282, 6, 6)
 
 
 def test_dw_pair_ff_block_stays_separate(chip):

@@ -691,8 +691,8 @@ def test_sum_backward_broadcast_row(hip):
     torch.testing.assert_close(g.float(), torch.full(x.shape, 0.25, device=dev))
 
 
-@pytest.mark.parametrize("S0,S1", [(4, 12), (8, 24), (4, 5)])
-def test_gemm_group_two_slab_gemms_bit_exact(hip, S0, S1):
+@pytest.mark.parametrize("S0,S1,tile", [(4, 12, 1282), (8, 24, 1282), (4, 5, 1282), (3, 3, 12884), (2, 6, 12883)])
+def test_gemm_group_two_slab_gemms_bit_exact(hip, S0, S1, tile):
     """Two weight-gradient slab GEMMs (the bench's dW_qkv batch of 3 and dW_o) launched as one
     grouped grid write exactly what two separate launches write; a group of one GEMM, and two of
     different tiles, launch one by one."""
@@ -706,13 +706,13 @@ def test_gemm_group_two_slab_gemms_bit_exact(hip, S0, S1):
     nkt = T // 64
     s0, s1 = hip.slab_count(nkt, S0), hip.slab_count(nkt, S1)
 
-    def run(group, tile1=1282):
+    def run(group, tile1=tile):
         sl0 = torch.full((s0, 3, 640, 512), float("nan"), device=dev)
         sl1 = torch.full((s1, 512, 640), float("nan"), device=dev)
         if group:
             hip.gemm_group_begin()
         hip.gemm(x, dq[0], sl0, 640, 512, T, 640, 512, 512, False, False, batch=3, sA=0, sC=640 * 512,
-                 splitk=s0, tile=1282, slabs=True, b_list=dq)
+                 splitk=s0, tile=tile, slabs=True, b_list=dq)
         hip.gemm(h, dy, sl1, 512, 640, T, 512, 640, 640, False, False, sC=512 * 640, splitk=s1, tile=tile1,
                  slabs=True)
         if group:
