@@ -475,8 +475,17 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
 # 0.2476 ms with it vs 0.2180 / 0.2202 without, B=8 0.1013 / 0.1006 vs 0.0809 / 0.0806 -- the
 # side-stream branch in the replayed graph costs far more than the 12 us cast it hides (as the
 # side-stream weight gradients did, ops/streams.py).  Opt-in: LJS_PRECAST=1.
-_PRECAST_ON = os.environ.get("LJS_PRECAST", "0") == "1"
+# LJS_PRECAST=join (the default): no side stream -- the next input's cast is queued on the step's
+# own stream just before a data-parallel backward waits for its gradient all-reduce
+# (parallel/data.GradReducer.finish), where the stream would otherwise idle behind the
+# collective's tail; single-process steps have no such wait and keep the cast in the forward.
+# Only inputs whose cast the forward actually runs (the plain cast pass, not a transposing or
+# fused path) are cast early.
+_PRECAST_MODE = os.environ.get("LJS_PRECAST", "join")
+_PRECAST_ON = _PRECAST_MODE == "1"
 _NEXT_INPUTS: List[torch.Tensor] = []
+_PLAIN_CAST = set()      # (numel, device index) of next-step inputs the forward cast plainly
+PRECAST_STATS = {"taken": 0}
 _PRECAST = {}            # key -> (bf16 copy, event, source)
 _PRECAST_SIDE = {}       # device index -> side stream
 
@@ -488,7 +497,7 @@ def _pc_key(t: torch.Tensor):
 def prefetch_next_input(*xs) -> None:
     """Register the next step's input(s) (tensors or sharded arrays; f32 CUDA shards only) for
     an early bf16 cast on a side stream during the coming step's backward."""
-    if not _PRECAST_ON:
+    if not (_PRECAST_ON or _PRECAST_MODE == "join"):
         return
     _register_cut_hook()
     for x in xs:
@@ -500,7 +509,26 @@ def prefetch_next_input(*xs) -> None:
                 _NEXT_INPUTS.append(t)
 
 
+def launch_join_precasts() -> None:
+    """LJS_PRECAST=join: cast the registered next-step inputs now, on each one's current stream
+    (called before a data-parallel backward joins its gradient all-reduce)."""
+    if _PRECAST_MODE != "join" or not _NEXT_INPUTS:
+        return
+    from ..spmd import graphs as _graphs
+    if isinstance(_graphs.current(), _graphs.MultiDeviceGraph):
+        _NEXT_INPUTS.clear()
+        return
+    todo = [t for t in _NEXT_INPUTS if (t.numel(), t.device.index) in _PLAIN_CAST]
+    _NEXT_INPUTS.clear()
+    for t in todo:
+        k = _pc_key(t)
+        if k not in _PRECAST:
+            _PRECAST[k] = (hip._cast_raw(t.reshape(-1), torch.bfloat16), None, t)
+
+
 def _launch_precasts(dev: torch.device) -> None:
+    if not _PRECAST_ON:
+        return
     from ..spmd import graphs as _graphs
     if isinstance(_graphs.current(), _graphs.MultiDeviceGraph):
         _NEXT_INPUTS.clear()      # (a single-controller multi-device capture: not forked there)
@@ -526,11 +554,17 @@ def _launch_precasts(dev: torch.device) -> None:
 
 
 def _take_precast(t: torch.Tensor):
+    if _NEXT_INPUTS and t.is_cuda and t.dtype == torch.float32 and any(
+            n.numel() == t.numel() and n.device == t.device for n in _NEXT_INPUTS):
+        # a registered next-step input cast by the plain pass (a [tokens, features] view of
+        # it): worth casting early
+        _PLAIN_CAST.add((t.numel(), t.device.index))
     if not _PRECAST or not t.is_cuda:
         return None
     ent = _PRECAST.pop(_pc_key(t), None)
     if ent is None:
         return None
+    PRECAST_STATS["taken"] += 1
     xb, ev, _ = ent
     if ev is not None:
         main = torch.cuda.current_stream(t.device)

@@ -224,6 +224,10 @@ class GradReducer:
         ``grads`` holds the unreduced per-leaf gradients (replica-free leaves pass through)."""
         global _ACTIVE_WIRE
         _ACTIVE_WIRE = None
+        # the next step's input cast (if a runner registered it) fills the stream's wait for the
+        # all-reduce tail below (ops/linear.py, LJS_PRECAST=join)
+        from ..ops import linear as _lin
+        _lin.launch_join_precasts()
         for pkey in list(self.pending):
             members = self.pending.pop(pkey)
             key = (pkey[0], pkey[1])

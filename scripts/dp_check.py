@@ -58,7 +58,24 @@ def main():
         g = ljs.grad(lambda p: model.apply({"params": p}, x).sum())(state.params)
         return state.apply_gradients(grads=g)
 
-    step = ljs.jit(train_step, in_shardings=(ss, xs), out_shardings=ss, donate_argnums=0, capture=capture)
+    # LJS_CHECK_MULTI=G: G steps per jitted call, each registering the next step's input as
+    # bench.py does (ops/linear.prefetch_next_input: the early input cast)
+    G = int(os.environ.get("LJS_CHECK_MULTI", "1"))
+    if G > 1:
+        from learning_jax_sharding_amd.ops import linear as _lin
+
+        def train_steps(state, x):
+            for i in range(G):
+                if i + 1 < G:
+                    _lin.prefetch_next_input(x)
+                state = train_step(state, x)
+            _lin.join_precasts()
+            return state
+        step = ljs.jit(train_steps, in_shardings=(ss, xs), out_shardings=ss, donate_argnums=0, capture=capture)
+        assert steps % G == 0, (steps, G)
+        steps //= G
+    else:
+        step = ljs.jit(train_step, in_shardings=(ss, xs), out_shardings=ss, donate_argnums=0, capture=capture)
     with mesh, nn.axis_rules(rules):
         for i in range(steps):
             state = step(state, x)
@@ -71,7 +88,10 @@ def main():
     stp = np.asarray(state.step)
     _log("gathered")
     if int(os.environ.get("RANK", "0")) == 0:
-        np.savez(out, *arrs, step=stp)
+        extra = {}
+        if G > 1:
+            extra["precast_taken"] = np.asarray(_lin.PRECAST_STATS["taken"])
+        np.savez(out, *arrs, step=stp, **extra)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

@@ -18,9 +18,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCRIPT = os.path.join(ROOT, "scripts", "dp_check.py")
 
 
-def _run(tmp_path, world, capture, steps=3, port=29517, wire="bf16", mesh=None, gb=4):
-    out = str(tmp_path / f"w{world}_c{capture}_{wire}_{mesh}.npz")
-    env = dict(os.environ, PYTHONPATH=ROOT, LJS_PLATFORM="gpu", LJS_DIST_BACKEND="gloo", LJS_GRAD_COMM_DTYPE=wire)
+def _run(tmp_path, world, capture, steps=3, port=29517, wire="bf16", mesh=None, gb=4, extra_env=None, tag=""):
+    out = str(tmp_path / f"w{world}_c{capture}_{wire}_{mesh}{tag}.npz")
+    env = dict(os.environ, PYTHONPATH=ROOT, LJS_PLATFORM="gpu", LJS_DIST_BACKEND="gloo", LJS_GRAD_COMM_DTYPE=wire,
+               **(extra_env or {}))
     env.pop("LJS_NUM_DEVICES", None)
     if world == 1:
         cmd = [sys.executable, SCRIPT, out, str(steps), str(int(capture)), str(gb)]
@@ -72,3 +73,17 @@ def test_2d_layout_matches_single_process(tmp_path, world, mesh):
         diff = np.abs(got[k] - ref[k])
         assert diff.max() <= 6e-3 + 1e-6, (k, diff.max())
         assert np.mean(diff > 2e-4 + 2e-3 * np.abs(ref[k])) < 5e-3, (k, np.mean(diff > 2e-4))
+
+
+def test_dp2_early_input_cast_bit_exact(tmp_path):
+    """LJS_PRECAST=join: in a data-parallel multi-step graph the next step's input cast is queued
+    before the gradient all-reduce join instead of in that step's forward -- the same bf16 values,
+    so the trained parameters are bit-identical to the in-forward cast."""
+    kw = dict(steps=4, gb=32, wire="fp32")
+    a = _run(tmp_path, 2, True, port=29561, extra_env={"LJS_CHECK_MULTI": "2", "LJS_PRECAST": "join"}, tag="j", **kw)
+    b = _run(tmp_path, 2, True, port=29571, extra_env={"LJS_CHECK_MULTI": "2", "LJS_PRECAST": "0"}, tag="o", **kw)
+    assert int(a["step"]) == 4 and int(b["step"]) == 4
+    assert int(a["precast_taken"]) > 0 and int(b["precast_taken"]) == 0
+    for k in a.files:
+        if k != "precast_taken":
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
