@@ -1530,9 +1530,10 @@ struct GroupRec {
   GemmArgs a;
   int kind;   // 1: 128x128 2x2 waves 2 stages, 2: 128x128 2x4 4 stages, 3: 128x128 2x4 3 stages
 };
-static bool g_group_on = false;
-static GroupRec g_group[2];
-static int g_group_n = 0;
+// (per host thread: another thread's GEMMs are never recorded into this thread's open group)
+static thread_local bool g_group_on = false;
+static thread_local GroupRec g_group[2];
+static thread_local int g_group_n = 0;
 
 template <int BM, int BN>
 GemmArgs group_prep(const GemmArgs& a, int* items) {

@@ -27,6 +27,7 @@ Epilogue fusions (``hip.gemm``'s operand R):
 from __future__ import annotations
 
 import os
+import threading
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -227,7 +228,9 @@ _SLAB_DT = torch.bfloat16 if os.environ.get("LJS_SLAB_BF16", "0") == "1" else to
 # projection's dW GEMMs ran as 480 + 480 items (8 and 24 splits, 63 MB of slabs); paired they are
 # 360 + 120 items of 6 splits each (31 MB).  Anything that reads a held GEMM's slabs launches it first.
 _DW_GROUP = os.environ.get("LJS_DW_GROUP", "1") == "1"
-_HELD: List = []
+# device index -> (held job, its stream); the lock: autograd runs one backward thread per device
+_HELD: dict = {}
+_HELD_LOCK = threading.RLock()
 
 
 class _DwJob:
@@ -258,31 +261,43 @@ def deferred_pending():
 
 
 def flush_held_dw():
-    """Launch the held weight-gradient GEMM (if any) on its own."""
-    while _HELD:
-        _HELD.pop()[0].run_alone()
+    """Launch the held weight-gradient GEMMs (if any) on their own, each on its own stream."""
+    if not _HELD:
+        return
+    with _HELD_LOCK:
+        while _HELD:
+            _, (job, st) = _HELD.popitem()
+            with torch.cuda.stream(st):
+                job.run_alone()
 
 
 def _hold_dw(job: _DwJob, ref: torch.Tensor) -> None:
-    """Hold ``job`` to be grouped with the next one, or launch it with the held one as a pair."""
+    """Hold ``job`` to be grouped with the next one on its device, or launch it with the held one
+    as a pair."""
     stream = torch.cuda.current_stream(ref.device)
-    if not _HELD:
-        _HELD.append((job, stream))
-        return
-    prev, pst = _HELD.pop()
-    pick = hip.pick_dw_pair(prev.K, prev.N, job.K, job.N, job.T) \
-        if pst == stream and prev.T == job.T else None
-    if pick is None:
-        prev.run_alone()
-        job.run_alone()
-        return
-    tile, s0, s1 = pick
-    hip.gemm_group_begin()
-    try:
-        prev.run(tile, s0)
-        job.run(tile, s1)
-    finally:
-        hip.gemm_group_end(ref)
+    with _HELD_LOCK:
+        held = _HELD.pop(ref.device.index, None)
+        if held is None:
+            _HELD[ref.device.index] = (job, stream)
+            return
+        prev, pst = held
+        if pst != stream:
+            with torch.cuda.stream(pst):
+                prev.run_alone()
+            _HELD[ref.device.index] = (job, stream)
+            return
+        pick = hip.pick_dw_pair(prev.K, prev.N, job.K, job.N, job.T) if prev.T == job.T else None
+        if pick is None:
+            prev.run_alone()
+            job.run_alone()
+            return
+        tile, s0, s1 = pick
+        hip.gemm_group_begin()
+        try:
+            prev.run(tile, s0)
+            job.run(tile, s1)
+        finally:
+            hip.gemm_group_end(ref)
 
 
 def _dw_slabs_wmajor(xb: torch.Tensor, dys, T: int, K: int, N: int, ws, pend):
