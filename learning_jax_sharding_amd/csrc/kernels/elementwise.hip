@@ -4,6 +4,7 @@
 #include "common.h"
 #include <stdlib.h>
 #include <type_traits>
+#include <algorithm>
 
 namespace {
 
@@ -594,12 +595,40 @@ __device__ __forceinline__ void finish_ticket(int* step, int s0, bool last) {
   if (last) __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Blocks past the Adam tiles (cast_n > 0): the next training step's f32 -> bf16 input cast
+// (ops/linear.py, the early input cast), run by the same launch so its streaming blocks fill the
+// CUs as the Adam blocks drain (both are bandwidth-bound) instead of starting a kernel after them.
+struct CastJob {
+  const float* src;
+  bf16_t* dst;
+  long n;
+};
+
 template <int kAdamRows, int kThreads>
 __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, int* __restrict__ step, int step_offset,
                                                          unsigned* __restrict__ ticket, float lr, float b1,
-                                                         float b2, float eps, float wd) {
+                                                         float b2, float eps, float wd, CastJob cast) {
   __shared__ float tr[kAdamRows][65];
   const int id = blockIdx.x;
+  if (cast.n > 0 && id >= batch.tile_start[batch.n]) {
+    // cast_f32_bf16's loop over the cast blocks (same rounding)
+    const int cb = id - batch.tile_start[batch.n], ncb = (int)gridDim.x - batch.tile_start[batch.n];
+    long i8 = ((long)cb * kThreads + threadIdx.x) * 8;
+    const long stride = (long)ncb * kThreads * 8;
+    for (; i8 + 8 <= cast.n; i8 += stride) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(cast.src + i8);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(cast.src + i8 + 4);
+      u32x4 o;
+      o[0] = pack_bf16x2(a[0], a[1]);
+      o[1] = pack_bf16x2(a[2], a[3]);
+      o[2] = pack_bf16x2(c[0], c[1]);
+      o[3] = pack_bf16x2(c[2], c[3]);
+      *reinterpret_cast<u32x4*>(cast.dst + i8) = o;
+    }
+    if (i8 < cast.n)
+      for (long j = i8; j < cast.n; ++j) cast.dst[j] = f2bf(cast.src[j]);
+    return;
+  }
   // tensor of this tile: every tile_start compared at once (the loop form chained one kernel-
   // argument load per tensor before the tile's first data load could issue)
   int ti = 0;
@@ -1485,8 +1514,11 @@ LJS_API int ljs_step_add(void* step, int n, hipStream_t s) {
 // table: n x 16 int64 {p, g, m, v, shadow_t, shadow_n, R, C, g_bf16, gS, qn, sn8, qt, st8, g_ld, g_ss}
 // (see AdamTensor); up to 32 per call
 LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset, void* ticket, float lr, float b1,
-                           float b2, float eps, float wd, hipStream_t s) {
+                           float b2, float eps, float wd, const void* cast_src, void* cast_dst, long cast_n,
+                           hipStream_t s) {
   if (n < 1 || n > kAdamMax) return (int)hipErrorInvalidValue;
+  CastJob cast{(const float*)cast_src, (bf16_t*)cast_dst, cast_src && cast_dst && !ticket ? cast_n : 0};
+  if (cast.n > 0 && ((((uintptr_t)cast.src) & 15) || (((uintptr_t)cast.dst) & 15))) return (int)hipErrorInvalidValue;
   AdamBatch b;
   // Tile height (x 64 columns): 32 rows by default -- 660 workgroups for the step's 1.3 M
   // parameters instead of 330 of 64 rows, which left a ragged second round on 256 CUs (B=8 step
@@ -1540,15 +1572,18 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   b.tile_start[n] = tiles;
   b.n = n;
   if (ticket && 1 + (tiles + 31) / 32 > (64 << 10) / 4) return (int)hipErrorInvalidValue;  // ticket words
+  // cast blocks: one 8-element chunk per thread per pass, at most 2048 blocks (grid-stride)
+  const long cast_blocks = cast.n > 0 ? std::min<long>(2048, (cast.n + 256 * 8 - 1) / (256 * 8)) : 0;
+  const unsigned grid = (unsigned)(tiles + cast_blocks);
   if (kAdamRows == 16)
-    hipLaunchKernelGGL((adam_multi_kernel<16, 256>), dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, lr, b1, b2, eps, wd);
+    hipLaunchKernelGGL((adam_multi_kernel<16, 256>), dim3(grid), dim3(256), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, lr, b1, b2, eps, wd, cast);
   else if (kAdamRows == 32)
-    hipLaunchKernelGGL((adam_multi_kernel<32, 256>), dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, lr, b1, b2, eps, wd);
+    hipLaunchKernelGGL((adam_multi_kernel<32, 256>), dim3(grid), dim3(256), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, lr, b1, b2, eps, wd, cast);
   else
-    hipLaunchKernelGGL((adam_multi_kernel<64, 256>), dim3(tiles), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, lr, b1, b2, eps, wd);
+    hipLaunchKernelGGL((adam_multi_kernel<64, 256>), dim3(grid), dim3(256), 0, s, b, (int*)step, step_offset,
+                       (unsigned*)ticket, lr, b1, b2, eps, wd, cast);
   return (int)hipGetLastError();
 }
 

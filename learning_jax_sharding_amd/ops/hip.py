@@ -66,7 +66,7 @@ _SIGS = {
     "ljs_adam_f32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
                      c_float, c_float, c_float, c_float, c_float, c_void_p],
     "ljs_adam_multi": [_LP, c_int, c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float,
-                       c_void_p],
+                       c_void_p, c_void_p, c_long, c_void_p],
     "ljs_step_add": [c_void_p, c_int, c_void_p],
     "ljs_mse_loss": [c_void_p, c_void_p, c_int, c_long, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_mse_colsum": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -1631,13 +1631,20 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
     pend = _defer_step_inc(step_i) if (increment_step and not use_ticket) else None
     offset = int(increment_step) + (pend or 0)
     rows = _early_adam(rows, step_i, lr, b1, b2, eps, wd, increment_step)
+    # the next step's input cast, run by the last launch's extra blocks (ops/linear.py early cast)
+    cast = None
+    if not use_ticket and rows and step_i.is_cuda:
+        from . import linear as _lin
+        cast = _lin.take_optimizer_precast(step_i.device)
     for i in range(0, len(rows), 32):
         chunk = rows[i:i + 32]
         tab = np.asarray([r[0] for r in chunk], dtype=np.int64).reshape(-1)
         arr = (ctypes.c_long * tab.size)(*tab.tolist())
         last = i + 32 >= len(rows)
+        cj = cast if last else None
         rc = lib().ljs_adam_multi(arr, len(chunk), _p(step_i), offset,
                                   _p(ticket) if (use_ticket and last) else None, lr, b1, b2, eps, wd,
+                                  _p(cj[0]) if cj else None, _p(cj[1]) if cj else None, cj[0].numel() if cj else 0,
                                   _stream(step_i))
         _ck(rc, "ljs_adam_multi")
     if increment_step and not use_ticket and pend is None:
@@ -1688,7 +1695,7 @@ def _early_adam(rows, step_i, lr, b1, b2, eps, wd, increment_step):
     arr = (ctypes.c_long * tab.size)(*tab.tolist())
     with torch.cuda.stream(side):
         rc = lib().ljs_adam_multi(arr, len(early), _p(step_i), int(increment_step), None, lr, b1, b2, eps, wd,
-                                  ctypes.c_void_p(side.cuda_stream))
+                                  None, None, 0, ctypes.c_void_p(side.cuda_stream))
     _ck(rc, "ljs_adam_multi (early)")
     main.wait_stream(side)
     ids = {id(r) for r in early}

@@ -541,6 +541,30 @@ def launch_join_precasts() -> None:
             _PRECAST[k] = (hip._cast_raw(t.reshape(-1), torch.bfloat16), None, t)
 
 
+def take_optimizer_precast(dev: torch.device):
+    """(f32 source, bf16 destination) of ONE registered next-step input on ``dev`` that the
+    optimizer launch casts with its extra blocks (hip.adam_multi), registered as that input's early
+    cast -- or None.  (LJS_PRECAST=join; a data-parallel step has cast it already at its gradient
+    join.)"""
+    if _PRECAST_MODE != "join" or not _NEXT_INPUTS or _OPT_PRECAST == "0":
+        return None
+    from ..spmd import graphs as _graphs
+    if isinstance(_graphs.current(), _graphs.MultiDeviceGraph):
+        return None
+    for i, t in enumerate(_NEXT_INPUTS):
+        if (t.device == dev and (t.numel(), t.device.index) in _PLAIN_CAST and t.is_contiguous()
+                and t.data_ptr() % 16 == 0 and _pc_key(t) not in _PRECAST):
+            del _NEXT_INPUTS[i]
+            dst = torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
+            _PRECAST[_pc_key(t)] = (dst, None, t)
+            return t.reshape(-1), dst.reshape(-1)
+    return None
+
+
+# LJS_OPT_PRECAST=0: single-process steps keep the next input's cast in its own forward
+_OPT_PRECAST = os.environ.get("LJS_OPT_PRECAST", "1")
+
+
 def _launch_precasts(dev: torch.device) -> None:
     if not _PRECAST_ON:
         return
