@@ -1530,12 +1530,11 @@ def adam(p, g, m, v, step, lr, b1, b2, eps, wd, inplace):
 class SlabGrad:
     """A weight gradient not yet combined: element (r, c) is the sum over s < S of
     ``slabs.view(-1)[offset + s * slab_stride + r * ld + c]`` (the split-K slabs of its GEMM)."""
-    __slots__ = ("slabs", "S", "offset", "ld", "slab_stride", "shape", "ready")
+    __slots__ = ("slabs", "S", "offset", "ld", "slab_stride", "shape")
 
     def __init__(self, slabs, S, offset, ld, slab_stride, shape):
         self.slabs, self.S, self.offset, self.ld, self.slab_stride = slabs, S, offset, ld, slab_stride
         self.shape = tuple(shape)
-        self.ready = None   # event recorded after the producing GEMM (early optimizer launches)
 
 
 class ConstGrad:
@@ -1565,7 +1564,7 @@ def _flush_step_incs() -> None:
 def _defer_step_inc(step: torch.Tensor):
     """Pending increments of ``step`` before this one (and one more recorded), or None when the
     increment must be launched now."""
-    if not _DEFER_INC or _EARLY_ADAM:
+    if not _DEFER_INC:
         return None
     from ..spmd import graphs as _graphs
     g = _graphs.current()
@@ -1630,7 +1629,6 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
     # _defer_step_inc): this launch reads the not-yet-incremented count, offset by what is pending
     pend = _defer_step_inc(step_i) if (increment_step and not use_ticket) else None
     offset = int(increment_step) + (pend or 0)
-    rows = _early_adam(rows, step_i, lr, b1, b2, eps, wd, increment_step)
     # the next step's input cast, run by the last launch's extra blocks (ops/linear.py early cast)
     cast = None
     if not use_ticket and rows and step_i.is_cuda:
@@ -1651,55 +1649,6 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
         _ck(lib().ljs_step_add(_p(step_i), 1, _stream(step_i)), "ljs_step_add")
     for p, _, _, _ in entries:
         shadow.mark_fresh(p)
-
-
-# Early optimizer launches: a weight whose gradient is still split-K slabs produced well before
-# the backward ends (the out-projection's dW, computed before the attention backward) is updated
-# on a side stream as soon as its GEMM has run (an event recorded after it), concurrent with the
-# rest of the backward; the main launch waits for it (it reads the same step counter).  In a
-# captured step the side launch is a parallel branch of the graph.  LJS_EARLY_ADAM=0: one launch.
-# Measured: b8 0.1003 vs 0.0875 ms, b64 0.2605-0.2625 vs 0.2459-0.2472 ms (gpurun_out/r3g): the
-# side branch costs more than the overlap buys -- off by default.
-_EARLY_ADAM = os.environ.get("LJS_EARLY_ADAM", "0") == "1"
-_ADAM_SIDE: Dict[int, "torch.cuda.Stream"] = {}
-
-
-def _early_adam(rows, step_i, lr, b1, b2, eps, wd, increment_step):
-    """Launch the rows whose slab gradient became ready before the latest one on a side stream
-    (joined into the current stream before returning); the rest are returned for the main
-    launch."""
-    if not _EARLY_ADAM or not step_i.is_cuda or not increment_step:
-        # (without the folded increment the step counter may be written by an op still queued
-        # on the main stream)
-        return rows
-    evs = [r[1].ready for r in rows if isinstance(r[1], SlabGrad) and r[1].ready is not None]
-    if len(evs) < 2:
-        return rows
-    last = evs[-1]
-    early = [r for r in rows if isinstance(r[1], SlabGrad) and r[1].ready is not None and r[1].ready is not last]
-    if not early or len(early) > 32:
-        return rows
-    main = torch.cuda.current_stream(step_i.device)
-    side = _ADAM_SIDE.get(step_i.device.index)
-    if side is None:
-        side = _ADAM_SIDE[step_i.device.index] = torch.cuda.Stream(step_i.device)
-    seen = set()
-    for r in early:
-        ev = r[1].ready
-        if id(ev) not in seen:
-            seen.add(id(ev))
-            side.wait_event(ev)
-        r[1].slabs.record_stream(side)
-    import numpy as np
-    tab = np.asarray([r[0] for r in early], dtype=np.int64).reshape(-1)
-    arr = (ctypes.c_long * tab.size)(*tab.tolist())
-    with torch.cuda.stream(side):
-        rc = lib().ljs_adam_multi(arr, len(early), _p(step_i), int(increment_step), None, lr, b1, b2, eps, wd,
-                                  None, None, 0, ctypes.c_void_p(side.cuda_stream))
-    _ck(rc, "ljs_adam_multi (early)")
-    main.wait_stream(side)
-    ids = {id(r) for r in early}
-    return [r for r in rows if id(r) not in ids]
 
 
 # ============================================================================ RNG

@@ -248,7 +248,7 @@ class _DwJob:
 
 def _group_ok(ref: torch.Tensor) -> bool:
     """Whether a slab-mode weight-gradient GEMM launched now may be grouped (see _DW_GROUP)."""
-    return _DW_GROUP and _DEFER is not None and ref.is_cuda and not hip._EARLY_ADAM and not _DW_SPLIT
+    return _DW_GROUP and _DEFER is not None and ref.is_cuda and not _DW_SPLIT
 
 
 def deferred_pending():
@@ -326,16 +326,9 @@ def _dw_slabs_wmajor(xb: torch.Tensor, dys, T: int, K: int, N: int, ws, pend):
                 done.append(True)
                 flush_held_dw()
                 hip.slab_reduce(slabs.view(S, nw * K, N), out.view(nw * K, N), N, 0)
-        ev = None
         for i in range(nw):
             if deferred[i]:
-                sg = hip.SlabGrad(slabs, S, i * K * N, N, nw * K * N, (K, N))
-                if hip._EARLY_ADAM:
-                    if ev is None:
-                        ev = torch.cuda.Event()
-                        ev.record()
-                    sg.ready = ev
-                pend[out[i].data_ptr()] = (sg, materialize)
+                pend[out[i].data_ptr()] = (hip.SlabGrad(slabs, S, i * K * N, N, nw * K * N, (K, N)), materialize)
             else:
                 materialize()
     if all(deferred) and _group_ok(xb):
@@ -378,13 +371,6 @@ def _dw_slabs(xb: torch.Tensor, dy: torch.Tensor, ld: int, T: int, K: int, Nt: i
                 hip.slab_reduce(slabs, out, cb, out_bs, out_bf16=twin)
         if defer is not None:
             defer(slabs, S, materialize)
-            if _DEFER is not None and slabs.is_cuda and hip._EARLY_ADAM:
-                # the optimizer may update this weight as soon as its slabs exist (hip._early_adam)
-                ev = torch.cuda.Event()
-                ev.record()
-                for desc, _ in _DEFER["pending"].values():
-                    if isinstance(desc, hip.SlabGrad) and desc.slabs is slabs:
-                        desc.ready = ev
         else:
             materialize()
     if slab_mode and defer is not None and _group_ok(xb):
@@ -479,30 +465,28 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
 
 # ---------------------------------------------------------------------------- input-cast prefetch
 # The reference's f32 activation is rounded to bf16 inside its first Dense (case6_attention.py:
-# 96-99); here that is a streaming cast pass in front of the QKV GEMM (12 us at 64 x 256 tokens,
-# nothing to overlap it with inside its own step).  A multi-step runner that knows the NEXT
-# step's input registers it (`prefetch_next_input`) before running a step; that step's first
-# dense backward then forks the next input's cast onto a side stream, where it runs beside the
-# backward's GEMMs / attention, and the next step's dense takes the result after an event wait
-# (`_take_precast`) instead of casting.  Every step still casts its own input exactly once: only
-# WHEN changes.  Runners join what was not taken (`join_precasts`) before their capture ends.
-# Measured (bench.py G-step graphs, gpurun_out/r5t, profiles/r5t_precast_lines.txt): B=64 0.2472 /
-# 0.2476 ms with it vs 0.2180 / 0.2202 without, B=8 0.1013 / 0.1006 vs 0.0809 / 0.0806 -- the
-# side-stream branch in the replayed graph costs far more than the 12 us cast it hides (as the
-# side-stream weight gradients did, ops/streams.py).  Opt-in: LJS_PRECAST=1.
-# LJS_PRECAST=join (the default): no side stream -- the next input's cast is queued on the step's
-# own stream just before a data-parallel backward waits for its gradient all-reduce
-# (parallel/data.GradReducer.finish), where the stream would otherwise idle behind the
-# collective's tail; single-process steps have no such wait and keep the cast in the forward.
-# Only inputs whose cast the forward actually runs (the plain cast pass, not a transposing or
-# fused path) are cast early.
+# 96-99); here that is a streaming cast pass in front of the QKV GEMM (11 us at 64 x 256 tokens).
+# A multi-step runner that knows the NEXT step's input registers it (`prefetch_next_input`) before
+# running a step; the cast of that input is then queued earlier, where it costs less, and the next
+# step's dense takes the copy (`_take_precast`) instead of casting.  Every step still casts its
+# own input exactly once: only WHEN changes.  Runners drop what was not taken (`join_precasts`)
+# before their capture ends.
+#  * single-process steps: the optimizer launch's extra blocks cast it (hip.adam_multi,
+#    `take_optimizer_precast`): B = 8 0.0719-0.0729 vs 0.0736-0.0742 ms (profiles/
+#    r5bb_opt_precast_lines.txt);
+#  * data-parallel steps: queued on the step's own stream just before the backward waits for its
+#    gradient all-reduce (parallel/data.GradReducer.finish, `launch_join_precasts`), where the
+#    stream would otherwise idle behind the collective's tail.
+# Only inputs whose cast the forward runs as the plain pass (not a transposing or fused path) are
+# cast early.  (A side-stream form -- the cast forked beside the backward -- measured much slower:
+# B=64 0.2472 vs 0.2180 ms, profiles/r5t_precast_lines.txt; removed.)  LJS_PRECAST=0: off.
 _PRECAST_MODE = os.environ.get("LJS_PRECAST", "join")
-_PRECAST_ON = _PRECAST_MODE == "1"
 _NEXT_INPUTS: List[torch.Tensor] = []
 _PLAIN_CAST = set()      # (numel, device index) of next-step inputs the forward cast plainly
 PRECAST_STATS = {"taken": 0}
-_PRECAST = {}            # key -> (bf16 copy, event, source)
-_PRECAST_SIDE = {}       # device index -> side stream
+_PRECAST = {}            # key -> (bf16 copy, source)
+# LJS_OPT_PRECAST=0: single-process steps keep the next input's cast in its own forward
+_OPT_PRECAST = os.environ.get("LJS_OPT_PRECAST", "1")
 
 
 def _pc_key(t: torch.Tensor):
@@ -511,10 +495,10 @@ def _pc_key(t: torch.Tensor):
 
 def prefetch_next_input(*xs) -> None:
     """Register the next step's input(s) (tensors or sharded arrays; f32 CUDA shards only) for
-    an early bf16 cast on a side stream during the coming step's backward."""
-    if not (_PRECAST_ON or _PRECAST_MODE == "join"):
+    an early bf16 cast during the coming step."""
+    if _PRECAST_MODE == "0":
         return
-    _register_cut_hook()
+    _register_capture_hook()
     for x in xs:
         loc = getattr(x, "local", None)
         ts = list(loc.values()) if isinstance(loc, dict) else [x]
@@ -524,13 +508,17 @@ def prefetch_next_input(*xs) -> None:
                 _NEXT_INPUTS.append(t)
 
 
-def launch_join_precasts() -> None:
-    """LJS_PRECAST=join: cast the registered next-step inputs now, on each one's current stream
-    (called before a data-parallel backward joins its gradient all-reduce)."""
-    if _PRECAST_MODE != "join" or not _NEXT_INPUTS:
-        return
+def _single_device_capture() -> bool:
     from ..spmd import graphs as _graphs
-    if isinstance(_graphs.current(), _graphs.MultiDeviceGraph):
+    return not isinstance(_graphs.current(), _graphs.MultiDeviceGraph)
+
+
+def launch_join_precasts() -> None:
+    """Cast the registered next-step inputs now, on the current stream (called before a
+    data-parallel backward joins its gradient all-reduce)."""
+    if _PRECAST_MODE == "0" or not _NEXT_INPUTS:
+        return
+    if not _single_device_capture():
         _NEXT_INPUTS.clear()
         return
     todo = [t for t in _NEXT_INPUTS if (t.numel(), t.device.index) in _PLAIN_CAST]
@@ -538,58 +526,23 @@ def launch_join_precasts() -> None:
     for t in todo:
         k = _pc_key(t)
         if k not in _PRECAST:
-            _PRECAST[k] = (hip._cast_raw(t.reshape(-1), torch.bfloat16), None, t)
+            _PRECAST[k] = (hip._cast_raw(t.reshape(-1), torch.bfloat16), t)
 
 
 def take_optimizer_precast(dev: torch.device):
     """(f32 source, bf16 destination) of ONE registered next-step input on ``dev`` that the
     optimizer launch casts with its extra blocks (hip.adam_multi), registered as that input's early
-    cast -- or None.  (LJS_PRECAST=join; a data-parallel step has cast it already at its gradient
-    join.)"""
-    if _PRECAST_MODE != "join" or not _NEXT_INPUTS or _OPT_PRECAST == "0":
-        return None
-    from ..spmd import graphs as _graphs
-    if isinstance(_graphs.current(), _graphs.MultiDeviceGraph):
+    cast -- or None."""
+    if _PRECAST_MODE == "0" or not _NEXT_INPUTS or _OPT_PRECAST == "0" or not _single_device_capture():
         return None
     for i, t in enumerate(_NEXT_INPUTS):
         if (t.device == dev and (t.numel(), t.device.index) in _PLAIN_CAST and t.is_contiguous()
                 and t.data_ptr() % 16 == 0 and _pc_key(t) not in _PRECAST):
             del _NEXT_INPUTS[i]
             dst = torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
-            _PRECAST[_pc_key(t)] = (dst, None, t)
+            _PRECAST[_pc_key(t)] = (dst, t)
             return t.reshape(-1), dst.reshape(-1)
     return None
-
-
-# LJS_OPT_PRECAST=0: single-process steps keep the next input's cast in its own forward
-_OPT_PRECAST = os.environ.get("LJS_OPT_PRECAST", "1")
-
-
-def _launch_precasts(dev: torch.device) -> None:
-    if not _PRECAST_ON:
-        return
-    from ..spmd import graphs as _graphs
-    if isinstance(_graphs.current(), _graphs.MultiDeviceGraph):
-        _NEXT_INPUTS.clear()      # (a single-controller multi-device capture: not forked there)
-        return
-    todo = [t for t in _NEXT_INPUTS if t.device == dev]
-    if not todo:
-        return
-    _NEXT_INPUTS[:] = [t for t in _NEXT_INPUTS if t.device != dev]
-    main = torch.cuda.current_stream(dev)
-    side = _PRECAST_SIDE.get(dev.index)
-    if side is None:
-        side = _PRECAST_SIDE[dev.index] = torch.cuda.Stream(dev)
-    ev0 = torch.cuda.Event()
-    ev0.record(main)
-    side.wait_event(ev0)
-    with torch.cuda.stream(side):
-        for t in todo:
-            t.record_stream(side)
-            xb = hip._cast_raw(t.reshape(-1), torch.bfloat16)
-            ev = torch.cuda.Event()
-            ev.record(side)
-            _PRECAST[_pc_key(t)] = (xb, ev, t)
 
 
 def _take_precast(t: torch.Tensor):
@@ -604,42 +557,19 @@ def _take_precast(t: torch.Tensor):
     if ent is None:
         return None
     PRECAST_STATS["taken"] += 1
-    xb, ev, _ = ent
-    if ev is not None:
-        main = torch.cuda.current_stream(t.device)
-        main.wait_event(ev)
-        xb.record_stream(main)
-    return xb.view(t.shape)
+    return ent[0].view(t.shape)
 
 
 def join_precasts() -> None:
-    """The current streams wait for every early cast nobody took (and forget them), and pending
-    registrations are dropped -- call before a capture or a step sequence ends (a capture
-    segment's end does it too: spmd/graphs.BEFORE_CUT)."""
+    """Forget every early cast nobody took and drop pending registrations -- call before a
+    capture or a step sequence ends (a whole capture's end does it too)."""
     _NEXT_INPUTS.clear()
-    while _PRECAST:
-        _, (xb, ev, src) = _PRECAST.popitem()
-        if ev is not None:
-            main = torch.cuda.current_stream(xb.device)
-            main.wait_event(ev)
-            xb.record_stream(main)
+    _PRECAST.clear()
 
 
-def _join_forks() -> None:
-    # before a capture segment ends: the main streams wait for the forked casts (whose copies
-    # stay registered for the next step's dense: the next segment finds them already joined)
-    for k, (xb, ev, src) in list(_PRECAST.items()):
-        if ev is not None:
-            main = torch.cuda.current_stream(xb.device)
-            main.wait_event(ev)
-            xb.record_stream(main)
-            _PRECAST[k] = (xb, None, src)
-
-
-def _register_cut_hook() -> None:
+def _register_capture_hook() -> None:
     from ..spmd import graphs as _graphs
-    if _join_forks not in _graphs.BEFORE_CUT:
-        _graphs.BEFORE_CUT.append(_join_forks)
+    if join_precasts not in _graphs.AFTER_CAPTURE:
         _graphs.AFTER_CAPTURE.append(join_precasts)
 
 
@@ -747,8 +677,6 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *dys):
-        if _NEXT_INPUTS and dys and isinstance(dys[0], torch.Tensor) and dys[0].is_cuda:
-            _launch_precasts(dys[0].device)   # the next step's input cast, beside this backward
         lead, K, M, N, nw, relu, xdtype, has_b = ctx.meta
         order = getattr(ctx, "order", None)          # (the fp8 dense reuses this backward in row order)
         pshape = ctx.pshape if order is not None else tuple(lead)

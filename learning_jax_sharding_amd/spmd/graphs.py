@@ -36,8 +36,8 @@ __all__ = ["SegmentedGraph", "MultiDeviceGraph", "current", "run_collective", "j
 _ACTIVE: List[Optional["SegmentedGraph"]] = [None]
 
 
-# callables run before a capture segment ends: side-stream work forked inside the segment (an
-# input-cast prefetch, ops/linear.py) is joined back so the segment's capture closes cleanly
+# callables run before a capture segment ends: work deferred inside the segment that must be in
+# it (the optimizer's pending count increments, ops/hip._flush_step_incs) is launched there
 BEFORE_CUT: List[Callable[[], None]] = []
 
 

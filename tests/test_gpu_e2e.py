@@ -160,13 +160,11 @@ def test_jit_graph_multi_step_capture_matches_single_steps(gpu_devices):
         np.testing.assert_array_equal(np.asarray(b), np.asarray(a))
 
 
-@pytest.mark.parametrize("where", ["side", "optimizer"])
-def test_jit_graph_multi_step_input_cast_prefetch_bit_exact(gpu_devices, monkeypatch, where):
+def test_jit_graph_multi_step_input_cast_prefetch_bit_exact(gpu_devices, monkeypatch):
     """A multi-step graph whose steps register the next step's input (ops/linear.
-    prefetch_next_input): the next cast runs on a side stream during the backward ("side",
-    LJS_PRECAST=1) or in the optimizer launch's extra blocks ("optimizer", the default) and the
-    next step's dense takes it -- the state equals single-step replays bit for bit, each step's
-    cast ran, and nothing stays registered after the capture."""
+    prefetch_next_input): the next cast runs in the optimizer launch's extra blocks and the next
+    step's dense takes it -- the state equals single-step replays bit for bit, each step's cast
+    ran, and nothing stays registered after the capture."""
     gpu_devices(1)
     import learning_jax_sharding_amd as ljs
     from learning_jax_sharding_amd import optim
@@ -184,12 +182,8 @@ def test_jit_graph_multi_step_input_cast_prefetch_bit_exact(gpu_devices, monkeyp
         g = ljs.grad(lambda p: model.apply({"params": p}, x).sum())(state.params)
         return state.apply_gradients(grads=g)
 
-    if where == "side":
-        monkeypatch.setattr(lin, "_PRECAST_ON", True)   # (opt-in: LJS_PRECAST=1)
-    else:
-        monkeypatch.setattr(lin, "_PRECAST_ON", False)
-        monkeypatch.setattr(lin, "_PRECAST_MODE", "join")
-        monkeypatch.setattr(lin, "_OPT_PRECAST", "1")
+    monkeypatch.setattr(lin, "_PRECAST_MODE", "join")
+    monkeypatch.setattr(lin, "_OPT_PRECAST", "1")
     taken = []
     orig = lin._take_precast
 
