@@ -378,9 +378,9 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
 
         def train_steps(state, x):  # G complete training steps, each on the previous one's state
             for i in range(G):
-                # the next step's input is known: its bf16 cast may run beside this step's
-                # backward on a side stream (ops/linear.prefetch_next_input); each step still
-                # casts its own input once
+                # the next step's input is known: its bf16 cast runs in this step's optimizer
+                # launch (or before a data-parallel gradient join; ops/linear.prefetch_next_input);
+                # each step still casts its own input once, inside this graph
                 if i + 1 < G:
                     _lin.prefetch_next_input(x)
                 state = train_step(state, x)
