@@ -267,6 +267,9 @@ def flush_held_dw():
     with _HELD_LOCK:
         while _HELD:
             _, (job, st) = _HELD.popitem()
+            if st is None:
+                job.run_alone()
+                continue
             with torch.cuda.stream(st):
                 job.run_alone()
 
@@ -274,7 +277,7 @@ def flush_held_dw():
 def _hold_dw(job: _DwJob, ref: torch.Tensor) -> None:
     """Hold ``job`` to be grouped with the next one on its device, or launch it with the held one
     as a pair."""
-    stream = torch.cuda.current_stream(ref.device)
+    stream = torch.cuda.current_stream(ref.device) if ref.is_cuda else None
     with _HELD_LOCK:
         held = _HELD.pop(ref.device.index, None)
         if held is None:
