@@ -554,46 +554,13 @@ struct AdamBatch {
   int n;
 };
 
-// `step_offset`/`ticket`: with a ticket the kernel uses t = *step + step_offset and its last
-// arriving block stores *step + 1 (the optimizer's count increment, folded in: no extra launch).
-// kThreads: 256 (16 rows x 64 columns per pass).  512 / 1024 (more waves per tile, fewer loads per
-// thread) measured the same, 20.9 / 21.7 / 21.5 us in the B=64 step (gpurun_out/r5m): the loads in
-// flight per tile do not change with the thread count.
-//
-// The count increment's ticket (opt-in, ops/hip.py LJS_ADAM_STEP_INC=ticket; two-level,
-// ticket_last_2lvl's words).  Each block draws its group word as soon as every wave holds its step
-// value and its first loads are issued, and reads the result once its loads have landed (before
-// the Adam math, so the wait costs nothing); each group's last arriver then draws the top word, and
-// the overall last stores step + 1 when it ends.  Drawn at the end after a full barrier (the round-4
-// form) the increment cost the store drain plus two serial atomic round trips per block: 13.8 vs
-// 9.1 us for the step's parameter set with plain gradients and no increment; drawn early, 13.2; one
-// word for all blocks, 12.8; a separate one-lane launch, 10.8 (scripts/adam_probe.py,
-// profiles/r5n_adam_probe_*.txt) -- hence the launch is the default.  The draw is a vector atomic
-// from inline asm: through the builtin, the compiler's wave-level atomic rewrite broadcast the
-// result (v_readfirstlane) and so waited for the atomic -- and every load before it -- at the draw.
-__device__ __forceinline__ unsigned draw_ticket(unsigned* ticket, int s0) {
-  asm volatile("" ::"s"(__builtin_amdgcn_readfirstlane(s0)));   // this wave has its step value
-  __builtin_amdgcn_s_barrier();                                  // ... and so has every wave
-  unsigned tk = 0;
-  if (threadIdx.x == 0) {
-    unsigned* w = ticket + 1 + (blockIdx.x >> 5);
-    asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(tk) : "v"(w), "v"(1u) : "memory");
-  }
-  return tk;
-}
-// thread 0 of the block drawing the overall last ticket gets true
-__device__ __forceinline__ bool settle_ticket(unsigned* ticket, unsigned tk) {
-  if (threadIdx.x != 0) return false;
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(tk)::"memory");   // the draw's result
-  const unsigned grp = blockIdx.x >> 5, n = gridDim.x;
-  const unsigned in_grp = n - (grp << 5) < 32u ? n - (grp << 5) : 32u;
-  if (tk != in_grp - 1) return false;
-  __hip_atomic_store(ticket + 1 + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return ticket_last(ticket, (n + 31) >> 5);
-}
-__device__ __forceinline__ void finish_ticket(int* step, int s0, bool last) {
-  if (last) __hip_atomic_store(step, s0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// `step_offset`: the kernel uses t = *step + step_offset (the optimizer's count as of the last
+// increment plus the increments still pending, ops/hip.py adam_multi).  kThreads: 256 (16 rows x 64
+// columns per pass).  512 / 1024 (more waves per tile, fewer loads per thread) measured the same,
+// 20.9 / 21.7 / 21.5 us in the B=64 step (gpurun_out/r5m).  The count increment is its own one-lane
+// launch, one per graph segment: an in-kernel two-level arrival ticket (the last-arriving block
+// stores the new count) measured no better in the step and cost 13.2 vs 10.8 us in the probe
+// (scripts/adam_probe.py, profiles/r5n_adam_probe_*.txt), so it was removed.
 
 // Blocks past the Adam tiles (cast_n > 0): the next training step's f32 -> bf16 input cast
 // (ops/linear.py, the early input cast), run by the same launch so its streaming blocks fill the
@@ -606,8 +573,8 @@ struct CastJob {
 
 template <int kAdamRows, int kThreads>
 __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, int* __restrict__ step, int step_offset,
-                                                         unsigned* __restrict__ ticket, float lr, float b1,
-                                                         float b2, float eps, float wd, CastJob cast) {
+                                                         float lr, float b1, float b2, float eps, float wd,
+                                                         CastJob cast) {
   __shared__ float tr[kAdamRows][65];
   const int id = blockIdx.x;
   if (cast.n > 0 && id >= batch.tile_start[batch.n]) {
@@ -670,8 +637,6 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
       vv[q] = *(const __attribute__((address_space(1))) f32x4*)(Vv + i);
       pv[q] = *(const __attribute__((address_space(1))) f32x4*)(P + i);
     }
-    unsigned tk = 0;
-  if (ticket) tk = draw_ticket(ticket, s0);
     if (T.gS > 0) {
       // the slab sum of slab_reduce_kernel (same order, bit-identical) with the loads of all NQ
       // rows of a 4-slab group in flight together; f32 or bf16 slabs (T.g_bf16)
@@ -762,7 +727,6 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
         gv[q] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(T.g) + gi);
       }
     }
-    const bool last = ticket && settle_ticket(ticket, tk);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int rl = r0 + RPP * q;
@@ -839,7 +803,6 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
         }
       }
     }
-    if (ticket) finish_ticket(step, s0, last);
   };
   if (T.vec && (tc_i + 1) * 64 <= T.C) {
     // per-tensor tile height (the launch's choice): shorter tiles for tensors with many gradient
@@ -853,9 +816,6 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
     }
     return;
   }
-  unsigned tk = 0;
-  if (ticket) tk = draw_ticket(ticket, s0);
-  const bool last = ticket && settle_ticket(ticket, tk);
 #pragma unroll 4
   for (int rr = 0; rr < kAdamRows / (kThreads / 64); ++rr) {
     const int rl = ty + (kThreads / 64) * rr, row = tr_i * kAdamRows + rl;
@@ -887,7 +847,6 @@ __global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamBatch batch, i
       if (c < T.C && ocol < T.R) reinterpret_cast<bf16_t*>(T.st)[(long)c * T.R + ocol] = f2bf(tr[r][cl]);
     }
   }
-  if (ticket) finish_ticket(step, s0, last);
 }
 
 // ------------------------------------------------------------------ Philox RNG
@@ -1517,7 +1476,8 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
                            float b2, float eps, float wd, const void* cast_src, void* cast_dst, long cast_n,
                            hipStream_t s) {
   if (n < 1 || n > kAdamMax) return (int)hipErrorInvalidValue;
-  CastJob cast{(const float*)cast_src, (bf16_t*)cast_dst, cast_src && cast_dst && !ticket ? cast_n : 0};
+  if (ticket) return (int)hipErrorInvalidValue;   // (the in-kernel count ticket was removed)
+  CastJob cast{(const float*)cast_src, (bf16_t*)cast_dst, cast_src && cast_dst ? cast_n : 0};
   if (cast.n > 0 && ((((uintptr_t)cast.src) & 15) || (((uintptr_t)cast.dst) & 15))) return (int)hipErrorInvalidValue;
   AdamBatch b;
   // Tile height (x 64 columns): 32 rows by default -- 660 workgroups for the step's 1.3 M
@@ -1571,19 +1531,18 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   }
   b.tile_start[n] = tiles;
   b.n = n;
-  if (ticket && 1 + (tiles + 31) / 32 > (64 << 10) / 4) return (int)hipErrorInvalidValue;  // ticket words
   // cast blocks: one 8-element chunk per thread per pass, at most 2048 blocks (grid-stride)
   const long cast_blocks = cast.n > 0 ? std::min<long>(2048, (cast.n + 256 * 8 - 1) / (256 * 8)) : 0;
   const unsigned grid = (unsigned)(tiles + cast_blocks);
   if (kAdamRows == 16)
     hipLaunchKernelGGL((adam_multi_kernel<16, 256>), dim3(grid), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, lr, b1, b2, eps, wd, cast);
+                       lr, b1, b2, eps, wd, cast);
   else if (kAdamRows == 32)
     hipLaunchKernelGGL((adam_multi_kernel<32, 256>), dim3(grid), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, lr, b1, b2, eps, wd, cast);
+                       lr, b1, b2, eps, wd, cast);
   else
     hipLaunchKernelGGL((adam_multi_kernel<64, 256>), dim3(grid), dim3(256), 0, s, b, (int*)step, step_offset,
-                       (unsigned*)ticket, lr, b1, b2, eps, wd, cast);
+                       lr, b1, b2, eps, wd, cast);
   return (int)hipGetLastError();
 }
 

@@ -1578,21 +1578,15 @@ def _defer_step_inc(step: torch.Tensor):
     return pend
 
 
-# How adam_multi's ``increment_step`` advances the count: "kernel" (default) a one-lane launch after
-# the Adam launches; "ticket" the last-arriving block of the last Adam launch (a two-level arrival
-# ticket drawn early in the kernel).  The step's parameter set with plain gradients, in a graph
-# (scripts/adam_probe.py, profiles/r5n_adam_probe_*.txt): no increment 9.1 us, + launch 10.8,
-# ticket 13.2; steps B=64 0.2095 / 0.2132 vs 0.2113 / 0.2128 ms, B=8 0.0824 / 0.0825 vs
-# 0.0829 / 0.0828 (profiles/r5o_adam_ab_lines.txt).
-_STEP_INC = os.environ.get("LJS_ADAM_STEP_INC", "kernel")
 
 
 def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step: bool = False) -> None:
     """In-place fused Adam over many params (one launch per 32): entries = [(p, g, m, v)].
 
     Also rewrites each param's registered bf16 and MX-fp8 shadows (see :mod:`.shadow`).  With
-    ``increment_step`` the bias corrections use ``step + 1`` and the last launch's last
-    arriving block stores ``step + 1`` (int32 ``step`` updated in place, no extra kernel)."""
+    ``increment_step`` the bias corrections use ``step + 1`` and int32 ``step`` is incremented in
+    place by a one-lane launch -- inside a graph capture one launch per segment for all its
+    steps (``_defer_step_inc``)."""
     from . import shadow
     import numpy as np
     rows = []
@@ -1623,15 +1617,13 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
     if increment_step:
         assert step.dtype == torch.int32 and step.is_contiguous()
     step_i = step if step.dtype == torch.int32 else step.to(torch.int32)
-    use_ticket = increment_step and _STEP_INC == "ticket"
-    ticket = _workspace(step_i.device, "adam_ticket", 64 << 10) if use_ticket else None  # two-level tickets
     # inside a capture the increments are deferred (one launch per capture segment, see
     # _defer_step_inc): this launch reads the not-yet-incremented count, offset by what is pending
-    pend = _defer_step_inc(step_i) if (increment_step and not use_ticket) else None
+    pend = _defer_step_inc(step_i) if increment_step else None
     offset = int(increment_step) + (pend or 0)
     # the next step's input cast, run by the last launch's extra blocks (ops/linear.py early cast)
     cast = None
-    if not use_ticket and rows and step_i.is_cuda:
+    if rows and step_i.is_cuda:
         from . import linear as _lin
         cast = _lin.take_optimizer_precast(step_i.device)
     for i in range(0, len(rows), 32):
@@ -1641,11 +1633,11 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
         last = i + 32 >= len(rows)
         cj = cast if last else None
         rc = lib().ljs_adam_multi(arr, len(chunk), _p(step_i), offset,
-                                  _p(ticket) if (use_ticket and last) else None, lr, b1, b2, eps, wd,
+                                  None, lr, b1, b2, eps, wd,
                                   _p(cj[0]) if cj else None, _p(cj[1]) if cj else None, cj[0].numel() if cj else 0,
                                   _stream(step_i))
         _ck(rc, "ljs_adam_multi")
-    if increment_step and not use_ticket and pend is None:
+    if increment_step and pend is None:
         _ck(lib().ljs_step_add(_p(step_i), 1, _stream(step_i)), "ljs_step_add")
     for p, _, _, _ in entries:
         shadow.mark_fresh(p)

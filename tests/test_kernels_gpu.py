@@ -733,11 +733,9 @@ def test_gemm_group_two_slab_gemms_bit_exact(hip, S0, S1, tile):
     hip.gemm_group_end(x)             # empty group: nothing launched
 
 
-@pytest.mark.parametrize("mode", ["kernel", "ticket"])
-def test_adam_multi_folded_step_increment(hip, mode, monkeypatch):
-    """increment_step advances the device count by one per call -- by the one-lane launch (default)
-    or the in-kernel arrival ticket -- and the bias corrections use the new count."""
-    monkeypatch.setattr(hip, "_STEP_INC", mode)
+def test_adam_multi_folded_step_increment(hip):
+    """increment_step advances the device count by one per call (the one-lane launch) and the bias
+    corrections use the new count."""
     ws = [torch.randn(64 * 7, 130, device=dev) for _ in range(40)]  # > 32 tensors: two launches
     gs = [torch.randn_like(w) for w in ws]
     ms = [torch.zeros_like(w) for w in ws]
