@@ -396,6 +396,11 @@ _DW_SMALL_TILE = int(os.environ.get("LJS_DW_SMALL_TILE", "12884"))
 # weight of the slab traffic (written by the GEMM, summed by the combine or the fused Adam) in
 # the split-count cost model (tuning knob)
 _DW_TRAFFIC_W = float(os.environ.get("LJS_DW_TRAFFIC_W", "1"))
+# ... in the split count of a weight-gradient GEMM launched on its own (not paired): its slabs are
+# then always read back by a separate slab_reduce (a data-parallel step) or a lone deferred combine,
+# so they weigh more -- dW_o at 16384 tokens 16 splits instead of 24: fake-4 dp rehearsal
+# 0.2147-0.2172 vs 0.2211-0.2224 ms x3 (profiles/r5bm_dw_single_traffic_lines.txt)
+_DW_SINGLE_TRAFFIC_W = float(os.environ.get("LJS_DW_SINGLE_TRAFFIC_W", "4"))
 # weight-grad tile above 4096 tokens: 1282 (cost-model split count) or, as an A/B switch, 644 /
 # 12884 with one round of slabs
 _DW_BIG_TILE = int(os.environ.get("LJS_DW_BIG_TILE", "1282"))
@@ -416,7 +421,7 @@ def _cus() -> int:
         return 256
 
 
-def _dw_single(K: int, N: int, T: int):
+def _dw_single(K: int, N: int, T: int, traffic_w: Optional[float] = None):
     """(tile, K-chunks, slab mode) of a weight-gradient slab GEMM [K, N] = X^T dY over T tokens.
 
     T > 4096: 128x128 tiles (2 blocks per CU) in slab mode, the split count chosen by a cost
@@ -426,6 +431,7 @@ def _dw_single(K: int, N: int, T: int):
     tiles) 16 x 16 -> 24 x 11.  At T <= 4096 the 8-wave 128x128 tile (one block per CU) in slab
     mode; ``LJS_DW_SMALL_TILE=644``: the 64x64 tile with the largest power-of-two batched split
     keeping <= 512 items and >= 512 tokens per chunk (the round-2 default before)."""
+    w = _DW_SINGLE_TRAFFIC_W if traffic_w is None else traffic_w
     if K % 64 or N % 64 or T % 64:
         return 1282, pick_splitk_dma(K, N, T, 1), False, None
     if T > 4096 and not _DW_SLAB_MODE:
@@ -451,7 +457,7 @@ def _dw_single(K: int, N: int, T: int):
             # ~1.2 us per K-tile round of a full chip of 128x128 blocks, ~1 us per round of
             # prologue/epilogue, and the reduction reads each f32 slab once (~5 TB/s)
             rounds = -(-tiles * S // slots)
-            cost = rounds * (kps * 1.2 + 1.0) + _DW_TRAFFIC_W * S * K * N * 4 / 5e6
+            cost = rounds * (kps * 1.2 + 1.0) + w * S * K * N * 4 / 5e6
             if best_cost is None or cost < best_cost - 1e-9:
                 best, best_cost = S, cost
         return 1282, best, True, best_cost
@@ -462,7 +468,7 @@ def _dw_single(K: int, N: int, T: int):
         for S in range(1, min(32, nkt) + 1):
             if slab_count(nkt, S) != S:
                 continue
-            cost = -(-tiles * S // _cus()) * (-(-nkt // S) * 1.2 + 1.0) + _DW_TRAFFIC_W * S * K * N * 4 / 5e6
+            cost = -(-tiles * S // _cus()) * (-(-nkt // S) * 1.2 + 1.0) + w * S * K * N * 4 / 5e6
             if best_cost is None or cost < best_cost - 1e-9:
                 best, best_cost = S, cost
         return 12884, best, True, best_cost
@@ -527,7 +533,7 @@ def pick_dw_pair(K0: int, N0: int, K1: int, N1: int, T: int):
                 cost = kps * 1.2 + 1.0 + _DW_TRAFFIC_W * (s0 * size0 + s1 * size1) * 4 / 5e6
                 if best_cost is None or cost < best_cost - 1e-9:
                     best, best_cost = (tile, s0, s1), cost
-        c0, c1 = _dw_single(K0, N0, T)[3], _dw_single(K1, N1, T)[3]
+        c0, c1 = _dw_single(K0, N0, T, _DW_TRAFFIC_W)[3], _dw_single(K1, N1, T, _DW_TRAFFIC_W)[3]
         if best is not None and c0 is not None and c1 is not None and c0 + c1 <= best_cost:
             best = None
     _PAIR_PICKS[key] = best

@@ -43,7 +43,7 @@ def test_dw_pair_ff_block_stays_separate(chip):
 def test_dw_single_picks_unchanged(chip):
     # the separate launches (a lone held GEMM, or grouping off)
     assert hip.pick_dw_slabs(640, 1536, 16384) == (1282, 8, True)
-    assert hip.pick_dw_slabs(512, 640, 16384) == (1282, 24, True)
+    assert hip.pick_dw_slabs(512, 640, 16384) == (1282, 16, True)   # (single-launch slab weight)
     assert hip.pick_dw_slabs(640, 1536, 2048) == (12884, 4, True)
 
 
