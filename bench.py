@@ -221,29 +221,50 @@ def main():
             wd.phase(name, timeout)
 
     env = dict(n=n, world=world, torch=torch, ljs=ljs, dist=dist, dist_on=dist_on, cuda=cuda,
-               barrier_sync=barrier_sync, phase=phase)
-    res = _measure(args, args.mesh, env)
+               barrier_sync=barrier_sync, phase=phase, probe=dist_on and world > 1)
+    res = _measure_with_fallback(args, args.mesh, env)
     comm = "none"
     if dist_on:
         c = get_comm()
         comm = dist.get_backend() + ("+native-rccl" if getattr(c, "_native", None) is not None else "")
-    rec, printed = None, []
+    rec = None
+    detail = _comm_detail(env, res) if dist_on and world > 1 else None
     if rank == 0:
         rec = _record(args, res, n, n_gpus, cuda, comm)
+        if detail is not None:
+            rec["comm_detail"] = detail
+    import threading
+    print_lock, printed = threading.Lock(), []
+
+    def print_once():
+        # the main thread and the watchdog thread (on_fail) may both try: exactly one prints
+        with print_lock:
+            if rec is not None and not printed:
+                printed.append(1)
+                print(json.dumps(rec), flush=True)
+
     # the reference's own 2-D DP x TP layout (case6_attention.py:155-162,183-187; BASELINE config 4)
     # timed in the same job as a secondary result: the headline stays the DP layout
     if _want_secondary(args, n):
         def on_fail(reason):
-            # a hang or RCCL error inside the secondary measurement must not cost the headline
-            if rec is not None and not printed:
-                printed.append(1)
+            # a hang or RCCL error inside the secondary measurement: the headline, measured before
+            # it, is still printed (with the error), and the job still exits with the watchdog's
+            # non-zero code (None keeps comm/watchdog.EXIT_CODE): a run that hung never reads as a pass
+            if rec is not None:
                 rec["secondary"] = {"mesh": "2d", "error": reason[:300]}
-                print(json.dumps(rec), flush=True)
-            return 0
+            print_once()
+            return None
         if wd is not None:
             wd.on_fail = on_fail
         try:
-            res2 = _measure(args, "2d", env, phase_timeout=float(os.environ.get("LJS_BENCH_SECONDARY_TIMEOUT_S", "240")))
+            env["probe"] = False
+            if dist_on and hasattr(get_comm(), "routes"):
+                get_comm().routes.clear()   # the secondary layout's routes are reported on their own
+            res2 = _measure_with_fallback(args, "2d", env,
+                                          phase_timeout=float(os.environ.get("LJS_BENCH_SECONDARY_TIMEOUT_S", "240")))
+            # the 2-D layout's own collectives (gathers, all-to-alls): which path carried them
+            # (collective: every rank)
+            d2 = _comm_detail(env, res2) if dist_on and world > 1 else None
             if rec is not None:
                 rec["secondary"] = {
                     "mesh": list(res2["mshape"]), "parallelism": _parallelism(args, res2["mshape"]),
@@ -253,14 +274,16 @@ def main():
                     "graph_segments": res2["segs"], "steps_per_graph": res2["G"],
                     "warmup_steps_run": res2["warm_run"], "rules": args.rules,
                 }
+                if d2 is not None:
+                    rec["secondary"]["comm_routes"] = d2["routes"]
+                    rec["secondary"]["routes_agree_across_ranks"] = d2["routes_agree_across_ranks"]
+                    rec["secondary"]["p2p_fallbacks"] = d2["p2p_fallbacks"]
         except Exception as e:   # (same on every rank: the measurement is SPMD)
             if rec is not None:
                 rec["secondary"] = {"mesh": "2d", "error": f"{type(e).__name__}: {e}"[:300]}
         if wd is not None:
             wd.on_fail = None
-    if rec is not None and not printed:
-        printed.append(1)
-        print(json.dumps(rec), flush=True)
+    print_once()
     if dist_on:
         phase("shutdown")
         dist.barrier()
@@ -268,6 +291,55 @@ def main():
             wd.stop()
         get_comm().close()          # ncclCommDestroy of the native communicators
         dist.destroy_process_group()
+
+
+class _Remeasure(Exception):
+    """A peer-memory collective failed at run time (a barrier timed out): every rank has moved to
+    RCCL (comm/backend.DistComm.p2p_health) and the layout is measured again on it."""
+
+
+def _p2p_check(env, where: str) -> None:
+    if not env["dist_on"]:
+        return
+    from learning_jax_sharding_amd.comm.backend import get_comm
+    c = get_comm()
+    if hasattr(c, "p2p_health"):
+        reason = c.p2p_health()     # collective: every rank checks here, all agree
+        if reason is not None:
+            raise _Remeasure(f"{where}: {reason}")
+
+
+def _measure_with_fallback(args, mesh_arg, env, phase_timeout=None):
+    """``_measure``, once more on RCCL if a peer-memory collective failed during it (the job is not
+    aborted: the failure and the fallback are recorded in comm_detail.p2p_fallbacks)."""
+    try:
+        return _measure(args, mesh_arg, env, phase_timeout)
+    except _Remeasure as e:
+        print(f"bench.py: {e}; peer-memory collectives off, measuring again on RCCL", file=sys.stderr, flush=True)
+        res = _measure(args, mesh_arg, env, phase_timeout)
+        res["remeasured"] = str(e)[:300]
+        return res
+
+
+def _comm_detail(env, res):
+    """Which collective path ran (every rank's view, checked for agreement), RCCL's own rank counts,
+    the gradient buckets of the last backward, and the timed eager all-reduce of the gradient size
+    through each path (``res['probe']``, measured before the timed region)."""
+    from learning_jax_sharding_amd.comm.backend import get_comm
+    from learning_jax_sharding_amd.parallel import data as _data
+    dist = env["dist"]
+    c = get_comm()
+    det = c.comm_detail() if hasattr(c, "comm_detail") else {"backend": dist.get_backend()}
+    mine = [(r["kind"], r["bytes"], r["path"]) for r in det.get("routes", [])]
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, mine)
+    det["routes_agree_across_ranks"] = all(a == allr[0] for a in allr)
+    det["grad_buckets"] = [{"bytes": b, "dtype": dt, "groups": [list(g) for g in gr]} for b, dt, gr in _data.LAST_BUCKETS]
+    if res.get("probe") is not None:
+        det["all_reduce_probe"] = res["probe"]
+    if res.get("remeasured"):
+        det["remeasured"] = res["remeasured"]
+    return det
 
 
 def _want_secondary(args, n) -> bool:
@@ -354,12 +426,19 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
                 return ljs.ops.core.mse_loss(y, target)
             return y.sum()
         grads = ljs.grad(loss_fn)(state.params)
-        return state.apply_gradients(grads=grads)
+        state = state.apply_gradients(grads=grads)
+        if clock_probe:
+            # diagnostics: the shader clock after every step (csrc/kernels/diag.hip; captured into
+            # the graphs like the step's kernels, so every replayed step records one)
+            from learning_jax_sharding_amd.ops import hip as _hip
+            _hip.clock_probe(torch.device("cuda", torch.cuda.current_device()))
+        return state
 
     def fwd_step(state, x):
         return model.apply({"params": state.params}, x)
 
     capture = not args.no_graph and torch.cuda.is_available()
+    clock_probe = os.environ.get("LJS_CLOCK_PROBE") and torch.cuda.is_available()
     aten_trace = os.environ.get("LJS_ATEN_TRACE")   # diagnostics: eager steps, one traced (utils/aten_trace.py)
     if aten_trace:
         capture = False
@@ -427,6 +506,16 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
         if extra:
             run(extra)
             warm_run += extra
+        # a peer-memory barrier that timed out during warmup: every rank moves to RCCL and this
+        # layout is measured again (comm_detail.p2p_fallbacks records it)
+        _p2p_check(env, f"warmup ({mesh_arg})")
+        probe = None
+        if env.get("probe"):
+            from learning_jax_sharding_amd.parallel import data as _data
+            gbytes = sum(b for b, _, _ in _data.LAST_BUCKETS)
+            if gbytes:
+                from learning_jax_sharding_amd.comm.probe import all_reduce_paths
+                probe = all_reduce_paths(gbytes)
         if aten_trace:
             from learning_jax_sharding_amd.utils.aten_trace import AtenTrace
             with AtenTrace(cuda_only=not os.environ.get("LJS_ATEN_TRACE_ALL"),
@@ -442,7 +531,13 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
         barrier_sync()
         t1 = time.perf_counter()
         phase(f"report ({mesh_arg})", phase_timeout)
+        _p2p_check(env, f"timed steps ({mesh_arg})")
     elapsed = t1 - t0
+    if clock_probe and int(os.environ.get("RANK", "0")) == 0:
+        from learning_jax_sharding_amd.ops import hip as _hip
+        recs = _hip.clock_probe_records(torch.device("cuda", torch.cuda.current_device()))
+        with open(os.environ["LJS_CLOCK_PROBE"], "w") as f:
+            json.dump({"warm_run": warm_run, "steps": args.steps, "records": recs}, f)
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if cuda else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -468,7 +563,7 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
     del state, step, multi
     return dict(ms=ms, tflops_total=flops / (ms * 1e-3) / 1e12, tokens_per_s=B * S / (ms * 1e-3),
                 host_ms=(th - t0) / args.steps * 1e3, mshape=mshape, B=B, S=S, M=M, G=G, segs=segs,
-                warm_run=warm_run, capture=capture, peak_gb=peak_gb)
+                warm_run=warm_run, capture=capture, peak_gb=peak_gb, probe=probe)
 
 
 def _record(args, res, n, n_gpus, cuda, comm):

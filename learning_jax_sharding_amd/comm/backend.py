@@ -22,6 +22,7 @@ partitioner's collective plan can be printed and tested.
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -33,6 +34,13 @@ from ..runtime.devices import is_distributed, local_devices, process_index
 __all__ = ["get_comm", "reset_comm", "LocalComm", "DistComm", "Transfer"]
 
 Groups = Sequence[Tuple[int, ...]]
+
+
+def _p2p_inject() -> str:
+    """Fault injection for the peer-memory fallback paths (tests): ``LJS_P2P_INJECT=build`` makes
+    every group build fail on every member, ``runtime`` makes the next :meth:`DistComm.p2p_health`
+    report a barrier timeout."""
+    return os.environ.get("LJS_P2P_INJECT", "")
 
 
 
@@ -284,6 +292,12 @@ class DistComm:
         self._lock = threading.Lock()
         self._p2p_groups = {}
         self._fake = dist.get_backend() == "fake"
+        # what actually carried each collective (comm_detail(): the benchmark record says which
+        # path ran, so a multi-GPU result can be checked against it) and every peer-memory group
+        # that fell back to RCCL, with the reason
+        self.routes: Dict[Tuple, Dict] = {}
+        self.p2p_fallbacks: List[Dict] = []
+        self._p2p_off: Optional[str] = None   # set once a runtime P2P failure moved everything to RCCL
         # native RCCL rank communicators (comm/native.py RankRccl): collectives issued on the
         # current stream, so they are captured into HIP graphs instead of cutting them
         self._native = None
@@ -347,11 +361,94 @@ class DistComm:
         key = tuple(tuple(int(v) for v in g) for g in groups)
         return self._native.partition(key)
 
+    def _note_route(self, kind: str, g, x: torch.Tensor, path: str) -> None:
+        key = (kind, tuple(g), str(x.dtype).replace("torch.", ""), x.numel() * x.element_size())
+        ent = self.routes.get(key)
+        if ent is None or ent["path"] != path:
+            self.routes[key] = ent = {"path": path, "calls": 0}
+        ent["calls"] += 1
+
+    def _bulk_path(self, nh) -> str:
+        if nh is not None:
+            return "rccl"
+        return "none (rehearsal)" if self._fake else f"torch-{dist.get_backend()}"
+
+    def _p2p_path(self, grp, nbytes: int, kind: str) -> str:
+        if kind == "all_reduce":
+            return "p2p-oneshot" if nbytes <= grp.oneshot_max else "p2p-twoshot"
+        return "p2p"
+
+    def comm_detail(self) -> Dict:
+        """Which communication ran, as this rank saw it: the backend, RCCL's own rank count of
+        the world communicator and of every partition communicator (ncclCommCount), the path
+        that carried each collective shape, and every peer-memory fallback with its reason."""
+        det: Dict = {"backend": dist.get_backend(), "world": dist.get_world_size(), "rccl_nranks": None,
+                     "rccl_partitions": [], "p2p": {"mode": None, "max_bytes": None, "groups_built": 0},
+                     "routes": [], "p2p_fallbacks": list(self.p2p_fallbacks)}
+        from . import p2p
+        det["p2p"] = {"mode": p2p.mode(), "max_bytes": p2p.max_bytes(),
+                      "groups_built": sum(1 for v in self._p2p_groups.values() if v),
+                      "disabled": self._p2p_off}
+        if self._native is not None:
+            det["rccl_nranks"] = self._native.query()["nranks"]
+            for groups, h in self._native.partitions().items():
+                if h:
+                    mine = next((list(gg) for gg in groups if self.me in gg), [])
+                    det["rccl_partitions"].append({"group": mine, "nranks": self._native.query(h)["nranks"]})
+        for (kind, g, dt, nb), ent in sorted(self.routes.items(), key=lambda kv: (kv[0][0], -kv[0][3])):
+            det["routes"].append({"kind": kind, "group": list(g), "dtype": dt, "bytes": nb, "path": ent["path"],
+                                  "calls": ent["calls"]})
+        return det
+
+    def p2p_health(self) -> Optional[str]:
+        """Check every built peer-memory group's barrier error word (a flag barrier that timed out
+        because a peer never arrived: the collective's data is invalid, nothing hangs).  The
+        verdict is agreed by ALL ranks (one MAX all-reduce over the world group), and on a failure
+        anywhere every rank stops using peer-memory collectives for the rest of the run: later
+        collectives - and graphs captured after this - go through RCCL.  Returns the failure
+        reason (same on every rank) or None.  Collective: call it at the same point on every rank."""
+        reason = None
+        for srt, grp in list(self._p2p_groups.items()):
+            if not grp:
+                continue
+            try:
+                grp.check_error()
+            except RuntimeError as e:
+                reason = f"ranks {list(srt)}: {e}"
+                break
+        if not reason and self._p2p_off is None and _p2p_inject() == "runtime":
+            reason = "injected runtime barrier timeout (LJS_P2P_INJECT=runtime)"
+        flag = torch.tensor([1 if reason else 0], dtype=torch.int32,
+                            device=torch.device("cuda", torch.cuda.current_device())
+                            if dist.get_backend() == "nccl" else "cpu")
+        if not self._fake:
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if int(flag.item()) == 0:
+            return None
+        reason = reason or "a peer rank's p2p barrier timed out"
+        self._disable_p2p(reason)
+        return reason
+
+    def _disable_p2p(self, reason: str) -> None:
+        for srt, grp in list(self._p2p_groups.items()):
+            if grp:
+                self.p2p_fallbacks.append({"group": list(srt), "when": "runtime", "reason": reason[:200]})
+                try:
+                    grp.close()
+                except Exception:   # pragma: no cover - a wedged group still must not stop the fallback
+                    pass
+            self._p2p_groups[srt] = False
+        if not self._p2p_groups:
+            self.p2p_fallbacks.append({"group": None, "when": "runtime", "reason": reason[:200]})
+        self._p2p_off = reason
+
     def _p2p(self, g, pg, x, chunked=False):
         """Direct peer-memory collective group over IPC buffers (comm/p2p.py), members in
         sorted-rank order like the process group; None when disabled or not applicable.  The
         decision depends only on values every member shares, so members agree on it."""
         from . import p2p
+        if self._p2p_off is not None:
+            return None
         if pg is None or not p2p.enabled() or not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16):
             return None
         if p2p.mode() == "auto" and not self._distinct_gpus():
@@ -366,10 +463,13 @@ class DistComm:
                 return None   # the handle exchange cannot run inside a capture: bulk path
             devs = [x.device if r == self.me else torch.device("cuda", 0) for r in srt]
             try:
+                if _p2p_inject() == "build":
+                    raise p2p.P2PUnavailable("injected build failure (LJS_P2P_INJECT=build)")
                 grp = p2p.P2PGroup(devs, p2p.max_bytes(), rank=srt.index(self.me), pg=pg)
             except p2p.P2PUnavailable as e:   # every member raised: the group stays on RCCL
                 import warnings
                 warnings.warn(f"peer-memory collectives unavailable for ranks {srt} ({e}); using RCCL")
+                self.p2p_fallbacks.append({"group": list(srt), "when": "build", "reason": str(e)[:200]})
                 grp = False
             self._p2p_groups[srt] = grp
         if grp is False:
@@ -410,6 +510,8 @@ class DistComm:
         n = len(g)
         grp = self._p2p(g, pg, x)
         nh = None if grp is not None else self._nat(groups, x)
+        self._note_route("all_gather", g, x, self._p2p_path(grp, 0, "all_gather") if grp is not None
+                         else self._bulk_path(nh))
         if grp is not None:
             buf = grp.all_gather({grp.rank: x.contiguous()})[grp.rank]
         else:
@@ -434,9 +536,11 @@ class DistComm:
         xt = _hip().rank_major(x, dim, n, None if self._member_order_ok(g) else [g.index(d) for d in sorted(g)])
         grp = self._p2p(g, pg, xt, chunked=True)
         if grp is not None:
+            self._note_route("reduce_scatter", g, xt, "p2p")
             return {self.me: grp.reduce_scatter({grp.rank: xt.contiguous()})[grp.rank]}
         out = torch.empty_like(xt[0])          # the chunk's own dim order
         nh = self._nat(groups, xt)
+        self._note_route("reduce_scatter", g, xt, self._bulk_path(nh))
         if nh is not None:
             self._native.reduce_scatter(nh, xt, out)
             return {self.me: out}
@@ -454,6 +558,8 @@ class DistComm:
         if pg is not None:
             grp = self._p2p(g, pg, x)
             nh = None if grp is not None else self._nat(groups, x)
+            self._note_route("all_reduce", g, x, self._p2p_path(grp, x.numel() * x.element_size(), "all_reduce")
+                             if grp is not None else self._bulk_path(nh))
             if grp is not None:
                 grp.all_reduce({grp.rank: x}, out={grp.rank: x})
             elif nh is not None:
@@ -476,6 +582,7 @@ class DistComm:
         send = _hip().rank_major(x, split_dim, n, [perm[g.index(r)] for r in srt])
         grp = self._p2p(g, pg, send, chunked=True)
         nh = None if grp is not None else self._nat(groups, send)
+        self._note_route("all_to_all", g, send, "p2p" if grp is not None else self._bulk_path(nh))
         if grp is not None:
             recv = grp.all_to_all({grp.rank: send.contiguous()})[grp.rank]
         elif nh is not None:

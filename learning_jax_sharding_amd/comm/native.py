@@ -59,6 +59,8 @@ def runtime():
                                            ctypes.POINTER(_VP)],
                     "ljs_comm_split_rank": [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_VP)],
                     "ljs_comm_nranks": [_VP],
+                    "ljs_comm_query": [_VP, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_int)],
                 }
                 for name, argt in sig.items():
                     fn = getattr(L, name)
@@ -356,6 +358,19 @@ class RankRccl:
                 mine = next((g for g in groups if self.rank in g), ())
                 return f"partition {list(map(list, groups))} (this rank's group {list(mine)})"
         return f"communicator {h:#x}"
+
+    def query(self, h: Optional[int] = None) -> Dict[str, int]:
+        """RCCL's own view of a communicator (default: the world one): ncclCommCount,
+        ncclCommUserRank, ncclCommCuDevice."""
+        h = self._world_h if h is None else h
+        n, r, d = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        NativeRccl._check(runtime().ljs_comm_query(h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d)),
+                          "ncclCommCount")
+        return {"nranks": n.value, "rank": r.value, "device": d.value}
+
+    def partitions(self) -> Dict[Tuple[Tuple[int, ...], ...], Optional[int]]:
+        with self._mu:
+            return dict(self._parts)
 
     def check(self) -> None:
         """Failure detection: raise on the first asynchronous RCCL error of any of

@@ -47,9 +47,9 @@ class CommWatchdog:
         self.poll_s = float(poll_s)
         self.grace_s = float(grace_s)
         self._exit = exit_fn or os._exit
-        self._phase = "startup"
-        self._t0 = time.monotonic()
-        self._deadline = self.timeout_s
+        # (phase name, start, deadline) replaced as ONE object and read once per poll: the polling
+        # thread never pairs a new, shorter deadline with the previous phase's start time
+        self._state = ("startup", time.monotonic(), self.timeout_s)
         # called (reason) -> exit code, after the abort and before the exit: a caller that still has
         # a result to report (bench.py's headline, measured before a secondary layout hung) prints
         # it here and may choose the exit status
@@ -67,8 +67,11 @@ class CommWatchdog:
 
     def phase(self, name: str, timeout_s: Optional[float] = None) -> None:
         """Enter a new phase: its deadline (``timeout_s``, default the watchdog's) starts now."""
-        self._deadline = self.timeout_s if timeout_s is None else float(timeout_s)
-        self._phase, self._t0 = name, time.monotonic()
+        self._state = (name, time.monotonic(), self.timeout_s if timeout_s is None else float(timeout_s))
+
+    @property
+    def _phase(self) -> str:
+        return self._state[0]
 
     def stop(self) -> None:
         self._stop.set()
@@ -96,8 +99,9 @@ class CommWatchdog:
                     nat.check()
                 except Exception as e:  # an asynchronous RCCL error on some communicator
                     reason = f"asynchronous RCCL error: {e}"
-            if reason is None and time.monotonic() - self._t0 > self._deadline:
-                reason = f"phase exceeded its {self._deadline:g} s deadline (hang: a peer rank lost or wedged)"
+            _, t0, deadline = self._state
+            if reason is None and time.monotonic() - t0 > deadline:
+                reason = f"phase exceeded its {deadline:g} s deadline (hang: a peer rank lost or wedged)"
             if reason is not None:
                 self._fail(reason)
                 return
@@ -105,8 +109,9 @@ class CommWatchdog:
     def _fail(self, reason: str) -> None:
         self.failed = reason
         rank = os.environ.get("RANK", "?")
+        phase, t0, _ = self._state
         lines = [f"[ljs watchdog] rank {rank}: {reason}",
-                 f"[ljs watchdog] phase: {self._phase!r}, {time.monotonic() - self._t0:.1f} s in"]
+                 f"[ljs watchdog] phase: {phase!r}, {time.monotonic() - t0:.1f} s in"]
         nat = self._native()
         if nat is not None:
             try:   # a diagnostic: whatever it raises, the abort and the exit below still run
@@ -125,7 +130,7 @@ class CommWatchdog:
         code = EXIT_CODE
         if self.on_fail is not None:
             try:
-                rc = self.on_fail(f"{reason} (phase {self._phase!r})")
+                rc = self.on_fail(f"{reason} (phase {phase!r})")
                 if rc is not None:
                     code = int(rc)
             except Exception as e:  # pragma: no cover - defensive

@@ -162,6 +162,18 @@ LJS_RT_API int ljs_comm_split_rank(void* parent, int color, int key, void** hand
 
 LJS_RT_API int ljs_comm_nranks(void* handle) { return static_cast<Comm*>(handle)->nranks; }
 
+// what RCCL itself reports for a rank communicator (ncclCommCount / ncclCommUserRank / its device),
+// not what the caller asked for: the benchmark record's proof that a communicator spans N ranks
+LJS_RT_API int ljs_comm_query(void* handle, int* count, int* rank, int* device) {
+  Comm* c = static_cast<Comm*>(handle);
+  if (c == nullptr || c->comms.size() != 1) return (int)ncclInvalidUsage;
+  ncclResult_t r = ncclCommCount(c->comms[0], count);
+  if (r != ncclSuccess) return (int)r;
+  r = ncclCommUserRank(c->comms[0], rank);
+  if (r != ncclSuccess) return (int)r;
+  return (int)ncclCommCuDevice(c->comms[0], device);
+}
+
 LJS_RT_API int ljs_comm_destroy(void* handle) {
   Comm* c = static_cast<Comm*>(handle);
   for (auto& cm : c->comms) ncclCommDestroy(cm);

@@ -31,6 +31,7 @@ int ljs_comm_init(int n, const int* devs, void** handle);
 int ljs_comm_unique_id_size();
 int ljs_comm_get_unique_id(void* out);
 int ljs_comm_init_rank(const void* unique_id, int nranks, int rank, int dev, void** handle);
+int ljs_comm_query(void* handle, int* count, int* rank, int* device);
 int ljs_comm_split_rank(void* parent, int color, int key, void** handle);
 int ljs_comm_nranks(void* handle);
 int ljs_comm_destroy(void* handle);
@@ -215,6 +216,11 @@ ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
 ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
   check_live(comm);
   *rank = comm->rank;
+  return ncclSuccess;
+}
+ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device) {
+  check_live(comm);
+  *device = comm->dev;
   return ncclSuccess;
 }
 ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* e) {
@@ -424,6 +430,9 @@ void test_init_failure_and_rank_path() {
   void* s = reinterpret_cast<void*>(0x1);
   EXPECT(ljs_comm_split_rank(r, -1, 0, &s) == 0 && s == nullptr);
   EXPECT(ljs_comm_split_rank(r, 3, 0, &s) == 0 && s != nullptr && ljs_comm_nranks(s) == 1);
+  int qn = -1, qr = -1, qd = -1;   // RCCL's own view (ncclCommCount / UserRank / CuDevice)
+  EXPECT(ljs_comm_query(r, &qn, &qr, &qd) == 0 && qn == 1 && qr == 0 && qd == 0);
+  EXPECT(ljs_comm_query(s, &qn, &qr, &qd) == 0 && qn == 1 && qr == 0);
   EXPECT(ljs_comm_destroy(s) == 0);
   EXPECT(ljs_comm_destroy(r) == 0);
 }

@@ -68,6 +68,7 @@ _SIGS = {
     "ljs_adam_multi": [_LP, c_int, c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float,
                        c_void_p, c_void_p, c_long, c_void_p],
     "ljs_step_add": [c_void_p, c_int, c_void_p],
+    "ljs_clock_probe": [c_void_p, c_void_p, c_uint, c_uint, c_void_p],
     "ljs_mse_loss": [c_void_p, c_void_p, c_int, c_long, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_mse_colsum": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p],
@@ -1567,6 +1568,16 @@ def _flush_step_incs() -> None:
             _ck(lib().ljs_step_add(_p(st), n, _stream(st)), "ljs_step_add")
 
 
+def flush_step_inc(step: torch.Tensor) -> None:
+    """Launch ``step``'s pending deferred increments now (in stream order), so a kernel that reads
+    the count after this point -- anything but the next Adam launch, which adds the pending
+    offset itself -- sees the incremented value (optim/adam.CountLocal calls this on reads)."""
+    ent = _PENDING_INC.get(step.data_ptr())
+    if ent is not None and ent[1]:
+        _ck(lib().ljs_step_add(_p(ent[0]), ent[1], _stream(ent[0])), "ljs_step_add")
+        ent[1] = 0
+
+
 def _defer_step_inc(step: torch.Tensor):
     """Pending increments of ``step`` before this one (and one more recorded), or None when the
     increment must be launched now."""
@@ -1643,10 +1654,44 @@ def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step:
                                   _p(cj[0]) if cj else None, _p(cj[1]) if cj else None, cj[0].numel() if cj else 0,
                                   _stream(step_i))
         _ck(rc, "ljs_adam_multi")
+        if cj is not None:
+            _lin.commit_optimizer_precast(cj)
     if increment_step and pend is None:
         _ck(lib().ljs_step_add(_p(step_i), 1, _stream(step_i)), "ljs_step_add")
     for p, _, _, _ in entries:
         shadow.mark_fresh(p)
+
+
+# ============================================================================ clock probe
+_CLOCK: Dict[int, tuple] = {}   # device index -> (records [cap, 4] int64, counter int32)
+
+
+def clock_probe(dev: torch.device, ticks: int = 300, cap: int = 8192) -> None:
+    """Record the shader clock here in the stream (csrc/kernels/diag.hip): one lane spins for
+    ``ticks`` of the 100 MHz counter (3 us) and stores delta s_memtime / delta s_memrealtime; a
+    diagnostic, launched by bench.py after every step under LJS_CLOCK_PROBE (graph-capturable)."""
+    dev = torch.device(dev)
+    ent = _CLOCK.get(dev.index)
+    if ent is None:
+        ent = _CLOCK[dev.index] = (torch.zeros((cap, 4), dtype=torch.int64, device=dev),
+                                   torch.zeros(1, dtype=torch.int32, device=dev))
+    rec, ctr = ent
+    _ck(lib().ljs_clock_probe(_p(rec), _p(ctr), rec.shape[0], int(ticks), torch.cuda.current_stream(dev).cuda_stream),
+        "ljs_clock_probe")
+
+
+def clock_probe_records(dev: torch.device) -> List[dict]:
+    """Every record so far, in launch order: shader clock (MHz), start (us of the 100 MHz counter)."""
+    ent = _CLOCK.get(torch.device(dev).index)
+    if ent is None:
+        return []
+    torch.cuda.synchronize(dev)
+    rec, ctr = ent
+    n = min(int(ctr.item()), rec.shape[0])
+    out = []
+    for d_sclk, d_ref, ref0, xcc in rec[:n].cpu().tolist():
+        out.append({"sclk_mhz": round(d_sclk / max(1, d_ref) * 100.0, 1), "t_us": ref0 / 100.0, "xcc": int(xcc)})
+    return out
 
 
 # ============================================================================ RNG

@@ -533,9 +533,10 @@ def launch_join_precasts() -> None:
 
 
 def take_optimizer_precast(dev: torch.device):
-    """(f32 source, bf16 destination) of ONE registered next-step input on ``dev`` that the
-    optimizer launch casts with its extra blocks (hip.adam_multi), registered as that input's early
-    cast -- or None."""
+    """(f32 source, bf16 destination, input) of ONE registered next-step input on ``dev`` that the
+    optimizer launch casts with its extra blocks (hip.adam_multi) -- or None.  The destination
+    becomes that input's early cast only once the launch that writes it has been accepted
+    (:func:`commit_optimizer_precast`): a rejected launch leaves no unwritten buffer registered."""
     if _PRECAST_MODE == "0" or not _NEXT_INPUTS or _OPT_PRECAST == "0" or not _single_device_capture():
         return None
     for i, t in enumerate(_NEXT_INPUTS):
@@ -543,9 +544,14 @@ def take_optimizer_precast(dev: torch.device):
                 and t.data_ptr() % 16 == 0 and _pc_key(t) not in _PRECAST):
             del _NEXT_INPUTS[i]
             dst = torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
-            _PRECAST[_pc_key(t)] = (dst, t)
-            return t.reshape(-1), dst.reshape(-1)
+            return t.reshape(-1), dst.reshape(-1), t
     return None
+
+
+def commit_optimizer_precast(cast) -> None:
+    """Register the early cast of :func:`take_optimizer_precast` after its launch succeeded."""
+    src, dst, t = cast
+    _PRECAST[_pc_key(t)] = (dst.view(t.shape), t)
 
 
 def _take_precast(t: torch.Tensor):

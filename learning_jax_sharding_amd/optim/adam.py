@@ -135,7 +135,7 @@ class _Adam:
         """Fused ``update`` + ``apply_updates``: one kernel per shard; in place when donated."""
         st, empty = state
         count = st.count
-        inplace = all(_state.is_donated(t) for t in count.local.values())
+        inplace = all(_state.is_donated(t) for t in dict.values(count.local))
         pl, ptd = T.tree_flatten(params, is_leaf=_is_arr)
         gl = T.tree_leaves(grads, is_leaf=_is_arr)
         ml = T.tree_leaves(st.mu, is_leaf=_is_arr)
@@ -187,6 +187,40 @@ def _grad_local(g: ShardedArray, d: int) -> torch.Tensor:
     return loc[d]
 
 
+class CountLocal(dict):
+    """Local tensors of a step counter whose increments may be deferred inside a multi-step
+    graph capture (ops/hip._defer_step_inc: one count launch per graph).  The next Adam launch
+    adds the pending offset itself and reads the dict raw (``dict.items``); any OTHER read from a
+    jitted function's body -- ``state.step`` folded into an RNG key, an LR schedule -- first
+    launches the pending increments, so in-graph reads see the same count as eager steps."""
+
+    def _flush(self):
+        if _state.in_user_code():
+            from ..ops import hip
+            for t in dict.values(self):
+                hip.flush_step_inc(t)
+        return self
+
+    def __getitem__(self, k):
+        return dict.__getitem__(self._flush(), k)
+
+    def __iter__(self):
+        return dict.__iter__(self._flush())
+
+    def values(self):
+        return dict.values(self._flush())
+
+    def items(self):
+        return dict.items(self._flush())
+
+    def get(self, k, default=None):
+        return dict.get(self._flush(), k, default)
+
+
+def _raw(count: ShardedArray) -> dict:
+    return dict(dict.items(count.local))
+
+
 def _adam_multi_apply(self, pl, gl, ml, vl, count, inplace):
     """MI355X path: every local shard of every param in ONE multi-tensor kernel per device
     (it also refreshes the params' bf16 GEMM shadows).  Returns None to use the per-leaf path."""
@@ -211,14 +245,18 @@ def _adam_multi_apply(self, pl, gl, ml, vl, count, inplace):
                 tp, tm, tv = pt.clone(), mt.clone(), vt.clone()
             new_loc[i][0][d], new_loc[i][1][d], new_loc[i][2][d] = tp, tm, tv
             by_dev.setdefault(d, []).append((tp, _grad_local(g, d), tm, tv))
-    fold = inplace and all(t.dtype == torch.int32 and t.is_cuda for t in count.local.values()) \
-        and set(count.local) == set(by_dev)
+    cl = _raw(count)
+    fold = inplace and all(t.dtype == torch.int32 and t.is_cuda for t in cl.values()) and set(cl) == set(by_dev)
     if fold:
-        new_count = count   # incremented in place by the kernel's last arriving block
+        # incremented in place (one-lane launch, deferred inside a capture); reads of the returned
+        # counter from the jitted body flush the deferred increments first (CountLocal)
+        new_count = ShardedArray((), torch.int32, count.sharding, {})
+        new_count.local = CountLocal(cl)
     else:
-        new_count = ShardedArray((), torch.int32, count.sharding, {d: t + 1 for d, t in count.local.items()})
+        new_count = ShardedArray((), torch.int32, count.sharding, {d: t + 1 for d, t in cl.items()})
+    nl = _raw(new_count)
     for d, entries in by_dev.items():
-        hip.adam_multi(entries, new_count.local[d], self._lr(), self.b1, self.b2, self.eps, self.weight_decay,
+        hip.adam_multi(entries, nl[d], self._lr(), self.b1, self.b2, self.eps, self.weight_decay,
                        increment_step=fold)
     mk = lambda a, loc: ShardedArray(a.shape, a.dtype, a.sharding, loc)  # noqa: E731
     return ([mk(a[0], l[0]) for a, l in zip(arrs, new_loc)], [mk(a[2], l[1]) for a, l in zip(arrs, new_loc)],

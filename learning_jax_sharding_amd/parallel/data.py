@@ -49,6 +49,9 @@ _LAZY_WIRE_GRADS = os.environ.get("LJS_LAZY_WIRE_GRADS", "1") == "1"
 # which the bucket sends instead of casting the f32 buffer itself
 _ACTIVE_WIRE: Optional[torch.dtype] = None
 _TWINS: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+# the gradient buckets of the last backward, in launch order: (bytes on the wire, dtype, groups)
+# -- bench.py's comm_detail reports them
+LAST_BUCKETS: List[Tuple[int, str, Tuple]] = []
 
 
 def active_wire_dtype() -> Optional[torch.dtype]:
@@ -154,6 +157,7 @@ class GradReducer:
         global _ACTIVE_WIRE
         _ACTIVE_WIRE = self.wire_dtype
         _TWINS.clear()
+        LAST_BUCKETS.clear()
         handles = []
         for i, t in enumerate(inputs):
             if self.groups[i] is None:
@@ -212,6 +216,7 @@ class GradReducer:
         from ..spmd import plan as _plan
         _plan.record("all_reduce", groups=tuple(groups), note="grad.bucket", dtype=str(buf.dtype).replace("torch.", ""),
                      bytes_in=buf.numel() * buf.element_size(), overlapped=True)
+        LAST_BUCKETS.append((buf.numel() * buf.element_size(), str(buf.dtype).replace("torch.", ""), tuple(groups)))
         comm = get_comm()
         _, handle = graphs.run_collective(fn, async_=True,
                                           capturable=comm.graph_safe("all_reduce", buf, [tuple(g) for g in groups]),

@@ -150,7 +150,7 @@ class Jitted:
                 if isinstance(l, ShardedArray):
                     donated.update(id(t) for t in l.local.values())
         placed = self._placement(full)
-        with _state.donating(donated), _state.placement(placed):
+        with _state.donating(donated), _state.placement(placed), _state.user_code():
             out = self.fun(*full, **kwargs)
         if self.out_shardings is not None:
             out = _apply_shardings(out, self.out_shardings)
@@ -314,6 +314,8 @@ def reduce_replica_grads(pairs: List[Tuple[ShardedArray, Dict[int, torch.Tensor]
     memory reason to split, and fewer, larger RCCL calls amortise latency on
     point-to-point xGMI rings.
     """
+    from ..parallel import data as _data
+    _data.LAST_BUCKETS.clear()
     out: List[Optional[Dict[int, torch.Tensor]]] = [None] * len(pairs)
     buckets: Dict[Tuple, List[int]] = {}
     for i, (p, g) in enumerate(pairs):
@@ -341,6 +343,9 @@ def reduce_replica_grads(pairs: List[Tuple[ShardedArray, Dict[int, torch.Tensor]
         for chunk in chunks:
             devs = list(pairs[chunk[0]][1].keys())
             flat = {d: torch.cat([pairs[i][1][d].reshape(-1) for i in chunk]) for d in devs}
+            f0 = next(iter(flat.values()))
+            _data.LAST_BUCKETS.append((f0.numel() * f0.element_size(), str(f0.dtype).replace("torch.", ""),
+                                       tuple(groups)))
             red = C.all_reduce(flat, groups, note="grad.replica_sum")
             for d in devs:
                 off = 0

@@ -59,3 +59,17 @@ def donating(tensor_ids):
 def is_donated(t) -> bool:
     s = getattr(_TLS, "donated", None)
     return bool(s) and id(t) in s
+
+
+def in_user_code() -> bool:
+    """True while a jitted function's own body runs (not the jit's argument / output handling)."""
+    return getattr(_TLS, "user", 0) > 0
+
+
+@contextmanager
+def user_code():
+    _TLS.user = getattr(_TLS, "user", 0) + 1
+    try:
+        yield
+    finally:
+        _TLS.user -= 1

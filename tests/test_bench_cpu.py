@@ -32,7 +32,7 @@ def test_bench_json_contract(model):
     assert rec["config"]["parallelism"] == ("fsdp1" if model == "fsdp" else "dp1")
 
 
-@pytest.mark.parametrize("gpus,mesh,par", [(4, "dp", "dp4"), (4, "2d", "dp2xtp2"), (8, "dp", "dp8"),
+@pytest.mark.parametrize("gpus,mesh,par", [(2, "dp", "dp2"), (4, "dp", "dp4"), (4, "2d", "dp2xtp2"), (8, "dp", "dp8"),
                                            (8, "2d", "dp4xtp2")])
 def test_bench_spawns_ranks(gpus, mesh, par):
     """`bench.py --gpus N` outside torchrun launches N rank processes (gloo host ranks here,
@@ -55,9 +55,22 @@ def test_bench_spawns_ranks(gpus, mesh, par):
     # value is the whole-job aggregate (the driver's contract); the per-GPU rate the metric names
     # is tflops_per_gpu = value / n_gpus
     assert abs(rec["value"] - rec["tflops_per_gpu"] * gpus) <= 1e-3 * gpus
+    # which communication ran: backend, paths per collective shape (agreed by every rank), the
+    # gradient buckets and the timed eager all-reduce of their size through each path
+    det = rec["comm_detail"]
+    assert det["backend"] == "gloo" and det["world"] == gpus and det["routes_agree_across_ranks"]
+    assert det["rccl_nranks"] is None          # gloo ranks: no RCCL communicator exists
+    assert det["routes"] and all(r["path"] == "torch-gloo" for r in det["routes"]), det["routes"]
+    assert det["grad_buckets"] and all(b["bytes"] > 0 for b in det["grad_buckets"])
+    probe = {p["path"]: p for p in det["all_reduce_probe"]}
+    assert probe["torch-gloo"]["us_per_call"] > 0 and "skipped" in probe["rccl"] and "skipped" in probe["p2p"]
+    assert probe["torch-gloo"]["bytes"] >= sum(b["bytes"] for b in det["grad_buckets"]) - 16
+    assert det["p2p_fallbacks"] == []
     # the reference's 2-D DP x TP layout is timed in the same job under the default DP mesh
     if mesh == "dp":
         sec = rec["secondary"]
+        assert sec["routes_agree_across_ranks"] and sec["comm_routes"]
+        assert any(r["kind"] in ("all_gather", "all_to_all") for r in sec["comm_routes"])
         assert "error" not in sec, sec
         assert sec["mesh"] == [gpus // 2, 2] and sec["parallelism"] == f"dp{gpus // 2}xtp2"
         assert sec["ms_per_step"] > 0 and sec["comm"].startswith("gloo")
@@ -100,6 +113,27 @@ def test_watchdog_on_fail_hook_reports_and_sets_exit():
         time.sleep(0.01)
     wd.stop()
     assert codes == [0] and seen and "secondary" in seen[0]
+
+
+def test_watchdog_on_fail_none_keeps_nonzero_exit():
+    """bench.py's hook prints the headline and returns None: the watchdog's non-zero EXIT_CODE
+    stands (a run that hung never exits 0), and a deadline lowered by ``phase`` is measured from
+    that phase's own start."""
+    import time
+    from learning_jax_sharding_amd.comm.watchdog import EXIT_CODE, CommWatchdog
+    codes, seen = [], []
+    wd = CommWatchdog(None, timeout_s=100.0, poll_s=0.01, exit_fn=codes.append, grace_s=0.0)
+    wd.on_fail = lambda reason: seen.append(reason)
+    wd.start()
+    time.sleep(0.1)
+    wd.phase("secondary", 0.3)    # shorter than the time already spent in "startup": no false hang
+    time.sleep(0.15)
+    assert not codes
+    t0 = time.time()
+    while not codes and time.time() - t0 < 5:
+        time.sleep(0.01)
+    wd.stop()
+    assert codes == [EXIT_CODE] and seen and "secondary" in seen[0]
 
 
 def test_bench_min_warmup_counts_every_untimed_step():

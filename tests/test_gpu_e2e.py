@@ -160,6 +160,46 @@ def test_jit_graph_multi_step_capture_matches_single_steps(gpu_devices):
         np.testing.assert_array_equal(np.asarray(b), np.asarray(a))
 
 
+def test_jit_graph_multi_step_reads_step_between_steps(gpu_devices):
+    """Inside a G-step graph the Adam count increments are deferred to one launch per graph
+    (ops/hip._defer_step_inc); a step that READS ``state.step`` (an RNG fold, an LR schedule) must
+    still see the count eager steps see: the read launches the pending increments first
+    (optim/adam.CountLocal).  Accumulated reads are compared against eager steps."""
+    gpu_devices(1)
+    import learning_jax_sharding_amd as ljs
+    from learning_jax_sharding_amd import optim
+    from learning_jax_sharding_amd.models import MultiHeadAttention
+    from learning_jax_sharding_amd.training import TrainState
+    model = MultiHeadAttention(640, heads=8, dim_head=64)
+    x = ljs.random.normal(ljs.random.PRNGKey(0), (2, 128, 640))
+
+    def make():
+        params = model.init(ljs.random.PRNGKey(1), x)["params"]
+        return TrainState.create(apply_fn=model.apply, params=params, tx=optim.adam(1e-3))
+
+    def steps3(carry, x):
+        state, acc = carry
+        for _ in range(3):
+            acc = acc + state.step.astype(torch.float32) * 10.0
+            g = ljs.grad(lambda p: model.apply({"params": p}, x).sum())(state.params)
+            state = state.apply_gradients(grads=g)
+        return state, acc + state.step.astype(torch.float32)
+
+    zero = ljs.numpy.asarray(np.zeros((), np.float32))
+    eager = ljs.jit(steps3, donate_argnums=0, capture=False)
+    graph = ljs.jit(steps3, donate_argnums=0, capture=True, warmup_calls=0)
+    se, sg = (make(), zero), (make(), zero)
+    for _ in range(2):   # the first graph call captures, the second replays
+        se = eager(se, x)
+        sg = graph(sg, x)
+    torch.cuda.synchronize()
+    ae, ag = (float(np.asarray(a[1]).reshape(-1)[0]) for a in (se, sg))
+    # per call: 10 * (c + c+1 + c+2) + (c+3) added at c = 0, then c = 3: 33 + 126 = 159
+    assert ae == 159.0, ae
+    assert int(np.asarray(se[0].step)) == 6 and int(np.asarray(sg[0].step)) == 6
+    assert ae == ag, (ae, ag)
+
+
 def test_jit_graph_multi_step_input_cast_prefetch_bit_exact(gpu_devices, monkeypatch):
     """A multi-step graph whose steps register the next step's input (ops/linear.
     prefetch_next_input): the next cast runs in the optimizer launch's extra blocks and the next
