@@ -50,10 +50,10 @@ def parse():
     p.add_argument("--steps", type=int, default=48)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--min-warmup", type=int, default=int(os.environ.get("LJS_BENCH_MIN_WARM", "64")),
-                   help="untimed steps in all before the timed region, at least (the first ~50 steps of a "
-                        "process run ~10 %% slower: --steps 20 --warmup 5 read 0.253-0.262 ms where 64 untimed "
-                        "steps read 0.227-0.238, gpurun_out/r3al, r4m; not the DVFS clock: 160 ms of scratch "
-                        "GEMMs before the warmup changed nothing); the JSON 'warmup' reports the total that ran")
+                   help="untimed steps in all before the timed region, at least: steps ~20-45 of a process run "
+                        "under a measured 8-12 %% clock dip (a power-management transient: the in-kernel clock "
+                        "probe of profiles/r6b_clock_ramp.md) and their kernels 5-7 %% slower; 64 untimed steps put "
+                        "the timed region after it.  The JSON 'warmup' reports the total that ran")
     p.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("LJS_BENCH_BPG", "64")))
     p.add_argument("--seq", type=int, default=256)
     p.add_argument("--dim", type=int, default=640)
@@ -497,9 +497,8 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
         run(max(1, args.warmup))
         warm_run += max(1, args.warmup)
         # untimed: at least --min-warmup steps in all (a fixed count, so every rank runs the
-        # same collectives) - after only W = 5 steps the GPU clock has not ramped: --steps 20
-        # --warmup 5 read 0.255-0.262 ms where --warmup 40 read 0.233-0.237 (gpurun_out/r3al) -
-        # ending in the G-step graph so the timed steps start in its buffers
+        # same collectives) - steps ~20-45 run under a measured clock dip (profiles/
+        # r6b_clock_ramp.md) - ending in the G-step graph so the timed steps start in its buffers
         extra = max(0, args.min_warmup - warm_run)
         if multi is not None and extra % G:
             extra += G - extra % G   # whole G-step graphs: the timed steps start in its buffers
