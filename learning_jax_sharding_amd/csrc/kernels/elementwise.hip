@@ -1171,9 +1171,7 @@ LJS_API int ljs_sum_all(const void* in, int is_bf16, long n, void* out, int out_
     // bench's bf16 output in flight at once: an HBM-latency-bound read otherwise)
     long per = 256L * (is_bf16 ? 8 : 4) * 16;
     int g = grid_for(n, (int)per);
-    static const int cap_env = getenv("LJS_SUM_BLOCKS") ? atoi(getenv("LJS_SUM_BLOCKS")) : 0;  // tuning
-    const int cap = cap_env > 0 && cap_env <= kMaxSumBlocks ? cap_env : kMaxSumBlocks;
-    if (g > cap) g = cap;
+    if (g > kMaxSumBlocks) g = kMaxSumBlocks;
     if (is_bf16)
       hipLaunchKernelGGL(sum_all_ticket_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)in, n, partials,
                          ticket, out, out_bf16);
@@ -1472,6 +1470,8 @@ LJS_API int ljs_step_add(void* step, int n, hipStream_t s) {
 
 // table: n x 16 int64 {p, g, m, v, shadow_t, shadow_n, R, C, g_bf16, gS, qn, sn8, qt, st8, g_ld, g_ss}
 // (see AdamTensor); up to 32 per call
+static int g_adam_rows = 0;
+LJS_API void ljs_adam_set_rows(int rows) { g_adam_rows = rows; }
 LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset, void* ticket, float lr, float b1,
                            float b2, float eps, float wd, const void* cast_src, void* cast_dst, long cast_n,
                            hipStream_t s) {
@@ -1484,8 +1484,8 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   // parameters instead of 330 of 64 rows, which left a ragged second round on 256 CUs (B=8 step
   // 0.0752-0.0753 vs 0.0775-0.0778 ms, B=64 0.1987-0.2007 vs 0.2005-0.2036, x3 interleaved,
   // profiles/r5aj_adam_rows_lines.txt); 64 when a tensor carries MX-fp8 shadows (written by 64-row
-  // tiles only).  LJS_ADAM_ROWS = 16 / 32 / 64 forces the launch's height.
-  static const int rows = getenv("LJS_ADAM_ROWS") ? atoi(getenv("LJS_ADAM_ROWS")) : 0;
+  // tiles only).  ljs_adam_set_rows (16 / 32 / 64; 0 = automatic) forces the launch's height (tests).
+  const int rows = g_adam_rows;
   bool any_mx = false;
   for (int i = 0; i < n; ++i) any_mx = any_mx || table[16 * i + 10] || table[16 * i + 12];
   const int kAdamRows = rows == 16 || rows == 32 || rows == 64 ? rows : (any_mx ? 64 : 32);
@@ -1493,9 +1493,8 @@ LJS_API int ljs_adam_multi(const long* table, int n, void* step, int step_offset
   // the launch's lightest slab gradient gets half-height tiles at r >= 2 (16-row at r >= 4), so
   // its blocks are not the kernel's tail -- W_o's 24 slabs against the QKV weights' 8 at B=64, 12
   // against 4 at B=8 before the weight-gradient pair's joint split counts (B=8 step 0.0805-0.0813
-  // vs 0.0824-0.0827 ms, profiles/r5x_b8_lines.txt).  LJS_ADAM_BALANCE=0: every tile the
-  // launch's height.
-  static const int balance = getenv("LJS_ADAM_BALANCE") ? atoi(getenv("LJS_ADAM_BALANCE")) : 1;
+  // vs 0.0824-0.0827 ms, profiles/r5x_b8_lines.txt).
+  constexpr int balance = 1;
   long gs_min = 0;
   for (int i = 0; i < n; ++i) {
     const long g = table[16 * i + 9];

@@ -983,9 +983,8 @@ hipError_t launch_f8(const F8Args& a, int tiles, hipStream_t s) {
     }
   }
   // plain f32 output (the FF weight gradients): its own instance -- the general kernel's 288
-  // registers (VGPR + AGPR) left one wave per SIMD (LJS_F8_FIX3=0 off)
-  static const int fix3 = getenv("LJS_F8_FIX3") ? atoi(getenv("LJS_F8_FIX3")) : 1;
-  if (fix3 && BM == 128 && NST == 2 && a.flags == 32 && a.bias == nullptr) {
+  // registers (VGPR + AGPR) left one wave per SIMD
+  if (BM == 128 && NST == 2 && a.flags == 32 && a.bias == nullptr) {
     hipLaunchKernelGGL((gemm_mx_fp8_kernel<128, 2, 3>), dim3(tiles), dim3(256), 0, s, a);
     return hipGetLastError();
   }

@@ -37,8 +37,6 @@ struct GemmArgs {
   float* psum;  // LDS-DMA kernels, bf16 out: per (item, wave) sums of the stored values, or null
   const void* res;  // R[b][row][col] at res + b * sR + row * ldr + col (ldr may be 0: one broadcast row)
   long ldr, sR;
-  bf16_t* acopy;    // f32-A kernels: the bf16 rounding of A ([M][K], dense), written by the items of
-                    // batch 0 / tile column 0 (the operand the backward's weight gradient reads)
   const bf16_t* bptr[4];  // flags & kBPtrs (slab mode): batch b's B operand (instead of B + b * sB)
   unsigned long long* trace;  // LJS_GEMM_TRACE builds only: per-wave timestamps (see gemm_trace)
 };
@@ -63,9 +61,6 @@ constexpr int kBPtrs = 4096;
 // slab mode, the block's LAST item: its f32 tile leaves through the (then idle) LDS ring as whole
 // 256-byte rows (16-byte chunk XOR row), not as 64-byte pieces of 16 rows per store instruction
 constexpr int kSlabVst = 8192;
-// slab mode with bf16 slabs: each split's partial sum is rounded to bf16 once (summed in f32 by
-// slab_reduce / the fused Adam) -- half the bytes of f32 slabs written here and read there
-constexpr int kSlabBf16 = 16384;
 
 // Epilogue operand R applied to 8 consecutive output values (after bias / ReLU, f32):
 //   residual add: out = bf16(bf16(v) + bf16(R))   (the unfused "y = dense(x); y + R" in bf16:
@@ -428,46 +423,6 @@ struct DmaTile {
   }
 };
 
-// An f32, k-contiguous operand tile (R rows x BK f32 = 256-byte rows): 1 KiB DMA pieces of 4 rows;
-// 16-byte chunk c of row r lands at chunk c ^ (r & 15) (conflict-free 2 x ds_read_b128 fragment
-// reads: the 16 rows of a lane group hit 16 different chunk positions)
-template <int R, int NW>
-struct DmaTileF32 {
-  static constexpr int PIECES = R * BK * 4 / 1024;
-  static constexpr int PER_WAVE = PIECES / NW;
-  static_assert(PIECES % NW == 0, "pieces must split evenly over the waves");
-  int voff[PER_WAVE];
-
-  __device__ __forceinline__ void init(long ld, int wave, int lane) {
-#pragma unroll
-    for (int i = 0; i < PER_WAVE; ++i) {
-      const int q = wave + NW * i;
-      const int row = 4 * q + (lane >> 4), slot = lane & 15;
-      voff[i] = (int)(((long)row * ld + 4 * (slot ^ (row & 15))) * 4);
-    }
-  }
-
-  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, bf16_t* lds, int soff, int wave) const {
-#pragma unroll
-    for (int i = 0; i < PER_WAVE; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_PTR(void))(lds + (wave + NW * i) * 512), 16, voff[i], soff,
-                                               0, 0);
-  }
-};
-
-// bf16 MFMA operand (8 consecutive k of row rb + lane & 15, k-step ks) from an f32 image, rounded
-// to nearest-even exactly like cast_f32_bf16
-__device__ __forceinline__ bf16x8 frag_f32(const bf16_t* lds, int rb, int ks, int lane) {
-  const int row = rb + (lane & 15);
-  const int kc = ks * 4 + (lane >> 4);
-  const unsigned char* base = reinterpret_cast<const unsigned char*>(lds) + row * 256;
-  const f32x4 lo = *reinterpret_cast<const f32x4*>(base + (((2 * kc) ^ (row & 15)) << 4));
-  const f32x4 hi = *reinterpret_cast<const f32x4*>(base + (((2 * kc + 1) ^ (row & 15)) << 4));
-  const u32x4 u = u32x4{pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
-                        pack_bf16x2(hi[2], hi[3])};
-  return __builtin_bit_cast(bf16x8, u);
-}
-
 struct WorkItem {
   int b, m0, n0, kt0, split;
 };
@@ -506,27 +461,16 @@ constexpr int kSC1 = 16;  // buffer-instruction cache policy bit: sc1 (gfx940-fa
 // (a 4-wave kernel whose LDS ring lets two blocks share a CU is told so: the pipelined main loop's
 // second fragment set and the epilogue registers would otherwise push VGPR + AGPR past 256 and
 // halve the resident blocks)
-// AF32: A is f32 (k-contiguous) -- the activation cast fused into the GEMM -- and the items of
-// batch 0 / tile column 0 also write A's bf16 rounding (p.acopy) for the backward.  1: an f32
-// LDS image (LDS-DMA), rounded at the fragment read; 2: register-staged -- each wave loads its
-// pieces of the next-but-two K-tile's A as f32 into VGPRs (global -> VGPR), and one K-tile later
-// rounds them and writes the bf16 image the LDS-DMA would have written (same swizzle), so the
-// ring, the fragment reads and the MFMA loop are the bf16 kernel's.
 // (the body of gemm_dma_kernel; `bid` / `G` are the block's index and the grid as far as this
 // GEMM is concerned -- a grouped launch, gemm_dma_group2_kernel, runs two GEMMs' items in one grid)
-template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0, int AF32 = 0>
+template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0>
 __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, const int G) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-  static_assert(!AF32 || A_KC, "f32 A is k-contiguous");
-  constexpr bool AIMG32 = AF32 == 1, AREG = AF32 == 2;
-  constexpr int A_TILE = BM * BK * (AIMG32 ? 2 : 1), B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
-  using TA = typename std::conditional<AIMG32, DmaTileF32<BM, NW>, DmaTile<BM, A_KC, NW>>::type;
+  constexpr int A_TILE = BM * BK, B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
+  using TA = DmaTile<BM, A_KC, NW>;
   using TB = DmaTile<BN, B_KC, NW>;
-  // vector-memory instructions per wave per K-tile (register-staged A: two 16-byte f32 loads
-  // per bf16 DMA piece)
-  constexpr int LA = AREG ? 2 * TA::PER_WAVE : TA::PER_WAVE;
-  constexpr int L = LA + TB::PER_WAVE;
+  constexpr int L = TA::PER_WAVE + TB::PER_WAVE;   // vector-memory instructions per wave per K-tile
   // Operands swapped (C^T = B^T A^T per 16x16 block): each lane ends with 4 CONSECUTIVE
   // columns of one output row.  bf16 output: lanes pair up into 16-byte row chunks and leave
   // through exactly S_EPI buffer stores per lane (masked lanes get an out-of-range offset, so
@@ -569,7 +513,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
 #endif
   stamp();
 
-  constexpr int AES = AF32 ? 4 : 2;  // A element bytes
+  constexpr int AES = 2;  // A element bytes
   const long a_bytes = AES * (A_KC ? (long)(p.M - 1) * p.lda + p.K : (long)(p.K - 1) * p.lda + p.M);
   const long b_bytes = 2 * (B_KC ? (long)(p.N - 1) * p.ldb + p.K : (long)(p.K - 1) * p.ldb + p.N);
   const long a_kt = A_KC ? (long)BK * AES : (long)BK * p.lda * 2;  // bytes per K-tile step
@@ -586,43 +530,6 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
   __amdgpu_buffer_rsrc_t ra, rb;
   int a_off = 0, b_off = 0;
   const int a_step = (int)a_kt, b_step = (int)b_kt;
-  // register-staged A (AREG): the loaded f32 pieces of one K-tile, the stage they go to, and the
-  // wave's vector-memory instructions issued after them (the counted wait before their rounding)
-  // The bf16 copy of A for the backward (p.acopy, [M][K]) leaves from the same registers: K-tile
-  // kt of a row block by its item j = b * ntn + n0 with kt % (batch * ntn) == j, so the copy is
-  // shared out over the row block's items (no f32 re-read).  Those stores are counted into the
-  // next K-tile wait (ac_x); masked rows get an out-of-range offset so the count is exact.
-  f32x4 areg[AREG ? 2 * TA::PER_WAVE : 1];
-  int a_pend = -1, a_young = 0, ac_x = 0;
-  int it_row0 = 0, it_kt0 = 0, it_j = 0;          // the issue-side item's row origin, K-tile, index
-  bool a_cp = false;
-  int a_cp_row0 = 0, a_cp_k0 = 0;
-  const int acJ = p.batch * ntn;
-  __amdgpu_buffer_rsrc_t rac;
-  if constexpr (AREG) rac = make_rsrc(p.acopy, p.acopy ? 2L * p.M * p.K : 0);
-  auto a_commit = [&]() {
-    if constexpr (AREG) {
-      if (a_pend < 0) return;
-      wait_vm_n(a_young);
-      bf16_t* base = smem + a_pend * STAGE;
-#pragma unroll
-      for (int i = 0; i < TA::PER_WAVE; ++i) {
-        const f32x4 lo = areg[2 * i], hi = areg[2 * i + 1];
-        const u32x4 v = u32x4{pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
-                              pack_bf16x2(hi[2], hi[3])};
-        *reinterpret_cast<u32x4*>(base + (wave + NW * i) * 512 + lane * 8) = v;
-        if (a_cp) {
-          const int row = 8 * (wave + NW * i) + (lane >> 3), slot = lane & 7;
-          const int grow = a_cp_row0 + row;
-          const int off = grow < p.M ? (int)(((long)grow * p.K + a_cp_k0 + 8 * (slot ^ ((row >> 1) & 7))) * 2)
-                                     : 0x7ffffff0;
-          __builtin_amdgcn_raw_buffer_store_b128(v, rac, off, 0, 0);
-        }
-      }
-      if (a_cp) ac_x += TA::PER_WAVE;
-      a_pend = -1;
-    }
-  };
   auto load_item = [&](int k) {
     const WorkItem w = decode_item(p, slot + G * k, ntm, ntn);
     ra = make_rsrc(reinterpret_cast<const unsigned char*>(p.A) + (long)w.b * p.sA * AES, a_bytes);
@@ -631,36 +538,9 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
         (int)((A_KC ? (long)w.m0 * BM * p.lda : (long)w.m0 * BM) * AES + w.kt0 * a_kt));
     b_off = __builtin_amdgcn_readfirstlane(
         (int)((B_KC ? (long)w.n0 * BN * p.ldb : (long)w.n0 * BN) * 2 + w.kt0 * b_kt));
-    if constexpr (AREG) {
-      it_row0 = w.m0 * BM;
-      it_kt0 = w.kt0;
-      it_j = w.b * ntn + w.n0;
-    }
   };
-  // A's pieces of the next K-tile: LDS-DMA, or (AREG) f32 loads into areg after rounding the
-  // pending ones into their stage
-  auto issue_a = [&](int st) {
-    if constexpr (AREG) {
-      a_commit();
-#pragma unroll
-      for (int i = 0; i < TA::PER_WAVE; ++i) {
-        areg[2 * i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, 2 * ta.voff[i], a_off, 0));
-        areg[2 * i + 1] =
-            __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, 2 * ta.voff[i] + 16, a_off, 0));
-      }
-      a_pend = st;
-      a_young = 0;
-      a_cp = p.acopy != nullptr && (it_kt0 + is_kt) % acJ == it_j;
-      a_cp_row0 = it_row0;
-      a_cp_k0 = (it_kt0 + is_kt) * BK;
-    } else {
-      ta.issue(ra, smem + st * STAGE, a_off, wave);
-    }
-  };
-  auto issue_b = [&](int st) {
-    tb.issue(rb, smem + st * STAGE + A_TILE, b_off, wave);
-    if constexpr (AREG) a_young += TB::PER_WAVE;
-  };
+  auto issue_a = [&](int st) { ta.issue(ra, smem + st * STAGE, a_off, wave); };
+  auto issue_b = [&](int st) { tb.issue(rb, smem + st * STAGE + A_TILE, b_off, wave); };
   auto issue_next = [&](int st) {
     if (is_kt == 0) load_item(is_item);
     issue_a(st);
@@ -708,9 +588,8 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
   const bool psum_on = !OUT_F32 && !PLAIN && p.psum != nullptr;
   float tsum = 0.f;
   const bool slabs = OUT_F32 && (PLAIN || (p.flags & kSlabs));  // (f32 PLAIN: slab mode only)
-  const bool slab16 = !PLAIN && slabs && (p.flags & kSlabBf16);
   const __amdgpu_buffer_rsrc_t rc = make_rsrc(
-      p.C, (OUT_F32 && !slab16 ? 4 : 2) *
+      p.C, (OUT_F32 ? 4 : 2) *
                ((long)((slabs ? p.splitk * p.batch : p.batch) - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
   bool after_epi = false;
 
@@ -720,11 +599,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
   auto wait_landed = [&](int g) {
     stamp();
     const bool tail = g + NST - 2 >= total;
-    if constexpr (AREG) {
-      // the register-staged A's bf16-copy stores (ac_x) are younger than this tile's B pieces too
-      wait_vm_n(tail ? 0 : L * (NST - 2) + (after_epi ? S_EPI + (psum_on ? 1 : 0) : 0) + ac_x);
-      ac_x = 0;
-    } else if constexpr (NST >= 3) {
+    if constexpr (NST >= 3) {
       if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else if (SWAP && after_epi && psum_on)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2) + S_EPI + 1) : "memory");
@@ -750,10 +625,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
     const bf16_t* As_ = smem + (g % NST) * STAGE;
     const bf16_t* Bs_ = As_ + A_TILE;
 #pragma unroll
-    for (int ii = 0; ii < TM; ++ii) {
-      if constexpr (AIMG32) af[ii] = frag_f32(As_, wr * (BM / WM) + ii * 16, ks, lane);
-      else af[ii] = frag<BM, A_KC>(As_, wr * (BM / WM) + ii * 16, ks, lane);
-    }
+    for (int ii = 0; ii < TM; ++ii) af[ii] = frag<BM, A_KC>(As_, wr * (BM / WM) + ii * 16, ks, lane);
 #pragma unroll
     for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, B_KC>(Bs_, wc * (BN / WN) + j * 16, ks, lane);
   };
@@ -793,18 +665,13 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
   // (one 8-wave block per CU has 256 VGPRs per wave: 10 fragments fit twice beside 24 accumulators)
   // (one 4-wave block per CU -- the wide wave tiles 128x64 .. 128x128 -- has 512 registers per
   // wave: both fragment sets fit beside up to 256 accumulators)
-  constexpr bool ONE_PER_CU = !(NW == 4 && NST * ((AIMG32 ? 2 : 1) * BM + BN) * 64 * 2 <= 80 * 1024);
+  constexpr bool ONE_PER_CU = !(NW == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024);
   constexpr bool PIPE = (TM + TN <= 8 || (NW == 8 && TM + TN <= 10) || (NW == 4 && ONE_PER_CU && TM + TN <= 16)) &&
                         A_KC && B_KC;   // (the last clause: 4-wave wide wave tiles, none instantiated since r5b)
-  static_assert(!AREG || (PIPE && !OUT_F32 && RES == 0), "register-staged A: the pipelined bf16-output loop");
-  if constexpr (AREG) {
-    if (total == 1) a_commit();   // (tile 0 rounded into its stage before its barrier)
-  }
   if (PIPE && total > 0) {
     wait_landed(0);
     read_frags(0, 0, ka, kb);
     if (NST - 1 < total) issue_next((NST - 1) % NST);
-    else a_commit();
   }
 
   for (int it = 0, f = 0; it < my_items; ++it) {
@@ -835,7 +702,6 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
       wait_landed(f + 1);
       read_frags(f + 1, 0, ka, kb);
       if (more) issue_half(f % NST, false);
-      else a_commit();   // (AREG: the last loaded K-tile still goes to its stage)
     }
     mfmas(la, lb);
     if (more) issue_half(f % NST, true);
@@ -845,29 +711,6 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
     const WorkItem w = decode_item(p, slot + G * it, ntm, ntn);
     const int m0 = w.m0 * BM + wr * (BM / WM), n0 = w.n0 * BN + wc * (BN / WN);
     const int g = lane >> 4;
-    if constexpr (AIMG32) {
-      // this row block's bf16 A for the backward (re-read from L2 where the DMA just streamed
-      // it), shared out by K-tile over the row block's batch x column items (item j copies
-      // K-tiles j, j + J, ...), so no item carries the whole row block's copy and the round's
-      // blocks finish together; drained before the epilogue so the counted waits below stay exact
-      const int J = p.batch * ntn, j = w.b * ntn + w.n0, nkt_all = p.K / BK;
-      if (p.acopy && j < nkt_all) {
-        const float* A32 = reinterpret_cast<const float*>(p.A);
-        const int my_kt = (nkt_all - j + J - 1) / J;
-        for (int c = tid; c < BM * 8 * my_kt; c += WM * WN * 64) {
-          const int t = c / (BM * 8), r8 = c - t * (BM * 8), row = r8 >> 3;
-          const int k = (j + t * J) * BK + (r8 & 7) * 8, grow = w.m0 * BM + row;
-          if (grow < p.M) {
-            const f32x4 lo = *reinterpret_cast<const f32x4*>(A32 + (long)grow * p.lda + k);
-            const f32x4 hi = *reinterpret_cast<const f32x4*>(A32 + (long)grow * p.lda + k + 4);
-            *reinterpret_cast<u32x4*>(p.acopy + (long)grow * p.K + k) =
-                u32x4{pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
-                      pack_bf16x2(hi[2], hi[3])};
-          }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
     if constexpr (!OUT_F32) {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]; lanes g, g^1 trade halves so
       // even g owns cols 16 j0 + 4 g .. +7 and odd g owns 16 j1 + 4 (g - 1) .. +7
@@ -976,7 +819,6 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
         tsum = 0.f;
       }
       after_epi = true;
-      if constexpr (AREG) a_young += S_EPI + (psum_on ? 1 : 0);
     } else {
       // lane holds C[16 ii + (lane & 15)][16 j + 4 g + 0..3]
       const bool vec = (p.ldc & 3) == 0 && (p.sC & 3) == 0 && ((((uintptr_t)p.C) & 15) == 0);
@@ -1000,18 +842,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
             const int r = 4 * q + (lane >> 4), c = lane & 15;
             const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + ((c ^ (r & 7)) << 4));
             const int row = m0 + r, col = n0 + 4 * c;
-            if (slab16) {
-              const u32x2 h = u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-              if (row < p.M && col + 4 <= p.N) {
-                __builtin_amdgcn_raw_buffer_store_b64(h, rc, (int)((cb + (long)row * p.ldc + col) * 2), 0, 0);
-              } else if (row < p.M) {
-                bf16_t* C = reinterpret_cast<bf16_t*>(p.C) + cb + (long)row * p.ldc + col;
-                const float f[4] = {v[0], v[1], v[2], v[3]};
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                  if (col + e < p.N) C[e] = f2bf(f[e]);
-              }
-            } else if (row < p.M && col + 4 <= p.N) {
+            if (row < p.M && col + 4 <= p.N) {
               const u32x4 bits = __builtin_bit_cast(u32x4, v);
               __builtin_amdgcn_raw_buffer_store_b128(bits, rc, (int)((cb + (long)row * p.ldc + col) * 4), 0, 0);
             } else if (row < p.M) {
@@ -1051,18 +882,6 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
           }
           acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           if (row >= p.M || col >= p.N) continue;
-          if (slab16) {
-            bf16_t* C16 = reinterpret_cast<bf16_t*>(p.C) + cb + (long)row * p.ldc + col;
-            if (vec && col + 4 <= p.N) {
-              const u32x2 h = u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-              __builtin_amdgcn_raw_buffer_store_b64(h, rc, (int)((cb + (long)row * p.ldc + col) * 2), 0, 0);
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                if (col + e < p.N) C16[e] = f2bf(v[e]);
-            }
-            continue;
-          }
           float* C = reinterpret_cast<float*>(p.C) + cb + (long)row * p.ldc + col;
           if (p.splitk > 1 && !slabs) {
 #pragma unroll
@@ -1091,17 +910,15 @@ __device__ __forceinline__ void gemm_dma_body(const GemmArgs& p, const int bid, 
       wait_landed(f);
       read_frags(f, 0, ka, kb);
       if (f + NST - 1 < total) issue_next((f + NST - 1) % NST);
-      else a_commit();
     }
   }
   stamp_end();
 }
 
-template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0, int AF32 = 0>
-__global__ __launch_bounds__(WM * WN * 64,
-                            (WM * WN == 4 && NST * ((AF32 == 1 ? 2 : 1) * BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
+template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OUT_F32, int RES = 0>
+__global__ __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
 gemm_dma_kernel(GemmArgs p) {
-  gemm_dma_body<BM, BN, WM, WN, NST, A_KC, B_KC, OUT_F32, RES, AF32>(p, blockIdx.x, gridDim.x);
+  gemm_dma_body<BM, BN, WM, WN, NST, A_KC, B_KC, OUT_F32, RES>(p, blockIdx.x, gridDim.x);
 }
 
 // Two GEMMs of the same kernel instance in ONE grid, one block per work item: blocks [0, g0) take
@@ -1112,9 +929,9 @@ template <int BM, int BN, int WM, int WN, int NST, bool A_KC, bool B_KC, bool OU
 __global__ __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
 gemm_dma_group2_kernel(GemmArgs p0, GemmArgs p1, int g0) {
   if ((int)blockIdx.x < g0)
-    gemm_dma_body<BM, BN, WM, WN, NST, A_KC, B_KC, OUT_F32, RES, 0>(p0, blockIdx.x, g0);
+    gemm_dma_body<BM, BN, WM, WN, NST, A_KC, B_KC, OUT_F32, RES>(p0, blockIdx.x, g0);
   else
-    gemm_dma_body<BM, BN, WM, WN, NST, A_KC, B_KC, OUT_F32, RES, 0>(p1, blockIdx.x - g0, gridDim.x - g0);
+    gemm_dma_body<BM, BN, WM, WN, NST, A_KC, B_KC, OUT_F32, RES>(p1, blockIdx.x - g0, gridDim.x - g0);
 }
 
 // ============================================================================ lean K-loop GEMM
@@ -1463,16 +1280,13 @@ LJS_LEAN_INST(128, 128, 2, 4, 3)
 LJS_LEAN_INST(128, 128, 2, 4, 4)
 LJS_LEAN_INST(64, 64, 2, 2, 4)
 #undef LJS_LEAN_INST
-// f32-A (cast-on-load) forward GEMMs: 128x128, 8 waves, 3 stages (144 KiB with the f32 A image)
-template __global__ void gemm_dma_kernel<128, 128, 2, 4, 3, true, true, false, 0, 1>(GemmArgs);
-template __global__ void gemm_dma_kernel<256, 128, 4, 2, 3, true, true, false, 0, 2>(GemmArgs);
 #undef LJS_DMA_INST_LAYOUTS
 #undef LJS_DMA_INST
 
 int g_cus = 0;
 unsigned long long* g_gemm_trace = nullptr;  // LJS_GEMM_TRACE builds: the next LDS-DMA launches' stamps
 
-template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF, int RES = 0, int AF32 = 0>
+template <int BM, int BN, int WM, int WN, int NST, bool AK, bool BKc, bool OF, int RES = 0>
 hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   if (!g_cus) {
     int dev = 0;
@@ -1482,24 +1296,22 @@ hipError_t launch_dma(const GemmArgs& a, hipStream_t s, int blocks_per_cu) {
   }
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   const int items = ntm * ntn * a.batch * a.splitk;
-  static const int order_env = getenv("LJS_GEMM_ORDER") ? atoi(getenv("LJS_GEMM_ORDER")) : 1;
   GemmArgs a2 = a;
   a2.trace = g_gemm_trace;
-  if (order_env && ntm < ntn) a2.flags |= kMFast;
-  static const int bpc_env = getenv("LJS_DMA_BPC") ? atoi(getenv("LJS_DMA_BPC")) : 0;  // tuning override
+  if (ntm < ntn) a2.flags |= kMFast;   // narrow dimension fastest: tiles sharing a panel run together
   // blocks_per_cu 0 = one block per work item (measured best at the bench shapes: the
   // dispatcher balances), else a persistent grid of blocks_per_cu x CUs
-  int bpc = bpc_env > 0 ? bpc_env : blocks_per_cu;
+  int bpc = blocks_per_cu;
   // Persistent grid when the items fill whole rounds of the resident slots: each block then
   // walks `rounds` items with the next item's first K-tiles in flight during the current
   // item's epilogue (measured at T = 16384: QKV projection 43.8 -> 39.9 us on 128x128 x 2/CU).
   // Otherwise one block per item, which lets the dispatcher balance a ragged last round.
-  constexpr int kLdsBytes = NST * ((AF32 == 1 ? 2 : 1) * BM + BN) * BK * 2;
+  constexpr int kLdsBytes = NST * (BM + BN) * BK * 2;
   constexpr int kNatural = (WM * WN == 4 && kLdsBytes <= 80 * 1024) ? 2 : 1;  // resident blocks / CU
-  if (bpc == 0 && bpc_env == 0 && items > g_cus * kNatural && items % (g_cus * kNatural) == 0) bpc = kNatural;
+  if (bpc == 0 && items > g_cus * kNatural && items % (g_cus * kNatural) == 0) bpc = kNatural;
   int grid = bpc > 0 ? g_cus * bpc : items;
   if (grid > items) grid = items;
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, NST, AK, BKc, OF, RES, AF32>), dim3(grid), dim3(WM * WN * 64), 0,
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, NST, AK, BKc, OF, RES>), dim3(grid), dim3(WM * WN * 64), 0,
                      s, a2);
   return hipGetLastError();
 }
@@ -1511,13 +1323,11 @@ hipError_t launch_dma_kk(const GemmArgs& a, hipStream_t s) {
     if (a.flags & kResF32) return launch_dma<BM, BN, WM, WN, NST, true, true, false, 2>(a, s, 0);
     return launch_dma<BM, BN, WM, WN, NST, true, true, false, 1>(a, s, 0);
   }
-  // plain epilogue (RES 3): LJS_GEMM_PLAIN=0 keeps the general kernel
-  static const int plain_env = getenv("LJS_GEMM_PLAIN") ? atoi(getenv("LJS_GEMM_PLAIN")) : 1;
-  if (plain_env && a.alpha == 1.f && !(a.flags & 3) && !a.psum)
+  // plain epilogue (RES 3: compile-time instance, PERF_NOTES r4 "plain instance")
+  if (a.alpha == 1.f && !(a.flags & 3) && !a.psum)
     return launch_dma<BM, BN, WM, WN, NST, true, true, false, 3>(a, s, 0);
   // bias (f32) + optional fused sum, alpha 1, no ReLU (RES 4)
-  static const int bsum_env = getenv("LJS_GEMM_BSUM") ? atoi(getenv("LJS_GEMM_BSUM")) : 1;
-  if (plain_env && bsum_env && a.alpha == 1.f && (a.flags & 7) == 6 && a.splitk == 1)
+  if (a.alpha == 1.f && (a.flags & 7) == 6 && a.splitk == 1)
     return launch_dma<BM, BN, WM, WN, NST, true, true, false, 4>(a, s, 0);
   return launch_dma<BM, BN, WM, WN, NST, true, true, false, 0>(a, s, 0);
 }
@@ -1539,19 +1349,17 @@ template <int BM, int BN>
 GemmArgs group_prep(const GemmArgs& a, int* items) {
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   *items = ntm * ntn * a.batch * a.splitk;
-  static const int order_env = getenv("LJS_GEMM_ORDER") ? atoi(getenv("LJS_GEMM_ORDER")) : 1;
   GemmArgs a2 = a;
   a2.trace = nullptr;
-  if (order_env && ntm < ntn) a2.flags |= kMFast;
+  if (ntm < ntn) a2.flags |= kMFast;
   return a2;
 }
 
 // weight-gradient (m/n-contiguous, f32 output) launch: the plain split-K slab instance (RES 3)
-// when the slabs are f32 and nothing else is asked for (LJS_GEMM_PLAIN=0: the general kernel)
+// when the slabs are f32 and nothing else is asked for
 template <int BM, int BN, int WM, int WN, int NST>
 hipError_t launch_slab(const GemmArgs& a, hipStream_t s) {
-  static const int plain_env = getenv("LJS_GEMM_PLAIN") ? atoi(getenv("LJS_GEMM_PLAIN")) : 1;
-  if (plain_env && (a.flags & kSlabs) && !(a.flags & (kSlabBf16 | 1 | 2 | 8 | 16)) && a.alpha == 1.f) {
+  if ((a.flags & kSlabs) && !(a.flags & (1 | 2 | 8 | 16)) && a.alpha == 1.f) {
     constexpr int kind = (BM == 128 && BN == 128 && WM == 2 && WN == 2 && NST == 2)   ? 1
                          : (BM == 128 && BN == 128 && WM == 2 && WN == 4 && NST == 4) ? 2
                          : (BM == 128 && BN == 128 && WM == 2 && WN == 4 && NST == 3) ? 3
@@ -1596,9 +1404,8 @@ hipError_t launch_lean(const GemmArgs& a, hipStream_t s) {
   }
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   const int items = ntm * ntn * a.batch;
-  static const int order_env = getenv("LJS_GEMM_ORDER") ? atoi(getenv("LJS_GEMM_ORDER")) : 1;
   GemmArgs a2 = a;
-  if (order_env && ntm < ntn) a2.flags |= kMFast;
+  if (ntm < ntn) a2.flags |= kMFast;
   constexpr int kLdsBytes = NST * (BM + BN) * BK * 2;
   constexpr int kNatural = (WM * WN == 4 && kLdsBytes <= 80 * 1024) ? 2 : 1;
   int grid = items;
@@ -1641,7 +1448,6 @@ hipError_t dispatch_layout(const GemmArgs& a, int a_kc, int b_kc, int out_f32, h
 // Returns 0 on success.  Preconditions checked here (the Python wrapper checks them too):
 // K % 8 == 0; for an m/n-contiguous operand its M (or N) % 8 == 0; 16-byte aligned bases
 // and leading dimensions that are multiples of 8 elements.
-constexpr int kAF32 = 2048;  // A is f32 (k-contiguous): rounded to bf16 in the GEMM (acopy: its bf16 copy)
 
 // LJS_GEMM_TRACE builds: the LDS-DMA launches that follow write their per-wave timelines to
 // `buf` (blocks x waves x kTraceSlots u64, zeroed by the caller); null turns it off.  Returns
@@ -1678,8 +1484,7 @@ LJS_API int ljs_gemm_set_trace(void* buf) {
 LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
                           long lda, long ldb, long ldc, long sA, long sB, long sC, long sBias, int batch,
                           int a_kc, int b_kc, int out_f32, int flags, float alpha, int splitk, int tile,
-                          void* psum, int* psum_count, const void* res, long ldr, long sR, void* acopy,
-                          hipStream_t stream) {
+                          void* psum, int* psum_count, const void* res, long ldr, long sR, hipStream_t stream) {
   if (K % 8 || (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
   if (splitk > 1 && !out_f32) return (int)hipErrorInvalidValue;
   // the epilogue operand applies to bf16 outputs (its 16-byte loads need aligned 8-column chunks)
@@ -1701,7 +1506,6 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   a.res = res;
   a.ldr = ldr;
   a.sR = sR;
-  a.acopy = (bf16_t*)acopy;
   a.trace = nullptr;
   if (flags & kBPtrs) {
     // B is a HOST array of `batch` (<= 4) device pointers, one B operand per batch
@@ -1712,23 +1516,6 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   } else {
     for (int i = 0; i < 4; ++i) a.bptr[i] = nullptr;
   }
-  if (flags & kAF32) {
-    // f32 A: the 8-wave 128x128 LDS-DMA kernel only (bf16 output, k-contiguous operands, no
-    // split, no epilogue operand / fused sum); every condition is the caller's to meet
-    if (!a_kc || !b_kc || out_f32 || splitk > 1 || (flags & (kResAdd | kResMask | 8 | 16)) || psum || K % 64 ||
-        lda % 4 || N % 8 || ldc % 8 || (((uintptr_t)A) & 15) || (acopy && (sA != 0 && batch > 1)) ||
-        (long)M * lda * 4 >= (1L << 31) || (long)N * ldb >= (1L << 30))
-      return (int)hipErrorInvalidValue;
-    a.kt_per_split = K / 64;
-    a.splitk = 1;
-    a.flags = flags & ~kAF32;
-    // 2561: the 256x128 8-wave kernel with A register-staged (global f32 -> VGPR -> bf16 LDS
-    // image); else the 8-wave 128x128 kernel over an f32 LDS image
-    if (tile == 2561 && (long)M * lda * 4 < (1L << 30))
-      return (int)launch_dma<256, 128, 4, 2, 3, true, true, false, 0, 2>(a, stream, 0);
-    return (int)launch_dma<128, 128, 2, 4, 3, true, true, false, 0, 1>(a, stream, 0);
-  }
-
   if (psum_count) *psum_count = 0;
   // A/B: tile code + 100000 forces the lean K-loop kernel where it applies, + 200000 the general one
   const bool gen_req = tile >= 200000;
@@ -1796,9 +1583,8 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch * a.splitk * nw;
   }
   // the lean K-loop kernel for the k-contiguous bf16-output LDS-DMA tiles without split-K
-  // (LJS_GEMM_LEAN=0: the general kernel; tile code + 100000 forces the lean one for A/B)
-  static const int lean_env = getenv("LJS_GEMM_LEAN") ? atoi(getenv("LJS_GEMM_LEAN")) : 1;
-  if ((lean_env || lean_req) && !gen_req && a_kc && b_kc && !out_f32 && a.splitk == 1 && !(flags & kBPtrs) && dma_ok &&
+  // (tile code + 100000 forces the lean one, + 200000 the general one: A/B and bit-exact tests)
+  if (!gen_req && a_kc && b_kc && !out_f32 && a.splitk == 1 && !(flags & kBPtrs) && dma_ok &&
       dma_store_ok) {
     if (tile == 2561) return (int)launch_lean_kk<256, 128, 4, 2, 3>(a, stream);
     if (tile == 2562) return (int)launch_lean_kk<256, 192, 4, 2, 2>(a, stream);

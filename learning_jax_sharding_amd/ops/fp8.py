@@ -25,7 +25,6 @@ import os
 import torch
 
 from . import hip
-from . import streams as _streams
 from .linear import _Linear, _bf16, _inv_perm
 
 __all__ = ["quantize_mx_ref", "dequantize_mx_ref", "mx_linear_ref", "quant_rows", "quant_cols", "gemm_mx",
@@ -212,8 +211,8 @@ def gemm_mx(qa, sa, qb, sb, M: int, N: int, K: int, out: Optional[torch.Tensor],
 # tile for the N=640 GEMMs of the FF block (down projection + residual 42.9 vs 53.2 us, dX 36.0
 # vs 49.0 us: one round of 256 tiles, a third fewer bytes per FLOP); the epilogue-heavy K=640
 # GEMMs (up projection / dA with both MX copies) stay on the 4-wave 128x128 kernel, whose two
-# blocks per CU overlap one block's epilogue with the other's K-loop.  LJS_F8_AUTO=0: always 1282.
-_F8_AUTO = os.environ.get("LJS_F8_AUTO", "1") == "1"
+# blocks per CU overlap one block's epilogue with the other's K-loop.
+_F8_AUTO = True
 
 
 def _auto_tile(M: int, N: int, K: int, flags: int, nsplit: int) -> int:
@@ -225,7 +224,7 @@ def _auto_tile(M: int, N: int, K: int, flags: int, nsplit: int) -> int:
     return 0
 
 
-_F8_N640_TILE = int(os.environ.get("LJS_F8_N640_TILE", "256160"))
+_F8_N640_TILE = 256160
 
 
 class _Fp8Linear(torch.autograd.Function):
@@ -377,7 +376,7 @@ def _quant_both(x2: torch.Tensor):
 
 # upper bound on the split count (tuning / A/B: each split is one more f32 slab that the fused Adam
 # or the slab reduction reads back)
-_MX_SPLIT_MAX = int(os.environ.get("LJS_MX_WGRAD_SPLIT_MAX", "64"))
+_MX_SPLIT_MAX = 64
 
 
 def _pick_split(tiles: int, nkt: int) -> int:
@@ -522,7 +521,7 @@ class _FFBlockFp8(torch.autograd.Function):
         return out.get("dx"), out.get("wi"), out.get("wo"), dres
 
 
-_FUSED_COLSUM = os.environ.get("LJS_F8_FUSED_COLSUM", "1") == "1"
+_FUSED_COLSUM = True
 
 
 def _lazy_rows_sum(cs: torch.Tensor):

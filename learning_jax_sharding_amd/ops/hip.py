@@ -33,7 +33,7 @@ _SIGS = {
     "ljs_gemm_group_end": [c_void_p],
     "ljs_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long,
                       c_long, c_long, c_long, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p,
-                      ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p, c_void_p],
+                      ctypes.POINTER(c_int), c_void_p, c_long, c_long, c_void_p],
     "ljs_sum_partials": [c_void_p, c_int, c_void_p, c_int, c_void_p],
     "ljs_mse_colsum_ws_bytes": [c_int, c_int],
     "ljs_gemm_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long,
@@ -68,6 +68,7 @@ _SIGS = {
     "ljs_adam_multi": [_LP, c_int, c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_float,
                        c_void_p, c_void_p, c_long, c_void_p],
     "ljs_step_add": [c_void_p, c_int, c_void_p],
+    "ljs_adam_set_rows": [c_int],
     "ljs_clock_probe": [c_void_p, c_void_p, c_uint, c_uint, c_void_p],
     "ljs_mse_loss": [c_void_p, c_void_p, c_int, c_long, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "ljs_mse_colsum": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -99,7 +100,8 @@ def lib():
 
 def set_attention_fwd_resident(waves: int):
     """Forward kernel for key lengths <= 256: 0 = tiled (K/V tiles through registers), 4 or 8 =
-    K/V-resident (whole K/V of a head in LDS by one LDS-DMA burst; waves x 16 queries per block)."""
+    K/V-resident (whole K/V of a head in LDS by one LDS-DMA burst; waves x 16 queries per block),
+    -1 = the default (8, or 4 below 256 blocks)."""
     fn = lib().ljs_attn_set_fwd_res
     fn.argtypes = [c_int]
     fn.restype = None
@@ -108,8 +110,8 @@ def set_attention_fwd_resident(waves: int):
 
 def set_attention_bwd_kv_dma(enabled: Optional[bool]):
     """Fused short-key backward: K / V land in LDS by LDS-DMA in flight with the first query block
-    (True) or through registers (False); None re-reads ``LJS_ATTN_BWD_KV_DMA`` (default 2:
-    LDS-DMA when a block sweeps at most 128 queries).  Bit-identical either way."""
+    (True) or through registers (False); None = automatic (LDS-DMA when a block sweeps at most
+    128 queries).  Bit-identical either way."""
     fn = lib().ljs_attn_set_bwd_kv_dma
     fn.argtypes = [c_int]
     fn.restype = None
@@ -118,8 +120,8 @@ def set_attention_bwd_kv_dma(enabled: Optional[bool]):
 
 def set_attention_vst(enabled: Optional[bool]):
     """Attention output row tiles (forward O, backward dK / dV) stored through an LDS image as
-    whole 128-byte rows with 16-byte stores (True), or per lane as 8-byte pieces (False); None
-    re-reads ``LJS_ATTN_VST`` (default on).  Bit-identical either way."""
+    whole 128-byte rows with 16-byte stores (True, the default via None), or per lane as 8-byte
+    pieces (False).  Bit-identical either way."""
     fn = lib().ljs_attn_set_vst
     fn.argtypes = [c_int]
     fn.restype = None
@@ -160,14 +162,6 @@ def set_attention_bwd_pair(enabled: Optional[bool]):
     fn.argtypes = [c_int]
     fn.restype = None
     fn(1 if enabled is None or enabled else 0)
-
-
-def set_attention_fwd_nsub(nsub: int):
-    """Forward query sub-tiles per wave (1 or 2; 0 = default)."""
-    fn = lib().ljs_attn_set_fwd_nsub
-    fn.argtypes = [c_int]
-    fn.restype = None
-    fn(int(nsub))
 
 
 def available() -> bool:
@@ -225,7 +219,7 @@ def _longs(vals) -> ctypes.Array:
 # ============================================================================ GEMM
 # output stores with sc1 (drop the written lines from L2 so the output stream does not evict the
 # operand panels that neighbouring blocks re-read)
-_GEMM_SC1 = os.environ.get("LJS_GEMM_SC1", "1") == "1"
+_GEMM_SC1 = True
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldc: int,
@@ -234,8 +228,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
          accumulate: bool = False, splitk: int = 1, tile: Optional[int] = None, a_off: int = 0, b_off: int = 0,
          c_off: int = 0, zero_c: bool = False, psum: Optional[torch.Tensor] = None,
          res: Optional[torch.Tensor] = None, res_ld: int = 0, res_mode: str = "add", sR: int = 0,
-         slabs: bool = False, acopy: Optional[torch.Tensor] = None,
-         b_list: Optional[Sequence[torch.Tensor]] = None) -> int:
+         slabs: bool = False, b_list: Optional[Sequence[torch.Tensor]] = None) -> int:
     """Raw launcher.  A/B bf16; C bf16 or f32 (split-K/accumulate need f32 C).
 
     ``lda``/``ldb`` may be 0 for an operand that repeats one row (a broadcast gradient).
@@ -247,25 +240,21 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     broadcast row; bf16 C only) is an epilogue operand: ``res_mode="add"`` adds it as a residual
     (``bf16(bf16(y) + bf16(res))``, bit-exact with the unfused add), ``"mask"`` keeps the outputs
     where ``res > 0`` (a ReLU backward fused into the dX GEMM).
-    ``A`` may be f32 (k-contiguous, bf16 output, no split / epilogue operand / fused sum): the
-    GEMM rounds it to bf16 as it reads it (the activation cast fused in) and, with ``acopy`` (bf16
-    [M][K]), also writes that rounding for the backward.
     ``b_list`` (slab mode, batch <= 4): batch b's B operand is ``b_list[b]`` (separate tensors).
     ``slabs`` (f32 C, m/n-contiguous operands, an LDS-DMA tile): split s of batch b's K range
     writes its own slab ``C + (s * batch + b) * sC``; ``splitk`` must be :func:`slab_count`-consistent (the
     last split may run past K, where it reads zeros), so the split need not divide the K-tiles.
     """
-    assert A.dtype in (torch.bfloat16, torch.float32) and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
-    # bf16 slabs (slab mode, C bf16): the f32-output slab kernels, each partial rounded once
-    slab16 = slabs and C.dtype == torch.bfloat16
-    out_f32 = C.dtype == torch.float32 or slab16
+    assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, (A.dtype, B.dtype)
+    assert not slabs or C.dtype == torch.float32, "split-K slabs are f32"
+    out_f32 = C.dtype == torch.float32
     if tile is None:
         tile = pick_tile(M, N, K, batch, a_kc, b_kc, out_f32, splitk, ldc, A.dtype, bias, sBias, relu, accumulate,
-                         zero_c, psum, res, acopy, slabs, sA, sB, sC, ldb)
+                         zero_c, psum, res, slabs, sA, sB, sC, ldb)
     flags = (1 if relu else 0) | (2 if bias is not None else 0) | \
         (4 if (bias is not None and bias.dtype == torch.float32) else 0) | (8 if accumulate else 0) | \
         (16 if zero_c else 0) | (32 if _GEMM_SC1 else 0) | (512 if slabs else 0) | \
-        (2048 if A.dtype == torch.float32 else 0) | (8192 if (slabs and _SLAB_VST) else 0) | (16384 if slab16 else 0)
+        (8192 if (slabs and _SLAB_VST) else 0)
     if res is not None:
         assert not out_f32 and res.dtype in (torch.bfloat16, torch.float32), (C.dtype, res.dtype)
         flags |= (64 if res_mode == "add" else 128) | (256 if res.dtype == torch.float32 else 0)
@@ -283,7 +272,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     rc = lib().ljs_gemm_bf16(ctypes.c_void_p(A.data_ptr() + a_off * eA), b_arg,
                              ctypes.c_void_p(C.data_ptr() + c_off * C.element_size()), _p(bias), M, N, K, lda, ldb,
                              ldc, sA, sB, sC, sBias, batch, int(a_kc), int(b_kc), int(out_f32), flags, alpha,
-                             splitk, tile, _p(psum), ctypes.byref(cnt), _p(res), res_ld, sR, _p(acopy), _stream(C))
+                             splitk, tile, _p(psum), ctypes.byref(cnt), _p(res), res_ld, sR, _stream(C))
     _ck(rc, "ljs_gemm_bf16")
     return cnt.value
 
@@ -344,23 +333,24 @@ def _psum_for(t: torch.Tensor):
 # 256x128 tile for large k-contiguous bf16 GEMMs: with the DMA pieces issued after each k-step's
 # fragment reads it beats the 128x128 x 2/CU kernel at the QKV projection (37.9 vs 40.4 us) and
 # the FF up-projection (60.7 vs 65.2 us; scripts/gemm_tiles_out.py)
-_TILE_2561 = os.environ.get("LJS_GEMM_TILE2561", "1") == "1"
+_TILE_2561 = True
 # 256x192 tile (8 waves of 64x96, 2 stages; a weight-major batch folded into one GEMM): fewer DMA
 # pieces and fragment reads per MFMA than 256x128, one stage less in flight.  On by default with the
 # lean K-loop kernel (round 5: QKV 33.5 vs 39.2 us isolated, B=64 step 0.2124 / 0.2159 vs 0.2250 /
-# 0.2189 ms, gpurun_out/r5g); LJS_GEMM_TILE2562=0 for the 256x128 tile
-_TILE_2562 = os.environ.get("LJS_GEMM_TILE2562", "1") == "1"
-# slab-mode GEMMs: the last item's f32 tile leaves through LDS as whole rows (kSlabVst)
-_SLAB_VST = os.environ.get("LJS_SLAB_VST", "1") == "1"
+# 0.2189 ms, gpurun_out/r5g)
+_TILE_2562 = True
+# slab-mode GEMMs: the last item's f32 tile leaves through LDS as whole rows (kSlabVst; the GPU
+# tests switch it off to check the per-lane form bit-exact)
+_SLAB_VST = True
 
 
 # 128x160 tiles when they (and not 128x128 tiles) fill whole rounds of 512 resident blocks
-_TILE_1602 = os.environ.get("LJS_GEMM_TILE1602", "1") == "1"
+_TILE_1602 = True
 
 
 def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f32: bool, splitk: int = 1,
               ldc: int = 0, a_dtype=None, bias=None, sBias: int = 0, relu: bool = False, accumulate: bool = False,
-              zero_c: bool = False, psum=None, res=None, acopy=None, slabs: bool = False, sA: int = 0, sB: int = 0,
+              zero_c: bool = False, psum=None, res=None, slabs: bool = False, sA: int = 0, sB: int = 0,
               sC: int = 0, ldb: int = 0) -> int:
     """Kernel/tile choice (measured on MI355X at the bench shapes, ``scripts/gemm_one.py``): the
     LDS-DMA kernels (codes 2562 = 256x192 8 waves, 2561 = 256x128 8 waves, 1602 = 128x160 4 waves,
@@ -390,23 +380,13 @@ def pick_tile(M: int, N: int, K: int, batch: int, a_kc: bool, b_kc: bool, out_f3
     return 128 if tiles128 >= 160 else 64
 
 
-_DW_SLAB_MODE = os.environ.get("LJS_DW_SLAB_MODE", "1") == "1"  # A/B switch: 0 = power-of-two batched slabs
-# weight-grad tile at <= 4096 tokens: 12884 (8-wave 128x128, 4 stages, uneven slab splits) measured
-# 0.1033-0.1053 ms vs 0.1071-0.1076 for 644 (64x64, power-of-two batched slabs) at B=8
-_DW_SMALL_TILE = int(os.environ.get("LJS_DW_SMALL_TILE", "12884"))
-# weight of the slab traffic (written by the GEMM, summed by the combine or the fused Adam) in
-# the split-count cost model (tuning knob)
-_DW_TRAFFIC_W = float(os.environ.get("LJS_DW_TRAFFIC_W", "1"))
-# ... in the split count of a weight-gradient GEMM launched on its own (not paired): its slabs are
-# then always read back by a separate slab_reduce (a data-parallel step) or a lone deferred combine,
-# so they weigh more -- dW_o at 16384 tokens 16 splits instead of 24: fake-4 dp rehearsal
-# 0.2147-0.2172 vs 0.2211-0.2224 ms x3 (profiles/r5bm_dw_single_traffic_lines.txt)
-_DW_SINGLE_TRAFFIC_W = float(os.environ.get("LJS_DW_SINGLE_TRAFFIC_W", "4"))
-# weight-grad tile above 4096 tokens: 1282 (cost-model split count) or, as an A/B switch, 644 /
-# 12884 with one round of slabs
-_DW_BIG_TILE = int(os.environ.get("LJS_DW_BIG_TILE", "1282"))
-# (A/B) rounds of resident blocks the 644 / 12884 split fills (more, shorter slabs)
-_DW_BIG_ROUNDS = int(os.environ.get("LJS_DW_BIG_ROUNDS", "1"))
+# ... the slab traffic's weight in the split count of a weight-gradient GEMM launched on its own
+# (not paired): its slabs are then always read back by a separate slab_reduce (a data-parallel
+# step) or a lone deferred combine, so they weigh more -- dW_o at 16384 tokens 16 splits instead
+# of 24: fake-4 dp rehearsal 0.2147-0.2172 vs 0.2211-0.2224 ms x3
+# (profiles/r5bm_dw_single_traffic_lines.txt); the pair's model weighs them 1
+_DW_SINGLE_TRAFFIC_W = 4.0
+_DW_TRAFFIC_W = 1.0
 
 
 def slab_count(nkt: int, S: int) -> int:
@@ -430,27 +410,14 @@ def _dw_single(K: int, N: int, T: int, traffic_w: Optional[float] = None):
     traffic -- instead of a power of two dividing the K-tiles: the FF weight gradients (100
     tiles) ran 400 items on 512 block slots (78 %), now 5 x 52 K-tiles = 500 items; dW_o (20
     tiles) 16 x 16 -> 24 x 11.  At T <= 4096 the 8-wave 128x128 tile (one block per CU) in slab
-    mode; ``LJS_DW_SMALL_TILE=644``: the 64x64 tile with the largest power-of-two batched split
-    keeping <= 512 items and >= 512 tokens per chunk (the round-2 default before)."""
+    mode."""
     w = _DW_SINGLE_TRAFFIC_W if traffic_w is None else traffic_w
     if K % 64 or N % 64 or T % 64:
         return 1282, pick_splitk_dma(K, N, T, 1), False, None
-    if T > 4096 and not _DW_SLAB_MODE:
-        return 1282, pick_splitk_dma(K, N, T, 1), False, None
-    if T > 4096 and _DW_BIG_TILE in (644, 12884):
-        # (A/B: fewer, longer slabs -- 64x64 tiles at 2 blocks/CU or 8-wave 128x128 at 1 block/CU,
-        # split count filling one round of resident blocks)
-        nkt = T // 64
-        bm = 64 if _DW_BIG_TILE == 644 else 128
-        tiles = -(-K // bm) * -(-N // bm)
-        slots = (2 if _DW_BIG_TILE == 644 else 1) * _cus() * _DW_BIG_ROUNDS
-        S = max(1, min(nkt, slots // max(1, tiles)))
-        while S > 1 and slab_count(nkt, S) != S:
-            S -= 1
-        return _DW_BIG_TILE, S, True, None
-    if T > 4096 or _DW_SMALL_TILE == 1282:
-        nkt, tiles, slots = T // 64, -(-K // 128) * -(-N // 128), 2 * _cus()
-        best, best_cost = 1, None
+    nkt, tiles = T // 64, -(-K // 128) * -(-N // 128)
+    best, best_cost = 1, None
+    if T > 4096:
+        slots = 2 * _cus()
         for S in range(1, min(64, nkt) + 1):
             if slab_count(nkt, S) != S:
                 continue
@@ -462,22 +429,15 @@ def _dw_single(K: int, N: int, T: int, traffic_w: Optional[float] = None):
             if best_cost is None or cost < best_cost - 1e-9:
                 best, best_cost = S, cost
         return 1282, best, True, best_cost
-    if _DW_SMALL_TILE == 12884:
-        # (A/B: 8-wave 128x128, 4 stages, one block per CU, uneven slab splits)
-        nkt, tiles = T // 64, -(-K // 128) * -(-N // 128)
-        best, best_cost = 1, None
-        for S in range(1, min(32, nkt) + 1):
-            if slab_count(nkt, S) != S:
-                continue
-            cost = -(-tiles * S // _cus()) * (-(-nkt // S) * 1.2 + 1.0) + w * S * K * N * 4 / 5e6
-            if best_cost is None or cost < best_cost - 1e-9:
-                best, best_cost = S, cost
-        return 12884, best, True, best_cost
-    tiles = (K // 64) * (N // 64)
-    s = 1
-    while tiles * s * 2 <= 512 and T % (64 * s * 2) == 0 and T // (s * 2) >= 512:
-        s *= 2
-    return 644, s, False, None
+    # T <= 4096: 8-wave 128x128, 4 stages, one block per CU, uneven slab splits (0.1033-0.1053 ms
+    # vs 0.1071-0.1076 for the 64x64 tile with power-of-two batched slabs at B = 8)
+    for S in range(1, min(32, nkt) + 1):
+        if slab_count(nkt, S) != S:
+            continue
+        cost = -(-tiles * S // _cus()) * (-(-nkt // S) * 1.2 + 1.0) + w * S * K * N * 4 / 5e6
+        if best_cost is None or cost < best_cost - 1e-9:
+            best, best_cost = S, cost
+    return 12884, best, True, best_cost
 
 
 def pick_dw_slabs(K: int, N: int, T: int):
@@ -487,8 +447,8 @@ def pick_dw_slabs(K: int, N: int, T: int):
 
 
 _PAIR_PICKS: Dict[tuple, Optional[tuple]] = {}
-# "S0,S1": force the pair's split counts (A/B)
-_DW_PAIR = os.environ.get("LJS_DW_PAIR", "")
+# "S0,S1[,tile]": force the pair's split counts (tests)
+_DW_PAIR = ""
 
 
 def pick_dw_pair(K0: int, N0: int, K1: int, N1: int, T: int):
@@ -514,7 +474,7 @@ def pick_dw_pair(K0: int, N0: int, K1: int, N1: int, T: int):
     # T <= 4096: the 8-wave 128x128 tile at one block per CU, as for a single weight gradient there
     # (B = 8 pair at 3 + 3 splits: 12.66 us vs 14.49 for the 1282 pair at 6 + 6, and half the slabs;
     # at T = 16384 72.0 vs 53.8, profiles/r5au_dw_pair_8w_probe.txt)
-    tile, slots = (12884, _cus()) if (T <= 4096 and _DW_SMALL_TILE == 12884) else (1282, 2 * _cus())
+    tile, slots = (12884, _cus()) if T <= 4096 else (1282, 2 * _cus())
     best, best_cost = None, None
     if _DW_PAIR:
         v = [int(t) for t in _DW_PAIR.split(",")]
@@ -1595,6 +1555,20 @@ def _defer_step_inc(step: torch.Tensor):
     return pend
 
 
+
+
+_ADAM_ROWS = [0]
+
+
+def set_adam_rows(rows: int) -> None:
+    """Force the fused Adam's tile height (16 / 32 / 64; 0 = automatic: 32, or 64 when a tensor
+    carries MX-fp8 shadows).  For tests of the kernel's tile paths; bit-identical results."""
+    lib().ljs_adam_set_rows(int(rows))
+    _ADAM_ROWS[0] = int(rows)
+
+
+def adam_rows() -> int:
+    return _ADAM_ROWS[0]
 
 
 def adam_multi(entries, step: torch.Tensor, lr, b1, b2, eps, wd, increment_step: bool = False) -> None:

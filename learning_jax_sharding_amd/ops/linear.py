@@ -34,7 +34,6 @@ import numpy as np
 import torch
 
 from . import hip
-from . import streams as _streams
 from . import shadow
 
 __all__ = ["linear"]
@@ -87,9 +86,9 @@ def _splitk(M: int, N: int, K: int, batch: int, tile: int) -> int:
     return s
 
 
-_DW_SPLIT = int(os.environ.get("LJS_DW_SPLIT", "0"))
+_DW_SPLIT = 0   # (tests: force the K-chunk count)
 # large bf16 dense outputs also carry their fused per-tile sums (see hip._PSUM): y.sum() is free
-_FUSED_SUM = os.environ.get("LJS_FUSED_SUM", "1") == "1"  # tuning override of the K-chunk count
+_FUSED_SUM = os.environ.get("LJS_FUSED_SUM", "1") == "1"
 
 
 # Deferred weight-gradient combines.  Inside value_and_grad on one device (no gradient
@@ -170,7 +169,7 @@ class defer_wgrads:
         """``enabled``: leaves' gradients may stay slabs (one device, the fused Adam sums them);
         ``proxies``: only slab-consumer outputs' may (several devices)."""
         self.state = None
-        if (enabled or proxies) and _DEFER_ON and not _streams.enabled():
+        if (enabled or proxies) and _DEFER_ON:
             safe = defer_safe_leaves(outs, leaves=enabled)
             if safe:
                 self.state = {"safe": safe, "pending": {}}
@@ -211,12 +210,9 @@ def _defer_ok(*ts) -> bool:
     return d is not None and all(t is not None and t.dtype == torch.float32 and _key(t) in d["safe"] for t in ts)
 
 
-# split-K weight-gradient slabs in bf16 (LJS_SLAB_BF16=1, opt-in): each split's partial sum is
-# rounded once and the S partials are summed in f32 (slab_reduce / the fused Adam), so dW carries
-# at most the error of the reference's one bf16 rounding of the whole sum (bf16 dot output,
-# case6_attention.py's Dense(dtype=bf16) backward) spread over S smaller partials -- and the slab
-# stream the GEMM writes and Adam re-reads is halved (63 -> 31 MB per B=64 step)
-_SLAB_DT = torch.bfloat16 if os.environ.get("LJS_SLAB_BF16", "0") == "1" else torch.float32
+# split-K weight-gradient slabs are f32 (bf16 slabs halved the slab bytes but measured no step gain
+# and drifted the 2-rank 2-D parity past its tolerance: PERF_NOTES r4; removed in round 6)
+_SLAB_DT = torch.float32
 
 
 # Grouped weight-gradient launches (LJS_DW_GROUP=1, the default): inside a deferring backward
@@ -599,22 +595,14 @@ class _Linear(torch.autograd.Function):
         # weight-major outputs ([nw][M][N]: each projection dense on its own) for a seq-major
         # fused projection, so its K / V gather over the sequence are contiguous blocks
         wmajor = nw > 1 and order[0] != 0
-        # f32 activations (the reference's f32 input under a bf16 Dense): the GEMM rounds them as
-        # it reads them and writes the bf16 copy the backward needs -- no separate cast pass
-        cast_on_load = (not swap and not wmajor and x2.is_cuda and x2.dtype == torch.float32
-                        and x2.is_contiguous() and res is None and b is None and not relu and K % 64 == 0
-                        and N % 8 == 0 and out_dtype == torch.bfloat16 and x2.data_ptr() % 16 == 0
-                        and M * nw * N >= (1 << 20))
-        # "auto": where the f32 A is register-staged (the 256x128 tile: global f32 -> VGPR -> bf16
-        # LDS image, the bf16 copy stored from the same registers); the f32-LDS-image kernels stay
-        # opt-in ("1", measured slower)
-        if cast_on_load and _CAST_ON_LOAD != "1":
-            cast_on_load = _CAST_ON_LOAD == "auto" and hip.pick_tile(M, N, K, nw, True, True, False, 1,
-                                                                     nw * N) == 2561
+        # f32 activations (the reference's f32 input under a bf16 Dense) are rounded by one cast
+        # pass -- or, for a multi-step runner's next input, by the previous step's optimizer launch
+        # (take_optimizer_precast).  Rounding inside the GEMM (an f32 A operand, LDS image or
+        # register-staged) measured slower in both forms and was removed (PERF_NOTES r2, r4).
         if swap:   # batch-major x -> seq-major bf16 rows, rounded in the same pass
             xb = hip.swap01_bf16(x.contiguous()).view(M, K)
         else:
-            xb = None if cast_on_load else _bf16(x2 if x2.is_contiguous() else x2.contiguous())
+            xb = _bf16(x2 if x2.is_contiguous() else x2.contiguous())
         # weights gathered on a side stream (parallel/fsdp.Prefetcher.prefetch(defer_wait=True)):
         # the stream waits for them only now, after the activation's cast pass was queued
         take_pending_waits(x.device)
@@ -652,16 +640,9 @@ class _Linear(torch.autograd.Function):
             r_ld = r2.stride(0)
             if nw != 1 or od != torch.bfloat16 or N % 8:
                 r2 = None
-        if cast_on_load and partials is None:
-            xb = torch.empty((M, K), dtype=torch.bfloat16, device=x.device)
-            cnt = hip.gemm(x2, wt, out, M, N, K, K, K, nw * N, True, True, batch=nw, sA=0, sB=sB, sC=N,
-                           acopy=xb)
-        else:
-            if cast_on_load:  # (a fused output sum wanted: the cast pass, then the plain GEMM)
-                xb = _bf16(x2)
-            cnt = hip.gemm(xb, wt, out, M, N, K, K, K, N if wmajor else nw * N, True, True, batch=nw, sA=0, sB=sB,
-                           sC=M * N if wmajor else N, bias=bias, sBias=0, relu=relu, psum=partials, res=r2,
-                           res_ld=r_ld)
+        cnt = hip.gemm(xb, wt, out, M, N, K, K, K, N if wmajor else nw * N, True, True, batch=nw, sA=0, sB=sB,
+                       sC=M * N if wmajor else N, bias=bias, sBias=0, relu=relu, psum=partials, res=r2,
+                       res_ld=r_ld)
         cols = [out[i] if wmajor else out[:, i * N:(i + 1) * N] for i in range(nw)]
         ys = [c.view(pshape + (N,)).permute(inv) for c in cols]
         if res is not None and r2 is None:
@@ -775,14 +756,11 @@ class _Linear(torch.autograd.Function):
             dx = dx.to(xdtype).view(pshape + (K,)).permute(_inv_perm(order))
             if premask:
                 _register(_PREMASKED, dx, xb.data_ptr())
-        # ---- dW (MN-contiguous operands: X^T and dY read in place), on the side stream inside
-        # value_and_grad (ops/streams.py): it overlaps the layers' input-gradient chain
+        # ---- dW (MN-contiguous operands: X^T and dY read in place), on the compute stream (a side
+        # stream overlapping the input-gradient chain measured slower at every bench shape: two
+        # chip-sized persistent grids share the CUs as two rounds + a tail, PERF_NOTES r2; removed)
         want = [i for i in live if ctx.needs_input_grad[5 + i]]
-        with _streams.side(dev, [xb, joint, joint_bf16] + [mats[i][0] for i in want]) as produced:
-            _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, dev, tail)
-            produced.extend(d for d in dws if d is not None)
-            if joint is not None:
-                produced.append(joint)
+        _wgrads(ctx, xb, ws, mats, want, dws, joint, joint_bf16, K, M, N, nw, wire, dev, tail)
         # ---- db
         if want_db and live:
             tot = None
@@ -987,42 +965,22 @@ class _FFBlock(torch.autograd.Function):
                 _dp.register_wire_twin(o, twin)
             return o
 
-        def run_wo():  # weight gradients on the side stream inside value_and_grad (ops/streams.py)
+        def run_wo():
             if ctx.needs_input_grad[2]:
-                with _streams.side(dev, [a, t]) as produced:
-                    out["wo"] = wgrad(a, t, ld, F, M, w_out)
-                    produced.append(out["wo"])
+                out["wo"] = wgrad(a, t, ld, F, M, w_out)
 
         def run_wi():
             if ctx.needs_input_grad[1]:
-                with _streams.side(dev, [x2, dA]) as produced:
-                    out["wi"] = wgrad(x2, dA, F, M, F, w_in)
-                    produced.append(out["wi"])
+                out["wi"] = wgrad(x2, dA, F, M, F, w_in)
         _ff_bwd_order(run_dx, run_wo, run_wi)
         return out.get("dx"), out.get("wi"), out.get("wo"), None
 
 
-# f32 activations rounded inside the consuming GEMM (opt-in, LJS_CAST_ON_LOAD=1): measured slower
-# than the separate cast pass + bf16 GEMM at both bench shapes (QKV at 16384 tokens: cast + 2561
-# tile 52.7 us vs 59.6 us for the f32-A kernel alone, 75.6 with the bf16 copy the backward needs;
-# at 2048 tokens 19.4 vs 18.5 us; scripts/col_one.py) -- the f32 A image doubles the operand bytes
-# and LDS reads of the K-loop, which costs more than the cast pass it saves.  Re-measured inside the
-# step with the bf16 copy shared out over the items: B=8 even (0.0898-0.0904 vs 0.0896-0.0899 ms),
-# B=16 and B=64 slower (profiles/PERF_NOTES.md)
-# Round 4, the register-staged form (the 256x128 tile: global f32 -> VGPR -> bf16 LDS image, the
-# bf16 copy stored from the same registers; bit-exact, tests/test_kernels_gpu.py
-# test_gemm_f32_a_register_staged): QKV 64.8 us vs 49.3 for cast + bf16 GEMM isolated, 73.2 vs
-# 55.4 in the step, B=64 0.2551-0.2578 vs 0.2351-0.2399 ms (gpurun_out/r4j) -- the f32 loads are
-# waited on one K-tile after their issue, where the LDS-DMA ring hides two.
-# "0" (default): the cast pass; "auto": the register-staged / ping-pong forms where they apply;
-# "1": every f32-A kernel
-_CAST_ON_LOAD = os.environ.get("LJS_CAST_ON_LOAD", "0")
 
 # order of the FF block's backward GEMMs after dA (dX, dW_out, dW_in): which operands are still
 # in the Infinity Cache when each runs.  dW_in right after dA (which it reads, 84 MB at the bench
 # shape) measured best: bf16 layer 0.700 -> 0.692 ms, fp8 0.746 -> 0.739 ms over dx,wo,wi
-# (A/B switch, e.g. LJS_FF_BWD_ORDER=dx,wo,wi)
-_FF_BWD_ORDER = [t for t in os.environ.get("LJS_FF_BWD_ORDER", "wi,dx,wo").split(",") if t]
+_FF_BWD_ORDER = ["wi", "dx", "wo"]
 
 
 def _ff_bwd_order(run_dx, run_wo, run_wi):

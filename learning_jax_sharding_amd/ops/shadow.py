@@ -173,11 +173,11 @@ def register_mx_proxy(w: torch.Tensor, mx: Dict[str, Tuple[torch.Tensor, torch.T
 
 
 def mx_eligible(w: torch.Tensor) -> bool:
-    """Weights whose MX-fp8 shadows the fused Adam can keep (64 x 64 tiles of its 4-wide path)."""
-    import os
+    """Weights whose MX-fp8 shadows the fused Adam can keep (64 x 64 tiles of its 4-wide path;
+    a launch carrying MX shadows always runs 64-row tiles unless a test forces another height)."""
+    from . import hip
     return (w.is_cuda and w.dim() == 2 and w.dtype == torch.float32 and w.is_contiguous()
-            and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0
-            and os.environ.get("LJS_ADAM_ROWS", "64") == "64")
+            and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and hip.adam_rows() in (0, 64))
 
 
 def get_mx(w: torch.Tensor, kind: str):

@@ -518,9 +518,6 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
             if outs and inputs:
                 # under a segmented capture the backward must run on this thread: HIP ends a
                 # graph capture only on the thread that began it, and collectives cut captures
-                # weight gradients fork onto side streams (ops/streams.py) unless data-parallel
-                # hooks consume gradients as they are produced; joined before they are returned
-                from ..ops import streams as _streams
                 from ..ops import linear as _lin
                 side = reducer is None and all(t.is_cuda for t in inputs)
                 # one device, no gradient all-reduce: weight-gradient combines may be left to the
@@ -530,8 +527,7 @@ def value_and_grad(fun: Callable, argnums=0, has_aux: bool = False):
                 dfr = _lin.defer_wgrads(outs, one_dev, proxies=side and not _multi_process())
                 # (LJS_ATEN_TRACE: on this thread, so the tracer sees the backward's call sites)
                 mt = _graphs.current() is None and not os.environ.get("LJS_ATEN_TRACE")
-                with torch.autograd.set_multithreading_enabled(mt), \
-                        _streams.wgrad_scope(side), dfr:
+                with torch.autograd.set_multithreading_enabled(mt), dfr:
                     gs = torch.autograd.grad(outs, inputs, seeds, allow_unused=True)
             else:
                 gs = [None] * len(inputs)

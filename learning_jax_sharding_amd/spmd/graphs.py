@@ -240,8 +240,8 @@ def join(handle) -> None:
 # staging buffer and barrier sequence, comm/p2p.py _enter) waits on it: an event recorded inside
 # a capture cannot be waited on outside it.
 _LAST_REPLAY: Dict[int, Any] = {}
-# LJS_REPLAY_EVENT=1: record the completion event after every replay (A/B)
-_EAGER_REPLAY_EVENT = os.environ.get("LJS_REPLAY_EVENT", "0") == "1"
+# record the completion event after every replay instead of lazily (tests)
+_EAGER_REPLAY_EVENT = False
 
 
 def _note_replay(streams: Dict[int, Any]) -> None:

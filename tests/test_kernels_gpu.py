@@ -153,16 +153,13 @@ def attn_bwd_impl(request, hip):
     hip.set_attention_bwd_fused(None)
 
 
-@pytest.fixture(params=[(1, 0), (2, 0), (1, 4), (1, 8), (1, 16), (1, 108), (1, 116)],
-                ids=["tiled1", "tiled2", "res4", "res8", "res16", "pers8", "pers16"])
+@pytest.fixture(params=[(1, 0), (1, 4), (1, 8)], ids=["tiled1", "res4", "res8"])
 def attn_fwd_nsub(request, hip):
-    """Forward kernel variant: tiled with 1 / 2 query sub-tiles per wave, or K/V-resident with
-    4 / 8 / 16 waves per block, or its persistent double-buffered form (108 / 116: 8 / 16 waves) (Sk <= 256; longer keys fall back to the tiled kernel)."""
-    nsub, res = request.param
-    hip.set_attention_fwd_nsub(nsub)
+    """Forward kernel variant: tiled (K/V tiles through registers), or K/V-resident with 4 / 8
+    waves per block (Sk <= 256; longer keys fall back to the tiled kernel)."""
+    _, res = request.param
     hip.set_attention_fwd_resident(res)
     yield request.param
-    hip.set_attention_fwd_nsub(0)
     hip.set_attention_fwd_resident(-1)
 
 
@@ -421,7 +418,7 @@ def test_adam_multi_and_shadows(hip):
 @pytest.mark.parametrize("S", [3, 7, 11, 24])
 def test_adam_multi_slab_grads_bit_exact(hip, S):
     """Adam reading split-K slabs directly (the kernel's slab sum, double-buffered in <= 32-row
-    tiles under LJS_ADAM_ROWS=32) equals slab_reduce + Adam on the combined gradient, bit for bit."""
+    tiles of the default 32-row launch) equals slab_reduce + Adam on the combined gradient, bit for bit."""
     shapes = [(640, 512), (512, 640)]
     ws = [torch.randn(*sh, device=dev) for sh in shapes]
     slabs = [torch.randn(S, *sh, device=dev) for sh in shapes]
@@ -1049,61 +1046,6 @@ def test_fp8_gemm_transposed_copy_splitk_bcast_and_fp8_mask(hip):
     assert torch.equal(m1, m2)
 
 
-@pytest.mark.parametrize("M,N,K,batch", [(2048, 512, 640, 3), (300, 136, 128, 1), (16384, 512, 640, 3),
-                                         (520, 256, 1024, 1), (384, 128, 640, 1)])
-def test_gemm_f32_a_cast_on_load(hip, M, N, K, batch):
-    """The f32-A LDS-DMA GEMM (activation cast fused into the fragment reads) == cast pass + bf16
-    GEMM bit for bit, and its bf16 copy of A == the cast pass's output."""
-    x = _rand(M, K, dtype=torch.float32, seed=90)
-    w = _rand(batch, N, K, seed=91)
-    ref_x = x.bfloat16()
-    ref = torch.empty(M, batch * N, dtype=torch.bfloat16, device=dev)
-    hip.gemm(ref_x, w, ref, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N)
-    out = torch.full((M, batch * N), float("nan"), dtype=torch.bfloat16, device=dev)
-    xb = torch.full((M, K), float("nan"), dtype=torch.bfloat16, device=dev)
-    hip.gemm(x, w, out, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N, acopy=xb)
-    assert torch.equal(out, ref)
-    assert torch.equal(xb, ref_x)
-
-
-@pytest.mark.parametrize("M,N,K,batch", [(16384, 512, 640, 3), (2048, 512, 640, 3), (300, 136, 128, 1),
-                                         (520, 256, 1024, 1), (4096 + 72, 128, 640, 2)])
-def test_gemm_f32_a_register_staged(hip, M, N, K, batch):
-    """The 256x128 kernel with A register-staged (global f32 -> VGPR -> bf16 LDS image; tile
-    2561 + f32 A) == cast pass + bf16 GEMM bit for bit; the bf16 copy it writes from the same
-    registers (shared out over each row block's items by K-tile) == the cast pass's output."""
-    x = _rand(M, K, dtype=torch.float32, seed=94)
-    w = _rand(batch, N, K, seed=95)
-    ref_x = x.bfloat16()
-    ref = torch.empty(M, batch * N, dtype=torch.bfloat16, device=dev)
-    hip.gemm(ref_x, w, ref, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N, tile=1282)
-    out = torch.full((M, batch * N), float("nan"), dtype=torch.bfloat16, device=dev)
-    xb = torch.full((M, K), float("nan"), dtype=torch.bfloat16, device=dev)
-    hip.gemm(x, w, out, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N, acopy=xb, tile=2561)
-    torch.cuda.synchronize()
-    assert torch.equal(out, ref)
-    assert torch.equal(xb, ref_x)
-    out2 = torch.full((M, batch * N), float("nan"), dtype=torch.bfloat16, device=dev)
-    hip.gemm(x, w, out2, M, N, K, K, K, batch * N, True, True, batch=batch, sA=0, sB=N * K, sC=N, tile=2561)
-    assert torch.equal(out2, ref)
-
-
-def test_linear_f32_input_cast_on_load(hip, monkeypatch):
-    """hip.linear on an f32 activation: the cast-on-load GEMM path gives the same outputs and
-    weight gradients as the separate-cast path."""
-    from learning_jax_sharding_amd.ops import linear as L
-    x = _rand(4096, 640, dtype=torch.float32, seed=92)
-    ws = [(_rand(640, 512, dtype=torch.float32, seed=93 + i) * 0.05).requires_grad_() for i in range(3)]
-    res = {}
-    for flag in ("0", "1"):
-        monkeypatch.setattr(L, "_CAST_ON_LOAD", flag)
-        ys = hip.linear(x, ws, None, torch.bfloat16, False, torch.bfloat16)
-        gs = torch.autograd.grad(ys, ws, [torch.ones_like(y) for y in ys])
-        res[flag] = [y.clone() for y in ys] + [g.clone() for g in gs]
-    for a, b in zip(res["0"], res["1"]):
-        assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("sk", [128, 512])
 def test_attention_fwd_inkernel_lse_merge(causal, sk):
@@ -1249,7 +1191,7 @@ def test_fp8_gemm_fused_column_sums(hip, tile):
 def test_fp8_transformer_layer_large_tiles_and_fused_colsum(gpu_devices):
     """At 4096 tokens the fp8 FF block's N=640 GEMMs take the 8-wave tiles and its dX GEMM writes
     the column sums the attention out-projection's bias gradient reads: that bias gradient ==
-    the column sums of the same step with the fused sums off (LJS_F8_FUSED_COLSUM path), and
+    the column sums of the same step with the fused sums off (fp8._FUSED_COLSUM = False), and
     every gradient is finite."""
     gpu_devices(1)
     import learning_jax_sharding_amd as ljs
@@ -1296,7 +1238,7 @@ def test_slab_gemm_staged_epilogue_bit_exact(hip, T, K, N, tile, S):
         slabs = torch.full((S, K, N), float("nan"), dtype=torch.float32, device=dev)
         hip.gemm(x, dy, slabs, K, N, T, K, N, N, False, False, sC=K * N, splitk=S, tile=tile, slabs=True)
         outs.append(slabs)
-    hip._SLAB_VST = os.environ.get("LJS_SLAB_VST", "1") == "1"
+    hip._SLAB_VST = True
     assert torch.equal(outs[0], outs[1])
     ref = (x.float().t() @ dy.float())
     torch.testing.assert_close(outs[0].sum(0), ref, rtol=2e-2, atol=2e-1)
