@@ -34,6 +34,20 @@ constexpr int BLK = 64;    // queries / keys per tile
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int FKR = 256;   // max keys of the K/V-resident forward
 
+// Division by a launch constant without the integer-division sequence (~20 scalar instructions
+// each on gfx950): q = (umulhi(n, m) + n) >> s for n < 2^31, m and s from the host (Granlund-
+// Montgomery; d = 1 gives m = 1, s = 0).  The resident forward's 8 waves each decode their tile
+// in their prologue, so this is per-wave latency before the K/V DMA can issue.
+struct FastDiv {
+  unsigned m;
+  int s, d;
+};
+static inline FastDiv make_fastdiv(int d) {
+  int s = 0;
+  while ((1L << s) < d) ++s;
+  const unsigned long long m = ((1ULL << 32) * ((1ULL << s) - (unsigned long long)d)) / (unsigned long long)d + 1;
+  return FastDiv{(unsigned)m, s, d};
+}
 struct AttnArgs {
   const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* o; const bf16_t* dout;
   bf16_t* out;                     // fwd: O ; bwd dkv: dK ; bwd dq: dQ
@@ -54,9 +68,13 @@ struct AttnArgs {
   long oa_sb, oa_ss, oa_sh;
   int acc_mode;
   int vst;           // outputs 16-byte aligned with row strides % 8 == 0: row tiles leave through an
-                     // LDS image as full 128-byte rows (stage_rows16 / flush_rows), LJS_ATTN_VST
+                     // LDS image as full 128-byte rows (stage_rows16 / flush_rows)
+  FastDiv fd_nx, fd_h;  // resident forward: its query-block count and H as launch-constant divisors
 };
 
+#ifndef LJS_ATTN_FASTIDX
+#define LJS_ATTN_FASTIDX 0   // (A/B) the resident forward's tile decode by launch-constant divisors
+#endif
 // A/B switches (compile-time): the resident forward's key loop fully unrolled at 256 keys, and
 // the fused backward's dQ slices without per-slice guards when all 256 keys are valid
 #ifndef LJS_ATTN_FWD_UNROLL
@@ -120,6 +138,19 @@ __device__ __forceinline__ Tile3 tile3(int nx, int H) {
   r.x = t % nx;
   r.h = (t / nx) % H;
   r.b = t / (nx * H);
+  return r;
+}
+
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)((__umulhi((unsigned)n, f.m) + (unsigned)n) >> f.s);
+}
+__device__ __forceinline__ Tile3 tile3f(const FastDiv& nx, const FastDiv& H) {
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int q1 = fdiv(t, nx), q2 = fdiv(q1, H);
+  Tile3 r;
+  r.x = t - q1 * nx.d;
+  r.h = q1 - q2 * H.d;
+  r.b = q2;
   return r;
 }
 
@@ -404,7 +435,11 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Vs[FKR * D];
   constexpr int QB = 16 * NW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if LJS_ATTN_FASTIDX
+  const Tile3 tl = tile3f(a.fd_nx, a.fd_h);
+#else
   const Tile3 tl = tile3((a.Sq + QB - 1) / QB, a.H);
+#endif
   const int qb = tl.x, h = tl.h, b = tl.b;
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
@@ -424,6 +459,30 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
     const u32x4 rk = rsrc_u4(kb, 2 * ((long)(a.Sk - 1) * a.k_ss + D));
     const u32x4 rv = rsrc_u4(vb, 2 * ((long)(a.Sk - 1) * a.v_ss + D));
     const int npieces = nkt * (BLK / 8);  // 8 rows x 128 B per 1 KiB piece, key-tile major
+#if LJS_ATTN_FASTIDX
+    // 32-bit offsets (the launcher checks (Sk - 1) x stride x 2 + 128 < 2^31 for this kernel); the
+    // full 256-key case unrolled, so each piece's offset is a lane constant plus an immediate
+    const int ks32 = (int)a.k_ss, vs32 = (int)a.v_ss;
+    if (npieces == FKR / 8) {
+#pragma unroll
+      for (int i = 0; i < FKR / 8 / NW; ++i) {
+        const int pc = wave + NW * i;
+        const int row = 8 * pc + (lane >> 3);
+        const int c = ((lane & 7) ^ (((row >> 1) & 3) << 1)) * 8;
+        const bool ok = row < a.Sk;
+        dma_lds_x4(rk, ok ? (row * ks32 + c) * 2 : 0x7ffffff0, Ks + pc * 512);
+        dma_lds_x4(rv, ok ? (row * vs32 + c) * 2 : 0x7ffffff0, Vs + pc * 512);
+      }
+    } else {
+      for (int pc = wave; pc < npieces; pc += NW) {
+        const int row = 8 * pc + (lane >> 3);
+        const int c = ((lane & 7) ^ (((row >> 1) & 3) << 1)) * 8;
+        const bool ok = row < a.Sk;
+        dma_lds_x4(rk, ok ? (row * ks32 + c) * 2 : 0x7ffffff0, Ks + pc * 512);
+        dma_lds_x4(rv, ok ? (row * vs32 + c) * 2 : 0x7ffffff0, Vs + pc * 512);
+      }
+    }
+#else
     for (int pc = wave; pc < npieces; pc += NW) {
       const int row = 8 * pc + (lane >> 3);
       const int c = ((lane & 7) ^ (((row >> 1) & 3) << 1)) * 8;
@@ -431,6 +490,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
       dma_lds_x4(rk, ok ? (int)(((long)row * a.k_ss + c) * 2) : 0x7ffffff0, Ks + pc * 512);
       dma_lds_x4(rv, ok ? (int)(((long)row * a.v_ss + c) * 2) : 0x7ffffff0, Vs + pc * 512);
     }
+#endif
   }
   FwdState st;
 #pragma unroll
@@ -1696,6 +1756,8 @@ static int attn_fwd_impl(const void* q, const void* k, const void* v, void* o, v
     int nw = g_fwd_res == 4 ? 4 : 8;
     if (nw == 8 && (Sq + 127) / 128 * H * B < 256) nw = 4;
     const int nqb = (Sq + 16 * nw - 1) / (16 * nw);
+    a.fd_nx = make_fastdiv(nqb);
+    a.fd_h = make_fastdiv(H);
     if (nw == 8) hipLaunchKernelGGL(attn_fwd_res_kernel<8>, dim3(nqb * H * B), dim3(512), 0, stream, a);
     else hipLaunchKernelGGL(attn_fwd_res_kernel<4>, dim3(nqb * H * B), dim3(256), 0, stream, a);
     return (int)hipGetLastError();

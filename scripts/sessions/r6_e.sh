@@ -13,6 +13,7 @@ for rep in 1 2 3; do
   step $O/b64_base_$rep.txt timeout -k 10 300 python bench.py --steps 20 --warmup 5
   step $O/b64_mf32_$rep.txt timeout -k 10 300 env LJS_KERNELS_LIB=$V/mf32/libljs_kernels.so python bench.py --steps 20 --warmup 5
   step $O/b64_sgb_$rep.txt timeout -k 10 300 env LJS_KERNELS_LIB=$V/sgb/libljs_kernels.so python bench.py --steps 20 --warmup 5
+  step $O/b64_fastidx_$rep.txt timeout -k 10 300 env LJS_KERNELS_LIB=$V/fastidx/libljs_kernels.so python bench.py --steps 20 --warmup 5
 done
 for rep in 1 2; do
   step $O/b8_base_$rep.txt timeout -k 10 300 python bench.py --batch-per-gpu 8 --steps 20 --warmup 5
