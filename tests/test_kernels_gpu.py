@@ -780,6 +780,56 @@ def test_fp8_quantization_matches_reference(hip):
         assert torch.equal(q1, qr5) and torch.equal(s1, sr5) and torch.equal(q2, qt) and torch.equal(s2, st)
 
 
+def test_fp8_quantization_f32_emits_bf16_copy(hip):
+    """The f32-input forms round x to bf16 inside the quantization pass and write that copy: bit-
+    identical to a cast pass followed by the bf16 quantization (the MX layer's input cast fused)."""
+    from learning_jax_sharding_amd.ops import fp8 as F
+    x = _rand(1024, 704, dtype=torch.float32, seed=45) * 2
+    x[64:96, 5] = 0
+    x[3, 7] = 3e4
+    for src in (x[:, :640], x[:, 64:].contiguous()):
+        ref = src.bfloat16()
+        if src.is_contiguous():
+            xb = torch.full(src.shape, 7.0, dtype=torch.bfloat16, device=dev)
+            (q1, s1), (q2, s2) = F._quant_both(src, xb)
+            (r1, t1), (r2, t2) = F._quant_both(ref)
+            assert torch.equal(xb, ref)
+            assert torch.equal(q1, r1) and torch.equal(s1, t1) and torch.equal(q2, r2) and torch.equal(s2, t2)
+        else:
+            with pytest.raises(AssertionError):
+                F._quant_both(src, None)
+        xr = torch.full((src.shape[0], src.shape[1]), 7.0, dtype=torch.bfloat16, device=dev)
+        qa, sa = F.quant_rows(src, xb=xr)
+        qb, sb = F.quant_rows(src)
+        assert torch.equal(xr, ref) and torch.equal(qa, qb) and torch.equal(sa, sb)
+
+
+def test_fp8_ff_block_f32_input_has_no_cast_pass(hip):
+    """An f32 input to the MX FF block: the output and grads equal the bf16-input block's (the
+    fused cast is the same rounding), and no standalone f32->bf16 cast kernel runs."""
+    from learning_jax_sharding_amd.ops import fp8 as F
+    from learning_jax_sharding_amd.ops import hip as H
+    x = _rand(256, 128, dtype=torch.float32, seed=46)
+    wi = (_rand(128, 512, dtype=torch.float32, seed=47) * 0.05).requires_grad_()
+    wo = (_rand(512, 128, dtype=torch.float32, seed=48) * 0.05).requires_grad_()
+    calls = []
+    orig = H._cast_raw
+    H._cast_raw = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+    try:
+        y = F._FFBlockFp8.apply(x, wi, wo, x)
+    finally:
+        H._cast_raw = orig
+    assert not calls
+    wi2 = wi.detach().clone().requires_grad_()
+    wo2 = wo.detach().clone().requires_grad_()
+    xb = x.bfloat16()
+    y2 = F._FFBlockFp8.apply(xb, wi2, wo2, xb)
+    assert torch.equal(y, y2)
+    y.float().sum().backward()
+    y2.float().sum().backward()
+    assert torch.equal(wi.grad, wi2.grad) and torch.equal(wo.grad, wo2.grad)
+
+
 @pytest.mark.parametrize("tile", [1282, 1283, 2562, 2563])
 @pytest.mark.parametrize("M,N,K", [(128, 128, 128), (300, 136, 256), (1024, 2560, 640), (512, 640, 2560)])
 @pytest.mark.parametrize("bias,relu,out_f32", [(False, False, True), (True, True, False)])
