@@ -72,9 +72,6 @@ struct AttnArgs {
   FastDiv fd_nx, fd_h;  // resident forward: its query-block count and H as launch-constant divisors
 };
 
-#ifndef LJS_ATTN_FASTIDX
-#define LJS_ATTN_FASTIDX 0   // (A/B) the resident forward's tile decode by launch-constant divisors
-#endif
 // A/B switches (compile-time): the resident forward's key loop fully unrolled at 256 keys, and
 // the fused backward's dQ slices without per-slice guards when all 256 keys are valid
 #ifndef LJS_ATTN_FWD_UNROLL
@@ -435,11 +432,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Vs[FKR * D];
   constexpr int QB = 16 * NW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#if LJS_ATTN_FASTIDX
+  // tile decode by launch-constant divisors (Granlund-Montgomery, FastDiv): B=64 step 0.1968-0.1990
+  // vs 0.1975-0.2017 ms with integer divisions, x3 interleaved (gpurun_out/r6e)
   const Tile3 tl = tile3f(a.fd_nx, a.fd_h);
-#else
-  const Tile3 tl = tile3((a.Sq + QB - 1) / QB, a.H);
-#endif
   const int qb = tl.x, h = tl.h, b = tl.b;
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
@@ -459,7 +454,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
     const u32x4 rk = rsrc_u4(kb, 2 * ((long)(a.Sk - 1) * a.k_ss + D));
     const u32x4 rv = rsrc_u4(vb, 2 * ((long)(a.Sk - 1) * a.v_ss + D));
     const int npieces = nkt * (BLK / 8);  // 8 rows x 128 B per 1 KiB piece, key-tile major
-#if LJS_ATTN_FASTIDX
     // 32-bit offsets (the launcher checks (Sk - 1) x stride x 2 + 128 < 2^31 for this kernel); the
     // full 256-key case unrolled, so each piece's offset is a lane constant plus an immediate
     const int ks32 = (int)a.k_ss, vs32 = (int)a.v_ss;
@@ -482,15 +476,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
         dma_lds_x4(rv, ok ? (row * vs32 + c) * 2 : 0x7ffffff0, Vs + pc * 512);
       }
     }
-#else
-    for (int pc = wave; pc < npieces; pc += NW) {
-      const int row = 8 * pc + (lane >> 3);
-      const int c = ((lane & 7) ^ (((row >> 1) & 3) << 1)) * 8;
-      const bool ok = row < a.Sk;
-      dma_lds_x4(rk, ok ? (int)(((long)row * a.k_ss + c) * 2) : 0x7ffffff0, Ks + pc * 512);
-      dma_lds_x4(rv, ok ? (int)(((long)row * a.v_ss + c) * 2) : 0x7ffffff0, Vs + pc * 512);
-    }
-#endif
   }
   FwdState st;
 #pragma unroll

@@ -953,12 +953,6 @@ gemm_dma_group2_kernel(GemmArgs p0, GemmArgs p1, int g0) {
 // The issue cursor's K-tiles past the block's last item go through a buffer descriptor with an
 // empty range: every lane is out of range whatever its offsets, so the pieces read zeros without a
 // memory access and retire at once (the block's final vmcnt(0) does not wait for an L2 round trip).
-#ifndef LJS_GEMM_MF32_DEFAULT
-#define LJS_GEMM_MF32_DEFAULT 0   // (variant builds: the 32x32x16 lean kernel where it applies)
-#endif
-#ifndef LJS_GEMM_SGB
-#define LJS_GEMM_SGB 0
-#endif
 template <int BM, int BN, int WM, int WN, int NST, int RES>
 __global__ __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
 gemm_lean_kernel(GemmArgs p) {
@@ -1062,42 +1056,6 @@ gemm_lean_kernel(GemmArgs p) {
     __builtin_amdgcn_s_barrier();
   };
 
-  // LJS_GEMM_SGB (compile-time A/B, verdict r5 item 2b): the k-step's fragment reads, DMA issues
-  // and MFMAs placed by sched_group_barrier instead of the compiler's order -- first half: one
-  // ds_read per NMF / NR MFMAs; second half: the next tile's k-step-0 reads one per MFMA, then the
-  // DMA pieces spread over the remaining MFMAs
-  constexpr int NR = TM + TN, NMF = TM * TN;
-  auto sgb_first = [&]() {
-#if LJS_GEMM_SGB
-    constexpr int per = NMF / NR > 0 ? NMF / NR : 1;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-      __builtin_amdgcn_sched_group_barrier(0x008, per, 0); // MFMA
-    }
-    if constexpr (NMF > per * NR) __builtin_amdgcn_sched_group_barrier(0x008, NMF - per * NR, 0);
-#endif
-  };
-  auto sgb_second = [&]() {
-#if LJS_GEMM_SGB
-    constexpr int r1 = NR < NMF ? NR : NMF;          // reads, one per MFMA
-    constexpr int rest = NMF - r1;
-    constexpr int per = rest / L > 0 ? rest / L : 1;
-#pragma unroll
-    for (int i = 0; i < r1; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-    }
-    if constexpr (NR > r1) __builtin_amdgcn_sched_group_barrier(0x100, NR - r1, 1);
-#pragma unroll
-    for (int i = 0; i < L; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);   // VMEM read (the LDS-DMA pieces)
-      __builtin_amdgcn_sched_group_barrier(0x008, per, 1);
-    }
-    if constexpr (rest > per * L) __builtin_amdgcn_sched_group_barrier(0x008, rest - per * L, 1);
-#endif
-  };
-
   // the stage of the (virtual) tile before the block's first: the first item start issues the
   // DMA of tile NST - 1 into it
   int so = (NST - 1) * STAGE;
@@ -1123,7 +1081,6 @@ gemm_lean_kernel(GemmArgs p) {
     for (int kk = 0; kk + 1 < nk; ++kk) {
       read_frags(so, 1, la, lb);
       mfmas(ka, kb);
-      sgb_first();
       const int nso = next_so(so);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");  // tile f + 1 landed
       barrier();                                   // ... for every wave; every read of tile f done
@@ -1131,7 +1088,6 @@ gemm_lean_kernel(GemmArgs p) {
       issue_a(so);                                 // tile f + NST into tile f's stage
       mfmas(la, lb);
       issue_b(so);
-      sgb_second();
       advance();
       so = nso;
     }
@@ -1245,235 +1201,6 @@ gemm_lean_kernel(GemmArgs p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ============================================================================ lean K-loop, 32x32x16 MFMA
-// The lean kernel on v_mfma_f32_32x32x16_bf16 (verdict r5 item 2a): per K-tile a wave issues half
-// the MFMA instructions of the 16x16x32 form (each covers a 32x32 block over 16 k, twice the work
-// in twice the cycles) and reads the same LDS bytes (a 32-row fragment per 16 k instead of a
-// 16-row one per 32 k, from the same swizzled image: conflict-free for ds_read_b128 -- a 16-lane
-// group's rows r, r + 1 share a 16-byte position (r >> 1) & 7 ^ c in opposite 128-byte halves).
-// Four k-steps per K-tile, fragments double-buffered one k-step ahead; the k-step 3 fragments
-// are read BEFORE the tile's barrier, so every read of the stage the next DMA refills is done
-// when the barrier releases.  Accumulator layout (operands swapped: D = C^T blocks): lane l holds
-// output row m = l & 31 and columns n = (r & 3) + 8 (r >> 2) + 4 (l >> 5), r = 0..15; lanes l and
-// l ^ 32 trade 4-column groups with one v_permlane32_swap per element so each ends with 8
-// consecutive columns (16-byte bf16 stores).  Compile-time plain (RES 3) and bias + fused sum
-// (RES 4) epilogues.  Same numerics as the 16x16x32 kernels up to f32 summation order (each MFMA
-// accumulates 16 products instead of 32 per step): tested against fp32 references.
-template <int R>
-__device__ __forceinline__ bf16x8 frag32(const bf16_t* lds, int rb, int ks, int lane) {
-  const int row = rb + (lane & 31);
-  const int kc = ks * 2 + (lane >> 5);
-  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + row * BK + swz_k(row, kc) * 8));
-}
-
-template <int BM, int BN, int WM, int WN, int NST, int RES>
-__global__ __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NST * (BM + BN) * 64 * 2 <= 80 * 1024) ? 2 : 1) void
-gemm_lean32_kernel(GemmArgs p) {
-  static_assert(RES == 3 || RES == 4, "plain or bias + fused-sum epilogue");
-  constexpr int NW = WM * WN;
-  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  static_assert(TM >= 1 && TN >= 1 && (BM / WM) % 32 == 0 && (BN / WN) % 32 == 0, "32x32 blocks per wave");
-  constexpr int A_TILE = BM * BK, B_TILE = BN * BK, STAGE = A_TILE + B_TILE;
-  using TA = DmaTile<BM, true, NW>;
-  using TB = DmaTile<BN, true, NW>;
-  constexpr int L = TA::PER_WAVE + TB::PER_WAVE;
-  static_assert(NST >= 2, "at least one K-tile in flight");
-  constexpr int S_EPI = TM * TN * 2;   // 16-byte stores per lane per item
-  static_assert(L * (NST - 1) + S_EPI + 1 <= 63, "vmcnt immediate range");
-  constexpr bool BSUM = RES == 4;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave / WN, wc = wave % WN;
-  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
-  const int items = p.batch * ntm * ntn;
-  const int G = gridDim.x;
-  const int slot = xcd_remap(blockIdx.x, G);
-  const int my_items = slot < items ? (items - slot + G - 1) / G : 0;
-  if (my_items == 0) return;
-  const int nk = p.kt_per_split;
-
-  const long a_bytes = 2 * ((long)(p.M - 1) * p.lda + p.K);
-  const long b_bytes = 2 * ((long)(p.N - 1) * p.ldb + p.K);
-  TA ta;
-  TB tb;
-  ta.init(p.lda, wave, lane);
-  tb.init(p.ldb, wave, lane);
-
-  int is_item = 0, is_kt = 0;
-  __amdgpu_buffer_rsrc_t ra, rb;
-  int a_off = 0, b_off = 0;
-  auto load_item = [&](int k) {
-    const WorkItem w = decode_item(p, slot + G * (k < my_items ? k : 0), ntm, ntn);
-    ra = make_rsrc(p.A + (long)w.b * p.sA, a_bytes);
-    rb = make_rsrc(p.B + (long)w.b * p.sB, b_bytes);
-    a_off = __builtin_amdgcn_readfirstlane((int)((long)w.m0 * BM * p.lda * 2));
-    b_off = __builtin_amdgcn_readfirstlane((int)((long)w.n0 * BN * p.ldb * 2));
-    if (k >= my_items) {   // past the block's last item: an empty range (every piece reads zeros)
-      ra = make_rsrc(p.A, 0);
-      rb = make_rsrc(p.B, 0);
-    }
-  };
-  auto issue_a = [&](int so) { ta.issue(ra, smem + so, a_off, wave); };
-  auto issue_b = [&](int so) { tb.issue(rb, smem + so + A_TILE, b_off, wave); };
-  auto advance = [&]() {
-    a_off += BK * 2;
-    b_off += BK * 2;
-    if (++is_kt == nk) {
-      is_kt = 0;
-      load_item(++is_item);
-    }
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  load_item(0);
-#pragma unroll
-  for (int s = 0; s < NST - 1; ++s) {
-    issue_a(s * STAGE);
-    issue_b(s * STAGE);
-    advance();
-  }
-  const bool st_sc1 = p.flags & 32;
-  const bool psum_on = BSUM && p.psum != nullptr;
-  const __amdgpu_buffer_rsrc_t rc = make_rsrc(p.C, 2 * ((long)(p.batch - 1) * p.sC + (long)(p.M - 1) * p.ldc + p.N));
-
-  bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-  auto read_frags = [&](int so, int ks, bf16x8* af, bf16x8* bfr) {
-    const bf16_t* As_ = smem + so;
-    const bf16_t* Bs_ = As_ + A_TILE;
-#pragma unroll
-    for (int ii = 0; ii < TM; ++ii) af[ii] = frag32<BM>(As_, wr * (BM / WM) + ii * 32, ks, lane);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bfr[j] = frag32<BN>(Bs_, wc * (BN / WN) + j * 32, ks, lane);
-  };
-  auto mfmas = [&](const bf16x8* af, const bf16x8* bfr) {
-#pragma unroll
-    for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[ii], acc[ii][j], 0, 0, 0);  // C^T block
-  };
-  auto next_so = [](int so) { return so + STAGE == NST * STAGE ? 0 : so + STAGE; };
-  auto barrier = []() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-
-  int so = (NST - 1) * STAGE;
-  auto item_start = [&](bool after_epi) {
-    if (!after_epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");
-    else if (psum_on) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2) + S_EPI + 1) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2) + S_EPI) : "memory");
-    barrier();
-    const int nso = next_so(so);
-    read_frags(nso, 0, fa0, fb0);
-    issue_a(so);
-    issue_b(so);
-    advance();
-    so = nso;
-  };
-  item_start(false);
-
-  float tsum = 0.f;
-  for (int it = 0; it < my_items; ++it) {
-    for (int kk = 0; kk + 1 < nk; ++kk) {
-      read_frags(so, 1, fa1, fb1);
-      mfmas(fa0, fb0);
-      read_frags(so, 2, fa0, fb0);
-      mfmas(fa1, fb1);
-      read_frags(so, 3, fa1, fb1);
-      mfmas(fa0, fb0);
-      const int nso = next_so(so);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NST - 2)) : "memory");  // tile f + 1 landed
-      barrier();                                   // ... for every wave; every read of tile f done
-      read_frags(nso, 0, fa0, fb0);
-      issue_a(so);                                 // tile f + NST into tile f's stage
-      mfmas(fa1, fb1);
-      issue_b(so);
-      advance();
-      so = nso;
-    }
-    // the item's last K-tile
-    read_frags(so, 1, fa1, fb1);
-    mfmas(fa0, fb0);
-    read_frags(so, 2, fa0, fb0);
-    mfmas(fa1, fb1);
-    read_frags(so, 3, fa1, fb1);
-    mfmas(fa0, fb0);
-    mfmas(fa1, fb1);
-
-    // ------------------------------------------------------------ epilogue of this item
-    const WorkItem w = decode_item(p, slot + G * it, ntm, ntn);
-    const int m0 = w.m0 * BM + wr * (BM / WM), n0 = w.n0 * BN + wc * (BN / WN);
-    const int h = lane >> 5;
-#pragma unroll
-    for (int ii = 0; ii < TM; ++ii) {
-      const int row = m0 + ii * 32 + (lane & 31);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          // register groups 2q (cols 16q + 4h ..) and 2q + 1 (cols 16q + 8 + 4h ..): after the swap
-          // lane h = 0 holds cols 16q .. 16q + 7, lane h = 1 cols 16q + 8 .. 16q + 15
-          float v[8];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[ii][j][8 * q + e]),
-                                                            __float_as_uint(acc[ii][j][8 * q + 4 + e]), false, false);
-            v[e] = __uint_as_float(r[0]);
-            v[4 + e] = __uint_as_float(r[1]);
-          }
-          const int col = n0 + 32 * j + 16 * q + 8 * h;
-          if constexpr (BSUM) {
-            const long bo = (long)w.b * p.sBias + col;
-            const bool bias_vec = ((((uintptr_t)p.bias) & 15) == 0) && (p.sBias % 8) == 0 && col + 8 <= p.N;
-            const float* bp = reinterpret_cast<const float*>(p.bias);
-            if (bias_vec) {
-              const f32x4 lo = *reinterpret_cast<const f32x4*>(bp + bo);
-              const f32x4 hi = *reinterpret_cast<const f32x4*>(bp + bo + 4);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                v[e] += lo[e];
-                v[4 + e] += hi[e];
-              }
-            } else {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] += col + e < p.N ? bp[bo + e] : 0.f;
-            }
-          }
-          u32x4 pk;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
-          const bool ok = row < p.M && col < p.N;  // N % 8 == 0 (launcher): chunks are whole
-          const int off = ok ? (int)(((long)w.b * p.sC + (long)row * p.ldc + col) * 2) : 0x7ffffff0;
-          if (st_sc1) __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, kSC1);
-          else __builtin_amdgcn_raw_buffer_store_b128(pk, rc, off, 0, 0);
-          if (psum_on && ok) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) tsum += __uint_as_float(pk[e] << 16) + __uint_as_float(pk[e] & 0xffff0000u);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;
-      }
-    }
-    if (psum_on) {
-      tsum = warp_sum64(tsum);
-      if (lane == 0) p.psum[(long)(slot + G * it) * NW + wave] = tsum;
-      tsum = 0.f;
-    }
-    if (it + 1 < my_items) item_start(true);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 // explicit instantiations: hipcc (ROCm 7.2) otherwise leaves some of these kernels' host stubs
 // undefined when they are only named inside launch_dma's instantiations
@@ -1554,16 +1281,6 @@ LJS_LEAN_INST(128, 128, 2, 4, 3)
 LJS_LEAN_INST(128, 128, 2, 4, 4)
 LJS_LEAN_INST(64, 64, 2, 2, 4)
 #undef LJS_LEAN_INST
-#define LJS_LEAN32_INST(BM, BN, WM, WN, NST)                                  \
-  template __global__ void gemm_lean32_kernel<BM, BN, WM, WN, NST, 3>(GemmArgs); \
-  template __global__ void gemm_lean32_kernel<BM, BN, WM, WN, NST, 4>(GemmArgs);
-LJS_LEAN32_INST(256, 128, 4, 2, 3)
-LJS_LEAN32_INST(256, 192, 4, 2, 2)
-LJS_LEAN32_INST(128, 160, 4, 1, 2)
-LJS_LEAN32_INST(128, 128, 2, 2, 2)
-LJS_LEAN32_INST(128, 128, 2, 4, 3)
-LJS_LEAN32_INST(128, 128, 2, 4, 4)
-#undef LJS_LEAN32_INST
 #undef LJS_DMA_INST_LAYOUTS
 #undef LJS_DMA_INST
 
@@ -1698,39 +1415,6 @@ hipError_t launch_lean(const GemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int NST, int RES>
-hipError_t launch_lean32(const GemmArgs& a, hipStream_t s) {
-  if (!g_cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (g_cus <= 0) g_cus = 256;
-  }
-  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
-  const int items = ntm * ntn * a.batch;
-  GemmArgs a2 = a;
-  if (ntm < ntn) a2.flags |= kMFast;
-  constexpr int kLdsBytes = NST * (BM + BN) * BK * 2;
-  constexpr int kNatural = (WM * WN == 4 && kLdsBytes <= 80 * 1024) ? 2 : 1;
-  int grid = items;
-  if (items > g_cus * kNatural && items % (g_cus * kNatural) == 0) grid = g_cus * kNatural;
-  hipLaunchKernelGGL((gemm_lean32_kernel<BM, BN, WM, WN, NST, RES>), dim3(grid), dim3(WM * WN * 64), 0, s, a2);
-  return hipGetLastError();
-}
-
-// the 32x32x16 lean kernel where its epilogue applies (plain, or f32 bias + fused sum); else the
-// 16x16x32 one
-template <int BM, int BN, int WM, int WN, int NST>
-hipError_t launch_lean32_kk(const GemmArgs& a, hipStream_t s, bool* done) {
-  *done = true;
-  if (!(a.flags & (kResAdd | kResMask))) {
-    if (a.alpha == 1.f && !(a.flags & 3) && !a.psum) return launch_lean32<BM, BN, WM, WN, NST, 3>(a, s);
-    if (a.alpha == 1.f && (a.flags & 7) == 6) return launch_lean32<BM, BN, WM, WN, NST, 4>(a, s);
-  }
-  *done = false;
-  return hipSuccess;
-}
-
 template <int BM, int BN, int WM, int WN, int NST>
 hipError_t launch_lean_kk(const GemmArgs& a, hipStream_t s) {
   if (a.flags & (kResAdd | kResMask)) {
@@ -1835,8 +1519,6 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
   }
   if (psum_count) *psum_count = 0;
   // A/B: tile code + 100000 forces the lean K-loop kernel where it applies, + 200000 the general one
-  const bool mf32_req = tile >= 300000;
-  if (mf32_req) tile -= 300000;
   const bool gen_req = tile >= 200000;
   if (gen_req) tile -= 200000;
   const bool lean_req = tile >= 100000;
@@ -1902,20 +1584,7 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     if (psum_count) *psum_count = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch * a.splitk * nw;
   }
   // the lean K-loop kernel for the k-contiguous bf16-output LDS-DMA tiles without split-K
-  // (tile code + 100000 forces the lean one, + 200000 the general one, + 300000 the 32x32x16 lean
-  // one: A/B and bit-exact tests)
-  if ((mf32_req || (LJS_GEMM_MF32_DEFAULT && !lean_req && !gen_req)) && a_kc && b_kc && !out_f32 && a.splitk == 1 &&
-      !(flags & kBPtrs) && dma_ok && dma_store_ok) {
-    bool done = false;
-    hipError_t e32 = hipSuccess;
-    if (tile == 2561) e32 = launch_lean32_kk<256, 128, 4, 2, 3>(a, stream, &done);
-    else if (tile == 2562) e32 = launch_lean32_kk<256, 192, 4, 2, 2>(a, stream, &done);
-    else if (tile == 1602) e32 = launch_lean32_kk<128, 160, 4, 1, 2>(a, stream, &done);
-    else if (tile == 1282) e32 = launch_lean32_kk<128, 128, 2, 2, 2>(a, stream, &done);
-    else if (tile == 12883) e32 = launch_lean32_kk<128, 128, 2, 4, 3>(a, stream, &done);
-    else if (tile == 12884) e32 = launch_lean32_kk<128, 128, 2, 4, 4>(a, stream, &done);
-    if (done) return (int)e32;
-  }
+  // (tile code + 100000 forces the lean one, + 200000 the general one: A/B and bit-exact tests)
   if (!gen_req && a_kc && b_kc && !out_f32 && a.splitk == 1 && !(flags & kBPtrs) && dma_ok &&
       dma_store_ok) {
     if (tile == 2561) return (int)launch_lean_kk<256, 128, 4, 2, 3>(a, stream);
