@@ -514,6 +514,207 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
   }
 }
 
+// ============================================================================ fused Q/K/V projection + forward
+// One workgroup item = one (batch, head) of a self-attention block whose sequence is exactly 256
+// tokens: the projection GEMM's 256 x 192 output tile [Q_h | K_h | V_h] (x rows b*256.., the three
+// stacked transposed weights' rows h*64..) and then the attention forward of that head over it,
+// from LDS.  The Q/K/V tile still goes to global memory (the backward reads it, and it is the
+// dense's output), but the forward's read of it back from HBM / L2 (Q, K, V: 3/4 of the forward's
+// bytes) and the separate kernel's load phase are gone, and the projection's store tail overlaps
+// the attention math of the same block.
+//   * GEMM: 8 waves of 64 x 96 (4 x 2), 16x16x32 bf16 MFMA with the B rows as the MFMA A operand
+//     (C^T blocks), K-tiles of 64 by LDS-DMA into a two-slot ring [0, 56 KiB) / [96 KiB, 152 KiB),
+//     one K-tile in flight -- the same per-element MFMA sequence as gemm_lean_kernel<256, 192>, so
+//     the Q/K/V values are bit-identical to the unfused projection;
+//   * epilogue: bf16 rows to global [T][3N] and into LDS images Q / K / V [256][64] (img16
+//     swizzle) over [0, 96 KiB) -- the next item's first K-tile streams into the other slot;
+//   * attention: wave w owns queries 32 w .. 32 w + 31 (two 16-query sub-tiles), key tiles in
+//     order through fwd_tile<false> (the resident forward's per-query sequence: bit-identical O and
+//     lse), O staged through the wave's own (consumed) Q rows and stored as whole 128-byte rows.
+struct QkvAttnArgs {
+  const bf16_t* x;   // [T][K] bf16, row stride ldx
+  const bf16_t* w;   // [3][N][K] bf16: transposed Q / K / V weights, k-contiguous
+  bf16_t* qkv;       // [T][3N]: Q | K | V column blocks
+  bf16_t* o;         // [T][N] = [B][S][H][D]
+  float* lse;        // [B][H][S]
+  int T, K, N, H, ldx;
+  float scale_log2;
+};
+
+constexpr int QA_S = 256, QA_BN = 192, QA_BK = 64;
+constexpr int QA_A_TILE = QA_S * QA_BK, QA_STAGE = (QA_S + QA_BN) * QA_BK;   // elements
+constexpr int QA_SLOT_C = 48 * 1024;                                          // elements (96 KiB)
+constexpr int QA_LDS = QA_SLOT_C + QA_STAGE;                                  // 152 KiB
+
+__device__ __forceinline__ int qa_swz(int row, int c16) { return c16 ^ ((row >> 1) & 7); }
+
+__global__ __launch_bounds__(512, 1) void qkv_attn_fwd_kernel(QkvAttnArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[QA_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int items = (p.T / QA_S) * p.H;
+  const int G = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, G);
+  const int my_items = slot < items ? (items - slot + G - 1) / G : 0;
+  if (my_items == 0) return;
+  const int nk = p.K / QA_BK;   // even (launcher): tile t of an item lands in slot C (even t) / A (odd t)
+
+  // LDS-DMA pieces (8 rows x 128 B): A 32 per K-tile (4 per wave), B 24 (3 per wave)
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.x, 2 * ((long)(p.T - 1) * p.ldx + p.K));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.w, 2 * (3L * p.N * p.K));
+  int va[4], vb[3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (wave + 8 * i) + (lane >> 3), c = lane & 7;
+    va[i] = (row * p.ldx + 8 * qa_swz(row, c)) * 2;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int row = 8 * (wave + 8 * i) + (lane >> 3), c = lane & 7;   // B-tile row: weight row / 64, row % 64
+    vb[i] = ((((row >> 6) * p.N) + (row & 63)) * p.K + 8 * qa_swz(row, c)) * 2;
+  }
+  auto item_of = [&](int k) { return slot + G * k; };
+  // K-tile kt of item k into its slot (the item's row / column bases as the uniform offset)
+  auto issue = [&](int k, int kt) {
+    const int it = item_of(k);
+    const int b = it / p.H, h = it - b * p.H;
+    bf16_t* st = smem + ((kt & 1) ? 0 : QA_SLOT_C);
+    const int sa = __builtin_amdgcn_readfirstlane(b * QA_S * p.ldx * 2 + kt * QA_BK * 2);
+    const int sb = __builtin_amdgcn_readfirstlane(h * 64 * p.K * 2 + kt * QA_BK * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_PTR(void))(st + (wave + 8 * i) * 512), 16, va[i], sa, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_PTR(void))(st + QA_A_TILE + (wave + 8 * i) * 512), 16, vb[i],
+                                               sb, 0, 0);
+  };
+  auto frag = [&](const bf16_t* img, int rb0, int ks) {
+    const int row = rb0 + (lane & 15), kc = ks * 4 + (lane >> 4);
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(img + row * QA_BK + qa_swz(row, kc) * 8));
+  };
+
+  AttnArgs a = {};
+  a.out = p.o;
+  a.lse = p.lse;
+  a.H = p.H;
+  a.Sq = QA_S;
+  a.Sk = QA_S;
+  a.o_sb = (long)QA_S * p.N;
+  a.o_ss = p.N;
+  a.o_sh = D;
+  a.scale_log2 = p.scale_log2;
+  bf16_t* const Qi = smem;               // [256][64] images, img16 swizzle
+  bf16_t* const Ki = smem + QA_S * D;
+  bf16_t* const Vi = smem + 2 * QA_S * D;
+
+  auto barrier = []() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  bf16x8 ka[4], kb[6], la[4], lb[6];
+  auto read_frags = [&](int kt, int ks, bf16x8* af, bf16x8* bfr) {
+    const bf16_t* As = smem + ((kt & 1) ? 0 : QA_SLOT_C);
+    const bf16_t* Bs = As + QA_A_TILE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(As, wr * 64 + i * 16, ks);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) bfr[j] = frag(Bs, wc * 96 + j * 16, ks);
+  };
+  f32x4 acc[4][6];
+  auto mfmas = [&](const bf16x8* af, const bf16x8* bfr) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc[i][j] = mfma16x16x32(bfr[j], af[i], acc[i][j]);   // C^T blocks
+  };
+
+  issue(0, 0);
+  for (int k = 0; k < my_items; ++k) {
+    const int it = item_of(k);
+    const int b = it / p.H, h = it - b * p.H;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the lean K-loop (gemm_lean_kernel): k-step 1's fragments are read under k-step 0's MFMAs,
+    // the next tile's k-step 0 under k-step 1's; one K-tile in flight.  Item start: tile 0 landed
+    // for every wave (and every wave is done with the previous item's images, which tile 1 covers)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    read_frags(0, 0, ka, kb);
+    issue(k, 1);
+    for (int kt = 0; kt + 1 < nk; ++kt) {
+      read_frags(kt, 1, la, lb);
+      mfmas(ka, kb);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile kt + 1 landed (this wave's pieces)
+      barrier();                                           // ... every wave's; tile kt's reads done
+      read_frags(kt + 1, 0, ka, kb);
+      if (kt + 2 < nk) issue(k, kt + 2);                   // into tile kt's slot
+      else if (k + 1 < my_items) issue(k + 1, 0);          // slot C (tile nk - 2's; nk is even)
+      mfmas(la, lb);
+    }
+    read_frags(nk - 1, 1, la, lb);
+    mfmas(ka, kb);
+    mfmas(la, lb);
+    // ---- epilogue: every wave is done with the last tile's slot (A) before the images cover it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    {
+      const int g = lane >> 4;
+      const bool even = (g & 1) == 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wr * 64 + i * 16 + (lane & 15);
+        bf16_t* grow = p.qkv + (long)(b * QA_S + r) * (3 * p.N);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int c = wc * 96 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);   // 8 columns, one of Q / K / V
+          float v[8];
+          pair_rows16(acc[i][2 * q], acc[i][2 * q + 1], even, v);
+          u32x4 pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+          const int which = c >> 6, d = c & 63;
+          *reinterpret_cast<u32x4*>(grow + which * p.N + h * D + d) = pk;
+          *reinterpret_cast<u32x4*>(smem + which * QA_S * D + img16(r, d >> 3)) = pk;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // ---- attention over the images: wave w, queries 32 w + 16 s + (lane & 15)
+    {
+      FwdState st[2];
+      bf16x8 qf[2][2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st[s].o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        st[s].m = -INFINITY;
+        st[s].l = 0.f;
+        qf[s][0] = frag_rows(Qi, 32 * wave + 16 * s, 0, lane);
+        qf[s][1] = frag_rows(Qi, 32 * wave + 16 * s, 1, lane);
+      }
+#pragma unroll 1
+      for (int kt = 0; kt < QA_S / BLK; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          fwd_tile<false>(a, st[s], Ki + kt * BLK * D, Vi + kt * BLK * D, qf[s], kt * BLK, 32 * wave + 16 * s + (lane & 15),
+                          lane);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const float lt = row4_sum(st[s].l);
+        // O through this wave's own Q rows (read into qf above, by this wave only)
+        fwd_store_vst(a, st[s].o, st[s].m, lt, b, h, 32 * wave + 16 * s, lane, Qi + (32 * wave + 16 * s) * D);
+      }
+    }
+    // (the next item's first barrier orders these image reads before its tile 1 covers them)
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Block = 4 waves x NSUB sub-tiles of 16 queries (64 NSUB queries of one head).  Each K/V tile
 // staged through LDS serves all NSUB sub-tiles of every wave (NSUB x fewer K/V loads per
 // query).  Sub-tile s of wave w holds queries 16 (4 s + w) + lane,
@@ -1701,6 +1902,7 @@ LJS_API void ljs_attn_set_vst(int v) { g_vst = v < 0 ? 1 : v; }
 static bool vst_ok(const void* p, const long* st) {
   return (((uintptr_t)p) & 15) == 0 && st[0] % 8 == 0 && st[1] % 8 == 0 && st[2] % 8 == 0;
 }
+static int g_attn_cus = 0;   // CUs of the current device (the fused projection's grid)
 //  * K/V-resident forward for Sk <= 256: 8 (or 4) waves per block; 0 = the tiled kernel
 static int g_fwd_res = 8;
 LJS_API void ljs_attn_set_fwd_res(int v) { g_fwd_res = v < 0 ? 8 : v; }
@@ -1771,6 +1973,32 @@ LJS_API int ljs_attn_fwd_acc(const void* q, const void* k, const void* v, void* 
                        stream);
 }
 
+
+// fused Q/K/V projection + attention forward (qkv_attn_fwd_kernel): x [T][K] bf16 (row stride
+// ldx), w [3][N][K] bf16 (the stacked transposed Q/K/V weights), N = H * 64, T = B * 256 tokens
+// (sequence 256, batch-major rows); writes qkv [T][3N], o [T][N] ([B][256][H][64]) and lse
+// [B][H][256] (log2 domain, as ljs_attn_fwd).  scale: the softmax scale.
+LJS_API int ljs_qkv_attn_fwd(const void* x, long ldx, const void* w, void* qkv, void* o, void* lse, int T, int K, int N,
+                             int H, float scale, hipStream_t stream) {
+  if (T <= 0 || T % QA_S || K < 2 * QA_BK || K % (2 * QA_BK) || N != H * D || H <= 0 || ldx < K || ldx % 8 ||
+      (((uintptr_t)x | (uintptr_t)w | (uintptr_t)qkv | (uintptr_t)o) & 15) ||
+      (long)T * ldx * 2 >= (1L << 31) || 3L * N * K * 2 >= (1L << 31))
+    return (int)hipErrorInvalidValue;
+  if (!g_attn_cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_attn_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_attn_cus <= 0) g_attn_cus = 256;
+  }
+  QkvAttnArgs a;
+  a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.qkv = (bf16_t*)qkv; a.o = (bf16_t*)o; a.lse = (float*)lse;
+  a.T = T; a.K = K; a.N = N; a.H = H; a.ldx = (int)ldx;
+  a.scale_log2 = scale * LOG2E;
+  const int items = T / QA_S * H;
+  const int grid = items < g_attn_cus ? items : g_attn_cus;   // one 8-wave block per CU, items dealt round-robin
+  hipLaunchKernelGGL(qkv_attn_fwd_kernel, dim3(grid), dim3(512), 0, stream, a);
+  return (int)hipGetLastError();
+}
 
 // dq/dk/dv outputs get their own strides; delta is a [B][H][Sq] f32 workspace
 LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,

@@ -515,8 +515,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
         amax = bf2f(f2bf(amax));
-        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
-        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        amax = row4_max(amax);   // lanes l, l ^ 16, l ^ 32, l ^ 48: two lane swaps, no ds_bpermute
         const int x = mx_exponent(amax);
         const float sc = mx_scale_pow2(x);
         u32x4 pb;
@@ -538,8 +537,7 @@ __global__ __launch_bounds__(BM * 2) void gemm_mx_fp8_kernel(F8Args p) {
           v[e] = bf2f(f2bf(v[e]));
           amax = fmaxf(amax, fabsf(v[e]));
         }
-        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
-        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        amax = row4_max(amax);   // lanes l, l ^ 16, l ^ 32, l ^ 48: two lane swaps, no ds_bpermute
         const int x = mx_exponent(amax);
         const float inv = ldexpf(1.f, -x);
         const u32x2 qq = u32x2{pack4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),

@@ -18,6 +18,7 @@ reference's literal einsum/softmax formulation (used by the parity tests).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Any, Optional
 
@@ -122,7 +123,14 @@ class MultiHeadAttention(Module):
                 ws = qkv_pf.tree()
             else:
                 ws = [wq, wk, wv]
-            query_proj, key_proj, value_proj = core.dense(hidden_states, ws, None, compute_dtype=dt)
+            # the attention forward rides in the projection kernel when every device holds whole
+            # sequences and all heads (ops/linear.attention_next: single device / data parallel)
+            from ..ops import linear as _lin
+            hint = (self.impl == "fused" and qkv_pf is None and hidden_states.ndim == 3
+                    and tuple(hidden_states.tile.tile_shape[1:]) == (1, 1)
+                    and all(tuple(w.tile.tile_shape) == (1, 1) for w in (wq, wk, wv)))
+            with (_lin.attention_next(self.heads, self.dim_head, self.scale) if hint else contextlib.nullcontext()):
+                query_proj, key_proj, value_proj = core.dense(hidden_states, ws, None, compute_dtype=dt)
             if qkv_pf is not None:
                 qkv_pf.wait()
         else:

@@ -26,6 +26,7 @@ Epilogue fusions (``hip.gemm``'s operand R):
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 from typing import List, Optional, Sequence, Tuple
@@ -87,6 +88,53 @@ def _splitk(M: int, N: int, K: int, batch: int, tile: int) -> int:
 
 
 _DW_SPLIT = 0   # (tests: force the K-chunk count)
+
+# The attention that follows a fused Q/K/V projection (models/attention.py announces it): the
+# projection then runs hip.qkv_attn_fwd -- the GEMM and each (batch, head)'s attention forward in
+# one kernel -- and leaves (o, lse) for the attention op (hip._take_fused_attention).
+# LJS_QKV_ATTN=0: the GEMM alone (the attention runs its own kernel).
+_QKV_ATTN = os.environ.get("LJS_QKV_ATTN", "1") != "0"
+_ATTN_NEXT: List[Optional[tuple]] = [None]
+
+
+@contextlib.contextmanager
+def attention_next(heads: int, dim_head: int, scale: float):
+    """Inside: a 3-weight dense whose outputs are the q / k / v of a non-causal self-attention
+    with ``heads`` x ``dim_head`` heads and softmax ``scale`` (fused when the shapes allow)."""
+    prev = _ATTN_NEXT[0]
+    _ATTN_NEXT[0] = (int(heads), int(dim_head), float(scale)) if _QKV_ATTN else None
+    try:
+        yield
+    finally:
+        _ATTN_NEXT[0] = prev
+
+
+def _fuse_attention_ok(x, xb, wt, nw, N, K, b, relu, res, od, out_dtype, wmajor, order, swap) -> Optional[tuple]:
+    fz = _ATTN_NEXT[0]
+    if fz is None or nw != 3 or b is not None or relu or res is not None or swap or wmajor:
+        return None
+    heads, dh, _ = fz
+    if not (od == torch.bfloat16 and out_dtype == torch.bfloat16 and x.is_cuda and x.dim() == 3
+            and order == (0, 1, 2) and x.shape[1] == 256 and dh == 64 and N == heads * 64 and K % 128 == 0
+            and xb.dtype == torch.bfloat16 and xb.stride(1) == 1 and xb.stride(0) % 8 == 0
+            and xb.data_ptr() % 16 == 0 and wt.is_contiguous() and wt.data_ptr() % 16 == 0):
+        return None
+    # one 8-wave block per CU over (batch, head) items: below one item per CU the fused kernel
+    # leaves CUs idle that the separate GEMM + attention fill (B = 8, 64 items: step 0.0796 vs
+    # 0.0732 ms; B = 64, 512 items: 0.1948-0.1966 vs 0.1999-0.2042, gpurun_out/r6g)
+    if (x.shape[0] * heads) < _cu_count(x.device):
+        return None
+    return fz
+
+
+_CUS: dict = {}
+
+
+def _cu_count(dev: torch.device) -> int:
+    n = _CUS.get(dev.index)
+    if n is None:
+        n = _CUS[dev.index] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return n
 # large bf16 dense outputs also carry their fused per-tile sums (see hip._PSUM): y.sum() is free
 _FUSED_SUM = os.environ.get("LJS_FUSED_SUM", "1") == "1"
 
@@ -640,9 +688,15 @@ class _Linear(torch.autograd.Function):
             r_ld = r2.stride(0)
             if nw != 1 or od != torch.bfloat16 or N % 8:
                 r2 = None
-        cnt = hip.gemm(xb, wt, out, M, N, K, K, K, N if wmajor else nw * N, True, True, batch=nw, sA=0, sB=sB,
-                       sC=M * N if wmajor else N, bias=bias, sBias=0, relu=relu, psum=partials, res=r2,
-                       res_ld=r_ld)
+        fz = _fuse_attention_ok(x, xb, wt, nw, N, K, b, relu, res, od, out_dtype, wmajor, order, swap)
+        if fz is not None:
+            o_att, lse_att = hip.qkv_attn_fwd(xb, wt, out, fz[0], fz[2])
+            hip.register_fused_attention(out, o_att, lse_att, fz[0], fz[2])
+            cnt = 0
+        else:
+            cnt = hip.gemm(xb, wt, out, M, N, K, K, K, N if wmajor else nw * N, True, True, batch=nw, sA=0, sB=sB,
+                           sC=M * N if wmajor else N, bias=bias, sBias=0, relu=relu, psum=partials, res=r2,
+                           res_ld=r_ld)
         cols = [out[i] if wmajor else out[:, i * N:(i + 1) * N] for i in range(nw)]
         ys = [c.view(pshape + (N,)).permute(inv) for c in cols]
         if res is not None and r2 is None:

@@ -533,3 +533,26 @@ def test_fp8_ff_block_2d_gathers_mx_shadows(gpu_devices):
         a, b = np.asarray(g1[k], np.float64), np.asarray(g4[k], np.float64)
         rel = np.linalg.norm(b - a) / max(np.linalg.norm(a), 1e-12)
         assert rel < 3e-2, (k, rel)
+
+
+def test_fused_qkv_attention_matches_unfused(gpu_devices, monkeypatch):
+    """The attention block with the attention forward fused into the Q/K/V projection kernel
+    (ops/linear.attention_next -> hip.qkv_attn_fwd) gives the loss and gradients of the separate
+    projection + attention kernels (up to the f32 rounding differences of the two forward kernels'
+    softmax state: see test_qkv_attn_fwd_bit_exact), and the fused result is what the attention op
+    used."""
+    from learning_jax_sharding_amd.ops import hip as H
+    from learning_jax_sharding_amd.ops import linear as L
+    res = {}
+    monkeypatch.setattr(L, "_cu_count", lambda dev: 1)   # (4 x 8 items: below the one-per-CU gate)
+    for on in (False, True):
+        monkeypatch.setattr(L, "_QKV_ATTN", on)
+        before = H.FUSED_ATTN_STATS["taken"]
+        res[on] = _run_block((1, 1), B=4, S=256)
+        res[(on, "taken")] = H.FUSED_ATTN_STATS["taken"] - before
+    assert res[(False, "taken")] == 0 and res[(True, "taken")] >= 1
+    assert abs(res[True][0] - res[False][0]) <= 1e-4 * abs(res[False][0])
+    fa, fb = res[True][1], res[False][1]
+    from learning_jax_sharding_amd.tree_util import tree_leaves
+    for a, b in zip(tree_leaves(fa), tree_leaves(fb)):
+        assert np.abs(a - b).max() <= 1e-2 * np.abs(b).max()

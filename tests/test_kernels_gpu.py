@@ -1375,3 +1375,44 @@ def test_gemm_lean_bit_exact(hip, tile, M, N, K, batch, mode):
     ref = (A.float() @ B.float().reshape(batch * N, K).t()) if batch > 1 else A.float() @ B[0].float().t()
     if mode == "plain":
         assert ((c1.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
+@pytest.mark.parametrize("B,H,K", [(2, 8, 640), (3, 2, 256), (5, 4, 128)])
+def test_qkv_attn_fwd_bit_exact(hip, B, H, K):
+    """The fused Q/K/V projection + attention forward (attention.hip qkv_attn_fwd_kernel) writes
+    the same Q/K/V bits as the batched projection GEMM (same per-element MFMA sequence) and O / lse
+    equal to the resident forward's over those views up to f32 rounding of the softmax state (a
+    handful of rows differ by one bf16 ulp: the two kernels' instruction selection for the running
+    sum differs), and as close to an fp32 reference; item counts below and above the CU count
+    exercise the block's item loop."""
+    T, N = B * 256, 64 * H
+    x = _rand(T, K, seed=31)
+    wt = (_rand(3, N, K, seed=32) * 0.05).contiguous()
+    out = torch.full((T, 3 * N), float("nan"), device=dev).bfloat16()
+    scale = 64 ** -0.5
+    o, lse = hip.qkv_attn_fwd(x, wt, out, H, scale)
+    ref = torch.empty_like(out)
+    hip.gemm(x, wt, ref, T, N, K, K, K, 3 * N, True, True, batch=3, sA=0, sB=N * K, sC=N)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    q, k, v = (ref.view(B, 256, 3, H, 64)[:, :, i] for i in range(3))
+    o_ref, lse_ref = hip.attn_fwd_lse(q, k, v, scale)
+    torch.cuda.synchronize()
+    o4 = o.view(B, 256, H, 64).float()
+    torch.testing.assert_close(o4, o_ref.float(), rtol=0, atol=4e-3)
+    assert ((o4 - o_ref.float()).abs().amax(-1) > 0).float().mean().item() < 0.02
+    torch.testing.assert_close(lse.view(B, H, 256), lse_ref, rtol=1e-6, atol=1e-5)
+    s_ = torch.einsum("bshd,bthd->bhst", q.float(), k.float()) * scale
+    o_t = torch.einsum("bhst,bthd->bshd", torch.softmax(s_, -1).bfloat16().float(), v.float())
+    assert (o4 - o_t).abs().max().item() <= 1.25 * (o_ref.float() - o_t).abs().max().item() + 1e-3
+
+
+def test_qkv_attn_fwd_rejects_bad_shapes(hip):
+    x = _rand(512, 640)
+    wt = _rand(3, 512, 640)
+    with pytest.raises(AssertionError):
+        hip.qkv_attn_fwd(x[:300], wt, torch.empty(300, 1536, dtype=torch.bfloat16, device=dev), 8, 0.125)
+    # the launcher's own checks (K not a multiple of 128)
+    rc = hip.lib().ljs_qkv_attn_fwd(hip._p(x), 640, hip._p(wt), hip._p(x), hip._p(x), hip._p(x), 512, 576, 512, 8,
+                                    0.125, None)
+    assert rc != 0
