@@ -358,6 +358,74 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
 }
 
 
+// fwd_tile for TWO 16-query sub-tiles over the same 64-key tile, in two halves so a caller can
+// issue the next key tile's score MFMAs (fwd_s2) before this tile's softmax and P.V (fwd_pv2):
+// each K / V fragment is read from LDS once for both sub-tiles.  Per query the same operations in
+// the same order as fwd_tile<false> (no masking: Sk % 64 == 0, non-causal).
+__device__ __forceinline__ void fwd_s2(f32x4 (&s)[2][4], const bf16_t* Kt, const bf16x8 (&qf)[2][2], int lane) {
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) {
+    const bf16x8 k0 = frag_rows(Kt, 16 * jt, 0, lane), k1 = frag_rows(Kt, 16 * jt, 1, lane);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      s[t][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      s[t][jt] = mfma16x16x32(k0, qf[t][0], s[t][jt]);
+      s[t][jt] = mfma16x16x32(k1, qf[t][1], s[t][jt]);
+    }
+  }
+}
+// the softmax update and P.V of fwd_tile2 on scores already computed by fwd_s2
+__device__ __forceinline__ void fwd_pv2(const AttnArgs& a, FwdState (&st)[2], f32x4 (&s)[2][4], const bf16_t* Vt,
+                                        int lane) {
+  const int g = lane >> 4;
+  bf16x8 pb[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float tmax = fmaxf(fmaxf(s[t][0][0], s[t][0][1]), fmaxf(s[t][0][2], s[t][0][3]));
+#pragma unroll
+    for (int jt = 1; jt < 4; ++jt)
+      tmax = fmaxf(tmax, fmaxf(fmaxf(s[t][jt][0], s[t][jt][1]), fmaxf(s[t][jt][2], s[t][jt][3])));
+    tmax = row4_max(tmax);
+    const float m_new = fmaxf(st[t].m, tmax * a.scale_log2);
+    const float m_use = m_new;
+    const float alpha = fast_exp2(st[t].m - m_use);
+    const f32x2 sc2 = {a.scale_log2, a.scale_log2}, mm2 = {m_use, m_use};
+    f32x2 ps2 = {0.f, 0.f};
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x2 x = pk_fms(f32x2{s[t][jt][2 * h], s[t][jt][2 * h + 1]}, sc2, mm2);
+        const f32x2 pv = {fast_exp2(x[0]), fast_exp2(x[1])};
+        s[t][jt][2 * h] = pv[0];
+        s[t][jt][2 * h + 1] = pv[1];
+        ps2 = pk_add(ps2, pv);
+      }
+    const float psum = ps2[0] + ps2[1];
+    const bool rescale = !__all(m_new == st[t].m);
+    st[t].l = st[t].l * alpha + psum;
+    st[t].m = m_new;
+    const f32x2 al2 = {alpha, alpha};
+#pragma unroll
+    for (int dt = 0; dt < 4 && rescale; ++dt) {
+      const f32x2 lo = pk_mul(f32x2{st[t].o[dt][0], st[t].o[dt][1]}, al2);
+      const f32x2 hi = pk_mul(f32x2{st[t].o[dt][2], st[t].o[dt][3]}, al2);
+      st[t].o[dt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+    }
+    pb[t][0] = frag_acc(s[t][0], s[t][1]);
+    pb[t][1] = frag_acc(s[t][2], s[t][3]);
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 va = frag_tr(Vt, 32 * s2 + 4 * g, 32 * s2 + 16 + 4 * g, 16 * dt, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) st[t].o[dt] = mfma16x16x32(va, pb[t][s2], st[t].o[dt]);
+    }
+  }
+}
+
 // forward epilogue of one query row (this lane's 16 d-values of it): normalise, and - for
 // blockwise / ring attention - merge with the running (O, lse) of the key blocks seen so far
 // (log-sum-exp in the log2 domain; +inf lse marks "no unmasked key yet"), all in registers.
@@ -539,7 +607,15 @@ struct QkvAttnArgs {
   float* lse;        // [B][H][S]
   int T, K, N, H, ldx;
   float scale_log2;
+  unsigned long long* trace;   // LJS_QA_TRACE builds: per (block, wave, item) 4 shader-clock stamps
 };
+
+#ifndef LJS_QA_PIPE
+#define LJS_QA_PIPE 1   // (A/B build define) 0: key tiles one after the other (no score-MFMA lookahead)
+#endif
+#ifndef LJS_QA_TRACE
+#define LJS_QA_TRACE 0   // (diagnostic build define) phase stamps: item start, K-loop end, epilogue end, attention end
+#endif
 
 constexpr int QA_S = 256, QA_BN = 192, QA_BK = 64;
 constexpr int QA_A_TILE = QA_S * QA_BK, QA_STAGE = (QA_S + QA_BN) * QA_BK;   // elements
@@ -630,10 +706,23 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_fwd_kernel(QkvAttnArgs p) {
       for (int j = 0; j < 6; ++j) acc[i][j] = mfma16x16x32(bfr[j], af[i], acc[i][j]);   // C^T blocks
   };
 
+  // (diagnostic builds) lane 0 of each wave stores a shader-clock stamp: a vector store under the
+  // lane-0 exec mask; items past the 8th of a block are not recorded
+  auto stamp = [&](int k, int ph) {
+#if LJS_QA_TRACE
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (p.trace && lane == 0 && k < 8) p.trace[(((long)blockIdx.x * 8 + wave) * 8 + k) * 4 + ph] = t;
+#else
+    (void)k;
+    (void)ph;
+#endif
+  };
+
   issue(0, 0);
   for (int k = 0; k < my_items; ++k) {
     const int it = item_of(k);
     const int b = it / p.H, h = it - b * p.H;
+    stamp(k, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -658,6 +747,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_fwd_kernel(QkvAttnArgs p) {
     read_frags(nk - 1, 1, la, lb);
     mfmas(ka, kb);
     mfmas(la, lb);
+    stamp(k, 1);
     // ---- epilogue: every wave is done with the last tile's slot (A) before the images cover it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -667,7 +757,6 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_fwd_kernel(QkvAttnArgs p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = wr * 64 + i * 16 + (lane & 15);
-        bf16_t* grow = p.qkv + (long)(b * QA_S + r) * (3 * p.N);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           const int c = wc * 96 + 16 * (even ? 2 * q : 2 * q + 1) + 4 * (g & ~1);   // 8 columns, one of Q / K / V
@@ -677,13 +766,22 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_fwd_kernel(QkvAttnArgs p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
           const int which = c >> 6, d = c & 63;
-          *reinterpret_cast<u32x4*>(grow + which * p.N + h * D + d) = pk;
           *reinterpret_cast<u32x4*>(smem + which * QA_S * D + img16(r, d >> 3)) = pk;
         }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    stamp(k, 2);
+    // the Q / K / V tile to global from the images as whole 128-byte rows (8 lanes per row),
+    // draining under the attention below.  Wave w copies rows 32 w .. 32 w + 31 of each image: its
+    // Q rows are exactly the ones it later overwrites with its own O staging (no other wave's)
+#pragma unroll 4
+    for (int i = 0; i < 12; ++i) {
+      const int which = i >> 2, r = 32 * wave + 8 * (i & 3) + (lane >> 3), c = lane & 7;
+      const u32x4 val = *reinterpret_cast<const u32x4*>(smem + which * QA_S * D + img16(r, c));
+      *reinterpret_cast<u32x4*>(p.qkv + (long)(b * QA_S + r) * (3 * p.N) + which * p.N + h * D + c * 8) = val;
+    }
     // ---- attention over the images: wave w, queries 32 w + 16 s + (lane & 15)
     {
       FwdState st[2];
@@ -697,12 +795,26 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_fwd_kernel(QkvAttnArgs p) {
         qf[s][0] = frag_rows(Qi, 32 * wave + 16 * s, 0, lane);
         qf[s][1] = frag_rows(Qi, 32 * wave + 16 * s, 1, lane);
       }
+      // key tiles software-pipelined by two: tile kt + 1's score MFMAs are issued before tile kt's
+      // softmax, so the MFMA pipe works while the VALU does the exponentials
+#if LJS_QA_PIPE
+      f32x4 sa[2][4], sb[2][4];
+      fwd_s2(sa, Ki, qf, lane);
 #pragma unroll 1
-      for (int kt = 0; kt < QA_S / BLK; ++kt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          fwd_tile<false>(a, st[s], Ki + kt * BLK * D, Vi + kt * BLK * D, qf[s], kt * BLK, 32 * wave + 16 * s + (lane & 15),
-                          lane);
+      for (int kt = 0; kt < QA_S / BLK; kt += 2) {
+        fwd_s2(sb, Ki + (kt + 1) * BLK * D, qf, lane);
+        fwd_pv2(a, st, sa, Vi + kt * BLK * D, lane);
+        if (kt + 2 < QA_S / BLK) fwd_s2(sa, Ki + (kt + 2) * BLK * D, qf, lane);
+        fwd_pv2(a, st, sb, Vi + (kt + 1) * BLK * D, lane);
+      }
+#else
+#pragma unroll 1
+      for (int kt = 0; kt < QA_S / BLK; ++kt) {
+        f32x4 sc[2][4];
+        fwd_s2(sc, Ki + kt * BLK * D, qf, lane);
+        fwd_pv2(a, st, sc, Vi + kt * BLK * D, lane);
+      }
+#endif
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const float lt = row4_sum(st[s].l);
@@ -710,6 +822,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_fwd_kernel(QkvAttnArgs p) {
         fwd_store_vst(a, st[s].o, st[s].m, lt, b, h, 32 * wave + 16 * s, lane, Qi + (32 * wave + 16 * s) * D);
       }
     }
+    stamp(k, 3);
     // (the next item's first barrier orders these image reads before its tile 1 covers them)
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1979,7 +2092,7 @@ LJS_API int ljs_attn_fwd_acc(const void* q, const void* k, const void* v, void* 
 // (sequence 256, batch-major rows); writes qkv [T][3N], o [T][N] ([B][256][H][64]) and lse
 // [B][H][256] (log2 domain, as ljs_attn_fwd).  scale: the softmax scale.
 LJS_API int ljs_qkv_attn_fwd(const void* x, long ldx, const void* w, void* qkv, void* o, void* lse, int T, int K, int N,
-                             int H, float scale, hipStream_t stream) {
+                             int H, float scale, void* trace, hipStream_t stream) {
   if (T <= 0 || T % QA_S || K < 2 * QA_BK || K % (2 * QA_BK) || N != H * D || H <= 0 || ldx < K || ldx % 8 ||
       (((uintptr_t)x | (uintptr_t)w | (uintptr_t)qkv | (uintptr_t)o) & 15) ||
       (long)T * ldx * 2 >= (1L << 31) || 3L * N * K * 2 >= (1L << 31))
@@ -1994,6 +2107,7 @@ LJS_API int ljs_qkv_attn_fwd(const void* x, long ldx, const void* w, void* qkv, 
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.qkv = (bf16_t*)qkv; a.o = (bf16_t*)o; a.lse = (float*)lse;
   a.T = T; a.K = K; a.N = N; a.H = H; a.ldx = (int)ldx;
   a.scale_log2 = scale * LOG2E;
+  a.trace = (unsigned long long*)trace;
   const int items = T / QA_S * H;
   const int grid = items < g_attn_cus ? items : g_attn_cus;   // one 8-wave block per CU, items dealt round-robin
   hipLaunchKernelGGL(qkv_attn_fwd_kernel, dim3(grid), dim3(512), 0, stream, a);

@@ -41,7 +41,7 @@ _SIGS = {
     "ljs_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, _LP, _LP, _LP, _LP,
                      c_float, c_int, c_int, c_void_p],
     "ljs_qkv_attn_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
-                         c_void_p],
+                         c_void_p, c_void_p],
     "ljs_attn_fwd_acc": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, _LP, _LP, _LP,
                          _LP, c_float, c_int, c_int, c_void_p, _LP, c_int, c_void_p],
     "ljs_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -1378,9 +1378,11 @@ def _bs_like(shape, ref: torch.Tensor) -> torch.Tensor:
 _FUSED_ATTN: Dict[tuple, tuple] = {}
 
 
-def qkv_attn_fwd(xb: torch.Tensor, wt: torch.Tensor, out: torch.Tensor, H: int, scale: float):
+def qkv_attn_fwd(xb: torch.Tensor, wt: torch.Tensor, out: torch.Tensor, H: int, scale: float,
+                 trace: Optional[torch.Tensor] = None):
     """out [T][3N] = xb [T][K] . wt[i]^T (wt: [3][N][K] bf16) AND the attention forward of every
-    (batch, head) over it (sequence 256): returns (o [T][N] bf16, lse [T/256][H][256] f32)."""
+    (batch, head) over it (sequence 256): returns (o [T][N] bf16, lse [T/256][H][256] f32).
+    ``trace``: int64 [blocks][8][8][4] phase stamps (LJS_QA_TRACE builds only; scripts/qkv_attn_phases.py)."""
     T, K = xb.shape
     N = wt.shape[1]
     assert (xb.dtype == torch.bfloat16 and wt.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
@@ -1389,7 +1391,7 @@ def qkv_attn_fwd(xb: torch.Tensor, wt: torch.Tensor, out: torch.Tensor, H: int, 
     o = torch.empty((T, N), dtype=torch.bfloat16, device=xb.device)
     lse = torch.empty((T // 256, H, 256), dtype=torch.float32, device=xb.device)
     _ck(lib().ljs_qkv_attn_fwd(_p(xb), xb.stride(0), _p(wt), _p(out), _p(o), _p(lse), T, K, N, H, float(scale),
-                               _stream(xb)), "ljs_qkv_attn_fwd")
+                               _p(trace) if trace is not None else None, _stream(xb)), "ljs_qkv_attn_fwd")
     return o, lse
 
 

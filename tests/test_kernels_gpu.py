@@ -1414,5 +1414,5 @@ def test_qkv_attn_fwd_rejects_bad_shapes(hip):
         hip.qkv_attn_fwd(x[:300], wt, torch.empty(300, 1536, dtype=torch.bfloat16, device=dev), 8, 0.125)
     # the launcher's own checks (K not a multiple of 128)
     rc = hip.lib().ljs_qkv_attn_fwd(hip._p(x), 640, hip._p(wt), hip._p(x), hip._p(x), hip._p(x), 512, 576, 512, 8,
-                                    0.125, None)
+                                    0.125, None, None)
     assert rc != 0
