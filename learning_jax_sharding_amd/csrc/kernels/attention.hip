@@ -358,9 +358,8 @@ __device__ __forceinline__ void fwd_tile(const AttnArgs& a, FwdState& st, const 
 }
 
 
-// fwd_tile for TWO 16-query sub-tiles over the same 64-key tile, in two halves so a caller can
-// issue the next key tile's score MFMAs (fwd_s2) before this tile's softmax and P.V (fwd_pv2):
-// each K / V fragment is read from LDS once for both sub-tiles.  Per query the same operations in
+// fwd_tile for TWO 16-query sub-tiles over the same 64-key tile, as the scores (fwd_s2) and the
+// softmax update + P.V (fwd_pv2): each K / V fragment is read from LDS once for both sub-tiles.  Per query the same operations in
 // the same order as fwd_tile<false> (no masking: Sk % 64 == 0, non-causal).
 __device__ __forceinline__ void fwd_s2(f32x4 (&s)[2][4], const bf16_t* Kt, const bf16x8 (&qf)[2][2], int lane) {
 #pragma unroll
@@ -610,9 +609,6 @@ struct QkvAttnArgs {
   unsigned long long* trace;   // LJS_QA_TRACE builds: per (block, wave, item) 4 shader-clock stamps
 };
 
-#ifndef LJS_QA_PIPE
-#define LJS_QA_PIPE 1   // (A/B build define) 0: key tiles one after the other (no score-MFMA lookahead)
-#endif
 #ifndef LJS_QA_TRACE
 #define LJS_QA_TRACE 0   // (diagnostic build define) phase stamps: item start, K-loop end, epilogue end, attention end
 #endif
@@ -795,26 +791,15 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_fwd_kernel(QkvAttnArgs p) {
         qf[s][0] = frag_rows(Qi, 32 * wave + 16 * s, 0, lane);
         qf[s][1] = frag_rows(Qi, 32 * wave + 16 * s, 1, lane);
       }
-      // key tiles software-pipelined by two: tile kt + 1's score MFMAs are issued before tile kt's
-      // softmax, so the MFMA pipe works while the VALU does the exponentials
-#if LJS_QA_PIPE
-      f32x4 sa[2][4], sb[2][4];
-      fwd_s2(sa, Ki, qf, lane);
-#pragma unroll 1
-      for (int kt = 0; kt < QA_S / BLK; kt += 2) {
-        fwd_s2(sb, Ki + (kt + 1) * BLK * D, qf, lane);
-        fwd_pv2(a, st, sa, Vi + kt * BLK * D, lane);
-        if (kt + 2 < QA_S / BLK) fwd_s2(sa, Ki + (kt + 2) * BLK * D, qf, lane);
-        fwd_pv2(a, st, sb, Vi + (kt + 1) * BLK * D, lane);
-      }
-#else
+      // (key tiles in order; issuing tile kt + 1's score MFMAs before tile kt's softmax measured
+      // slower: 13.2k vs 12.5k cycles per item, profiles/r6n_fused_pipe_phases.txt -- the phase is
+      // bound by the SIMD's issue of MFMA + VALU + v_exp_f32, not by their serialisation)
 #pragma unroll 1
       for (int kt = 0; kt < QA_S / BLK; ++kt) {
         f32x4 sc[2][4];
         fwd_s2(sc, Ki + kt * BLK * D, qf, lane);
         fwd_pv2(a, st, sc, Vi + kt * BLK * D, lane);
       }
-#endif
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const float lt = row4_sum(st[s].l);
