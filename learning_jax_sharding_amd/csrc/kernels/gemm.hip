@@ -1601,6 +1601,7 @@ LJS_API int ljs_gemm_bf16(const void* A, const void* B, void* C, const void* bia
     e = launch_dma<256, 128, 4, 2, 3, false, false, true>(a, stream, 0);
   } else if (tile == 12856) {
     e = launch_dma<128, 256, 2, 4, 3, false, false, true>(a, stream, 0);
+
   } else if (tile == 1602) {
     e = launch_dma_kk<128, 160, 4, 1, 2>(a, stream);
   } else if (tile == 2562) {

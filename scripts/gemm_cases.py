@@ -114,6 +114,14 @@ def cases():
     out["dwo_ring"] = (dwo_fn, ["1282:24", "1284:24", "1284:12", "12883:24", "12883:12", "12884:24", "12884:12", "644:1", "644:2", "644:6", "644:8", "1282:12"],
                        2 * T * 512 * 640)
 
+    # wider tiles at the weight-gradient shape (fewer operand bytes per FLOP, one block per CU):
+    # 128x256 (12856, 3 stages), 256x128 (2563, 3 stages) -- and a 256x256 2-stage tile measured
+    # in round 6 and removed (profiles/r6p_dw_wide_tiles.txt)
+    out["dwqkv_wide"] = (dwqkv_fn, ["1282:6", "1282:8", "12856:4", "12856:6", "12856:8", "2563:4", "2563:6"],
+                         2 * T * 640 * 1536)
+    out["dwo_wide"] = (dwo_fn, ["1282:6", "1282:24", "12856:6", "12856:8", "12856:12", "2563:6", "2563:12"],
+                       2 * T * 512 * 640)
+
     def dwgroup_fn(spec):
         # "tile0:S0/tile1:S1[:sep]": the dW_qkv batch and dW_o as one grouped grid (or separate)
         parts = spec.split("/")
@@ -149,7 +157,7 @@ def cases():
     return out
 
 
-_GRAPH_CASES = {"dwgroup", "dwgroup_big", "dwgroup_8w", "dwqkv_ring", "dwo_ring"}
+_GRAPH_CASES = {"dwgroup", "dwgroup_big", "dwgroup_8w", "dwqkv_ring", "dwo_ring", "dwqkv_wide", "dwo_wide"}
 
 
 def main():

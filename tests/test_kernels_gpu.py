@@ -1416,3 +1416,21 @@ def test_qkv_attn_fwd_rejects_bad_shapes(hip):
     rc = hip.lib().ljs_qkv_attn_fwd(hip._p(x), 640, hip._p(wt), hip._p(x), hip._p(x), hip._p(x), 512, 576, 512, 8,
                                     0.125, None, None)
     assert rc != 0
+
+
+@pytest.mark.parametrize("tile,S", [(1282, 6), (12856, 6), (2563, 4)])
+@pytest.mark.parametrize("M,N,T", [(640, 512, 4096), (512, 640, 2048), (320, 200, 640)])
+def test_gemm_weight_grad_slab_tiles(hip, tile, S, M, N, T):
+    """The weight-gradient (m/n-contiguous operands, f32 split-K slabs) tiles: the slabs sum to the
+    fp32 reference C = A^T B over the token dimension, ragged M / N included."""
+    A = _rand(T, M, seed=21)
+    B = _rand(T, N, seed=22)
+    nkt = -(-T // 64)
+    Se = hip.slab_count(nkt, S)
+    sl = torch.full((Se, M, N), float("nan"), device=dev)
+    hip.gemm(A, B, sl, M, N, T, M, N, N, False, False, sC=M * N, splitk=Se, tile=tile, slabs=True)
+    torch.cuda.synchronize()
+    ref = A.float().t() @ B.float()
+    got = sl.sum(0)
+    assert not torch.isnan(got).any()
+    torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
