@@ -70,7 +70,11 @@ struct AttnArgs {
   int vst;           // outputs 16-byte aligned with row strides % 8 == 0: row tiles leave through an
                      // LDS image as full 128-byte rows (stage_rows16 / flush_rows)
   FastDiv fd_nx, fd_h;  // resident forward: its query-block count and H as launch-constant divisors
+  unsigned long long* trace;   // LJS_ATTN_BWD_TRACE builds: fused-backward phase stamps
 };
+#ifndef LJS_ATTN_BWD_TRACE
+#define LJS_ATTN_BWD_TRACE 0   // (diagnostic build define) fused backward: stamps per (block, wave)
+#endif
 
 // A/B switches (compile-time): the resident forward's key loop fully unrolled at 256 keys, and
 // the fused backward's dQ slices without per-slice guards when all 256 keys are valid
@@ -1747,6 +1751,17 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int h = blockIdx.x, b = blockIdx.y;
   const int key0 = wave * 32;
+  // (diagnostic builds) shader-clock stamps: 0 start, 1 first query block ready, 2 + it after
+  // query block it, 7 end; a vector store from lane 0
+  auto bstamp = [&](int k) {
+#if LJS_ATTN_BWD_TRACE
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (a.trace && lane == 0) a.trace[(((long)b * gridDim.x + h) * (FT / 64) + wave) * 8 + k] = t;
+#else
+    (void)k;
+#endif
+  };
+  bstamp(0);
   const bool active = key0 < a.Sk;
   const int nk32 = (a.Sk + 31) / 32;
 
@@ -1826,6 +1841,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
   __syncthreads();
   if (nqt > 0) finish(0);
   __syncthreads();
+  bstamp(1);
 
   f32x4 dk[2][4], dv[2][4];
 #pragma unroll
@@ -1942,6 +1958,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
         if (q0 + r < a.Sq)
           *reinterpret_cast<u32x4*>(a.out3 + b * a.out3_sb + (long)(q0 + r) * a.out3_ss + h * a.out3_sh + c * 8) = v;
       }
+      if (it < 5) bstamp(2 + it);
     }
   };
   if constexpr (SW == 1) {
@@ -1966,6 +1983,7 @@ __global__ __launch_bounds__(FT) void attn_bwd_fused_kernel(AttnArgs a) {
       flush_rows<32>(Ks + key0 * D, a.out + b * a.out_sb + h * a.out_sh, a.out_ss, key0, a.Sk, lane);
       flush_rows<32>(Vs + key0 * D, a.out2 + b * a.out2_sb + h * a.out2_sh, a.out2_ss, key0, a.Sk, lane);
     }
+    bstamp(7);
     return;
   }
 #pragma unroll
@@ -2012,6 +2030,9 @@ LJS_API void ljs_attn_set_bwd_kv_dma(int v) { g_bwd_kv_dma = v < 0 ? 2 : v; }
 //    automatic by grid size
 static int g_bwd_fused = 2;
 LJS_API void ljs_attn_set_bwd_fused(int v) { g_bwd_fused = v < 0 ? 2 : v; }
+//  * (diagnostic) the fused backward's phase-stamp buffer (LJS_ATTN_BWD_TRACE builds): [B][H][waves][8]
+static unsigned long long* g_attn_trace = nullptr;
+LJS_API void ljs_attn_set_trace(void* p) { g_attn_trace = (unsigned long long*)p; }
 
 // strides are in elements, ordered (batch, seq, head); head_dim must be 64 and contiguous.
 static int attn_fwd_impl(const void* q, const void* k, const void* v, void* o, void* lse, int B, int Sq, int Sk,
@@ -2128,6 +2149,7 @@ LJS_API int ljs_attn_bwd(const void* q, const void* k, const void* v, const void
     f.out2 = (bf16_t*)dv; f.out2_sb = dvs[0]; f.out2_ss = dvs[1]; f.out2_sh = dvs[2];
     f.out3 = (bf16_t*)dq; f.out3_sb = dqs[0]; f.out3_ss = dqs[1]; f.out3_sh = dqs[2];
     f.vst = vst_ok(dk, dks) && vst_ok(dv, dvs) && vst_ok(dq, dqs) ? g_vst : 0;
+    f.trace = g_attn_trace;
     // 2 = automatic: the DMA form when a block sweeps at most two query blocks (the 2-D mesh's
     // 128 local queries against 256 gathered keys: the K / V prologue is a third of the block's
     // time there, and overlapping it with the first query block's loads measured 58.8 -> 57.1 us,

@@ -40,6 +40,7 @@ _SIGS = {
                      c_long, c_long, c_long, c_int, c_void_p],
     "ljs_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, _LP, _LP, _LP, _LP,
                      c_float, c_int, c_int, c_void_p],
+    "ljs_attn_set_trace": [c_void_p],
     "ljs_qkv_attn_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                          c_void_p, c_void_p],
     "ljs_attn_fwd_acc": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, _LP, _LP, _LP,
