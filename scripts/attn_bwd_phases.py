@@ -2,7 +2,7 @@
 (LJS_ATTN_BWD_TRACE build):
 
     LJS_KERNELS_LIB=learning_jax_sharding_amd/_lib/variants/bwdtrace/libljs_kernels.so \\
-        python scripts/attn_bwd_phases.py [B]
+        python scripts/attn_bwd_phases.py [B] [kvdma]
 
 Per block (averaged over blocks and waves, shader-clock cycles): prologue (start -> first query
 block's Q / dO / O and delta ready), each query block of the sweep, and the dK / dV epilogue;
@@ -18,6 +18,8 @@ from learning_jax_sharding_amd.ops import hip  # noqa: E402
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    if len(sys.argv) > 2 and sys.argv[2] == "kvdma":   # K / V by LDS-DMA beside the first block's
+        hip.set_attention_bwd_kv_dma(True)
     H, S, D = 8, 256, 64
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(5)
