@@ -1400,7 +1400,15 @@ def _fused_key(t: torch.Tensor, scale: float):
     return (t.data_ptr(), t._version, t.device.index, float(scale))
 
 
+def clear_fused_attention() -> None:
+    """Drop a fused forward nobody took (also run when a graph capture ends)."""
+    _FUSED_ATTN.clear()
+
+
 def register_fused_attention(out: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, H: int, scale: float) -> None:
+    from ..spmd import graphs as _graphs
+    if clear_fused_attention not in _graphs.AFTER_CAPTURE:
+        _graphs.AFTER_CAPTURE.append(clear_fused_attention)
     _FUSED_ATTN.clear()   # one pending forward at a time
     _FUSED_ATTN[_fused_key(out, scale)] = (o, lse, tuple(out.shape), H)
 

@@ -61,3 +61,14 @@ def test_gate_needs_announcement_and_shapes():
             assert L._ATTN_NEXT[0] is None                      # LJS_QKV_ATTN=0
     finally:
         L._QKV_ATTN = old
+
+
+def test_capture_end_drops_untaken_forward():
+    from learning_jax_sharding_amd.spmd import graphs
+    out, o, lse, q, k, v = _setup()
+    H.register_fused_attention(out, o, lse, 4, 0.125)
+    assert H.clear_fused_attention in graphs.AFTER_CAPTURE
+    for f in graphs.AFTER_CAPTURE:
+        if f is H.clear_fused_attention:
+            f()
+    assert H._take_fused_attention(q, k, v, 0.125, False, 0) is None
