@@ -514,7 +514,12 @@ def _measure(args, mesh_arg, env, phase_timeout=None):
             gbytes = sum(b for b, _, _ in _data.LAST_BUCKETS)
             if gbytes:
                 from learning_jax_sharding_amd.comm.probe import all_reduce_paths
-                probe = all_reduce_paths(gbytes)
+                # (diagnostic only: a path that raises on every rank alike is reported, and the
+                # measurement the record is for still runs)
+                try:
+                    probe = all_reduce_paths(gbytes)
+                except Exception as e:  # noqa: BLE001
+                    probe = [{"error": f"{type(e).__name__}: {e}"[:300]}]
         if aten_trace:
             from learning_jax_sharding_amd.utils.aten_trace import AtenTrace
             with AtenTrace(cuda_only=not os.environ.get("LJS_ATEN_TRACE_ALL"),
