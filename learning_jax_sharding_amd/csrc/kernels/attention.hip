@@ -597,11 +597,14 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_res_kernel(AttnArgs a) {
 //     (C^T blocks), K-tiles of 64 by LDS-DMA into a two-slot ring [0, 56 KiB) / [96 KiB, 152 KiB),
 //     one K-tile in flight -- the same per-element MFMA sequence as gemm_lean_kernel<256, 192>, so
 //     the Q/K/V values are bit-identical to the unfused projection;
-//   * epilogue: bf16 rows to global [T][3N] and into LDS images Q / K / V [256][64] (img16
-//     swizzle) over [0, 96 KiB) -- the next item's first K-tile streams into the other slot;
-//   * attention: wave w owns queries 32 w .. 32 w + 31 (two 16-query sub-tiles), key tiles in
-//     order through fwd_tile<false> (the resident forward's per-query sequence: bit-identical O and
-//     lse), O staged through the wave's own (consumed) Q rows and stored as whole 128-byte rows.
+//   * epilogue: the tile into LDS images Q / K / V [256][64] (img16 swizzle) over [0, 96 KiB) --
+//     the next item's first K-tile streams into the other slot -- and, after the images' barrier,
+//     from the images to global [T][3N] as whole 128-byte rows, draining under the attention
+//     (stores straight from the accumulators before the barrier: epilogue 7.3k vs 3.1k cycles);
+//   * attention: wave w owns queries 32 w .. 32 w + 31 (two 16-query sub-tiles sharing each K / V
+//     fragment read, fwd_s2 / fwd_pv2: the resident forward's per-query operations; O / lse agree
+//     with it up to the f32 rounding of the running softmax state), O staged through the wave's
+//     own (consumed) Q rows and stored as whole 128-byte rows.
 struct QkvAttnArgs {
   const bf16_t* x;   // [T][K] bf16, row stride ldx
   const bf16_t* w;   // [3][N][K] bf16: transposed Q / K / V weights, k-contiguous
