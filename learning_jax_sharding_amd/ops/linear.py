@@ -119,10 +119,12 @@ def _fuse_attention_ok(x, xb, wt, nw, N, K, b, relu, res, od, out_dtype, wmajor,
             and xb.dtype == torch.bfloat16 and xb.stride(1) == 1 and xb.stride(0) % 8 == 0
             and xb.data_ptr() % 16 == 0 and wt.is_contiguous() and wt.data_ptr() % 16 == 0):
         return None
-    # one 8-wave block per CU over (batch, head) items: below one item per CU the fused kernel
-    # leaves CUs idle that the separate GEMM + attention fill (B = 8, 64 items: step 0.0796 vs
-    # 0.0732 ms; B = 64, 512 items: 0.1948-0.1966 vs 0.1999-0.2042, gpurun_out/r6g)
-    if (x.shape[0] * heads) < _cu_count(x.device):
+    # one 8-wave block per CU over (batch, head) items: with fewer items than half the CUs the
+    # fused kernel leaves CUs idle that the separate GEMM + attention fill (B = 8, 64 items: step
+    # 0.0796 vs 0.0732 ms, gpurun_out/r6g); from half the CUs up it wins (B = 16, 128 items:
+    # 0.0968-0.0972 vs 0.0990-0.0997; B = 24: 0.1066-0.1080 vs 0.1111-0.1116,
+    # profiles/r6aa_fused_gate_lines.txt; B = 64: 0.1948-0.1966 vs 0.1999-0.2042)
+    if 2 * (x.shape[0] * heads) < _cu_count(x.device):
         return None
     return fz
 
@@ -135,6 +137,8 @@ def _cu_count(dev: torch.device) -> int:
     if n is None:
         n = _CUS[dev.index] = torch.cuda.get_device_properties(dev).multi_processor_count
     return n
+
+
 # large bf16 dense outputs also carry their fused per-tile sums (see hip._PSUM): y.sum() is free
 _FUSED_SUM = os.environ.get("LJS_FUSED_SUM", "1") == "1"
 

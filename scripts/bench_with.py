@@ -2,6 +2,7 @@
 which are not environment knobs):
 
     python scripts/bench_with.py bwd_fused=0 -- --steps 20 --warmup 5
+    python scripts/bench_with.py qkv_gate=1 -- --batch-per-gpu 16   (fused projection at any item count)
 """
 import os
 import runpy
@@ -19,6 +20,10 @@ def main():
            "dkv32": hip.set_attention_dkv32, "dq32": hip.set_attention_dq32, "bwd_pair": hip.set_attention_bwd_pair}
     for s in sets:
         k, v = s.split("=")
+        if k == "qkv_gate":   # the fused projection + attention's items-per-CU gate: items >= v
+            from learning_jax_sharding_amd.ops import linear
+            linear._cu_count = lambda dev, _v=int(v): _v
+            continue
         fns[k](bool(int(v)))
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.argv = [os.path.join(root, "bench.py")] + rest

@@ -544,7 +544,7 @@ def test_fused_qkv_attention_matches_unfused(gpu_devices, monkeypatch):
     from learning_jax_sharding_amd.ops import hip as H
     from learning_jax_sharding_amd.ops import linear as L
     res = {}
-    monkeypatch.setattr(L, "_cu_count", lambda dev: 1)   # (4 x 8 items: below the one-per-CU gate)
+    monkeypatch.setattr(L, "_cu_count", lambda dev: 1)   # (4 x 8 items: below the gate of one item per two CUs)
     for on in (False, True):
         monkeypatch.setattr(L, "_QKV_ATTN", on)
         before = H.FUSED_ATTN_STATS["taken"]
