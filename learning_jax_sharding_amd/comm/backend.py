@@ -87,6 +87,10 @@ class LocalComm:
         self._native = None
         self._p2p_groups = {}
 
+    def cuts_capture(self) -> bool:
+        """Whether collectives cut a segmented HIP-graph capture (never: single process)."""
+        return False
+
     def _p2p(self, g, xs, chunked=False):
         """Direct peer-memory collectives (comm/p2p.py) for small GPU messages when enabled."""
         from . import p2p
@@ -313,6 +317,12 @@ class DistComm:
                 self._native = None
 
     _GRAPH_KINDS = ("all_gather", "reduce_scatter", "all_reduce", "all_to_all")
+
+    def cuts_capture(self) -> bool:
+        """Whether the bulk collectives are cut points of a segmented HIP-graph capture: torch
+        process-group collectives (gloo, or RCCL without the native rank communicators) are; the
+        native communicators' and the rehearsal backend's are captured (:meth:`graph_safe`)."""
+        return not self._fake and self._native is None
 
     def graph_safe(self, kind: str, x: Optional[torch.Tensor] = None, groups: Optional[Groups] = None) -> bool:
         """Whether this collective can be captured inside a HIP graph (no capture cut): native

@@ -742,7 +742,8 @@ def _attention_local_first(q, k, v, kv_tile, scale, causal, q_offsets):
     devs = sorted(k.local)
     dev0 = k.local[devs[0]].device
     ev = None
-    if dev0.type == "cuda":
+    from ..spmd import graphs as _graphs
+    if dev0.type == "cuda" and _graphs.forks_ok():
         side = _LF_STREAMS.get(dev0.index)
         if side is None:
             side = _LF_STREAMS[dev0.index] = torch.cuda.Stream(dev0)

@@ -144,6 +144,9 @@ class Prefetcher:
             return self.prefetch(ws)
         devs = sorted({t.device.index for w in ws for t in w.local.values() if t.is_cuda})
         dev = devs[0]
+        from ..spmd import graphs as _graphs
+        if not _graphs.forks_ok():   # (a segmented capture cut at these gathers: no fork)
+            return _Handle(_wg.gather_bf16(ws, dst, gdim, note="prefetch.joint"), None, None)
         s = self._streams.get(dev)
         if s is None:
             s = self._streams[dev] = torch.cuda.Stream(device=dev)
@@ -164,7 +167,8 @@ class Prefetcher:
     def prefetch(self, tree: Any) -> _Handle:
         leaves = [l for l in T.tree_leaves(tree, is_leaf=_is_arr) if _is_arr(l)]
         devs = sorted({t.device.index for l in leaves for t in l.local.values() if t.is_cuda})
-        if not devs:
+        from ..spmd import graphs as _graphs
+        if not devs or not _graphs.forks_ok():   # (host arrays, or a capture cut at the gathers)
             return _Handle(T.tree_map(lambda l: self._gather_leaf(l) if _is_arr(l) else l, tree, is_leaf=_is_arr),
                            None, None)
         dev = devs[0]

@@ -121,7 +121,8 @@ def _rotate_async(bufs: List[Dict[int, torch.Tensor]], nxt: Dict[int, int]):
     hands back the rotated dicts (host devices: the hop simply runs)."""
     import contextlib
     t0 = next(iter(bufs[0].values()))
-    if not t0.is_cuda:
+    from ..spmd import graphs as _graphs
+    if not t0.is_cuda or not _graphs.forks_ok():   # (host arrays, or a capture cut at the hops)
         out = [_rotate(b, nxt) for b in bufs]
         return lambda: out
     gpus = sorted({t.device.index for b in bufs for t in b.values()})

@@ -57,12 +57,14 @@ def current() -> Optional["SegmentedGraph"]:
 def _copy_into(dst, src):
     if isinstance(dst, dict):
         for k, v in dst.items():
-            v.copy_(src[k])
+            _copy_into(v, src[k])
     elif isinstance(dst, (list, tuple)):
         for a, b in zip(dst, src):
             _copy_into(a, b)
     elif isinstance(dst, torch.Tensor):
-        dst.copy_(src)
+        # (detached: a static output may be the view an autograd Function returned at capture, e.g.
+        # a 2-D layout's gathered K / V -- its refresh is data movement, not a differentiable op)
+        dst.detach().copy_(src.detach() if isinstance(src, torch.Tensor) else src)
 
 
 class SegmentedGraph:
@@ -70,22 +72,35 @@ class SegmentedGraph:
         self.pool = torch.cuda.graph_pool_handle()
         self.items: List[tuple] = []
         self._g: Optional[torch.cuda.CUDAGraph] = None
+        self._origin: Optional[torch.cuda.Stream] = None   # the stream every segment begins / ends on
         self.comm_stream: Optional[torch.cuda.Stream] = None
         self.n_collectives = 0
 
     # ------------------------------------------------------------------ capture
     def _begin(self):
         self._g = torch.cuda.CUDAGraph()
+        cur = torch.cuda.current_stream()
         # HIP ends a capture only on the thread that began it, so value_and_grad runs the
         # backward single-threaded while a segmented capture is active (cuts happen inside it)
-        self._g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
+        with torch.cuda.stream(self._origin):
+            self._g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
+        if cur != self._origin:
+            # a cut made on a forked stream: that stream joins the new segment again
+            cur.wait_stream(self._origin)
 
     def _cut(self):
         _before_cut()
+        cur = torch.cuda.current_stream()
+        if cur != self._origin:
+            # a collective issued on a stream forked inside the capture (a side-stream gather):
+            # the fork joins the segment's own stream, which ends the capture (a capture must end
+            # on the stream it began on, with every fork joined)
+            self._origin.wait_stream(cur)
         with warnings.catch_warnings():
             # two adjacent cut points leave an empty segment: harmless, replays as a no-op
             warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
-            self._g.capture_end()
+            with torch.cuda.stream(self._origin):
+                self._g.capture_end()
         self.items.append(("graph", self._g))
         self._g = None
 
@@ -97,6 +112,7 @@ class SegmentedGraph:
         stream.wait_stream(torch.cuda.current_stream())
         prev = current()
         _ACTIVE[0] = self
+        self._origin = stream
         try:
             with torch.cuda.stream(stream):
                 self._begin()
@@ -219,6 +235,19 @@ def run_collective(fn: Callable[[], Any], async_: bool = False, capturable: bool
 
 
 _CUT_TRACE = os.environ.get("LJS_GRAPH_CUT_TRACE", "0") == "1"
+
+
+def forks_ok() -> bool:
+    """Whether work may be forked onto a side stream now (a prefetched gather, a ring hop).
+    Inside a segmented capture whose collectives are cut points (torch process-group
+    collectives: gloo, or RCCL without the native rank communicators) a fork still open at a cut
+    would leave the segment unjoined, so the forking sites run on the current stream there -- the
+    cut collectives run eagerly and in order anyway, there is nothing to overlap them with."""
+    seg = current()
+    if seg is None or isinstance(seg, MultiDeviceGraph):
+        return True
+    from ..comm.backend import get_comm
+    return not get_comm().cuts_capture()
 
 
 def join(handle) -> None:

@@ -75,6 +75,18 @@ def test_2d_layout_matches_single_process(tmp_path, world, mesh):
         assert np.mean(diff > 2e-4 + 2e-3 * np.abs(ref[k])) < 5e-3, (k, np.mean(diff > 2e-4))
 
 
+def test_2d_layout_graph_matches_eager(tmp_path):
+    """The 2-D layout under a segmented HIP-graph capture cut at its gloo collectives -- some of
+    them issued where the layout forks a side stream (prefetched gathers) -- replays to the eager
+    run's parameters.  (Before the capture's cuts were made stream-safe this raised "Capture must
+    end on the same stream it began on": profiles/r6ab_gloo_multirank_lines.txt, the 2-D secondary.)"""
+    eager = _run(tmp_path, 2, False, port=29621, wire="fp32", mesh="1x2", gb=4, tag="e")
+    graph = _run(tmp_path, 2, True, port=29641, wire="fp32", mesh="1x2", gb=4, tag="g")
+    assert int(graph["step"]) == 3 and int(eager["step"]) == 3
+    for k in eager.files:
+        np.testing.assert_allclose(graph[k], eager[k], rtol=1e-5, atol=1e-6, err_msg=f"graph {k}")
+
+
 def test_dp2_early_input_cast_bit_exact(tmp_path):
     """LJS_PRECAST=join: in a data-parallel multi-step graph the next step's input cast is queued
     before the gradient all-reduce join instead of in that step's forward -- the same bf16 values,

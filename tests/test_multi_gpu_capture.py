@@ -203,3 +203,31 @@ def test_jit_uses_multi_device_capture_when_steps_span_gpus(monkeypatch):
     j(1.0)                 # warm-up call (eager)
     j(1.0)                 # captured through the multi-device graph
     assert seen and seen[0] == (0, 1)
+
+
+def test_forks_ok_follows_capture_cuts(monkeypatch):
+    """Side-stream forks are skipped only inside a segmented capture whose collectives cut it
+    (torch process-group collectives); native RCCL / rehearsal collectives are captured, and a
+    single-controller multi-device capture never cuts."""
+    from learning_jax_sharding_amd.comm import backend
+
+    class _Comm:
+        def __init__(self, cuts):
+            self.cuts = cuts
+
+        def cuts_capture(self):
+            return self.cuts
+
+    assert graphs.forks_ok()                       # no capture
+    prev = graphs._ACTIVE[0]
+    try:
+        graphs._ACTIVE[0] = graphs.SegmentedGraph.__new__(graphs.SegmentedGraph)
+        monkeypatch.setattr(backend, "get_comm", lambda: _Comm(True))
+        assert not graphs.forks_ok()
+        monkeypatch.setattr(backend, "get_comm", lambda: _Comm(False))
+        assert graphs.forks_ok()
+        graphs._ACTIVE[0] = graphs.MultiDeviceGraph([0, 1], backend=object())
+        monkeypatch.setattr(backend, "get_comm", lambda: _Comm(True))
+        assert graphs.forks_ok()
+    finally:
+        graphs._ACTIVE[0] = prev

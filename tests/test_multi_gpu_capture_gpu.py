@@ -63,3 +63,34 @@ def test_multi_device_graph_real_backend_matches_eager(gpu_devices, monkeypatch)
     assert int(np.asarray(sg.step)) == 5 and int(np.asarray(se.step)) == 5
     for a, b in zip(ljs.tree_util.tree_leaves(se.params), ljs.tree_util.tree_leaves(sg.params)):
         np.testing.assert_allclose(np.asarray(b), np.asarray(a), rtol=1e-4, atol=1e-5)
+
+
+def test_segmented_capture_cut_on_forked_stream():
+    """A cut point (an eagerly replayed collective) issued on a stream forked inside a segmented
+    capture: the fork joins the segment's own stream before the segment ends, the next segment
+    begins there and re-forks the stream, and the replay recomputes every stage."""
+    from learning_jax_sharding_amd.spmd import graphs
+    x = torch.ones(4096, device="cuda")
+    side = torch.cuda.Stream()
+    seg = graphs.SegmentedGraph()
+
+    def step():
+        y = x * 2
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            z = y + 1
+            out, _ = seg.collective(lambda: z * 3)     # cut on the forked stream
+            w = out + 1
+            ev = torch.cuda.Event()
+            ev.record(side)
+        cur.wait_event(ev)
+        return w * 2
+
+    res = seg.capture(step)    # (captured segments do not run during the capture)
+    assert sum(1 for it in seg.items if it[0] == "graph") == 2
+    for v in (1.0, 2.0):
+        x.fill_(v)
+        seg.replay()
+        torch.cuda.synchronize()
+        assert torch.all(res == ((v * 2 + 1) * 3 + 1) * 2), (v, res[:4])
