@@ -53,19 +53,41 @@ __global__ void cast_bf16_f32(const bf16_t* __restrict__ in, float* __restrict__
 }
 
 // out[c][r] = bf16(in[r][c]) for an R x C f32 matrix (row stride ldi), 64x64 tiles through LDS.
-__global__ void cast_transpose_f32_bf16(const float* __restrict__ in, bf16_t* __restrict__ out, int R, int C,
-                                        long ldi, long ldo) {
-  __shared__ float tile[64][65];
-  int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 64 x 4
-  for (int i = ty; i < 64; i += 4) {
-    int r = r0 + i, c = c0 + tx;
-    tile[i][tx] = (r < R && c < C) ? in[(long)r * ldi + c] : 0.f;
+// out[c][r] = bf16(in[r][c]) through a 32 x 32 LDS tile: 16-byte f32 loads (8 lanes per input
+// row), 8-byte bf16 stores (8 lanes per output row), one pass each.  (The 64 x 64 form with
+// scalar loads / 2-byte stores gave a [320][512] weight shard 40 workgroups and 7.6 us -- the
+// 2-D layout's per-step transposed shadow, profiles/r6ag_fake4_2d_kernels.md.)
+__global__ __launch_bounds__(256) void cast_transpose_f32_bf16(const float* __restrict__ in, bf16_t* __restrict__ out,
+                                                               int R, int C, long ldi, long ldo, int vin, int vout) {
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int t = threadIdx.x;
+  {
+    const int lr = t >> 3, lc = (t & 7) * 4;
+    const int r = r0 + lr, c = c0 + lc;
+    float v[4];
+    if (vin && r < R && c + 3 < C) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(in + (long)r * ldi + c);
+      v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (r < R && c + e < C) ? in[(long)r * ldi + c + e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[lr][lc + e] = v[e];
   }
   __syncthreads();
-  for (int i = ty; i < 64; i += 4) {
-    int c = c0 + i, r = r0 + tx;
-    if (c < C && r < R) out[(long)c * ldo + r] = f2bf(tile[tx][i]);
+  const int oc = t >> 3, orr = (t & 7) * 4;   // output row (an input column), 4 output columns
+  const int c = c0 + oc, r = r0 + orr;
+  if (c >= C) return;
+  bf16_t* o = out + (long)c * ldo + r;
+  if (vout && r + 3 < R) {
+    *reinterpret_cast<u32x2*>(o) = u32x2{pack_bf16x2(tile[orr][oc], tile[orr + 1][oc]),
+                                         pack_bf16x2(tile[orr + 2][oc], tile[orr + 3][oc])};
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (r + e < R) o[e] = f2bf(tile[orr + e][oc]);
   }
 }
 
@@ -1154,8 +1176,12 @@ LJS_API int ljs_cast_bf16_f32(const void* in, void* out, long n, hipStream_t s) 
 }
 
 LJS_API int ljs_cast_transpose_f32_bf16(const void* in, void* out, int R, int C, long ldi, long ldo, hipStream_t s) {
-  dim3 grid((C + 63) / 64, (R + 63) / 64);
-  hipLaunchKernelGGL(cast_transpose_f32_bf16, grid, dim3(256), 0, s, (const float*)in, (bf16_t*)out, R, C, ldi, ldo);
+  if ((R + 31) / 32 > 65535) return (int)hipErrorInvalidValue;
+  dim3 grid((C + 31) / 32, (R + 31) / 32);
+  const int vin = ldi % 4 == 0 && (((uintptr_t)in) & 15) == 0;
+  const int vout = ldo % 4 == 0 && (((uintptr_t)out) & 7) == 0;
+  hipLaunchKernelGGL(cast_transpose_f32_bf16, grid, dim3(256), 0, s, (const float*)in, (bf16_t*)out, R, C, ldi, ldo,
+                     vin, vout);
   return (int)hipGetLastError();
 }
 

@@ -334,7 +334,12 @@ def test_elementwise(hip):
     s = torch.randn(17, 300, device=dev)
     torch.testing.assert_close(hip.softmax_lastdim(s), torch.softmax(s, -1), rtol=1e-5, atol=1e-6)
     w = torch.randn(640, 512, device=dev)
-    torch.testing.assert_close(hip.cast_transpose_bf16(w), w.t().bfloat16())
+    torch.testing.assert_close(hip.cast_transpose_bf16(w), w.t().bfloat16(), rtol=0, atol=0)
+    for R, C in ((320, 512), (37, 70), (1, 33), (65, 1)):   # ragged tiles, scalar tails
+        w = torch.randn(R, C, device=dev)
+        torch.testing.assert_close(hip.cast_transpose_bf16(w), w.t().bfloat16(), rtol=0, atol=0)
+    w = torch.randn(96, 130, device=dev)[:, 1:129]          # row stride 130, 4-byte-aligned base
+    torch.testing.assert_close(hip.cast_transpose_bf16(w), w.t().bfloat16(), rtol=0, atol=0)
 
 
 def test_adam_kernel(hip):
