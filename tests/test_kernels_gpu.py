@@ -1133,6 +1133,8 @@ def test_transpose_bf16_and_swap01(hip, shape):
     assert torch.equal(hip.transpose_bf16(x), x.t().contiguous())
     y = torch.randn(4, shape[0], 8, device="cuda").bfloat16()
     assert torch.equal(hip.swap01_bf16(y), y.transpose(0, 1).contiguous())
+    z = torch.randn(3, shape[0], 24, device="cuda")       # f32 in: rounded in the same pass
+    assert torch.equal(hip.swap01_bf16(z), z.transpose(0, 1).contiguous().bfloat16())
 
 
 @pytest.mark.parametrize("n", [1, 2, 4, 7, 100])
