@@ -149,8 +149,29 @@ def attention_reference(q, k, v, scale: float, causal: bool = False, q_offset: i
     return o.to(v.dtype)
 
 
+_WARNED_DH = set()
+
+
+def _hip_attn(q, k, v) -> bool:
+    """Whether the HIP attention kernels take these (b, s, heads, head_dim) operands: GPU tensors
+    with head_dim 64 (the reference's, ``case6_attention.py``) contiguous in the last dim.  Other
+    head dims run the torch formulation below on the GPU (same math, autograd through torch),
+    with a one-time warning."""
+    if not use_hip(q):
+        return False
+    if all(t.shape[-1] == 64 and t.stride(-1) == 1 for t in (q, k, v)):
+        return True
+    key = (q.shape[-1], v.shape[-1])
+    if key not in _WARNED_DH:
+        _WARNED_DH.add(key)
+        import warnings
+        warnings.warn(f"HIP attention kernels take head_dim 64; head_dim {q.shape[-1]} (v {v.shape[-1]}) runs "
+                      "the torch attention formulation on the GPU")
+    return False
+
+
 def attention(q, k, v, scale: float, causal: bool = False, q_offset: int = 0) -> torch.Tensor:
-    if use_hip(q):
+    if _hip_attn(q, k, v):
         return _hip().attention(q, k, v, scale, causal, q_offset)
     return attention_reference(q, k, v, scale, causal, q_offset)
 
@@ -172,7 +193,7 @@ def attention_fwd_lse(q, k, v, scale: float, causal: bool = False, q_offset: int
     """One (q block, kv block) flash forward: (o normalised within the block, lse) with lse in
     the HIP kernels' convention - log2 of the scaled-score partition function, +inf for rows
     without any unmasked key."""
-    if use_hip(q):
+    if _hip_attn(q, k, v):
         return _hip().attn_fwd_lse(q, k, v, scale, causal, q_offset)
     s = _block_scores(q, k, scale, causal, q_offset)
     m = s.amax(-1, keepdim=True)
@@ -191,7 +212,7 @@ def attention_fwd_merge(q, k, v, scale: float, causal: bool, q_offset: int, stat
     """One key block of a blockwise forward merged into ``state`` = [o_acc f32, lse] (None before the
     first block).  On GPU the merge happens in the kernel's epilogue; ``last`` makes it write and
     return the final output in v's dtype (else returns None)."""
-    if use_hip(q):
+    if _hip_attn(q, k, v):
         B, Sq, H, D = q.shape
         if state[0] is None:
             state[0] = torch.empty((B, Sq, H, D), dtype=torch.float32, device=q.device)
@@ -232,7 +253,7 @@ def _merge_lse(o, lse, o_s, lse_s):
 
 def attention_bwd_block(q, k, v, o, do, lse, scale: float, causal: bool = False, q_offset: int = 0):
     """One kv block's (dq, dk, dv) given the final output ``o`` and global (log2) ``lse``."""
-    if use_hip(q):
+    if _hip_attn(q, k, v):
         return _hip().attn_bwd_block(q, k, v, o, do, lse, scale, causal, q_offset)
     s = _block_scores(q, k, scale, causal, q_offset)
     p = torch.exp(s - (lse / _LOG2E)[..., None])

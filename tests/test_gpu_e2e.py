@@ -67,6 +67,26 @@ def test_block_gpu_case5_rules_odd_tokens(host_devices, gpu_devices):
             np.testing.assert_allclose(b, a, rtol=5e-2, atol=5e-2 * np.abs(a).max(), err_msg=f"{k}/{name}")
 
 
+@pytest.mark.parametrize("mesh_shape,dh", [((1, 1), 32), ((2, 2), 128)])
+def test_block_gpu_other_head_dims_match_host(host_devices, gpu_devices, mesh_shape, dh):
+    """head_dim other than the HIP kernels' 64 (heads x dh = 512 kept): the GPU run takes the torch
+    attention formulation (with a warning) around the HIP GEMMs and matches the host run."""
+    heads = 512 // dh
+    n = int(np.prod(mesh_shape))
+    host_devices(n)
+    vh, gh = _run_block(mesh_shape, heads=heads, dh=dh)
+    gpu_devices(n)
+    from learning_jax_sharding_amd.ops import hip
+    hip.lib()
+    with pytest.warns(UserWarning, match="head_dim 64"):
+        vg, gg = _run_block(mesh_shape, heads=heads, dh=dh)
+    assert abs(vh - vg) <= 3e-2 * max(1.0, abs(vh)), (vh, vg)
+    for k in gh:
+        for name in gh[k]:
+            a, b = gh[k][name], gg[k][name]
+            np.testing.assert_allclose(b, a, rtol=5e-2, atol=5e-2 * np.abs(a).max(), err_msg=f"{k}/{name}")
+
+
 def test_native_library_loaded(gpu_devices):
     gpu_devices(1)
     import learning_jax_sharding_amd as ljs
