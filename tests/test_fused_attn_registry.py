@@ -2,6 +2,7 @@
 gate): the attention op takes the fused forward's (o, lse) only for exactly the q / k / v column
 views of the registered projection output, with the same scale, non-causal; anything else falls
 back to its own kernel."""
+import pytest
 import torch
 
 from learning_jax_sharding_amd.ops import hip as H
@@ -72,3 +73,26 @@ def test_capture_end_drops_untaken_forward():
         if f is H.clear_fused_attention:
             f()
     assert H._take_fused_attention(q, k, v, 0.125, False, 0) is None
+
+
+def test_attention_head_dim_dispatch(monkeypatch):
+    """GPU attention entry points take the HIP kernels for head_dim 64 with a contiguous last dim
+    and the torch formulation (warned once per head-dim pair) for anything else."""
+    import warnings
+
+    import torch
+
+    from learning_jax_sharding_amd.ops import kernels as K
+    monkeypatch.setattr(K, "use_hip", lambda t: True)
+    monkeypatch.setattr(K, "_WARNED_DH", set())
+    q64 = torch.zeros(1, 4, 2, 64)
+    assert K._hip_attn(q64, q64, q64)
+    strided = torch.zeros(1, 4, 2, 128)[..., ::2]
+    with pytest.warns(UserWarning, match="head_dim 64"):
+        assert not K._hip_attn(strided, strided, strided)
+    q32 = torch.zeros(1, 4, 2, 32)
+    with pytest.warns(UserWarning, match="head_dim 32"):
+        assert not K._hip_attn(q32, q32, q32)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")     # once per head-dim pair
+        assert not K._hip_attn(q32, q32, q32)
